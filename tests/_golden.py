@@ -1,0 +1,35 @@
+"""Fixture loading helpers shared by the tests (test infrastructure)."""
+import json
+import pathlib
+
+import numpy as np
+
+GOLDEN = pathlib.Path(__file__).resolve().parent / "golden"
+
+
+def fixture_names():
+    return sorted(p.stem for p in GOLDEN.glob("fx*.npz"))
+
+
+def load(name):
+    z = np.load(GOLDEN / f"{name}.npz", allow_pickle=False)
+    d = {k: z[k] for k in z.files}
+    d["meta"] = json.loads(str(d["meta"]))
+    d["state_shapes"] = json.loads(str(d["state_shapes"]))
+    return d
+
+
+def cfg_of(meta):
+    from oracle.spff_oracle import SpffCfg
+    kw = {k: meta[k] for k in ("efilm", "fgate", "se", "specse") if k in meta}
+    return SpffCfg(in_ch=meta["in_ch"], num_classes=meta["K"], base=meta["base"], ksd=3, **kw)
+
+
+def state_of(d):
+    """Regenerate the fixture's parameters with the shared generator."""
+    from innovative3D.weightgen import synth_state
+    meta = d["meta"]
+    shapes = d["state_shapes"]
+    prefix = "model." if meta.get("lit") else ""
+    st = synth_state([(k, tuple(v)) for k, v in shapes.items()], meta["seed"], meta["jitter"])
+    return {k[len(prefix):] if k.startswith(prefix) else k: v for k, v in st.items()}

@@ -1,0 +1,288 @@
+#!/usr/bin/env python3
+"""Generate the golden parity fixtures by running the REFERENCE itself.
+
+Container-only tooling (the reference never travels to the GPU box).  Run:
+
+    python tests/golden/make_golden.py            # writes tests/golden/*.npz
+
+How the reference is run:
+* ``/root/reference`` is put on ``sys.path`` and ``innovative3D.config`` /
+  ``innovative3D.models`` / ``innovative3D.helpers`` are imported as-is.
+* Modules the reference imports but that take no part in the hot-path
+  arithmetic and are absent offline (pytorch_lightning, torchmetrics,
+  torchvision, pydicom, seaborn) are replaced by tiny stubs written to a temp
+  dir that is put first on ``sys.path``.  ``LightningModule`` is a plain
+  ``nn.Module`` with ``save_hyperparameters`` / no-op ``log``.
+* ``config.py:19`` unconditionally ``mkdir``s a /home/... path; the harness
+  turns ``Path.mkdir`` into a no-op for paths outside /tmp so nothing is
+  created outside this repo, and ``CHECKPOINT_DIR``/``LOG_DIR`` point to /tmp.
+
+Every fixture stores inputs AND outputs (so tests never need the reference):
+logits, CE, hard-dice loss part, total loss, the ``per_class_metrics_3d``
+9-tuple, and parameter gradients (full for base=8 nets, head/tail slices plus
+sum/L2 for base=32 nets).  Parameters come from
+``innovative3D.weightgen.synth_state`` (same generator the tests use).
+"""
+from __future__ import annotations
+
+import json
+import math
+import os
+import pathlib
+import sys
+import tempfile
+import textwrap
+
+import numpy as np
+
+HERE = pathlib.Path(__file__).resolve().parent
+REPO = HERE.parents[1]
+REF = pathlib.Path(os.environ.get("SPFF_REFERENCE", "/root/reference"))
+
+STUBS = {
+    "pytorch_lightning/__init__.py": """
+        import torch.nn as _nn
+        class _HP(dict):
+            def __getattr__(self, k):
+                try: return self[k]
+                except KeyError as e: raise AttributeError(k) from e
+        class LightningModule(_nn.Module):
+            def save_hyperparameters(self, *args, **kw):
+                hp = _HP()
+                for a in args:
+                    if isinstance(a, dict): hp.update(a)
+                hp.update(kw)
+                self.hparams = hp
+            def log(self, *a, **k): pass
+        class LightningDataModule: pass
+        class Trainer:
+            def __init__(self, *a, **k): raise RuntimeError("stub Trainer")
+        def seed_everything(seed=None, workers=False): return seed
+        from . import callbacks, loggers, utilities
+    """,
+    "pytorch_lightning/callbacks.py": """
+        class Callback: pass
+        class ModelCheckpoint(Callback):
+            def __init__(self, *a, **k): pass
+        class EarlyStopping(Callback):
+            def __init__(self, *a, **k): pass
+        class LearningRateMonitor(Callback):
+            def __init__(self, *a, **k): pass
+    """,
+    "pytorch_lightning/loggers.py": """
+        class Logger: pass
+        class CSVLogger(Logger):
+            def __init__(self, *a, **k): pass
+    """,
+    "pytorch_lightning/utilities/__init__.py": """
+        def rank_zero_only(fn): return fn
+        from . import rank_zero
+    """,
+    "pytorch_lightning/utilities/rank_zero.py": """
+        def rank_zero_only(fn): return fn
+    """,
+    "torchmetrics/__init__.py": """
+        class MeanMetric:
+            def __init__(self, *a, **k): raise RuntimeError("stub MeanMetric")
+    """,
+    "torchvision/__init__.py": "from . import transforms\n",
+    "torchvision/transforms/__init__.py": """
+        from . import functional
+        class InterpolationMode:
+            NEAREST = 0; BILINEAR = 2; BICUBIC = 3
+    """,
+    "torchvision/transforms/functional.py": """
+        def __getattr__(name):
+            def _f(*a, **k): raise RuntimeError("stub torchvision." + name)
+            return _f
+    """,
+    "pydicom/__init__.py": """
+        def dcmread(*a, **k): raise RuntimeError("stub pydicom")
+    """,
+    "seaborn/__init__.py": "",
+}
+
+
+def _install_harness():
+    stub_dir = pathlib.Path(tempfile.mkdtemp(prefix="spff_stubs_"))
+    for rel, src in STUBS.items():
+        p = stub_dir / rel
+        p.parent.mkdir(parents=True, exist_ok=True)
+        p.write_text(textwrap.dedent(src))
+    sys.path.insert(0, str(stub_dir))
+    sys.path.insert(1, str(REF))
+    sys.path.insert(2, str(REPO / "spff-unet-spcct_amd"))
+    os.environ.setdefault("CHECKPOINT_DIR", "/tmp/spff_ref_ckpt")
+    os.environ.setdefault("LOG_DIR", "/tmp/spff_ref_logs")
+    os.environ["PYTHONDONTWRITEBYTECODE"] = "1"
+    sys.dont_write_bytecode = True
+    _orig_mkdir = pathlib.Path.mkdir
+
+    def _guarded_mkdir(self, *a, **k):
+        if str(self).startswith("/tmp"):
+            return _orig_mkdir(self, *a, **k)
+        return None
+    pathlib.Path.mkdir = _guarded_mkdir
+
+
+def _import_reference():
+    _install_harness()
+    import innovative3D.config as C  # noqa: E402
+    import innovative3D.models as M  # noqa: E402
+    import innovative3D.helpers as Hh  # noqa: E402
+    return C, M, Hh
+
+
+def _labels(rng, shape, K, ignore_frac=0.03, absent=None):
+    y = rng.integers(0, K, size=shape)
+    if absent is not None:
+        y[y == absent] = (absent + 1) % K
+    m = rng.random(shape) < ignore_frac
+    y[m] = 255
+    return y.astype(np.int64)
+
+
+def _run_case(torch, Hh, core_or_lit, x_np, y_np, K, seed, mask_jitter, full_grads,
+              is_lit):
+    from innovative3D.weightgen import synth_state
+    x = torch.from_numpy(x_np)
+    y = torch.from_numpy(y_np)
+    model = core_or_lit
+    # first forward creates the lazy FourierGate masks (models.py:1532-1535)
+    with torch.no_grad():
+        model(x)
+    sd = model.state_dict()
+    synth = synth_state([(k, tuple(v.shape)) for k, v in sd.items()], seed, mask_jitter)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in synth.items()}, strict=True)
+    model.zero_grad(set_to_none=True)
+    logits = model(x)
+    ce = torch.nn.functional.cross_entropy(logits, y, ignore_index=255)
+    dice_part = Hh.macro_dice_loss(logits, y, K, 255, 1e-6)
+    loss = Hh.ce_plus_macro_dice_loss(logits, y, K, ignore_index=255)
+    loss.backward()
+    met = Hh.per_class_metrics_3d(logits.detach(), y, K, ignore_index=255)
+    out = {
+        "x": x_np, "labels": y_np,
+        "logits": logits.detach().numpy().astype(np.float32),
+        "ce": np.array(ce.item(), dtype=np.float64),
+        "dice_loss": np.array(dice_part, dtype=np.float64),
+        "loss": np.array(loss.item(), dtype=np.float64),
+        "met_dice": np.array(met[0], dtype=np.float64),
+        "met_sens": np.array(met[1], dtype=np.float64),
+        "met_spec": np.array(met[2], dtype=np.float64),
+        "met_scalars": np.array(met[3:], dtype=np.float64),
+    }
+    names = []
+    seen = set()
+    for k, p in model.named_parameters(remove_duplicate=False):
+        # ``_mask`` and ``freq_mask`` alias one tensor; keep the canonical key.
+        if id(p) in seen:
+            continue
+        seen.add(id(p))
+        names.append(k)
+        g = p.grad
+        if g is None:
+            g = torch.zeros_like(p)
+        g = g.detach().numpy().astype(np.float32)
+        if full_grads:
+            out["grad/" + k] = g
+        else:
+            flat = g.reshape(-1)
+            out["gradhead/" + k] = flat[:64].copy()
+            out["gradtail/" + k] = flat[-64:].copy()
+            out["gradsum/" + k] = np.array([flat.astype(np.float64).sum(),
+                                            np.sqrt((flat.astype(np.float64) ** 2).sum())])
+    out["param_names"] = np.array(names)
+    out["state_keys"] = np.array(list(sd.keys()))
+    out["state_shapes"] = np.array(json.dumps({k: list(v.shape) for k, v in sd.items()}))
+    return out
+
+
+def main():
+    C, M, Hh = _import_reference()
+    import torch
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    torch.use_deterministic_algorithms(False)
+    cases = {}
+
+    # --- Fx1: registry layout via the VARIANTS factory (config.py:423-428) ---
+    name, factory, _dm, _ck = [v for v in C.VARIANTS if v[0] == "SPFF-UNet"][0]
+    torch.manual_seed(0)
+    lit = factory()
+    rng = np.random.default_rng(11)
+    x = rng.standard_normal((1, 1, 5, 32, 32)).astype(np.float32)
+    y = _labels(rng, (1, 5, 32, 32), 13, absent=3)
+    cases["fx1_registry_k13"] = dict(
+        meta=dict(variant="SPFF-UNet", in_ch=1, base=32, K=13, seed=1, jitter=0.0, lit=True),
+        data=_run_case(torch, Hh, lit, x, y, 13, 1, 0.0, False, True))
+
+    # --- Fx1b: BASELINE config 1 (torch.manual_seed(0), randn, randint(0,9)) ---
+    torch.manual_seed(0)
+    lit9 = M.LitSPCT_EFiLM_FourierGate(num_classes=9)
+    torch.manual_seed(0)
+    x = torch.randn(1, 1, 5, 64, 64).numpy()
+    y = torch.randint(0, 9, (1, 5, 64, 64)).numpy().astype(np.int64)
+    cases["fx1b_config1_k9"] = dict(
+        meta=dict(variant="SPFF-UNet", in_ch=1, base=32, K=9, seed=2, jitter=0.0, lit=True),
+        data=_run_case(torch, Hh, lit9, x, y, 9, 2, 0.0, False, True))
+
+    def ns_core(in_ch, K, base, efilm=True, fgate=True, se=True, specse=True):
+        core = M.UNet3D_SpectralCore(in_channels=in_ch, num_classes=K, base=base, ksd=3,
+                                     use_se=se, use_specse=specse, use_spatial=False,
+                                     use_skip_gate=False)
+        if efilm or fgate:
+            core = M.upgrade_spct_with_novel_blocks(core, use_efilm=efilm,
+                                                    use_fouriergate=fgate, use_moe=False)
+        return core
+
+    # --- Fx2: north-star layout (Cin=5 channels, spatial D), base=8, full grads ---
+    rng = np.random.default_rng(22)
+    x = rng.standard_normal((1, 5, 16, 32, 32)).astype(np.float32)
+    y = _labels(rng, (1, 16, 32, 32), 9, absent=4)
+    cases["fx2_ns_base8"] = dict(
+        meta=dict(variant="SPFF-UNet", in_ch=5, base=8, K=9, seed=3, jitter=0.0, lit=False),
+        data=_run_case(torch, Hh, ns_core(5, 9, 8), x, y, 9, 3, 0.0, True, False))
+
+    # --- Fx3: FourierGate with non-unit mask & mag, even D (Nyquist), batch 2 ---
+    rng = np.random.default_rng(33)
+    x = rng.standard_normal((2, 5, 8, 16, 16)).astype(np.float32)
+    y = _labels(rng, (2, 8, 16, 16), 9, absent=2)
+    cases["fx3_fgate_even_b2"] = dict(
+        meta=dict(variant="SPFF-UNet", in_ch=5, base=8, K=9, seed=4, jitter=0.25, lit=False),
+        data=_run_case(torch, Hh, ns_core(5, 9, 8), x, y, 9, 4, 0.25, True, False))
+
+    # --- Fx3b: odd D=5 registry layout, jittered mask, batch 2, K=13 ---
+    rng = np.random.default_rng(44)
+    x = rng.standard_normal((2, 1, 5, 16, 16)).astype(np.float32)
+    y = _labels(rng, (2, 5, 16, 16), 13, absent=7)
+    cases["fx3b_fgate_odd_b2"] = dict(
+        meta=dict(variant="SPFF-UNet", in_ch=1, base=8, K=13, seed=5, jitter=0.25, lit=False),
+        data=_run_case(torch, Hh, ns_core(1, 13, 8), x, y, 13, 5, 0.25, True, False))
+
+    # --- Fx-ablations: the other SPCT-family registry variants, base=8 ---
+    abl = {
+        "E_SP_UNet": dict(efilm=True, fgate=False, se=True, specse=True),
+        "FG_SP_UNet": dict(efilm=False, fgate=True, se=True, specse=True),
+        "PlainCore_UNet": dict(efilm=False, fgate=False, se=False, specse=False),
+        "SP_UNet_core": dict(efilm=False, fgate=False, se=True, specse=True),
+    }
+    for i, (vname, fl) in enumerate(abl.items()):
+        rng = np.random.default_rng(55 + i)
+        x = rng.standard_normal((1, 5, 8, 16, 16)).astype(np.float32)
+        y = _labels(rng, (1, 8, 16, 16), 9)
+        cases["fxabl_" + vname] = dict(
+            meta=dict(variant=vname, in_ch=5, base=8, K=9, seed=6 + i, jitter=0.0, lit=False,
+                      **fl),
+            data=_run_case(torch, Hh, ns_core(5, 9, 8, **fl), x, y, 9, 6 + i, 0.0, True, False))
+
+    for cname, c in cases.items():
+        path = HERE / f"{cname}.npz"
+        d = dict(c["data"])
+        d["meta"] = np.array(json.dumps(c["meta"]))
+        np.savez_compressed(path, **d)
+        print(f"wrote {path.relative_to(REPO)}  loss={float(d['loss']):.6f}  "
+              f"({path.stat().st_size/1024:.0f} KiB)")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,77 @@
+"""Pin the CPU oracle against golden vectors produced by the reference itself
+(tests/golden/make_golden.py).  CPU-only."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from _golden import cfg_of, fixture_names, load, state_of
+from oracle import spff_oracle as O
+
+NAMES = fixture_names()
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_oracle_matches_reference(name):
+    d = load(name)
+    cfg = cfg_of(d["meta"])
+    st = state_of(d)
+    P = O.params_from_state(st)
+    x = torch.from_numpy(d["x"])
+    y = torch.from_numpy(d["labels"])
+    logits, loss, ce, dice = O.fwd_bwd(P, x, y, cfg)
+    ref = d["logits"]
+    err = float(np.abs(logits.numpy() - ref).max())
+    assert err <= 2e-5, err
+    assert torch.equal(logits.argmax(1), torch.from_numpy(ref).argmax(1))
+    assert math.isclose(float(ce), float(d["ce"]), rel_tol=1e-5)
+    assert math.isclose(dice, float(d["dice_loss"]), rel_tol=0, abs_tol=1e-12)
+    assert math.isclose(float(loss), float(d["loss"]), rel_tol=1e-5)
+    # metrics (exact given identical argmax)
+    met = O.per_class_metrics_3d(logits, y, cfg.num_classes, ignore_index=255)
+    np.testing.assert_array_equal(np.isnan(met[0]), np.isnan(d["met_dice"]))
+    np.testing.assert_allclose(np.array(met[0]), d["met_dice"], rtol=1e-12, equal_nan=True)
+    np.testing.assert_allclose(np.array(met[1]), d["met_sens"], rtol=1e-12, equal_nan=True)
+    np.testing.assert_allclose(np.array(met[2]), d["met_spec"], rtol=1e-12, equal_nan=True)
+    np.testing.assert_allclose(np.array(met[3:]), d["met_scalars"], rtol=1e-12, equal_nan=True)
+    # gradients
+    prefix = "model." if d["meta"].get("lit") else ""
+    for k in d["param_names"]:
+        k = str(k)
+        kk = k[len(prefix):]
+        kk = kk.replace("._mask", ".freq_mask")
+        g = P[kk].grad
+        g = np.zeros(P[kk].shape, np.float32) if g is None else g.numpy()
+        if "grad/" + k in d:
+            ref = d["grad/" + k]
+            scale = max(1e-6, float(np.abs(ref).max()))
+            assert float(np.abs(g - ref).max()) <= 1e-4 * scale + 1e-7, k
+        else:
+            flat = g.reshape(-1)
+            scale = max(1e-6, float(np.abs(d["gradhead/" + k]).max()))
+            np.testing.assert_allclose(flat[:64], d["gradhead/" + k], atol=1e-4 * scale + 1e-7)
+            np.testing.assert_allclose(flat[-64:], d["gradtail/" + k], atol=1e-4 * scale + 1e-7)
+            s = d["gradsum/" + k]
+            assert math.isclose(float(np.sqrt((flat.astype(np.float64) ** 2).sum())), float(s[1]),
+                                rel_tol=1e-4, abs_tol=1e-9), k
+
+
+def test_param_shapes_match_reference_state_dict():
+    for name in NAMES:
+        d = load(name)
+        cfg = cfg_of(d["meta"])
+        D = d["x"].shape[2]
+        prefix = "model." if d["meta"].get("lit") else ""
+        mine = O.param_shapes(cfg, D=D, prefix=prefix)
+        ref = d["state_shapes"]
+        assert list(mine.keys()) == list(ref.keys()), name
+        assert all(tuple(ref[k]) == tuple(v) for k, v in mine.items()), name
+
+
+def test_param_count_matches_survey():
+    # 5 491 284 params for the registry SPFF-UNet (K=13, Cin=1, base 32),
+    # plus 7 x (D//2+1) lazily created FourierGate mask entries.
+    cfg = O.SpffCfg(in_ch=1, num_classes=13, base=32)
+    n = sum(int(np.prod(s)) for s in O.param_shapes(cfg).values())
+    assert n == 5491284
