@@ -1,0 +1,208 @@
+#!/usr/bin/env python3
+"""bench.py -- BASELINE.json metric: voxels/s of SPFF-UNet forward + loss +
+backward (weight grads; optimizer step excluded, as in the metric's
+definition) on a batch of 2 x 5-channel 128^3 patches (K=13,
+base 32) per GPU, synthetic data resident in HBM before the timed region.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (data parallel, RCCL)
+
+One process per GPU; N > 1 is batch data parallelism (weak scaling): each rank
+runs its own batch, the valid-voxel count is all-reduced before the loss so
+the CE mean is the global one, and the flat gradient is all-reduced (RCCL).
+Rank 0 prints one JSON line.  The CPU baseline (rank 0, N=1) times the CPU
+oracle (oracle/spff_oracle.py, PyTorch-CPU restatement of the reference path)
+on a bounded sample of the same workload on the host cores.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import pathlib
+import statistics
+import sys
+import time
+
+ROOT = pathlib.Path(__file__).resolve().parent
+for _p in (str(ROOT), str(ROOT / "spff-unet-spcct_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 = f32 vector peak
+HBM_PEAK_GBS = 8000.0
+
+
+def build_model(K, base, in_ch, D, device, seed=0):
+    import innovative3D.models as M
+    from innovative3D.weightgen import synth_state
+    core = M.build_spct_energyfilm_fourier(num_classes=K, base=base, in_channels=in_ch)
+    for b in core._blocks():
+        b.fgate._ensure_mask(D, "cpu")
+    st = synth_state([(k, tuple(v.shape)) for k, v in core.state_dict().items()], seed=seed)
+    core.load_state_dict({k: torch.from_numpy(v) for k, v in st.items()})
+    return core.to(device), st
+
+
+def cpu_baseline(st, K, base, in_ch, H, W, depth, steps, threads):
+    """Oracle (PyTorch-CPU restatement of the reference) fwd+loss+bwd on host cores."""
+    from oracle import spff_oracle as O
+    from innovative3D.synthetic import synthetic_batch
+    torch.set_num_threads(threads)
+    cfg = O.SpffCfg(in_ch=in_ch, num_classes=K, base=base)
+    st_d = {k: v for k, v in st.items() if not k.endswith("._mask")}
+    # masks for the sample depth (all ones, as in the reference)
+    import numpy as np
+    for k in list(st_d):
+        if k.endswith("freq_mask"):
+            st_d[k] = np.ones((1, 1, depth // 2 + 1, 1, 1), np.float32)
+    P = O.params_from_state(st_d)
+    x, y = synthetic_batch(1, in_ch, depth, H, W, K, ignore_frac=0.01, seed=123)
+    times = []
+    for i in range(steps + 1):
+        t0 = time.perf_counter()
+        O.fwd_bwd(P, x, y, cfg)
+        dt = time.perf_counter() - t0
+        if i > 0:
+            times.append(dt)
+    med = statistics.median(times)
+    vox = depth * H * W
+    return {"value": vox / med, "unit": "voxels/s", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": f"oracle fwd+ce_plus_macro_dice+bwd on 1x{in_ch}x{depth}x{H}x{W} (K={K}, base "
+                      f"{base}) = 1/{(2 * 128) // depth} of the headline voxels; median of {steps} "
+                      f"steps after 1 warm-up ({med:.2f} s/step)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=2)
+    ap.add_argument("--size", type=int, default=128, help="D = H = W")
+    ap.add_argument("--in-ch", type=int, default=5)
+    ap.add_argument("--classes", type=int, default=13)
+    ap.add_argument("--base", type=int, default=32)
+    ap.add_argument("--cpu-baseline", choices=("auto", "skip"), default="auto")
+    ap.add_argument("--cpu-depth", type=int, default=32)
+    ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--pmc", default=str(ROOT / "profiles" / "r01_pmc_conv.json"),
+                    help="optional per-launch HBM traffic summary from rocprofv3 --pmc")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+
+    import innovative3D.helpers as Hh
+    from innovative3D import _engine as E
+    from innovative3D.synthetic import synthetic_batch
+
+    B, S, K = args.batch, args.size, args.classes
+    core, st = build_model(K, args.base, args.in_ch, S, device)
+    x, y = synthetic_batch(B, args.in_ch, S, S, S, K, ignore_frac=0.01, seed=1000 + rank,
+                           device=device)
+    params = [p for p in core.parameters()]
+
+    def step():
+        for p in params:
+            p.grad = None
+        logits = core(x)
+        cnt = None
+        if world > 1:
+            cnt = E.count_valid(y, 255)
+            dist.all_reduce(cnt)
+        loss, _conf = Hh.ce_dice_with_confusion(logits, y, K, 255, count_override=cnt)
+        loss.backward()
+        if world > 1:
+            gs = [p.grad for p in params if p.grad is not None]
+            flat = torch.cat([g.reshape(-1) for g in gs])
+            dist.all_reduce(flat)
+            o = 0
+            for g in gs:
+                n = g.numel()
+                g.copy_(flat[o:o + n].view_as(g))
+                o += n
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    plan = core._plan
+    plan.prof_enable(True)
+    plan.prof_collect()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    prof = plan.prof_collect()
+    plan.prof_enable(False)
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    vox_step = B * S * S * S
+    value = world * vox_step * args.steps / elapsed
+
+    # dominant kernel: k_conv3d_fwd (forward + dgrad convs, fp32 MFMA), timed live
+    ms = prof["conv_fwd"][0] + prof["conv_dgrad"][0]
+    fl = prof["conv_fwd"][1] + prof["conv_dgrad"][1]
+    nl = prof["conv_fwd"][2] + prof["conv_dgrad"][2]
+    achieved = fl / (ms * 1e-3) / 1e12 if ms > 0 else None
+    traffic = None
+    try:
+        pm = json.loads(pathlib.Path(args.pmc).read_text())
+        traffic = pm.get("hbm_bytes_per_launch")
+    except Exception:
+        traffic = None
+    roof = {"bound": "mfma", "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": (achieved / FP32_MFMA_PEAK_TFLOPS) if achieved else None, "traffic": traffic,
+            "kernel": "k_conv3d_fwd (3x3x3 implicit GEMM, fwd+dgrad)",
+            "avg_launch_ms": ms / max(1, nl), "launches": int(nl),
+            "algorithmic_flops_per_launch": fl / max(1, nl),
+            "per_class_ms_per_step": {k: v[0] / args.steps for k, v in prof.items()},
+            "per_class_tflops": {k: (v[1] / (v[0] * 1e-3) / 1e12 if v[0] > 0 else None)
+                                 for k, v in prof.items()},
+            "step_tflops": value / world * 2462016 / 1e12}
+    out = {
+        "metric": "voxels/sec fwd+bwd, SPFF-UNet 5-ch 128^3 patch",
+        "value": value, "unit": "voxels/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (x~N(0,1), labels U[0,K) with 1% ignore=255; weights from weightgen seed 0)",
+        "config": {"workload": f"SPFF-UNet fwd+ce_plus_macro_dice+bwd, batch {B} x {args.in_ch}ch x "
+                               f"{S}^3 per GPU, K={K}, base {args.base}",
+                   "global_batch": B * world, "shape": [B, args.in_ch, S, S, S],
+                   "parallelism": f"dp{world}"},
+        "loss": float(loss.item()),
+        "roofline": roof,
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and args.cpu_baseline == "auto":
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+        threads = min(threads, os.cpu_count() or threads)
+        out["cpu_baseline"] = cpu_baseline(st, K, args.base, args.in_ch, S, S, args.cpu_depth,
+                                           args.cpu_steps, threads)
+        out["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

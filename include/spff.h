@@ -1,0 +1,114 @@
+/* spff.h -- C ABI of the MI355X-native SPFF-UNet engine (libspff_hip.so).
+ *
+ * This is the drop-in boundary for the reference's hot path: the SPFF-UNet
+ * forward (innovative3D/models.py:693-701 UNet3D_SpectralCore.forward with the
+ * _DoubleConvSpectral_Novel blocks of models.py:1448-1544, built by
+ * build_spct_energyfilm_fourier models.py:1547-1555 behind
+ * LitSPCT_EFiLM_FourierGate models.py:1558-1564), the loss
+ * ce_plus_macro_dice_loss (helpers.py:797-803) and autograd's backward of both.
+ * The reference binds these through PyTorch; the Python mirror in
+ * spff-unet-spcct_amd/innovative3D binds them with ctypes.
+ *
+ * Conventions: plain device pointers + sizes, no torch types.  All calls are
+ * stream-ordered and asynchronous (hipStream_t passed as void*; NULL = default
+ * stream).  Activations are fp32; the network input is the reference layout
+ * [B][Cin][D][H][W]; logits/dlogits are channel-last [B][D][H][W][K] (a
+ * torch.channels_last_3d view of the reference's [B][K][D][H][W]).  Params /
+ * dparams are ONE flat fp32 buffer in reference state-dict order (see
+ * spff_param_info; the lazily created FourierGate mask appears once, under
+ * "...fgate.freq_mask", and stands for the aliased "...fgate._mask" key).
+ * Functions return 0 on success, a negative SPFF_E* code otherwise (never
+ * throw); spff_last_error() describes the last failure of the calling thread.
+ * A plan is not thread-safe and holds one forward's saved activations inside
+ * the caller's workspace until the matching backward.
+ */
+#ifndef SPFF_H_
+#define SPFF_H_
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SPFF_OK 0
+#define SPFF_EINVAL (-1)
+#define SPFF_EHIP (-2)
+#define SPFF_ESHAPE (-3)
+
+typedef struct spff_cfg {
+  int batch, in_ch, depth, height, width;  /* input [B][Cin][D][H][W] */
+  int num_classes;                          /* K (<= 32) */
+  int base;                                 /* f (power of two, >= 8) */
+  int ksd;                                  /* spectral kernel depth: 1 or 3 */
+  int use_efilm, use_fgate;                 /* novel block (models.py:1448) */
+  int use_se, use_specse;                   /* encoder post (models.py:684) */
+  int reserved[8];                          /* zero */
+} spff_cfg;
+
+typedef struct spff_plan spff_plan;
+
+/* plan lifetime (replaces build_class(...)() -> module construction, config.py:159-182) */
+int spff_plan_create(const spff_cfg* cfg, spff_plan** out);
+void spff_plan_destroy(spff_plan* plan);
+const char* spff_last_error(void);
+
+/* flat parameter layout (reference state-dict order, models.py:655-681) */
+int spff_num_params(const spff_plan* plan);
+int spff_param_info(const spff_plan* plan, int i, const char** name, int* ndim,
+                    int64_t shape[5], int64_t* offset, int64_t* numel);
+int64_t spff_param_floats(const spff_plan* plan);
+size_t spff_workspace_bytes(const spff_plan* plan);
+
+/* forward: x [B][Cin][D][H][W] -> logits [B][D][H][W][K]  (models.py:693-701) */
+int spff_forward(spff_plan* plan, const float* x, const float* params, float* logits,
+                 void* workspace, void* stream);
+/* backward of the last forward: dlogits [B][D][H][W][K] -> dparams (flat, every
+ * entry written).  Input gradient is not produced (the hot path never needs it). */
+int spff_backward(spff_plan* plan, const float* dlogits, const float* params, float* dparams,
+                  void* workspace, void* stream);
+/* device pointer + shape of a saved intermediate (debug / tests), e.g. "enc1.out" */
+int spff_saved_tensor(const spff_plan* plan, void* workspace, const char* name,
+                      const float** ptr, int64_t* nvox, int* channels);
+
+/* optional HIP-event timing of the MFMA kernels on the plan's stream (bench.py):
+ * classes 0 = conv3d fwd, 1 = conv3d dgrad (same kernel), 2 = conv3d wgrad,
+ * 3 = ConvTranspose / 1x1 head GEMMs.  collect() syncs on the recorded events
+ * and writes out[3*c + {0,1,2}] = {total ms, algorithmic FLOPs, launches}. */
+int spff_prof_enable(spff_plan* plan, int on);
+int spff_prof_collect(spff_plan* plan, double* out, int nclass);
+
+/* ce_plus_macro_dice_loss (helpers.py:797-803) on channel-last logits [V][K].
+ * out4 (device) = [ce, ce + 0.5*hard_dice_loss, hard_dice_loss, n_valid];
+ * dlogits = d(ce)/dlogits (softmax - onehot)/N_valid (0 for ignored voxels);
+ * conf (device) = K*(K+1) int64: conf[pred*(K+1) + label] over non-ignored
+ * voxels (argmax, first max wins), column K = labels outside [0,K) (the
+ * reference raises on those in the loss; they are excluded from CE here).
+ * count_override (device int64*, may be NULL): global N_valid for data-parallel
+ * runs (all-reduced by the caller); NULL -> counted locally. */
+size_t spff_loss_ws_bytes(int64_t nvox, int num_classes);
+int spff_loss(const float* logits, const int64_t* labels, int64_t nvox, int num_classes,
+              int ignore_index, double smooth, const int64_t* count_override, float* out4,
+              float* dlogits, int64_t* conf, void* ws, void* stream);
+/* argmax confusion only (per_class_metrics_3d, helpers.py:668-725) */
+int spff_confusion(const float* logits, const int64_t* labels, int64_t nvox, int num_classes,
+                   int ignore_index, int64_t* conf, void* stream);
+int spff_count_valid(const int64_t* labels, int64_t nvox, int ignore_index, int64_t* count,
+                     void* stream);
+/* x[i] *= *scale (scale is a device scalar) */
+int spff_scale(float* x, int64_t n, const float* scale, void* stream);
+
+/* op-level entry points (parity tests): channel-last activations, reference
+ * weight layout W[Cout][Cin][ksd][3][3].  ws >= spff_conv3d_ws_bytes(...). */
+size_t spff_conv3d_ws_bytes(int B, int D, int H, int W, int cin, int cout, int ksd);
+int spff_conv3d_fwd(const float* x, int ldx, const float* w, float* y, int B, int D, int H, int W,
+                    int cin, int cout, int ksd, void* ws, void* stream);
+int spff_conv3d_dgrad(const float* dy, const float* w, float* dx, int B, int D, int H, int W,
+                      int cin, int cout, int ksd, void* ws, void* stream);
+int spff_conv3d_wgrad(const float* x, int ldx, const float* dy, float* dw, int B, int D, int H,
+                      int W, int cin, int cout, int ksd, void* ws, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SPFF_H_ */

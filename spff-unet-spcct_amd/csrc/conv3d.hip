@@ -1,0 +1,379 @@
+// 3x3x3 ("ksd x 3 x 3") convolution as implicit GEMM on gfx950 fp32 MFMA.
+//
+// Replaces nn.Conv3d(cin, cout, (ksd,3,3), padding=(ksd//2,1,1), bias=False)
+// (reference models.py:616-618) -- forward, input-gradient and weight-gradient.
+//
+// Design (MI355X-first, see DESIGN.md "conv3d"):
+//  * Activations are channel-last [B][D][H][W][C] fp32.
+//  * Forward/dgrad: one workgroup (256 threads = 4 waves of 64) owns a
+//    TD x TH x TW = 2 x 8 x 16 = 256-voxel output tile x BN output channels.
+//    Per reduction chunk of CK input channels it stages the zero-padded input
+//    halo (TD+KD-1) x 10 x 18 x CK and the weight slab [taps][CK][BN] in LDS,
+//    then runs all KD*9 taps out of LDS: the halo is read 27x from LDS, never
+//    re-fetched from L2.  MFMA is v_mfma_f32_32x32x2_f32 (exact fp32, k-ordered
+//    fma chain) -- the parity-safe precision.
+//  * dgrad = the same kernel on dy with the flipped / transposed weight pack.
+//  * wgrad: rows = (tap, ci) pairs, cols = co, reduction over voxels; each
+//    workgroup owns all taps x 16 ci x 32 co and a contiguous range of
+//    1x8x16 voxel tiles, writes an fp32 partial slab; a second kernel sums the
+//    slabs in a fixed order (deterministic, no float atomics).
+#include "spff_internal.h"
+
+namespace spff {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+
+// ------------------------------------------------------------ weight pack --
+__global__ void k_conv_pack(const float* __restrict__ w, float* __restrict__ wt, int Cout,
+                            int Cin, int T, int kpad, int npad, int dgrad) {
+  // output element (tap, k, n) of wt[T][kpad][npad]
+  int64_t total = (int64_t)T * kpad * npad;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int n = (int)(i % npad);
+    int k = (int)((i / npad) % kpad);
+    int tap = (int)(i / ((int64_t)npad * kpad));
+    float v = 0.f;
+    if (!dgrad) {
+      // k = ci, n = co
+      if (k < Cin && n < Cout) v = w[((int64_t)n * Cin + k) * T + tap];
+    } else {
+      // k = co, n = ci, flipped tap
+      if (k < Cout && n < Cin) v = w[((int64_t)k * Cin + n) * T + (T - 1 - tap)];
+    }
+    wt[i] = v;
+  }
+}
+
+hipError_t conv_pack_weights(const float* w, float* wt, int Cout, int Cin, int KD, int kpad,
+                             int npad, bool dgrad, hipStream_t s) {
+  int T = KD * 9;
+  int64_t total = (int64_t)T * kpad * npad;
+  int grid = (int)std::min<int64_t>((total + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_conv_pack, dim3(grid), dim3(256), 0, s, w, wt, Cout, Cin, T, kpad, npad,
+                     dgrad ? 1 : 0);
+  return hipGetLastError();
+}
+
+int conv3d_bn(int Cout) { return Cout >= 64 ? 64 : 32; }
+
+// ------------------------------------------------------------ fwd / dgrad --
+template <int BN, int CK, int KD>
+__global__ __launch_bounds__(256) void k_conv3d_fwd(Src2 x, const float* __restrict__ wt,
+                                                    Dst2 y, Vol vol, int Cin, int kpad, int Cout,
+                                                    int npad, int tilesD, int tilesH,
+                                                    int tilesW) {
+  constexpr int TD = 2, TH = 8, TW = 16;
+  constexpr int HD = TD + KD - 1, HH = TH + 2, HWD = TW + 2;
+  constexpr int P = CK + 1;  // odd voxel pitch -> conflict-free 32-lane b32 reads
+  constexpr int XS = HD * HH * HWD * P;
+  constexpr int T = KD * 9;
+  constexpr int NB = BN / 32, MB = 2;
+  __shared__ float lds[XS + T * CK * BN];
+  float* Xs = lds;
+  float* Ws = lds + XS;
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int khalf = lane >> 5, l32 = lane & 31;
+  int t = blockIdx.x;
+  const int twi = t % tilesW; t /= tilesW;
+  const int thi = t % tilesH; t /= tilesH;
+  const int tdi = t % tilesD;
+  const int b = t / tilesD;
+  const int d0 = tdi * TD, h0 = thi * TH, w0 = twi * TW;
+  const int n0 = blockIdx.y * BN;
+  const int D = vol.D, H = vol.H, W = vol.W;
+
+  int hpos[MB];
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) {
+    int v = wave * 64 + mb * 32 + l32;
+    int td = v / (TH * TW), th = (v / TW) % TH, tw = v % TW;
+    hpos[mb] = (td * HH + th) * HWD + tw;
+  }
+
+  f32x16 acc[MB][NB];
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[mb][nb][r] = 0.f;
+
+  for (int c0 = 0; c0 < kpad; c0 += CK) {
+    if (c0) __syncthreads();
+    // ---- stage input halo (zero padded) ----
+    constexpr int Q = CK / 4;
+    for (int i = threadIdx.x; i < HD * HH * HWD * Q; i += 256) {
+      const int q = i % Q, pos = i / Q;
+      const int hw = pos % HWD, t2 = pos / HWD, hh = t2 % HH, hd = t2 / HH;
+      const int gd = d0 + hd - KD / 2, gh = h0 + hh - 1, gw = w0 + hw - 1;
+      const int c = c0 + 4 * q;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if ((unsigned)gd < (unsigned)D && (unsigned)gh < (unsigned)H &&
+          (unsigned)gw < (unsigned)W && c < Cin) {
+        const int64_t vox = (((int64_t)b * D + gd) * H + gh) * W + gw;
+        const float* p = c < x.split ? x.p0 + vox * x.ld0 + c : x.p1 + vox * x.ld1 + (c - x.split);
+        v = *reinterpret_cast<const float4*>(p);
+      }
+      float* d = Xs + pos * P + 4 * q;
+      d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+    }
+    // ---- stage weight slab [T][CK][BN] ----
+    for (int i = threadIdx.x; i < T * CK * (BN / 4); i += 256) {
+      const int j = i % (BN / 4), row = i / (BN / 4);
+      const int tap = row / CK, ci = row % CK;
+      const float4 v = *reinterpret_cast<const float4*>(
+          wt + ((int64_t)(tap * kpad + c0 + ci)) * npad + n0 + 4 * j);
+      *reinterpret_cast<float4*>(Ws + row * BN + 4 * j) = v;
+    }
+    __syncthreads();
+#pragma unroll 3
+    for (int tap = 0; tap < T; ++tap) {
+      const int kd = tap / 9, kh = (tap / 3) % 3, kw = tap % 3;
+      const int toff = (kd * HH + kh) * HWD + kw;
+#pragma unroll
+      for (int s = 0; s < CK / 2; ++s) {
+        const int ci = 2 * s + khalf;
+        float a[MB], bb[NB];
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb) a[mb] = Xs[(hpos[mb] + toff) * P + ci];
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) bb[nb] = Ws[(tap * CK + ci) * BN + nb * 32 + l32];
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+          for (int nb = 0; nb < NB; ++nb)
+            acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[mb], bb[nb], acc[mb][nb], 0, 0, 0);
+      }
+    }
+  }
+
+  // ---- epilogue: C[i][j], row i = voxel, col j = out channel ----
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int i = (r & 3) + 8 * (r >> 2) + 4 * khalf;
+      const int v = wave * 64 + mb * 32 + i;
+      const int td = v / (TH * TW), th = (v / TW) % TH, tw = v % TW;
+      const int gd = d0 + td, gh = h0 + th, gw = w0 + tw;
+      if (gd >= D || gh >= H || gw >= W) continue;
+      const int64_t vox = (((int64_t)b * D + gd) * H + gh) * W + gw;
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) {
+        const int n = n0 + nb * 32 + l32;
+        if (n >= Cout) continue;
+        float* p = n < y.split ? y.p0 + vox * y.ld0 + n : y.p1 + vox * y.ld1 + (n - y.split);
+        *p = acc[mb][nb][r];
+      }
+    }
+  }
+}
+
+hipError_t conv3d_fwd(const Src2& x, const float* wt, const Dst2& y, Vol vol, int KD, int Cin,
+                      int kpad, int Cout, int npad, hipStream_t s) {
+  const int BN = conv3d_bn(Cout);
+  if (npad % BN || kpad % 8) return hipErrorInvalidValue;
+  const int tilesD = cdiv(vol.D, 2), tilesH = cdiv(vol.H, 8), tilesW = cdiv(vol.W, 16);
+  dim3 grid(vol.B * tilesD * tilesH * tilesW, npad / BN);
+  if (BN == 64) {
+    if (KD == 3)
+      hipLaunchKernelGGL((k_conv3d_fwd<64, 4, 3>), grid, dim3(256), 0, s, x, wt, y, vol, Cin, kpad,
+                         Cout, npad, tilesD, tilesH, tilesW);
+    else
+      hipLaunchKernelGGL((k_conv3d_fwd<64, 4, 1>), grid, dim3(256), 0, s, x, wt, y, vol, Cin, kpad,
+                         Cout, npad, tilesD, tilesH, tilesW);
+  } else {
+    if (KD == 3)
+      hipLaunchKernelGGL((k_conv3d_fwd<32, 8, 3>), grid, dim3(256), 0, s, x, wt, y, vol, Cin, kpad,
+                         Cout, npad, tilesD, tilesH, tilesW);
+    else
+      hipLaunchKernelGGL((k_conv3d_fwd<32, 8, 1>), grid, dim3(256), 0, s, x, wt, y, vol, Cin, kpad,
+                         Cout, npad, tilesD, tilesH, tilesW);
+  }
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ wgrad --
+namespace {
+constexpr int WG_CI = 16, WG_CO = 32, WG_TH = 8, WG_TW = 16, WG_TV = WG_TH * WG_TW;
+struct WgradPlan {
+  int kpad, npad, tilesD, tilesH, tilesW, ntiles, nsplit, tps;
+};
+WgradPlan wgrad_plan(Vol vol, int Cin, int Cout) {
+  WgradPlan p;
+  p.kpad = cdiv(Cin, WG_CI) * WG_CI;
+  p.npad = cdiv(Cout, WG_CO) * WG_CO;
+  p.tilesD = vol.D;
+  p.tilesH = cdiv(vol.H, WG_TH);
+  p.tilesW = cdiv(vol.W, WG_TW);
+  p.ntiles = vol.B * p.tilesD * p.tilesH * p.tilesW;
+  const int nout = (p.kpad / WG_CI) * (p.npad / WG_CO);
+  int nsplit = std::max(1, cdiv(2048, nout));
+  nsplit = std::min(nsplit, std::max(1, p.ntiles / 2));
+  p.tps = cdiv(p.ntiles, nsplit);
+  p.nsplit = cdiv(p.ntiles, p.tps);
+  return p;
+}
+}  // namespace
+
+template <int KD>
+__global__ __launch_bounds__(256) void k_conv3d_wgrad(Src2 x, const float* __restrict__ dy,
+                                                      int lddy, float* __restrict__ part, Vol vol,
+                                                      int Cin, int kpad, int Cout, int npad,
+                                                      int tilesH, int tilesW, int ntiles,
+                                                      int tps) {
+  constexpr int HD = KD, HH = WG_TH + 2, HWD = WG_TW + 2;
+  constexpr int P = WG_CI + 1;
+  constexpr int XS = HD * HH * HWD * P;
+  constexpr int T = KD * 9;
+  constexpr int R = T * WG_CI;
+  constexpr int NBLK = (R + 31) / 32;
+  constexpr int NJ = (NBLK + 3) / 4;
+  __shared__ float lds[XS + WG_TV * WG_CO + 4];
+  float* Xs = lds;
+  float* Ys = lds + XS;
+  const int ZERO = XS + WG_TV * WG_CO;  // index of a 0.0 slot
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int khalf = lane >> 5, l32 = lane & 31;
+  const int split = blockIdx.x, ci0 = blockIdx.y * WG_CI, co0 = blockIdx.z * WG_CO;
+  const int D = vol.D, H = vol.H, W = vol.W;
+  if (threadIdx.x == 0) lds[ZERO] = 0.f;
+
+  // per-lane row -> (tap, ci) lds offset; invalid rows read the zero slot.
+  int off[NJ], mul[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int rb = wave + 4 * j;
+    const int rr = rb * 32 + l32;
+    if (rb < NBLK && rr < R) {
+      const int tap = rr / WG_CI, ci = rr % WG_CI;
+      const int kd = tap / 9, kh = (tap / 3) % 3, kw = tap % 3;
+      off[j] = ((kd * HH + kh) * HWD + kw) * P + ci;
+      mul[j] = P;
+    } else {
+      off[j] = ZERO;
+      mul[j] = 0;
+    }
+  }
+  f32x16 acc[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+
+  const int tbeg = split * tps;
+  const int tend = min(ntiles, tbeg + tps);
+  for (int tile = tbeg; tile < tend; ++tile) {
+    int t = tile;
+    const int twi = t % tilesW; t /= tilesW;
+    const int thi = t % tilesH; t /= tilesH;
+    const int d0 = t % D;
+    const int b = t / D;
+    const int h0 = thi * WG_TH, w0 = twi * WG_TW;
+    __syncthreads();
+    // halo of x: HD x 10 x 18 voxels x 16 channels
+    for (int i = threadIdx.x; i < HD * HH * HWD * (WG_CI / 4); i += 256) {
+      const int q = i % (WG_CI / 4), pos = i / (WG_CI / 4);
+      const int hw = pos % HWD, t2 = pos / HWD, hh = t2 % HH, hd = t2 / HH;
+      const int gd = d0 + hd - KD / 2, gh = h0 + hh - 1, gw = w0 + hw - 1;
+      const int c = ci0 + 4 * q;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if ((unsigned)gd < (unsigned)D && (unsigned)gh < (unsigned)H &&
+          (unsigned)gw < (unsigned)W && c < Cin) {
+        const int64_t vox = (((int64_t)b * D + gd) * H + gh) * W + gw;
+        const float* p = c < x.split ? x.p0 + vox * x.ld0 + c : x.p1 + vox * x.ld1 + (c - x.split);
+        v = *reinterpret_cast<const float4*>(p);
+      }
+      float* dd = Xs + pos * P + 4 * q;
+      dd[0] = v.x; dd[1] = v.y; dd[2] = v.z; dd[3] = v.w;
+    }
+    // dy tile: 128 voxels x 32 channels
+    for (int i = threadIdx.x; i < WG_TV * (WG_CO / 4); i += 256) {
+      const int q = i % (WG_CO / 4), k = i / (WG_CO / 4);
+      const int gh = h0 + k / WG_TW, gw = w0 + k % WG_TW;
+      const int c = co0 + 4 * q;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (gh < H && gw < W && c < Cout) {
+        const int64_t vox = (((int64_t)b * D + d0) * H + gh) * W + gw;
+        v = *reinterpret_cast<const float4*>(dy + vox * lddy + c);
+      }
+      *reinterpret_cast<float4*>(Ys + k * WG_CO + 4 * q) = v;
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int s = 0; s < WG_TV / 2; ++s) {
+      const int k = 2 * s + khalf;
+      const int hp = (k / WG_TW) * HWD + (k % WG_TW);
+      const float bv = Ys[k * WG_CO + l32];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        if (wave + 4 * j < NBLK) {
+          const float av = lds[hp * mul[j] + off[j]];
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[j], 0, 0, 0);
+        }
+      }
+    }
+  }
+  // write partial slab [split][tap][kpad][npad]
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int rb = wave + 4 * j;
+    if (rb >= NBLK) continue;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int i = (r & 3) + 8 * (r >> 2) + 4 * khalf;
+      const int rr = rb * 32 + i;
+      if (rr >= R) continue;
+      const int tap = rr / WG_CI, ci = rr % WG_CI;
+      part[(((int64_t)split * T + tap) * kpad + ci0 + ci) * npad + co0 + l32] = acc[j][r];
+    }
+  }
+}
+
+__global__ void k_wgrad_reduce(const float* __restrict__ part, float* __restrict__ dw, int nsplit,
+                               int T, int kpad, int npad, int Cin, int Cout) {
+  const int64_t total = (int64_t)T * Cin * Cout;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int co = (int)(i % Cout);
+    const int ci = (int)((i / Cout) % Cin);
+    const int tap = (int)(i / ((int64_t)Cout * Cin));
+    const int64_t stride = (int64_t)T * kpad * npad;
+    const float* p = part + ((int64_t)tap * kpad + ci) * npad + co;
+    float s = 0.f;
+    for (int k = 0; k < nsplit; ++k) s += p[k * stride];
+    dw[((int64_t)co * Cin + ci) * T + tap] = s;
+  }
+}
+
+size_t conv3d_wgrad_ws_bytes(Vol vol, int KD, int Cin, int Cout) {
+  WgradPlan p = wgrad_plan(vol, Cin, Cout);
+  return (size_t)p.nsplit * KD * 9 * p.kpad * p.npad * sizeof(float);
+}
+
+hipError_t conv3d_wgrad(const Src2& x, const float* dy, int lddy, float* dw, Vol vol, int KD,
+                        int Cin, int Cout, float* ws, hipStream_t s) {
+  WgradPlan p = wgrad_plan(vol, Cin, Cout);
+  dim3 grid(p.nsplit, p.kpad / WG_CI, p.npad / WG_CO);
+  if (KD == 3)
+    hipLaunchKernelGGL(k_conv3d_wgrad<3>, grid, dim3(256), 0, s, x, dy, lddy, ws, vol, Cin, p.kpad,
+                       Cout, p.npad, p.tilesH, p.tilesW, p.ntiles, p.tps);
+  else
+    hipLaunchKernelGGL(k_conv3d_wgrad<1>, grid, dim3(256), 0, s, x, dy, lddy, ws, vol, Cin, p.kpad,
+                       Cout, p.npad, p.tilesH, p.tilesW, p.ntiles, p.tps);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const int T = KD * 9;
+  int64_t total = (int64_t)T * Cin * Cout;
+  int g = (int)std::min<int64_t>((total + 255) / 256, 8192);
+  hipLaunchKernelGGL(k_wgrad_reduce, dim3(g), dim3(256), 0, s, ws, dw, p.nsplit, T, p.kpad,
+                     p.npad, Cin, Cout);
+  return hipGetLastError();
+}
+
+}  // namespace spff

@@ -1,0 +1,800 @@
+// SPFF-UNet engine: plan (parameter + workspace layout), forward, backward and
+// the C ABI of include/spff.h.
+//
+// Graph (reference UNet3D_SpectralCore.forward, models.py:693-701):
+//   e1 = post0(enc1(x)); e2 = post1(enc2(pool(e1))); e3 = post2(enc3(pool(e2)))
+//   b  = post3(bott(pool(e3)))
+//   d3 = dec3([up3(b) | e3]); d2 = dec2([up2(d3) | e2]); d1 = dec1([up1(d2) | e1])
+//   logits = out(d1)
+// Block (models.py:1473-1478 + _post 684-685):
+//   y1 = conv(x); a1 = lrelu(IN(y1)); y2 = conv(a1); out = lrelu(IN(y2))*P + Q
+// with the gate algebra (EFiLM, FourierGate, SpectralSE, SE) folded into the
+// per-(b,c,d) coefficients P, Q (gates.hip).  Saved for backward: y1, a1, y2,
+// out and the (b,c)/(b,c,d) statistics -- everything else is recomputed.
+#include "spff_internal.h"
+#include "spff.h"
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+using namespace spff;
+
+namespace spff {
+size_t upconv_pack_floats(int Cin, int Cout);
+size_t upconv_pack_dgrad_offset(int Cin, int Cout);
+}
+
+static thread_local std::string g_err;
+static int fail(int code, const std::string& m) {
+  g_err = m;
+  return code;
+}
+#define HIPCK(expr)                                                                        \
+  do {                                                                                     \
+    hipError_t _e = (expr);                                                                \
+    if (_e != hipSuccess)                                                                  \
+      return fail(SPFF_EHIP, std::string(#expr) + " -> " + hipGetErrorString(_e));         \
+  } while (0)
+// PROF: time one launch with HIP events on the plan's stream when enabled.
+#define PROF(P, CLS, FLOPS, expr)                                                        \
+  do {                                                                                   \
+    spff_plan* _p = (P);                                                                 \
+    spff_plan::ProfRec* _r = _p->prof_on ? prof_slot(_p, (CLS), (FLOPS)) : nullptr;      \
+    if (_r) HIPCK(hipEventRecord(_r->a, _p->st));                                        \
+    HIPCK(expr);                                                                         \
+    if (_r) HIPCK(hipEventRecord(_r->b, _p->st));                                        \
+  } while (0)
+#define CK(expr)               \
+  do {                         \
+    int _r = (expr);           \
+    if (_r != SPFF_OK) return _r; \
+  } while (0)
+
+namespace {
+
+static inline int rup(int a, int b) { return (a + b - 1) / b * b; }
+
+struct PEnt {
+  std::string name;
+  std::vector<int64_t> shape;
+  int64_t off, numel;
+};
+
+struct ConvL {
+  int Cin, Cout;
+  int64_t w;
+  int kpad_f, npad_f, kpad_d, npad_d;
+};
+
+struct Blk {
+  std::string name;
+  int lvl, Cin, C;
+  bool novel, efilm, fgate, post_se, post_spec;
+  ConvL c1, c2;
+  int64_t g1 = -1, b1 = -1, g2 = -1, b2 = -1;
+  int64_t fw0 = -1, fb0 = -1, fw2 = -1, fb2 = -1;
+  int64_t mag = -1, mask = -1;
+  int64_t sw0 = -1, sb0 = -1, sw2 = -1, sb2 = -1;
+  size_t y1, a1, y2, out;
+  size_t mean1, rstd1, al1, de1, mean2, rstd2, al2, de2;
+  size_t Sa, t, bt, hid, s1, g1s, sg2, p, h, e, P, Q;
+  bool tail() const { return efilm || fgate || post_se || post_spec; }
+};
+
+struct UpL {
+  int Cin, Cout, lvl_low;
+  int64_t w, b;
+  size_t pk, out;
+};
+
+}  // namespace
+
+struct spff_plan {
+  spff_cfg cfg;
+  Vol vol[4];
+  int f, KD, ldx, K;
+  std::vector<PEnt> params;
+  int64_t nparam = 0;
+  Blk blk[7];
+  UpL up[3];  // up3, up2, up1
+  int64_t out_w = -1, out_b = -1;
+  size_t head_pk = 0;
+  size_t x_cl = 0, pool[3] = {0, 0, 0}, pidx[3] = {0, 0, 0};
+  size_t red_ws = 0, red_out = 0, gscr = 0, Abuf = 0, Bbuf = 0, kk1 = 0, kk2 = 0, wg_ws = 0,
+         wt = 0;
+  size_t G_out = 0, G_dy2 = 0, G_da1 = 0, G_dx = 0, dskip[3] = {0, 0, 0};
+  size_t total = 0;
+  float* pe_dev = nullptr;
+  std::vector<float> pe_host;
+  // optional HIP-event timing of the MFMA kernels (bench.py roofline)
+  struct ProfRec { hipEvent_t a, b; int cls; double flops; };
+  std::vector<ProfRec> prof;
+  size_t prof_n = 0;
+  bool prof_on = false;
+  // per call
+  char* ws = nullptr;
+  const float* prm = nullptr;
+  float* dprm = nullptr;
+  hipStream_t st = nullptr;
+
+  float* F(size_t off) const { return reinterpret_cast<float*>(ws + off); }
+  const float* P(int64_t off) const { return off < 0 ? nullptr : prm + off; }
+  float* DP(int64_t off) const { return off < 0 ? nullptr : dprm + off; }
+  size_t alloc(size_t bytes) {
+    size_t o = total;
+    total += (bytes + 255) / 256 * 256;
+    return o;
+  }
+  int64_t reg(const std::string& name, std::vector<int64_t> shape) {
+    int64_t n = 1;
+    for (auto s : shape) n *= s;
+    params.push_back(PEnt{name, shape, nparam, n});
+    int64_t o = nparam;
+    nparam += n;
+    return o;
+  }
+};
+
+static spff_plan::ProfRec* prof_slot(spff_plan* p, int cls, double flops) {
+  if (p->prof_n == p->prof.size()) {
+    spff_plan::ProfRec r;
+    if (hipEventCreate(&r.a) != hipSuccess || hipEventCreate(&r.b) != hipSuccess) return nullptr;
+    p->prof.push_back(r);
+  }
+  spff_plan::ProfRec* r = &p->prof[p->prof_n++];
+  r->cls = cls;
+  r->flops = flops;
+  return r;
+}
+
+namespace {
+
+void reg_block(spff_plan* p, Blk& b) {
+  const std::string a = b.novel ? "pre" : "b1", bb = b.novel ? "body" : "b2";
+  const int KD = p->KD, C = b.C;
+  b.c1.w = p->reg(b.name + "." + a + ".0.weight", {C, b.Cin, KD, 3, 3});
+  b.g1 = p->reg(b.name + "." + a + ".1.weight", {C});
+  b.b1 = p->reg(b.name + "." + a + ".1.bias", {C});
+  b.c2.w = p->reg(b.name + "." + bb + ".0.weight", {C, C, KD, 3, 3});
+  b.g2 = p->reg(b.name + "." + bb + ".1.weight", {C});
+  b.b2 = p->reg(b.name + "." + bb + ".1.bias", {C});
+  if (b.efilm) {
+    b.fw0 = p->reg(b.name + ".efilm.mlp.0.weight", {32, 16, 1});
+    b.fb0 = p->reg(b.name + ".efilm.mlp.0.bias", {32});
+    b.fw2 = p->reg(b.name + ".efilm.mlp.2.weight", {2 * C, 32, 1});
+    b.fb2 = p->reg(b.name + ".efilm.mlp.2.bias", {2 * C});
+  }
+  if (b.fgate) {
+    b.mag = p->reg(b.name + ".fgate.mag_scale", {1});
+    b.mask = p->reg(b.name + ".fgate.freq_mask", {1, 1, p->vol[0].D / 2 + 1, 1, 1});
+  }
+}
+
+void conv_dims(ConvL& c, int Cin, int Cout) {
+  c.Cin = Cin;
+  c.Cout = Cout;
+  c.kpad_f = rup(Cin, 8);
+  c.npad_f = rup(Cout, conv3d_bn(Cout));
+  c.kpad_d = rup(Cout, 8);
+  c.npad_d = rup(Cin, conv3d_bn(Cin));
+}
+
+size_t conv_pack_bytes(const ConvL& c, int KD) {
+  size_t a = (size_t)KD * 9 * c.kpad_f * c.npad_f, b = (size_t)KD * 9 * c.kpad_d * c.npad_d;
+  return (a > b ? a : b) * sizeof(float);
+}
+
+void host_pe(int D, std::vector<float>& pe) {
+  // models.py:1495-1503 in fp32: denom = exp(i * (-ln(1e4)/8)), pe = [sin(pos*denom); cos(...)]
+  pe.assign(16 * (size_t)D, 0.f);
+  const float cst = (float)(-std::log(10000.0) / 8.0);
+  for (int i = 0; i < 8; ++i) {
+    const float denom = std::exp((float)i * cst);
+    for (int d = 0; d < D; ++d) {
+      const float arg = (float)d * denom;
+      pe[(size_t)i * D + d] = std::sin(arg);
+      pe[(size_t)(8 + i) * D + d] = std::cos(arg);
+    }
+  }
+}
+
+int build_plan(spff_plan* p) {
+  const spff_cfg& c = p->cfg;
+  if (c.batch < 1 || c.in_ch < 1 || c.depth < 1 || c.num_classes < 1 || c.num_classes > 32)
+    return fail(SPFF_EINVAL, "invalid batch/in_ch/depth/num_classes (K must be 1..32)");
+  if (c.base < 8 || (c.base & (c.base - 1)))
+    return fail(SPFF_EINVAL, "base must be a power of two >= 8");
+  if (c.ksd != 1 && c.ksd != 3) return fail(SPFF_EINVAL, "ksd must be 1 or 3");
+  if (c.height % 8 || c.width % 8 || c.height < 8 || c.width < 8)
+    return fail(SPFF_ESHAPE,
+                "H and W must be multiples of 8 (three (1,2,2) pools without the trilinear _cat "
+                "fallback of models.py:689-690)");
+  if (c.in_ch > 64) return fail(SPFF_EINVAL, "in_ch > 64 not supported");
+  p->f = c.base;
+  p->KD = c.ksd;
+  p->K = c.num_classes;
+  p->ldx = rup(c.in_ch, 8);
+  for (int l = 0; l < 4; ++l) p->vol[l] = Vol{c.batch, c.depth, c.height >> l, c.width >> l};
+  const int f = p->f;
+  const char* names[7] = {"enc1", "enc2", "enc3", "bott", "dec3", "dec2", "dec1"};
+  const int lvl[7] = {0, 1, 2, 3, 2, 1, 0};
+  const int cin[7] = {c.in_ch, f, 2 * f, 4 * f, 8 * f, 4 * f, 2 * f};
+  const int cc[7] = {f, 2 * f, 4 * f, 8 * f, 4 * f, 2 * f, f};
+  for (int i = 0; i < 7; ++i) {
+    Blk& b = p->blk[i];
+    b.name = names[i];
+    b.lvl = lvl[i];
+    b.Cin = cin[i];
+    b.C = cc[i];
+    b.efilm = c.use_efilm != 0;
+    b.fgate = c.use_fgate != 0;
+    b.novel = b.efilm || b.fgate;
+    b.post_se = i < 4 && c.use_se;
+    b.post_spec = i < 4 && c.use_specse;
+    conv_dims(b.c1, b.Cin, b.C);
+    conv_dims(b.c2, b.C, b.C);
+  }
+  // parameter registration in reference state-dict order (models.py:655-681)
+  reg_block(p, p->blk[0]);
+  reg_block(p, p->blk[1]);
+  reg_block(p, p->blk[2]);
+  reg_block(p, p->blk[3]);
+  const int upc[3][3] = {{8 * f, 4 * f, 2}, {4 * f, 2 * f, 1}, {2 * f, f, 0}};
+  const char* upn[3] = {"up3", "up2", "up1"};
+  for (int u = 0; u < 3; ++u) {
+    UpL& U = p->up[u];
+    U.Cin = upc[u][0];
+    U.Cout = upc[u][1];
+    U.lvl_low = upc[u][2] + 1;
+    U.w = p->reg(std::string(upn[u]) + ".weight", {U.Cin, U.Cout, 1, 2, 2});
+    U.b = p->reg(std::string(upn[u]) + ".bias", {U.Cout});
+    reg_block(p, p->blk[4 + u]);
+  }
+  p->out_w = p->reg("out.weight", {p->K, f, 1, 1, 1});
+  p->out_b = p->reg("out.bias", {p->K});
+  if (c.use_se) {
+    const int chs[4] = {f, 2 * f, 4 * f, 8 * f};
+    for (int i = 0; i < 4; ++i) {
+      const int C = chs[i], h = se_hidden(C);
+      const std::string pre = "se." + std::to_string(i) + ".fc.";
+      Blk& b = p->blk[i];
+      b.sw0 = p->reg(pre + "0.weight", {h, C, 1, 1, 1});
+      b.sb0 = p->reg(pre + "0.bias", {h});
+      b.sw2 = p->reg(pre + "2.weight", {C, h, 1, 1, 1});
+      b.sb2 = p->reg(pre + "2.bias", {C});
+    }
+  }
+
+  // ---- workspace layout ----
+  const int B = c.batch, D = c.depth;
+  const Vol& v0 = p->vol[0];
+  p->x_cl = p->alloc(nvox(v0) * p->ldx * sizeof(float));
+  size_t red_ws = 0, red_out = 0, gs = 0, bcd = 0, wg = 0, wt = 0;
+  for (int i = 0; i < 7; ++i) {
+    Blk& b = p->blk[i];
+    const Vol& v = p->vol[b.lvl];
+    const size_t act = nvox(v) * b.C * sizeof(float);
+    b.y1 = p->alloc(act);
+    b.a1 = p->alloc(act);
+    b.y2 = p->alloc(act);
+    b.out = p->alloc(act);
+    const size_t bc = (size_t)B * b.C * sizeof(float);
+    b.mean1 = p->alloc(bc); b.rstd1 = p->alloc(bc); b.al1 = p->alloc(bc); b.de1 = p->alloc(bc);
+    b.mean2 = p->alloc(bc); b.rstd2 = p->alloc(bc); b.al2 = p->alloc(bc); b.de2 = p->alloc(bc);
+    const size_t bcdz = (size_t)B * b.C * D * sizeof(float);
+    if (b.tail()) {
+      b.Sa = p->alloc(bcdz);
+      b.P = p->alloc(bcdz);
+      b.Q = p->alloc(bcdz);
+      b.s1 = p->alloc((size_t)B * D * 4);
+      b.g1s = p->alloc((size_t)B * D * 4);
+      b.sg2 = p->alloc((size_t)B * D * 4);
+      b.p = p->alloc(bc);
+      b.e = p->alloc(bc);
+      b.h = p->alloc((size_t)B * se_hidden(b.C) * 4);
+      b.t = p->alloc((size_t)b.C * D * 4);
+      b.bt = p->alloc((size_t)b.C * D * 4);
+      b.hid = p->alloc((size_t)32 * D * 4);
+    }
+    red_ws = std::max(red_ws, slab_reduce_ws_bytes(v, b.C, 2));
+    red_out = std::max(red_out, (size_t)B * b.C * D * 2 * sizeof(float));
+    gs = std::max(gs, gates_scratch_bytes(v, b.C));
+    bcd = std::max(bcd, bcdz);
+    wg = std::max(wg, conv3d_wgrad_ws_bytes(v, p->KD, b.Cin, b.C));
+    wg = std::max(wg, conv3d_wgrad_ws_bytes(v, p->KD, b.C, b.C));
+    wt = std::max(wt, conv_pack_bytes(b.c1, p->KD));
+    wt = std::max(wt, conv_pack_bytes(b.c2, p->KD));
+  }
+  for (int l = 0; l < 3; ++l) {
+    const Vol& vl = p->vol[l + 1];
+    const int C = f << l;  // channels of e_{l+1} pooled
+    p->pool[l] = p->alloc(nvox(vl) * C * sizeof(float));
+    p->pidx[l] = p->alloc(nvox(vl) * C);
+  }
+  for (int u = 0; u < 3; ++u) {
+    UpL& U = p->up[u];
+    const Vol& vh = p->vol[U.lvl_low - 1];
+    U.out = p->alloc(nvox(vh) * U.Cout * sizeof(float));
+    U.pk = p->alloc(upconv_pack_floats(U.Cin, U.Cout) * sizeof(float));
+    wg = std::max(wg, upconv_wgrad_ws_bytes(p->vol[U.lvl_low], U.Cin, U.Cout));
+  }
+  p->head_pk = p->alloc(head_pack_floats(f, p->K) * sizeof(float));
+  wg = std::max(wg, head_wgrad_ws_bytes(nvox(v0), f, p->K));
+  p->red_ws = p->alloc(red_ws);
+  p->red_out = p->alloc(red_out);
+  p->gscr = p->alloc(gs);
+  p->Abuf = p->alloc(bcd);
+  p->Bbuf = p->alloc(bcd);
+  p->kk1 = p->alloc((size_t)B * 8 * f * sizeof(float));
+  p->kk2 = p->alloc((size_t)B * 8 * f * sizeof(float));
+  p->wg_ws = p->alloc(wg);
+  p->wt = p->alloc(wt);
+  const size_t gbytes = nvox(v0) * f * sizeof(float);  // max over levels of V_l * C_l
+  p->G_out = p->alloc(gbytes);
+  p->G_dy2 = p->alloc(gbytes);
+  p->G_da1 = p->alloc(gbytes);
+  p->G_dx = p->alloc(gbytes);
+  for (int l = 0; l < 3; ++l) p->dskip[l] = p->alloc(nvox(p->vol[l]) * (f << l) * sizeof(float));
+
+  host_pe(D, p->pe_host);  // uploaded on the first forward (plan creation needs no GPU)
+  return SPFF_OK;
+}
+
+int ensure_pe(spff_plan* p) {
+  if (p->pe_dev) return SPFF_OK;
+  HIPCK(hipMalloc(&p->pe_dev, p->pe_host.size() * sizeof(float)));
+  HIPCK(hipMemcpy(p->pe_dev, p->pe_host.data(), p->pe_host.size() * sizeof(float),
+                  hipMemcpyHostToDevice));
+  return SPFF_OK;
+}
+
+GateParams gate_params(const spff_plan* p, const Blk& b) {
+  GateParams g;
+  g.pe = p->pe_dev;
+  g.fw0 = b.efilm ? p->P(b.fw0) : nullptr;
+  g.fb0 = b.efilm ? p->P(b.fb0) : nullptr;
+  g.fw2 = b.efilm ? p->P(b.fw2) : nullptr;
+  g.fb2 = b.efilm ? p->P(b.fb2) : nullptr;
+  g.mask = b.fgate ? p->P(b.mask) : nullptr;
+  g.mag = b.fgate ? p->P(b.mag) : nullptr;
+  g.sw0 = b.post_se ? p->P(b.sw0) : nullptr;
+  g.sb0 = b.post_se ? p->P(b.sb0) : nullptr;
+  g.sw2 = b.post_se ? p->P(b.sw2) : nullptr;
+  g.sb2 = b.post_se ? p->P(b.sb2) : nullptr;
+  g.specse = b.post_spec ? 1 : 0;
+  return g;
+}
+
+GateSaved gate_saved(const spff_plan* p, const Blk& b) {
+  GateSaved s;
+  s.t = p->F(b.t); s.bt = p->F(b.bt); s.hid = p->F(b.hid);
+  s.s1 = p->F(b.s1); s.g1 = p->F(b.g1s); s.sg2 = p->F(b.sg2);
+  s.p = p->F(b.p); s.h = p->F(b.h); s.e = p->F(b.e);
+  s.P = p->F(b.P); s.Q = p->F(b.Q);
+  return s;
+}
+
+int in_stats(spff_plan* p, const Vol& v, int C, size_t y, size_t mean, size_t rstd, size_t al,
+             size_t de, int64_t gamma, int64_t beta) {
+  RedArgs a{};
+  a.y = p->F(y);
+  HIPCK(slab_reduce(RED_SUM, a, v, C, p->F(p->red_out), p->F(p->red_ws), p->st));
+  HIPCK(in_mean(p->F(p->red_out), p->F(mean), v, C, p->st));
+  a.mean = p->F(mean);
+  HIPCK(slab_reduce(RED_SQDEV, a, v, C, p->F(p->red_out), p->F(p->red_ws), p->st));
+  HIPCK(in_rstd(p->F(p->red_out), p->P(gamma), p->P(beta), p->F(mean), p->F(rstd), p->F(al),
+                p->F(de), v, C, p->st));
+  return SPFF_OK;
+}
+
+int fwd_block(spff_plan* p, Blk& b, const Src2& in) {
+  const Vol& v = p->vol[b.lvl];
+  const int C = b.C, KD = p->KD;
+  HIPCK(conv_pack_weights(p->P(b.c1.w), p->F(p->wt), C, b.Cin, KD, b.c1.kpad_f, b.c1.npad_f,
+                          false, p->st));
+  const double V = (double)nvox(v), T = 9.0 * KD;
+  PROF(p, 0, 2.0 * V * b.Cin * C * T,
+       conv3d_fwd(in, p->F(p->wt), dst1(p->F(b.y1), C), v, KD, b.Cin, b.c1.kpad_f, C,
+                  b.c1.npad_f, p->st));
+  CK(in_stats(p, v, C, b.y1, b.mean1, b.rstd1, b.al1, b.de1, b.g1, b.b1));
+  HIPCK(act_apply(p->F(b.y1), p->F(b.a1), p->F(b.al1), p->F(b.de1), nullptr, nullptr, v, C,
+                  p->st));
+  HIPCK(conv_pack_weights(p->P(b.c2.w), p->F(p->wt), C, C, KD, b.c2.kpad_f, b.c2.npad_f, false,
+                          p->st));
+  PROF(p, 0, 2.0 * V * C * C * T,
+       conv3d_fwd(src1(p->F(b.a1), C), p->F(p->wt), dst1(p->F(b.y2), C), v, KD, C,
+                  b.c2.kpad_f, C, b.c2.npad_f, p->st));
+  CK(in_stats(p, v, C, b.y2, b.mean2, b.rstd2, b.al2, b.de2, b.g2, b.b2));
+  if (b.tail()) {
+    RedArgs a{};
+    a.y = p->F(b.y2);
+    a.al = p->F(b.al2);
+    a.de = p->F(b.de2);
+    HIPCK(slab_reduce(RED_ACT, a, v, C, p->F(b.Sa), p->F(p->red_ws), p->st));
+    GateParams gp = gate_params(p, b);
+    GateSaved sv = gate_saved(p, b);
+    HIPCK(gates_fwd(gp, p->F(b.Sa), sv, v, C, p->F(p->gscr), p->st));
+    HIPCK(act_apply(p->F(b.y2), p->F(b.out), p->F(b.al2), p->F(b.de2), p->F(b.P), p->F(b.Q), v,
+                    C, p->st));
+  } else {
+    HIPCK(act_apply(p->F(b.y2), p->F(b.out), p->F(b.al2), p->F(b.de2), nullptr, nullptr, v, C,
+                    p->st));
+  }
+  return SPFF_OK;
+}
+
+int bwd_block(spff_plan* p, Blk& b, const float* dout, const Dst2* dx, const Src2& in) {
+  const Vol& v = p->vol[b.lvl];
+  const int C = b.C, KD = p->KD;
+  const float* A = nullptr;
+  const float* Bc = nullptr;
+  if (b.tail()) {
+    RedArgs a{};
+    a.y = p->F(b.y2);
+    a.g = dout;
+    a.al = p->F(b.al2);
+    a.de = p->F(b.de2);
+    HIPCK(slab_reduce(RED_BWD_TAIL, a, v, C, p->F(p->red_out), p->F(p->red_ws), p->st));
+    GateParams gp = gate_params(p, b);
+    GateSaved sv = gate_saved(p, b);
+    GateGrads gg;
+    gg.fw0 = b.efilm ? p->DP(b.fw0) : nullptr;
+    gg.fb0 = b.efilm ? p->DP(b.fb0) : nullptr;
+    gg.fw2 = b.efilm ? p->DP(b.fw2) : nullptr;
+    gg.fb2 = b.efilm ? p->DP(b.fb2) : nullptr;
+    gg.mask = b.fgate ? p->DP(b.mask) : nullptr;
+    gg.mag = b.fgate ? p->DP(b.mag) : nullptr;
+    gg.sw0 = b.post_se ? p->DP(b.sw0) : nullptr;
+    gg.sb0 = b.post_se ? p->DP(b.sb0) : nullptr;
+    gg.sw2 = b.post_se ? p->DP(b.sw2) : nullptr;
+    gg.sb2 = b.post_se ? p->DP(b.sb2) : nullptr;
+    HIPCK(gates_bwd(gp, sv, p->F(b.Sa), p->F(p->red_out), gg, p->F(p->Abuf), p->F(p->Bbuf), v,
+                    C, p->F(p->gscr), p->st));
+    A = p->F(p->Abuf);
+    Bc = p->F(p->Bbuf);
+  }
+  float* dy2 = p->F(p->G_dy2);
+  float* da1 = p->F(p->G_da1);
+  {
+    RedArgs a{};
+    a.y = p->F(b.y2); a.g = dout; a.mean = p->F(b.mean2); a.rstd = p->F(b.rstd2);
+    a.al = p->F(b.al2); a.de = p->F(b.de2); a.A = A; a.Bc = Bc;
+    HIPCK(slab_reduce(RED_BWD_IN, a, v, C, p->F(p->red_out), p->F(p->red_ws), p->st));
+    HIPCK(in_bwd_stats(p->F(p->red_out), p->P(b.g2), p->DP(b.g2), p->DP(b.b2), p->F(p->kk1),
+                       p->F(p->kk2), v, C, p->st));
+    HIPCK(in_bwd_apply(p->F(b.y2), dout, dy2, p->F(b.mean2), p->F(b.rstd2), p->F(b.al2),
+                       p->F(b.de2), p->P(b.g2), A, Bc, p->F(p->kk1), p->F(p->kk2), v, C, p->st));
+  }
+  const double V = (double)nvox(v), T = 9.0 * KD;
+  PROF(p, 2, 2.0 * V * C * C * T,
+       conv3d_wgrad(src1(p->F(b.a1), C), dy2, C, p->DP(b.c2.w), v, KD, C, C, p->F(p->wg_ws),
+                    p->st));
+  HIPCK(conv_pack_weights(p->P(b.c2.w), p->F(p->wt), C, C, KD, b.c2.kpad_d, b.c2.npad_d, true,
+                          p->st));
+  PROF(p, 1, 2.0 * V * C * C * T,
+       conv3d_fwd(src1(dy2, C), p->F(p->wt), dst1(da1, C), v, KD, C, b.c2.kpad_d, C,
+                  b.c2.npad_d, p->st));
+  {
+    RedArgs a{};
+    a.y = p->F(b.y1); a.g = da1; a.mean = p->F(b.mean1); a.rstd = p->F(b.rstd1);
+    a.al = p->F(b.al1); a.de = p->F(b.de1);
+    HIPCK(slab_reduce(RED_BWD_IN, a, v, C, p->F(p->red_out), p->F(p->red_ws), p->st));
+    HIPCK(in_bwd_stats(p->F(p->red_out), p->P(b.g1), p->DP(b.g1), p->DP(b.b1), p->F(p->kk1),
+                       p->F(p->kk2), v, C, p->st));
+    HIPCK(in_bwd_apply(p->F(b.y1), da1, da1, p->F(b.mean1), p->F(b.rstd1), p->F(b.al1),
+                       p->F(b.de1), p->P(b.g1), nullptr, nullptr, p->F(p->kk1), p->F(p->kk2), v,
+                       C, p->st));
+  }
+  PROF(p, 2, 2.0 * V * b.Cin * C * T,
+       conv3d_wgrad(in, da1, C, p->DP(b.c1.w), v, KD, b.Cin, C, p->F(p->wg_ws), p->st));
+  if (dx) {
+    HIPCK(conv_pack_weights(p->P(b.c1.w), p->F(p->wt), C, b.Cin, KD, b.c1.kpad_d, b.c1.npad_d,
+                            true, p->st));
+    PROF(p, 1, 2.0 * V * b.Cin * C * T,
+         conv3d_fwd(src1(da1, C), p->F(p->wt), *dx, v, KD, C, b.c1.kpad_d, b.Cin, b.c1.npad_d,
+                    p->st));
+  }
+  return SPFF_OK;
+}
+
+Src2 src2(const float* a, const float* b, int C) { return Src2{a, b, C, C, C}; }
+
+int forward(spff_plan* p, const float* x, float* logits) {
+  const int f = p->f;
+  const spff_cfg& c = p->cfg;
+  HIPCK(ncdhw_to_ndhwc(x, p->F(p->x_cl), p->vol[0], c.in_ch, p->ldx, p->st));
+  Blk* B = p->blk;
+  CK(fwd_block(p, B[0], src1(p->F(p->x_cl), p->ldx)));
+  HIPCK(maxpool_fwd(p->F(B[0].out), p->F(p->pool[0]), reinterpret_cast<uint8_t*>(p->ws + p->pidx[0]),
+                    p->vol[0], f, p->st));
+  CK(fwd_block(p, B[1], src1(p->F(p->pool[0]), f)));
+  HIPCK(maxpool_fwd(p->F(B[1].out), p->F(p->pool[1]), reinterpret_cast<uint8_t*>(p->ws + p->pidx[1]),
+                    p->vol[1], 2 * f, p->st));
+  CK(fwd_block(p, B[2], src1(p->F(p->pool[1]), 2 * f)));
+  HIPCK(maxpool_fwd(p->F(B[2].out), p->F(p->pool[2]), reinterpret_cast<uint8_t*>(p->ws + p->pidx[2]),
+                    p->vol[2], 4 * f, p->st));
+  CK(fwd_block(p, B[3], src1(p->F(p->pool[2]), 4 * f)));
+  const float* prev = p->F(B[3].out);
+  for (int u = 0; u < 3; ++u) {
+    UpL& U = p->up[u];
+    float* pk = p->F(U.pk);
+    HIPCK(upconv_pack(p->P(U.w), pk, pk + upconv_pack_dgrad_offset(U.Cin, U.Cout), U.Cin, U.Cout,
+                      p->st));
+    PROF(p, 3, 2.0 * nvox(p->vol[U.lvl_low]) * U.Cin * 4.0 * U.Cout,
+         upconv_fwd(prev, pk, p->P(U.b), p->F(U.out), p->vol[U.lvl_low], U.Cin, U.Cout, p->st));
+    Blk& d = B[4 + u];
+    const Blk& skip = B[2 - u];
+    CK(fwd_block(p, d, src2(p->F(U.out), p->F(skip.out), U.Cout)));
+    prev = p->F(d.out);
+  }
+  float* hp = p->F(p->head_pk);
+  HIPCK(head_pack(p->P(p->out_w), hp, hp + head_pack_dgrad_offset(f, p->K), f, p->K, p->st));
+  PROF(p, 3, 2.0 * nvox(p->vol[0]) * f * p->K,
+       head_fwd(prev, hp, p->P(p->out_b), logits, nvox(p->vol[0]), f, p->K, p->st));
+  return SPFF_OK;
+}
+
+int backward(spff_plan* p, const float* dl) {
+  const int f = p->f;
+  Blk* B = p->blk;
+  const int64_t V0 = nvox(p->vol[0]);
+  float* hp = p->F(p->head_pk);
+  PROF(p, 3, 2.0 * V0 * f * p->K,
+       head_wgrad(p->F(B[6].out), dl, p->DP(p->out_w), p->DP(p->out_b), V0, f, p->K,
+                  p->F(p->wg_ws), p->st));
+  PROF(p, 3, 2.0 * V0 * f * p->K,
+       head_dgrad(dl, hp + head_pack_dgrad_offset(f, p->K), p->F(p->G_out), V0, f, p->K,
+                  p->st));
+  // decoder: dec1 (B[6]) <- up1 (up[2]) <- dec2 ... ; skip grads go to dskip[l]
+  for (int k = 0; k < 3; ++k) {
+    const int bi = 6 - k;          // dec1, dec2, dec3
+    const int ui = 2 - k;          // up1, up2, up3
+    Blk& d = B[bi];
+    UpL& U = p->up[ui];
+    const int C = d.C;             // = U.Cout = skip channels
+    const int lvl = d.lvl;
+    Dst2 dx{p->F(p->G_dx), p->F(p->dskip[lvl]), C, C, C};
+    CK(bwd_block(p, d, p->F(p->G_out), &dx, src2(p->F(U.out), p->F(B[lvl].out), C)));
+    const float* upin = (ui == 0) ? p->F(B[3].out) : p->F(B[bi - 1].out);
+    const Vol& low = p->vol[U.lvl_low];
+    PROF(p, 3, 2.0 * nvox(low) * U.Cin * 4.0 * U.Cout,
+         upconv_wgrad(upin, p->F(p->G_dx), C, p->DP(U.w), p->DP(U.b), low, U.Cin, U.Cout,
+                      p->F(p->wg_ws), p->st));
+    float* pk = p->F(U.pk);
+    PROF(p, 3, 2.0 * nvox(low) * U.Cin * 4.0 * U.Cout,
+         upconv_dgrad(p->F(p->G_dx), C, pk + upconv_pack_dgrad_offset(U.Cin, U.Cout),
+                      p->F(p->G_out), low, U.Cin, U.Cout, p->st));
+  }
+  // bottleneck + encoder
+  {
+    Dst2 dx = dst1(p->F(p->G_dx), 4 * f);
+    CK(bwd_block(p, B[3], p->F(p->G_out), &dx, src1(p->F(p->pool[2]), 4 * f)));
+  }
+  for (int l = 2; l >= 0; --l) {
+    const int C = f << l;
+    HIPCK(maxpool_bwd_add(p->F(p->G_dx), reinterpret_cast<const uint8_t*>(p->ws + p->pidx[l]),
+                          p->F(p->dskip[l]), C, p->F(p->dskip[l]), p->vol[l], C, p->st));
+    if (l > 0) {
+      Dst2 dx = dst1(p->F(p->G_dx), C / 2);
+      CK(bwd_block(p, B[l], p->F(p->dskip[l]), &dx, src1(p->F(p->pool[l - 1]), C / 2)));
+    } else {
+      CK(bwd_block(p, B[0], p->F(p->dskip[0]), nullptr, src1(p->F(p->x_cl), p->ldx)));
+    }
+  }
+  return SPFF_OK;
+}
+
+}  // namespace
+
+// =================================================================== C ABI ==
+extern "C" {
+
+const char* spff_last_error(void) { return g_err.c_str(); }
+
+int spff_plan_create(const spff_cfg* cfg, spff_plan** out) {
+  if (!cfg || !out) return fail(SPFF_EINVAL, "null argument");
+  spff_plan* p = new spff_plan();
+  p->cfg = *cfg;
+  int r = build_plan(p);
+  if (r != SPFF_OK) {
+    if (p->pe_dev) (void)hipFree(p->pe_dev);
+    delete p;
+    return r;
+  }
+  *out = p;
+  return SPFF_OK;
+}
+
+void spff_plan_destroy(spff_plan* p) {
+  if (!p) return;
+  for (auto& r : p->prof) {
+    (void)hipEventDestroy(r.a);
+    (void)hipEventDestroy(r.b);
+  }
+  if (p->pe_dev) (void)hipFree(p->pe_dev);
+  delete p;
+}
+
+int spff_num_params(const spff_plan* p) { return p ? (int)p->params.size() : 0; }
+
+int spff_param_info(const spff_plan* p, int i, const char** name, int* ndim, int64_t shape[5],
+                    int64_t* offset, int64_t* numel) {
+  if (!p || i < 0 || i >= (int)p->params.size()) return fail(SPFF_EINVAL, "param index");
+  const PEnt& e = p->params[i];
+  if (name) *name = e.name.c_str();
+  if (ndim) *ndim = (int)e.shape.size();
+  if (shape)
+    for (int k = 0; k < 5; ++k) shape[k] = k < (int)e.shape.size() ? e.shape[k] : 1;
+  if (offset) *offset = e.off;
+  if (numel) *numel = e.numel;
+  return SPFF_OK;
+}
+
+int64_t spff_param_floats(const spff_plan* p) { return p ? p->nparam : 0; }
+size_t spff_workspace_bytes(const spff_plan* p) { return p ? p->total : 0; }
+
+int spff_forward(spff_plan* p, const float* x, const float* params, float* logits, void* ws,
+                 void* stream) {
+  if (!p || !x || !params || !logits || !ws) return fail(SPFF_EINVAL, "null argument");
+  p->ws = static_cast<char*>(ws);
+  p->prm = params;
+  p->dprm = nullptr;
+  p->st = static_cast<hipStream_t>(stream);
+  CK(ensure_pe(p));
+  return forward(p, x, logits);
+}
+
+int spff_backward(spff_plan* p, const float* dlogits, const float* params, float* dparams,
+                  void* ws, void* stream) {
+  if (!p || !dlogits || !params || !dparams || !ws) return fail(SPFF_EINVAL, "null argument");
+  p->ws = static_cast<char*>(ws);
+  p->prm = params;
+  p->dprm = dparams;
+  p->st = static_cast<hipStream_t>(stream);
+  return backward(p, dlogits);
+}
+
+int spff_saved_tensor(const spff_plan* p, void* ws, const char* name, const float** ptr,
+                      int64_t* nv, int* ch) {
+  if (!p || !ws || !name || !ptr) return fail(SPFF_EINVAL, "null argument");
+  const char* base = static_cast<const char*>(ws);
+  const std::string n(name);
+  auto ret = [&](size_t off, const Vol& v, int c) {
+    *ptr = reinterpret_cast<const float*>(base + off);
+    if (nv) *nv = nvox(v);
+    if (ch) *ch = c;
+    return SPFF_OK;
+  };
+  if (n == "x_cl") return ret(p->x_cl, p->vol[0], p->ldx);
+  for (int i = 0; i < 7; ++i) {
+    const Blk& b = p->blk[i];
+    const Vol& v = p->vol[b.lvl];
+    if (n == b.name + ".y1") return ret(b.y1, v, b.C);
+    if (n == b.name + ".a1") return ret(b.a1, v, b.C);
+    if (n == b.name + ".y2") return ret(b.y2, v, b.C);
+    if (n == b.name + ".out") return ret(b.out, v, b.C);
+  }
+  for (int l = 0; l < 3; ++l)
+    if (n == "pool" + std::to_string(l + 1)) return ret(p->pool[l], p->vol[l + 1], p->f << l);
+  const char* upn[3] = {"up3", "up2", "up1"};
+  for (int u = 0; u < 3; ++u)
+    if (n == upn[u]) return ret(p->up[u].out, p->vol[p->up[u].lvl_low - 1], p->up[u].Cout);
+  return fail(SPFF_EINVAL, "unknown saved tensor " + n);
+}
+
+int spff_prof_enable(spff_plan* p, int on) {
+  if (!p) return fail(SPFF_EINVAL, "null plan");
+  p->prof_on = on != 0;
+  p->prof_n = 0;
+  return SPFF_OK;
+}
+
+int spff_prof_collect(spff_plan* p, double* out, int nclass) {
+  if (!p || !out) return fail(SPFF_EINVAL, "null argument");
+  for (int i = 0; i < 3 * nclass; ++i) out[i] = 0.0;
+  for (size_t i = 0; i < p->prof_n; ++i) {
+    spff_plan::ProfRec& r = p->prof[i];
+    HIPCK(hipEventSynchronize(r.b));
+    float ms = 0.f;
+    HIPCK(hipEventElapsedTime(&ms, r.a, r.b));
+    if (r.cls < nclass) {
+      out[3 * r.cls + 0] += ms;
+      out[3 * r.cls + 1] += r.flops;
+      out[3 * r.cls + 2] += 1.0;
+    }
+  }
+  p->prof_n = 0;
+  return SPFF_OK;
+}
+
+size_t spff_loss_ws_bytes(int64_t nv, int K) { return loss_ws_bytes(nv, K); }
+
+int spff_loss(const float* logits, const int64_t* labels, int64_t nv, int K, int ignore,
+              double smooth, const int64_t* count_override, float* out4, float* dlogits,
+              int64_t* conf, void* ws, void* stream) {
+  if (!logits || !labels || !out4 || !dlogits || !conf || !ws)
+    return fail(SPFF_EINVAL, "null argument");
+  if (K < 1 || K > 32) return fail(SPFF_EINVAL, "num_classes must be 1..32");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  HIPCK(loss_fwd(logits, labels, nv, K, ignore, smooth, count_override, out4, dlogits, conf,
+                 static_cast<float*>(ws), s));
+  return SPFF_OK;
+}
+
+int spff_confusion(const float* logits, const int64_t* labels, int64_t nv, int K, int ignore,
+                   int64_t* conf, void* stream) {
+  if (!logits || !labels || !conf) return fail(SPFF_EINVAL, "null argument");
+  if (K < 1 || K > 32) return fail(SPFF_EINVAL, "num_classes must be 1..32");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  HIPCK(confusion_only(logits, labels, nv, K, ignore, conf, s));
+  return SPFF_OK;
+}
+
+int spff_count_valid(const int64_t* labels, int64_t nv, int ignore, int64_t* count, void* stream) {
+  if (!labels || !count) return fail(SPFF_EINVAL, "null argument");
+  HIPCK(count_valid(labels, nv, ignore, count, static_cast<hipStream_t>(stream)));
+  return SPFF_OK;
+}
+
+int spff_scale(float* x, int64_t n, const float* scale, void* stream) {
+  if (!x || !scale) return fail(SPFF_EINVAL, "null argument");
+  HIPCK(scale_by_dev(x, n, scale, static_cast<hipStream_t>(stream)));
+  return SPFF_OK;
+}
+
+// ---- op-level conv entry points ----
+static size_t conv_op_pack_floats(int cin, int cout, int ksd) {
+  ConvL c;
+  conv_dims(c, cin, cout);
+  return conv_pack_bytes(c, ksd) / sizeof(float);
+}
+
+size_t spff_conv3d_ws_bytes(int B, int D, int H, int W, int cin, int cout, int ksd) {
+  Vol v{B, D, H, W};
+  return conv_op_pack_floats(cin, cout, ksd) * sizeof(float) + 256 +
+         conv3d_wgrad_ws_bytes(v, ksd, cin, cout);
+}
+
+int spff_conv3d_fwd(const float* x, int ldx, const float* w, float* y, int B, int D, int H, int W,
+                    int cin, int cout, int ksd, void* ws, void* stream) {
+  if (!x || !w || !y || !ws) return fail(SPFF_EINVAL, "null argument");
+  if (ldx % 4 || ldx < cin) return fail(SPFF_EINVAL, "ldx must be >= cin and a multiple of 4");
+  if (cout % 4) return fail(SPFF_EINVAL, "cout must be a multiple of 4");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  ConvL c;
+  conv_dims(c, cin, cout);
+  float* wt = static_cast<float*>(ws);
+  HIPCK(conv_pack_weights(w, wt, cout, cin, ksd, c.kpad_f, c.npad_f, false, s));
+  HIPCK(conv3d_fwd(src1(x, ldx), wt, dst1(y, cout), Vol{B, D, H, W}, ksd, cin, c.kpad_f, cout,
+                   c.npad_f, s));
+  return SPFF_OK;
+}
+
+int spff_conv3d_dgrad(const float* dy, const float* w, float* dx, int B, int D, int H, int W,
+                      int cin, int cout, int ksd, void* ws, void* stream) {
+  if (!dy || !w || !dx || !ws) return fail(SPFF_EINVAL, "null argument");
+  if (cout % 4 || cin % 4) return fail(SPFF_EINVAL, "channels must be multiples of 4");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  ConvL c;
+  conv_dims(c, cin, cout);
+  float* wt = static_cast<float*>(ws);
+  HIPCK(conv_pack_weights(w, wt, cout, cin, ksd, c.kpad_d, c.npad_d, true, s));
+  HIPCK(conv3d_fwd(src1(dy, cout), wt, dst1(dx, cin), Vol{B, D, H, W}, ksd, cout, c.kpad_d, cin,
+                   c.npad_d, s));
+  return SPFF_OK;
+}
+
+int spff_conv3d_wgrad(const float* x, int ldx, const float* dy, float* dw, int B, int D, int H,
+                      int W, int cin, int cout, int ksd, void* ws, void* stream) {
+  if (!x || !dy || !dw || !ws) return fail(SPFF_EINVAL, "null argument");
+  if (ldx % 4 || ldx < cin || cout % 4) return fail(SPFF_EINVAL, "bad channel strides");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  float* part = static_cast<float*>(ws) + conv_op_pack_floats(cin, cout, ksd) + 64;
+  HIPCK(conv3d_wgrad(src1(x, ldx), dy, cout, dw, Vol{B, D, H, W}, ksd, cin, cout, part, s));
+  return SPFF_OK;
+}
+
+}  // extern "C"

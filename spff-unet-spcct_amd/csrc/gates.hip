@@ -1,0 +1,466 @@
+// Gate algebra of the SPFF block tail at (b, c, d) granularity.
+//
+// Reference ops (models.py): EnergyFiLM3D 1479-1512, FourierGate3D 1515-1544,
+// _SpectralSE 611-614, _SEChannelLite 600-609.  Every one of them is a per-(c,d)
+// affine, a per-d scalar or a per-c scalar applied to the same tensor, so with
+//   a2 = lrelu(IN(y2)),  z = a2*(1+t[c,d]) + bt[c,d],
+//   Sa[b,c,d] = sum_hw a2   ->   Z[b,c,d] = sum_hw z = (1+t)*Sa + bt*HW
+// all means the gates need are (b,c,d)-level algebra on Z (DESIGN.md derives
+// it), and the block output is  out = a2 * P[b,c,d] + Q[b,c,d].
+// The FourierGate's rfft -> real mask -> irfft(n=D) is a real circulant
+// operator w = A s1 with A[d,d'] = (1/D) sum_k c_k M_k cos(2 pi k (d-d') / D)
+// (c_0 = 1, c_{D/2} = 1 for even D, else 2); it is evaluated as an explicit
+// double-precision DFT (D <= 512, negligible work).
+#include "spff_internal.h"
+#include <math.h>
+
+namespace spff {
+
+static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); }
+__device__ __forceinline__ double ck_coef(int k, int D) {
+  return (k == 0 || (D % 2 == 0 && k == D / 2)) ? 1.0 : 2.0;
+}
+__device__ __forceinline__ void cis(int k, int d, int D, double& c, double& s) {
+  const int m = (int)(((int64_t)k * d) % D);
+  const double ang = 6.283185307179586476925286766559 * (double)m / (double)D;
+  sincos(ang, &s, &c);
+}
+
+int se_hidden(int C) { return C / 16 > 4 ? C / 16 : 4; }
+
+// ------------------------------------------------------------- EFiLM fwd --
+// hid[j][d] = fw0[j] . pe[:,d] + fb0[j]; gb[o][d] = fw2[o] . relu(hid[:,d]) + fb2[o]
+__global__ void k_efilm_fwd(const float* __restrict__ pe, const float* __restrict__ fw0,
+                            const float* __restrict__ fb0, const float* __restrict__ fw2,
+                            const float* __restrict__ fb2, float* __restrict__ t,
+                            float* __restrict__ bt, float* __restrict__ hid, int C, int D) {
+  extern __shared__ float hs[];  // [32][D]
+  for (int i = threadIdx.x; i < 32 * D; i += blockDim.x) {
+    const int j = i / D, d = i % D;
+    float s = 0.f;
+    for (int q = 0; q < 16; ++q) s += fw0[j * 16 + q] * pe[q * D + d];
+    s += fb0[j];
+    hs[i] = s;
+    if (blockIdx.x == 0) hid[i] = s;
+  }
+  __syncthreads();
+  const int o0 = blockIdx.x * 32;
+  for (int i = threadIdx.x; i < 32 * D; i += blockDim.x) {
+    const int o = o0 + i / D, d = i % D;
+    if (o >= 2 * C) continue;
+    float s = 0.f;
+    for (int j = 0; j < 32; ++j) s += fw2[o * 32 + j] * fmaxf(hs[j * D + d], 0.f);
+    s += fb2[o];
+    if (o < C) t[o * D + d] = tanhf(s);
+    else bt[(o - C) * D + d] = s;
+  }
+}
+
+// ------------------------------------------------------------- gates fwd --
+__global__ void k_gates_fwd(GateParams gp, const float* __restrict__ Sa, GateSaved sv, Vol vol,
+                            int C, int Hse, int efilm) {
+  const int b = blockIdx.x;
+  const int D = vol.D, HW = vol.H * vol.W, L = D / 2 + 1;
+  extern __shared__ double shd[];
+  double* Sre = shd;                        // [L]
+  double* Sim = Sre + L;                    // [L]
+  float* s1 = reinterpret_cast<float*>(Sim + L);  // [D]
+  float* g1 = s1 + D;                       // [D]
+  float* sg2 = g1 + D;                      // [D]
+  float* p = sg2 + D;                       // [C]
+  float* h = p + C;                         // [Hse]
+  float* e = h + Hse;                       // [C]
+  const float* Sab = Sa + (int64_t)b * C * D;
+  auto Z = [&](int c, int d) -> float {
+    const float sa = Sab[c * D + d];
+    return efilm ? (1.f + sv.t[c * D + d]) * sa + sv.bt[c * D + d] * (float)HW : sa;
+  };
+  // s1[d] = mean_{c,hw} z
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    double s = 0.0;
+    for (int c = 0; c < C; ++c) s += (double)Z(c, d);
+    s1[d] = (float)(s / ((double)C * HW));
+  }
+  __syncthreads();
+  if (gp.mask) {
+    for (int k = threadIdx.x; k < L; k += blockDim.x) {
+      double re = 0.0, im = 0.0;
+      for (int d = 0; d < D; ++d) {
+        double c, s;
+        cis(k, d, D, c, s);
+        re += (double)s1[d] * c;
+        im -= (double)s1[d] * s;
+      }
+      Sre[k] = re;
+      Sim[k] = im;
+    }
+    __syncthreads();
+    const double mag = (double)gp.mag[0];
+    for (int d = threadIdx.x; d < D; d += blockDim.x) {
+      double w = 0.0;
+      for (int k = 0; k < L; ++k) {
+        double c, s;
+        cis(k, d, D, c, s);
+        const double Mk = (double)(gp.mask[k] * gp.mag[0]);
+        (void)mag;
+        w += ck_coef(k, D) * Mk * (Sre[k] * c - Sim[k] * s);
+      }
+      g1[d] = sigm((float)(w / D));
+    }
+  } else {
+    for (int d = threadIdx.x; d < D; d += blockDim.x) g1[d] = 1.f;
+  }
+  __syncthreads();
+  for (int d = threadIdx.x; d < D; d += blockDim.x) sg2[d] = gp.specse ? sigm(g1[d] * s1[d]) : 1.f;
+  __syncthreads();
+  if (gp.sw0) {
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+      double s = 0.0;
+      for (int d = 0; d < D; ++d) s += (double)(g1[d] * sg2[d]) * (double)Z(c, d);
+      p[c] = (float)(s / ((double)D * HW));
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < Hse; j += blockDim.x) {
+      float s = 0.f;
+      for (int c = 0; c < C; ++c) s += gp.sw0[j * C + c] * p[c];
+      h[j] = s + gp.sb0[j];
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+      float s = 0.f;
+      for (int j = 0; j < Hse; ++j) s += gp.sw2[c * Hse + j] * fmaxf(h[j], 0.f);
+      e[c] = sigm(s + gp.sb2[c]);
+    }
+  } else {
+    for (int c = threadIdx.x; c < C; c += blockDim.x) e[c] = 1.f;
+  }
+  __syncthreads();
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    sv.s1[b * D + d] = s1[d];
+    sv.g1[b * D + d] = g1[d];
+    sv.sg2[b * D + d] = sg2[d];
+  }
+  if (gp.sw0) {
+    for (int c = threadIdx.x; c < C; c += blockDim.x) { sv.p[b * C + c] = p[c]; sv.e[b * C + c] = e[c]; }
+    for (int j = threadIdx.x; j < Hse; j += blockDim.x) sv.h[b * Hse + j] = h[j];
+  }
+  for (int i = threadIdx.x; i < C * D; i += blockDim.x) {
+    const int c = i / D, d = i % D;
+    const float G = g1[d] * sg2[d] * e[c];
+    const float onept = efilm ? (1.f + sv.t[i]) : 1.f;
+    const float btv = efilm ? sv.bt[i] : 0.f;
+    sv.P[(int64_t)b * C * D + i] = onept * G;
+    sv.Q[(int64_t)b * C * D + i] = btv * G;
+  }
+}
+
+static size_t gates_fwd_shmem(int C, int D, int Hse) {
+  const int L = D / 2 + 1;
+  return 2 * L * sizeof(double) + (3 * D + 2 * C + Hse) * sizeof(float);
+}
+
+hipError_t gates_fwd(const GateParams& gp, const float* Sa, GateSaved& sv, Vol vol, int C,
+                     float* scratch, hipStream_t s) {
+  (void)scratch;
+  const int D = vol.D, Hse = se_hidden(C);
+  const int efilm = gp.fw0 != nullptr;
+  if (efilm) {
+    hipLaunchKernelGGL(k_efilm_fwd, dim3(cdiv(2 * C, 32)), dim3(256), 32 * D * sizeof(float), s,
+                       gp.pe, gp.fw0, gp.fb0, gp.fw2, gp.fb2, sv.t, sv.bt, sv.hid, C, D);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(k_gates_fwd, dim3(vol.B), dim3(256), gates_fwd_shmem(C, D, Hse), s, gp, Sa,
+                     sv, vol, C, Hse, efilm);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------- gates bwd --
+// scratch layout (floats): dt[B][C][D], dbt[B][C][D], sw2p[B][C][Hse], sb2p[B][C],
+// sw0p[B][Hse][C], sb0p[B][Hse], dMr[B][L], dgb[2C][D], dh[32][D]
+struct GScr {
+  float *dt, *dbt, *sw2p, *sb2p, *sw0p, *sb0p, *dMr, *dgb, *dh;
+};
+static GScr gscr(float* base, int B, int C, int D, int Hse) {
+  const int L = D / 2 + 1;
+  GScr g;
+  g.dt = base;
+  g.dbt = g.dt + (size_t)B * C * D;
+  g.sw2p = g.dbt + (size_t)B * C * D;
+  g.sb2p = g.sw2p + (size_t)B * C * Hse;
+  g.sw0p = g.sb2p + (size_t)B * C;
+  g.sb0p = g.sw0p + (size_t)B * Hse * C;
+  g.dMr = g.sb0p + (size_t)B * Hse;
+  g.dgb = g.dMr + (size_t)B * L;
+  g.dh = g.dgb + (size_t)2 * C * D;
+  return g;
+}
+size_t gates_scratch_bytes(Vol vol, int C) {
+  const int B = vol.B, D = vol.D, Hse = se_hidden(C), L = D / 2 + 1;
+  size_t n = 2 * (size_t)B * C * D + (size_t)B * C * Hse + (size_t)B * C + (size_t)B * Hse * C +
+             (size_t)B * Hse + (size_t)B * L + 2 * (size_t)C * D + 32 * (size_t)D;
+  return n * sizeof(float) + 256;
+}
+
+__global__ void k_gates_bwd(GateParams gp, GateSaved sv, const float* __restrict__ Sa,
+                            const float* __restrict__ Sg, GScr gs, float* __restrict__ Aout,
+                            float* __restrict__ Bout, Vol vol, int C, int Hse, int efilm) {
+  const int b = blockIdx.x;
+  const int D = vol.D, HW = vol.H * vol.W, L = D / 2 + 1;
+  extern __shared__ double shd[];
+  double* Sre = shd;
+  double* Sim = Sre + L;
+  double* Tre = Sim + L;
+  double* Tim = Tre + L;
+  float* fb = reinterpret_cast<float*>(Tim + L);
+  float* e = fb;            // [C]
+  float* c0 = e + C;        // [C]
+  float* dq = c0 + C;       // [C]
+  float* dh = dq + C;       // [Hse]
+  float* g1 = dh + Hse;     // [D]
+  float* sg2 = g1 + D;      // [D]
+  float* ds2 = sg2 + D;     // [D]
+  float* dw = ds2 + D;      // [D]
+  float* ds1 = dw + D;      // [D]
+  const int64_t bo = (int64_t)b * C * D;
+  auto Zf = [&](int c, int d) -> float {
+    const float sa = Sa[bo + c * D + d];
+    return efilm ? (1.f + sv.t[c * D + d]) * sa + sv.bt[c * D + d] * (float)HW : sa;
+  };
+  auto R1 = [&](int c, int d) -> float {  // sum_hw dout * z
+    const float sgd = Sg[(bo + c * D + d) * 2 + 0], sda = Sg[(bo + c * D + d) * 2 + 1];
+    return efilm ? (1.f + sv.t[c * D + d]) * sda + sv.bt[c * D + d] * sgd : sda;
+  };
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    g1[d] = sv.g1[b * D + d];
+    sg2[d] = sv.sg2[b * D + d];
+  }
+  __syncthreads();
+  // ---- channel SE ----
+  if (gp.sw0) {
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+      double de = 0.0;
+      for (int d = 0; d < D; ++d) de += (double)(g1[d] * sg2[d]) * (double)R1(c, d);
+      const float ev = sv.e[b * C + c];
+      e[c] = ev;
+      dq[c] = (float)de * ev * (1.f - ev);
+      gs.sb2p[b * C + c] = dq[c];
+      for (int j = 0; j < Hse; ++j)
+        gs.sw2p[((int64_t)b * C + c) * Hse + j] = dq[c] * fmaxf(sv.h[b * Hse + j], 0.f);
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < Hse; j += blockDim.x) {
+      float s = 0.f;
+      for (int c = 0; c < C; ++c) s += gp.sw2[c * Hse + j] * dq[c];
+      const float dhv = sv.h[b * Hse + j] > 0.f ? s : 0.f;
+      dh[j] = dhv;
+      gs.sb0p[b * Hse + j] = dhv;
+      for (int c = 0; c < C; ++c) gs.sw0p[((int64_t)b * Hse + j) * C + c] = dhv * sv.p[b * C + c];
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+      float s = 0.f;
+      for (int j = 0; j < Hse; ++j) s += gp.sw0[j * C + c] * dh[j];
+      c0[c] = s / ((float)D * (float)HW);
+    }
+  } else {
+    for (int c = threadIdx.x; c < C; c += blockDim.x) { e[c] = 1.f; c0[c] = 0.f; }
+  }
+  __syncthreads();
+  // ---- spectral SE: v = u * sg2[d] ----
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    if (gp.specse) {
+      double acc = 0.0;
+      for (int c = 0; c < C; ++c) acc += (double)e[c] * R1(c, d) + (double)c0[c] * Zf(c, d);
+      ds2[d] = sg2[d] * (1.f - sg2[d]) * g1[d] * (float)acc;
+    } else {
+      ds2[d] = 0.f;
+    }
+  }
+  __syncthreads();
+  const float invCHW = 1.f / ((float)C * (float)HW);
+  // du = dout*a + bb, a = e[c]*sg2[d], bb = c0[c]*sg2[d] + ds2[d]/(C*HW)
+  // ---- FourierGate: u = z * g1[d] ----
+  if (gp.mask) {
+    for (int d = threadIdx.x; d < D; d += blockDim.x) {
+      double acc = 0.0;
+      for (int c = 0; c < C; ++c) {
+        const float a = e[c] * sg2[d];
+        const float bb = c0[c] * sg2[d] + ds2[d] * invCHW;
+        acc += (double)a * R1(c, d) + (double)bb * Zf(c, d);
+      }
+      dw[d] = (float)acc * g1[d] * (1.f - g1[d]);
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < L; k += blockDim.x) {
+      double sre = 0.0, sim = 0.0, tre = 0.0, tim = 0.0;
+      for (int d = 0; d < D; ++d) {
+        double cc, ss;
+        cis(k, d, D, cc, ss);
+        const double s1 = (double)sv.s1[b * D + d];
+        sre += s1 * cc;
+        sim -= s1 * ss;
+        tre += (double)dw[d] * cc;
+        tim += (double)dw[d] * ss;
+      }
+      Sre[k] = sre; Sim[k] = sim; Tre[k] = tre; Tim[k] = tim;
+      gs.dMr[b * L + k] = (float)(ck_coef(k, D) / D * (sre * tre - sim * tim));
+    }
+    __syncthreads();
+    for (int d = threadIdx.x; d < D; d += blockDim.x) {
+      double acc = 0.0;
+      for (int k = 0; k < L; ++k) {
+        double cc, ss;
+        cis(k, d, D, cc, ss);
+        const double Mk = (double)(gp.mask[k] * gp.mag[0]);
+        acc += ck_coef(k, D) * Mk * (cc * Tre[k] + ss * Tim[k]);
+      }
+      ds1[d] = (float)(acc / D);
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < C * D; i += blockDim.x) {
+    const int c = i / D, d = i % D;
+    float al = e[c] * sg2[d];
+    float be = c0[c] * sg2[d] + ds2[d] * invCHW;
+    if (gp.mask) {
+      al = al * g1[d];
+      be = be * g1[d] + ds1[d] * invCHW;
+    }
+    if (efilm) {
+      const float sgd = Sg[(bo + i) * 2 + 0], sda = Sg[(bo + i) * 2 + 1];
+      gs.dt[bo + i] = al * sda + be * Sa[bo + i];
+      gs.dbt[bo + i] = al * sgd + be * (float)HW;
+      const float onept = 1.f + sv.t[i];
+      al *= onept;
+      be *= onept;
+    }
+    Aout[bo + i] = al;
+    Bout[bo + i] = be;
+  }
+}
+
+// sums over b of the per-b partials -> SE and FourierGate grads
+__global__ void k_gates_bwd_final(GateParams gp, GateGrads gg, GScr gs, int B, int C, int D,
+                                  int Hse) {
+  const int L = D / 2 + 1;
+  const int n1 = C * Hse, n2 = C, n3 = Hse * C, n4 = Hse, n5 = L;
+  const int tot = (gp.sw0 ? n1 + n2 + n3 + n4 : 0) + (gp.mask ? n5 + 1 : 0);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += gridDim.x * blockDim.x) {
+    int k = i;
+    if (gp.sw0) {
+      if (k < n1) { float s = 0.f; for (int b = 0; b < B; ++b) s += gs.sw2p[(int64_t)b * n1 + k]; gg.sw2[k] = s; continue; }
+      k -= n1;
+      if (k < n2) { float s = 0.f; for (int b = 0; b < B; ++b) s += gs.sb2p[(int64_t)b * n2 + k]; gg.sb2[k] = s; continue; }
+      k -= n2;
+      if (k < n3) { float s = 0.f; for (int b = 0; b < B; ++b) s += gs.sw0p[(int64_t)b * n3 + k]; gg.sw0[k] = s; continue; }
+      k -= n3;
+      if (k < n4) { float s = 0.f; for (int b = 0; b < B; ++b) s += gs.sb0p[(int64_t)b * n4 + k]; gg.sb0[k] = s; continue; }
+      k -= n4;
+    }
+    // FourierGate: M = mask * mag
+    if (k < n5) {
+      float s = 0.f;
+      for (int b = 0; b < B; ++b) s += gs.dMr[b * L + k];
+      gg.mask[k] = s * gp.mag[0];
+    } else {
+      float tot2 = 0.f;
+      for (int kk = 0; kk < L; ++kk) {
+        float s = 0.f;
+        for (int b = 0; b < B; ++b) s += gs.dMr[b * L + kk];
+        tot2 += s * gp.mask[kk];
+      }
+      gg.mag[0] = tot2;
+    }
+  }
+}
+
+// EFiLM MLP backward: dgb[o][d] (o<C: dt*(1-t^2), o>=C: dbt), then
+// dfw2 = dgb . relu(hid)^T, dfb2 = sum_d dgb, dh = (fw2^T dgb) * (hid>0),
+// dfw0 = dh . pe^T, dfb0 = sum_d dh.
+__global__ void k_efilm_bwd1(GScr gs, const float* __restrict__ t, int B, int C, int D) {
+  const int n = 2 * C * D;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int o = i / D, d = i % D;
+    float s = 0.f;
+    if (o < C) {
+      for (int b = 0; b < B; ++b) s += gs.dt[(int64_t)b * C * D + o * D + d];
+      const float tv = t[o * D + d];
+      s *= (1.f - tv * tv);
+    } else {
+      for (int b = 0; b < B; ++b) s += gs.dbt[(int64_t)b * C * D + (o - C) * D + d];
+    }
+    gs.dgb[i] = s;
+  }
+}
+__global__ void k_efilm_bwd2(GateParams gp, GateGrads gg, GScr gs, const float* __restrict__ hid,
+                             int C, int D) {
+  const int n = 2 * C * 33 + 32 * D;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    if (i < 2 * C * 33) {
+      const int o = i / 33, j = i % 33;
+      float s = 0.f;
+      if (j < 32) {
+        for (int d = 0; d < D; ++d) s += gs.dgb[o * D + d] * fmaxf(hid[j * D + d], 0.f);
+        gg.fw2[o * 32 + j] = s;
+      } else {
+        for (int d = 0; d < D; ++d) s += gs.dgb[o * D + d];
+        gg.fb2[o] = s;
+      }
+    } else {
+      const int k = i - 2 * C * 33;
+      const int j = k / D, d = k % D;
+      float s = 0.f;
+      for (int o = 0; o < 2 * C; ++o) s += gp.fw2[o * 32 + j] * gs.dgb[o * D + d];
+      gs.dh[k] = hid[k] > 0.f ? s : 0.f;
+    }
+  }
+}
+__global__ void k_efilm_bwd3(GateParams gp, GateGrads gg, GScr gs, int D) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 32 * 17) return;
+  const int j = i / 17, q = i % 17;
+  float s = 0.f;
+  if (q < 16) {
+    for (int d = 0; d < D; ++d) s += gs.dh[j * D + d] * gp.pe[q * D + d];
+    gg.fw0[j * 16 + q] = s;
+  } else {
+    for (int d = 0; d < D; ++d) s += gs.dh[j * D + d];
+    gg.fb0[j] = s;
+  }
+}
+
+static size_t gates_bwd_shmem(int C, int D, int Hse) {
+  const int L = D / 2 + 1;
+  return 4 * L * sizeof(double) + (3 * C + Hse + 5 * D) * sizeof(float);
+}
+
+hipError_t gates_bwd(const GateParams& gp, const GateSaved& sv, const float* Sa, const float* Sg,
+                     GateGrads& gg, float* A, float* Bc, Vol vol, int C, float* scratch,
+                     hipStream_t s) {
+  const int D = vol.D, B = vol.B, Hse = se_hidden(C);
+  const int efilm = gp.fw0 != nullptr;
+  GScr g = gscr(scratch, B, C, D, Hse);
+  hipLaunchKernelGGL(k_gates_bwd, dim3(B), dim3(256), gates_bwd_shmem(C, D, Hse), s, gp, sv, Sa,
+                     Sg, g, A, Bc, vol, C, Hse, efilm);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  if (gp.sw0 || gp.mask) {
+    hipLaunchKernelGGL(k_gates_bwd_final, dim3(64), dim3(256), 0, s, gp, gg, g, B, C, D, Hse);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
+  if (efilm) {
+    hipLaunchKernelGGL(k_efilm_bwd1, dim3(std::min(cdiv(2 * C * D, 256), 1024)), dim3(256), 0, s,
+                       g, sv.t, B, C, D);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_efilm_bwd2, dim3(cdiv(2 * C * 33 + 32 * D, 256)), dim3(256), 0, s, gp, gg,
+                       g, sv.hid, C, D);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_efilm_bwd3, dim3(cdiv(32 * 17, 256)), dim3(256), 0, s, gp, gg, g, D);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+}  // namespace spff

@@ -1,0 +1,387 @@
+// GEMM-shaped ops of the SPFF path on fp32 MFMA (v_mfma_f32_32x32x2_f32):
+//  * ConvTranspose3d(Cin->Cout, kernel (1,2,2), stride (1,2,2)) + bias
+//    (reference up1..up3, models.py:668-672): non-overlapping, so it is one GEMM
+//    [Vlow x Cin] . [Cin x 4*Cout] whose columns scatter to the 4 sub-lattices.
+//  * the 1x1x1 classifier head nn.Conv3d(f, K, 1) (models.py:674).
+// Forward / dgrad use k_gemm (C = A.B, A rows gathered by a functor, C rows
+// scattered by a functor).  Weight grads use k_atb (C = X^T.Y reduced over
+// voxels, split over voxel ranges into fp32 partial slabs summed in a fixed
+// order -> deterministic) which also produces the bias column sums.
+#include "spff_internal.h"
+
+namespace spff {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+static inline int64_t cdiv64(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// ------------------------------------------------------------- functors --
+struct LoadRowsVec {  // A[m][k] = p[m*ld + k]; ld, kmax multiples of 4
+  const float* p; int ld; int kmax; int64_t M;
+  __device__ float4 load4(int64_t m, int k) const {
+    if (m >= M || k >= kmax) return make_float4(0.f, 0.f, 0.f, 0.f);
+    return *reinterpret_cast<const float4*>(p + m * ld + k);
+  }
+};
+struct LoadRowsScalar {  // generic
+  const float* p; int ld; int kmax; int64_t M;
+  __device__ float4 load4(int64_t m, int k) const {
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (m >= M) return v;
+    const float* q = p + m * ld;
+    if (k + 0 < kmax) v.x = q[k + 0];
+    if (k + 1 < kmax) v.y = q[k + 1];
+    if (k + 2 < kmax) v.z = q[k + 2];
+    if (k + 3 < kmax) v.w = q[k + 3];
+    return v;
+  }
+};
+__device__ inline int64_t up_high_vox(int64_t m, int ij, int D, int Hl, int Wl) {
+  const int w = (int)(m % Wl);
+  int64_t t = m / Wl;
+  const int h = (int)(t % Hl);
+  t /= Hl;  // t = b*D + d
+  return (t * (2 * Hl) + 2 * h + (ij >> 1)) * (int64_t)(2 * Wl) + 2 * w + (ij & 1);
+}
+struct LoadUpGather {  // A[m][k], k = ij*Cout + co -> dy[high(m,ij)*ld + co]
+  const float* p; int ld; int Cout; int D, Hl, Wl; int64_t M;
+  __device__ float4 load4(int64_t m, int k) const {
+    if (m >= M || k >= 4 * Cout) return make_float4(0.f, 0.f, 0.f, 0.f);
+    const int ij = k / Cout, co = k % Cout;
+    return *reinterpret_cast<const float4*>(p + up_high_vox(m, ij, D, Hl, Wl) * ld + co);
+  }
+};
+struct StoreRows {  // C[m][n] -> p[m*ld + n] (+bias[n]), n < nmax
+  float* p; int ld; int nmax; const float* bias; int64_t M;
+  __device__ void store(int64_t m, int n, float v) const {
+    if (m < M && n < nmax) p[m * ld + n] = v + (bias ? bias[n] : 0.f);
+  }
+};
+struct StoreUp {  // C[m][n], n = ij*Cout + co -> y[high(m,ij)*Cout + co] + bias[co]
+  float* p; int Cout; const float* bias; int D, Hl, Wl; int64_t M;
+  __device__ void store(int64_t m, int n, float v) const {
+    if (m >= M || n >= 4 * Cout) return;
+    const int ij = n / Cout, co = n % Cout;
+    p[up_high_vox(m, ij, D, Hl, Wl) * Cout + co] = v + bias[co];
+  }
+};
+
+// ---------------------------------------------------------------- C = A.B --
+// Tile 128 rows x BN cols, 4 waves each 32 rows x BN.  B is row-major [kpad][npad].
+constexpr int G_BM = 128, G_BK = 16;
+template <class AL, class CS, int BN>
+__global__ __launch_bounds__(256) void k_gemm(AL A, const float* __restrict__ B, CS C, int kpad,
+                                              int npad) {
+  constexpr int PA = G_BK + 1;
+  constexpr int NB = BN / 32;
+  __shared__ float As[G_BM * PA];
+  __shared__ float Bs[G_BK * BN];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int khalf = lane >> 5, l32 = lane & 31;
+  const int64_t m0 = (int64_t)blockIdx.x * G_BM;
+  const int n0 = blockIdx.y * BN;
+  f32x16 acc[NB];
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[nb][r] = 0.f;
+  for (int k0 = 0; k0 < kpad; k0 += G_BK) {
+    if (k0) __syncthreads();
+    for (int i = threadIdx.x; i < G_BM * (G_BK / 4); i += 256) {
+      const int q = i % (G_BK / 4), r = i / (G_BK / 4);
+      const float4 v = A.load4(m0 + r, k0 + 4 * q);
+      float* d = As + r * PA + 4 * q;
+      d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+    }
+    for (int i = threadIdx.x; i < G_BK * (BN / 4); i += 256) {
+      const int q = i % (BN / 4), r = i / (BN / 4);
+      *reinterpret_cast<float4*>(Bs + r * BN + 4 * q) =
+          *reinterpret_cast<const float4*>(B + (int64_t)(k0 + r) * npad + n0 + 4 * q);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < G_BK / 2; ++s) {
+      const int k = 2 * s + khalf;
+      const float a = As[(wave * 32 + l32) * PA + k];
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb)
+        acc[nb] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, Bs[k * BN + nb * 32 + l32], acc[nb], 0,
+                                                        0, 0);
+    }
+  }
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int i = (r & 3) + 8 * (r >> 2) + 4 * khalf;
+      C.store(m0 + wave * 32 + i, n0 + nb * 32 + l32, acc[nb][r]);
+    }
+}
+
+template <class AL, class CS>
+static hipError_t launch_gemm(const AL& A, const float* B, const CS& C, int64_t M, int kpad,
+                              int npad, hipStream_t s) {
+  const int BN = (npad % 64 == 0) ? 64 : 32;
+  dim3 grid((unsigned)cdiv64(M, G_BM), npad / BN);
+  if (BN == 64)
+    hipLaunchKernelGGL((k_gemm<AL, CS, 64>), grid, dim3(256), 0, s, A, B, C, kpad, npad);
+  else
+    hipLaunchKernelGGL((k_gemm<AL, CS, 32>), grid, dim3(256), 0, s, A, B, C, kpad, npad);
+  return hipGetLastError();
+}
+
+// --------------------------------------------------------- C = X^T . Y -----
+// part[split][k1pad][npad] = sum over the split's rows of X[m][k1] * Y[m][n];
+// csum[split][npad] = sum of Y[m][n] (bias grads).  Tile 64 x 64, 4 waves 2x2.
+constexpr int T_BM = 64;
+template <class XL, class YL>
+__global__ __launch_bounds__(256) void k_atb(XL X, YL Y, float* __restrict__ part,
+                                             float* __restrict__ csum, int64_t M, int64_t rps,
+                                             int k1pad, int npad) {
+  constexpr int PX = 64 + 1;
+  __shared__ float Xs[T_BM * PX];
+  __shared__ float Ys[T_BM * 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int khalf = lane >> 5, l32 = lane & 31;
+  const int split = blockIdx.x, k10 = blockIdx.y * 64, n0 = blockIdx.z * 64;
+  const int wr = wave >> 1, wc = wave & 1;
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  float cs = 0.f;  // column sum for column n0 + (tid&63), rows (tid>>6) mod 4
+  const int64_t mb = (int64_t)split * rps, me = min(M, mb + rps);
+  for (int64_t m0 = mb; m0 < me; m0 += T_BM) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < T_BM * 16; i += 256) {
+      const int q = i % 16, r = i / 16;
+      const int64_t m = m0 + r;
+      const float4 xv = (m < me) ? X.load4(m, k10 + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+      float* d = Xs + r * PX + 4 * q;
+      d[0] = xv.x; d[1] = xv.y; d[2] = xv.z; d[3] = xv.w;
+      const float4 yv = (m < me) ? Y.load4(m, n0 + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+      *reinterpret_cast<float4*>(Ys + r * 64 + 4 * q) = yv;
+    }
+    __syncthreads();
+#pragma unroll 8
+    for (int s = 0; s < T_BM / 2; ++s) {
+      const int k = 2 * s + khalf;
+      const float a = Xs[k * PX + wr * 32 + l32];
+      const float b = Ys[k * 64 + wc * 32 + l32];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+    }
+    if (blockIdx.y == 0) {
+      for (int r = wave; r < T_BM; r += 4) cs += Ys[r * 64 + lane];
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int i = (r & 3) + 8 * (r >> 2) + 4 * khalf;
+    part[((int64_t)split * k1pad + k10 + wr * 32 + i) * npad + n0 + wc * 32 + l32] = acc[r];
+  }
+  if (blockIdx.y == 0) {
+    __shared__ float red[256];
+    red[threadIdx.x] = cs;
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      const float v = red[threadIdx.x] + red[threadIdx.x + 64] + red[threadIdx.x + 128] +
+                      red[threadIdx.x + 192];
+      csum[(int64_t)split * npad + n0 + threadIdx.x] = v;
+    }
+  }
+}
+
+// dW layouts: mode 0 = upconv W[Cin][Cout][1][2][2] from C[ci][ij*Cout+co]
+//             mode 1 = head   W[K][Cin]           from C[ci][k]
+__global__ void k_atb_reduce(const float* __restrict__ part, const float* __restrict__ csum,
+                             float* __restrict__ dw, float* __restrict__ db, int nsplit, int k1pad,
+                             int npad, int K1, int N, int Cout, int mode) {
+  const int total = K1 * N;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total + npad;
+       i += gridDim.x * blockDim.x) {
+    if (i < total) {
+      const int n = i % N, k1 = i / N;
+      const float* p = part + (int64_t)k1 * npad + n;
+      float s = 0.f;
+      for (int k = 0; k < nsplit; ++k) s += p[(int64_t)k * k1pad * npad];
+      if (mode == 0) {
+        const int ij = n / Cout, co = n % Cout;
+        dw[((int64_t)k1 * Cout + co) * 4 + ij] = s;
+      } else {
+        dw[(int64_t)n * K1 + k1] = s;
+      }
+    } else {
+      const int co = i - total;  // bias: sum over splits (and over ij for upconv)
+      if (co >= Cout) continue;
+      float s = 0.f;
+      const int nij = (mode == 0) ? 4 : 1;
+      for (int ij = 0; ij < nij; ++ij) {
+        float t = 0.f;
+        for (int k = 0; k < nsplit; ++k) t += csum[(int64_t)k * npad + ij * Cout + co];
+        s += t;
+      }
+      db[co] = s;
+    }
+  }
+}
+
+template <class XL, class YL>
+static hipError_t launch_atb(const XL& X, const YL& Y, int64_t M, int K1, int N, int Cout,
+                             int mode, float* dw, float* db, float* ws, hipStream_t s) {
+  const int k1pad = cdiv(K1, 64) * 64, npad = cdiv(N, 64) * 64;
+  const int nout = (k1pad / 64) * (npad / 64);
+  int64_t nsplit = std::max<int64_t>(1, cdiv64(1024, nout));
+  nsplit = std::min<int64_t>(nsplit, std::max<int64_t>(1, cdiv64(M, 4 * T_BM)));
+  int64_t rps = cdiv64(cdiv64(M, nsplit), T_BM) * T_BM;
+  nsplit = cdiv64(M, rps);
+  float* part = ws;
+  float* csum = ws + nsplit * k1pad * npad;
+  dim3 grid((unsigned)nsplit, k1pad / 64, npad / 64);
+  hipLaunchKernelGGL((k_atb<XL, YL>), grid, dim3(256), 0, s, X, Y, part, csum, M, rps, k1pad,
+                     npad);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const int total = K1 * N + npad;
+  hipLaunchKernelGGL(k_atb_reduce, dim3(cdiv(total, 256)), dim3(256), 0, s, part, csum, dw, db,
+                     (int)nsplit, k1pad, npad, K1, N, Cout, mode);
+  return hipGetLastError();
+}
+
+static size_t atb_ws_bytes(int64_t M, int K1, int N) {
+  const int k1pad = cdiv(K1, 64) * 64, npad = cdiv(N, 64) * 64;
+  const int nout = (k1pad / 64) * (npad / 64);
+  int64_t nsplit = std::max<int64_t>(1, cdiv64(1024, nout));
+  nsplit = std::min<int64_t>(nsplit, std::max<int64_t>(1, cdiv64(M, 4 * T_BM)));
+  int64_t rps = cdiv64(cdiv64(M, nsplit), T_BM) * T_BM;
+  nsplit = cdiv64(M, rps);
+  return (size_t)nsplit * (k1pad + 1) * npad * sizeof(float);
+}
+
+// ---------------------------------------------------------------- packing --
+// wf[ci][ij*Cout+co] = W[ci][co][ij] (kpad = roundup(Cin,16), npad = roundup(4Cout, 32))
+// wd[ij*Cout+co][ci] = W[ci][co][ij] (kpad = roundup(4Cout,16), npad = roundup(Cin, 32))
+static inline int up_f_kpad(int Cin) { return cdiv(Cin, G_BK) * G_BK; }
+static inline int up_f_npad(int Cout) { return cdiv(4 * Cout, 64) * 64; }
+static inline int up_d_kpad(int Cout) { return cdiv(4 * Cout, G_BK) * G_BK; }
+static inline int up_d_npad(int Cin) { return cdiv(Cin, 64) * 64; }
+
+__global__ void k_up_pack(const float* __restrict__ w, float* __restrict__ wf,
+                          float* __restrict__ wd, int Cin, int Cout, int fk, int fn, int dk,
+                          int dn) {
+  const int tf = fk * fn, td = dk * dn;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < tf + td; i += gridDim.x * blockDim.x) {
+    if (i < tf) {
+      const int n = i % fn, k = i / fn;
+      float v = 0.f;
+      if (k < Cin && n < 4 * Cout) v = w[((int64_t)k * Cout + n % Cout) * 4 + n / Cout];
+      wf[i] = v;
+    } else {
+      const int j = i - tf;
+      const int n = j % dn, k = j / dn;
+      float v = 0.f;
+      if (k < 4 * Cout && n < Cin) v = w[((int64_t)n * Cout + k % Cout) * 4 + k / Cout];
+      wd[j] = v;
+    }
+  }
+}
+
+hipError_t upconv_pack(const float* w, float* wf, float* wd, int Cin, int Cout, hipStream_t s) {
+  const int fk = up_f_kpad(Cin), fn = up_f_npad(Cout), dk = up_d_kpad(Cout), dn = up_d_npad(Cin);
+  const int total = fk * fn + dk * dn;
+  hipLaunchKernelGGL(k_up_pack, dim3(cdiv(total, 256)), dim3(256), 0, s, w, wf, wd, Cin, Cout, fk,
+                     fn, dk, dn);
+  return hipGetLastError();
+}
+
+hipError_t upconv_fwd(const float* x, const float* wf, const float* bias, float* y, Vol low,
+                      int Cin, int Cout, hipStream_t s) {
+  const int64_t M = nvox(low);
+  LoadRowsVec A{x, Cin, Cin, M};
+  StoreUp C{y, Cout, bias, low.D, low.H, low.W, M};
+  return launch_gemm(A, wf, C, M, up_f_kpad(Cin), up_f_npad(Cout), s);
+}
+
+hipError_t upconv_dgrad(const float* dy, int lddy, const float* wd, float* dx, Vol low, int Cin,
+                        int Cout, hipStream_t s) {
+  const int64_t M = nvox(low);
+  LoadUpGather A{dy, lddy, Cout, low.D, low.H, low.W, M};
+  StoreRows C{dx, Cin, Cin, nullptr, M};
+  return launch_gemm(A, wd, C, M, up_d_kpad(Cout), up_d_npad(Cin), s);
+}
+
+size_t upconv_wgrad_ws_bytes(Vol low, int Cin, int Cout) {
+  return atb_ws_bytes(nvox(low), Cin, 4 * Cout);
+}
+
+hipError_t upconv_wgrad(const float* x, const float* dy, int lddy, float* dw, float* db, Vol low,
+                        int Cin, int Cout, float* ws, hipStream_t s) {
+  const int64_t M = nvox(low);
+  LoadRowsVec X{x, Cin, Cin, M};
+  LoadUpGather Y{dy, lddy, Cout, low.D, low.H, low.W, M};
+  return launch_atb(X, Y, M, Cin, 4 * Cout, Cout, 0, dw, db, ws, s);
+}
+
+// ------------------------------------------------------------------- head --
+// The head's packed weights are produced on the fly by tiny kernels into ws.
+__global__ void k_head_pack(const float* __restrict__ w, float* __restrict__ wf,
+                            float* __restrict__ wd, int Cin, int K, int fk, int fn, int dk,
+                            int dn) {
+  const int tf = fk * fn, td = dk * dn;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < tf + td; i += gridDim.x * blockDim.x) {
+    if (i < tf) {  // wf[ci][k]
+      const int n = i % fn, k = i / fn;
+      wf[i] = (k < Cin && n < K) ? w[(int64_t)n * Cin + k] : 0.f;
+    } else {  // wd[k][ci]
+      const int j = i - tf;
+      const int n = j % dn, k = j / dn;
+      wd[j] = (k < K && n < Cin) ? w[(int64_t)k * Cin + n] : 0.f;
+    }
+  }
+}
+
+static inline int head_fk(int Cin) { return cdiv(Cin, G_BK) * G_BK; }
+static inline int head_fn(int K) { return cdiv(K, 32) * 32; }
+static inline int head_dk(int K) { return cdiv(K, G_BK) * G_BK; }
+static inline int head_dn(int Cin) { return cdiv(Cin, 32) * 32; }
+
+hipError_t head_fwd(const float* x, const float* wf, const float* b, float* y, int64_t V, int Cin,
+                    int K, hipStream_t s) {
+  LoadRowsVec A{x, Cin, Cin, V};
+  StoreRows C{y, K, K, b, V};
+  return launch_gemm(A, wf, C, V, head_fk(Cin), head_fn(K), s);
+}
+
+hipError_t head_pack(const float* w, float* wf, float* wd, int Cin, int K, hipStream_t s) {
+  const int fk = head_fk(Cin), fn = head_fn(K), dk = head_dk(K), dn = head_dn(Cin);
+  const int total = fk * fn + dk * dn;
+  hipLaunchKernelGGL(k_head_pack, dim3(cdiv(total, 256)), dim3(256), 0, s, w, wf, wd, Cin, K, fk,
+                     fn, dk, dn);
+  return hipGetLastError();
+}
+size_t head_pack_floats(int Cin, int K) {
+  return (size_t)head_fk(Cin) * head_fn(K) + (size_t)head_dk(K) * head_dn(Cin);
+}
+size_t head_pack_dgrad_offset(int Cin, int K) { return (size_t)head_fk(Cin) * head_fn(K); }
+size_t upconv_pack_floats(int Cin, int Cout) {
+  return (size_t)up_f_kpad(Cin) * up_f_npad(Cout) + (size_t)up_d_kpad(Cout) * up_d_npad(Cin);
+}
+size_t upconv_pack_dgrad_offset(int Cin, int Cout) {
+  return (size_t)up_f_kpad(Cin) * up_f_npad(Cout);
+}
+
+hipError_t head_dgrad(const float* dy, const float* wd, float* dx, int64_t V, int Cin, int K,
+                      hipStream_t s) {
+  LoadRowsScalar A{dy, K, K, V};
+  StoreRows C{dx, Cin, Cin, nullptr, V};
+  return launch_gemm(A, wd, C, V, head_dk(K), head_dn(Cin), s);
+}
+
+size_t head_wgrad_ws_bytes(int64_t V, int Cin, int K) { return atb_ws_bytes(V, Cin, K); }
+
+hipError_t head_wgrad(const float* x, const float* dy, float* dw, float* db, int64_t V, int Cin,
+                      int K, float* ws, hipStream_t s) {
+  LoadRowsVec X{x, Cin, Cin, V};
+  LoadRowsScalar Y{dy, K, K, V};
+  return launch_atb(X, Y, V, Cin, K, K, 1, dw, db, ws, s);
+}
+
+}  // namespace spff

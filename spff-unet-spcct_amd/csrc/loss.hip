@@ -1,0 +1,181 @@
+// Voxel-wise loss: F.cross_entropy(ignore_index) + 0.5 * (1 - hard macro-Dice)
+// (reference helpers.py:782-803) and the argmax confusion matrix that both
+// the hard-Dice term and per_class_metrics_3d (helpers.py:668-725) need.
+//
+// One HBM pass over logits [V][K] (channel-last) + int64 labels writes
+// dlogits = (softmax - onehot) / N_valid (0 for ignored voxels), per-block CE
+// partial sums (fixed grid -> fixed summation order -> deterministic) and an
+// integer K x K confusion histogram (LDS, then int64 atomics: order-free).
+// The ~100 .item() host syncs of the reference become zero: the finaliser
+// kernel computes ce, the hard-Dice term and the loss on the device.
+#include "spff_internal.h"
+#include <math.h>
+
+namespace spff {
+
+constexpr int LOSS_GRID = 1024, LOSS_T = 256, KMAX = 32;
+
+__global__ void k_count_valid(const int64_t* __restrict__ lab, int64_t V, int ignore,
+                              unsigned long long* __restrict__ cnt) {
+  unsigned long long c = 0;
+  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < V;
+       v += (int64_t)gridDim.x * blockDim.x)
+    c += (lab[v] != ignore) ? 1ull : 0ull;
+  __shared__ unsigned long long red[LOSS_T];
+  red[threadIdx.x] = c;
+  __syncthreads();
+  for (int s = LOSS_T / 2; s > 0; s >>= 1) {
+    if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) atomicAdd(cnt, red[0]);
+}
+
+template <bool WITH_CE>
+__global__ __launch_bounds__(LOSS_T) void k_loss(const float* __restrict__ x,
+                                                 const int64_t* __restrict__ lab, int64_t V, int K,
+                                                 int ignore, const int64_t* __restrict__ count,
+                                                 float* __restrict__ dx,
+                                                 unsigned long long* __restrict__ conf,
+                                                 double* __restrict__ part,
+                                                 unsigned long long* __restrict__ nbad) {
+  __shared__ unsigned int hist[KMAX * (KMAX + 1)];
+  __shared__ double red[LOSS_T];
+  const int K1 = K + 1;  // column K = label outside [0,K) (not ignored)
+  for (int i = threadIdx.x; i < K * K1; i += LOSS_T) hist[i] = 0;
+  __syncthreads();
+  const float invN = WITH_CE ? 1.f / (float)(*count) : 0.f;
+  double ce = 0.0;
+  unsigned int bad = 0;
+  for (int64_t v = blockIdx.x * (int64_t)LOSS_T + threadIdx.x; v < V;
+       v += (int64_t)gridDim.x * LOSS_T) {
+    const float* xv = x + v * K;
+    float xs[KMAX];
+    float m = xv[0];
+    int am = 0;
+    xs[0] = m;
+    for (int k = 1; k < K; ++k) {
+      const float t = xv[k];
+      xs[k] = t;
+      if (t > m || (isnan(t) && !isnan(m))) { m = t; am = k; }
+    }
+    const int64_t y = lab[v];
+    const bool valid = (y != ignore);
+    if (valid && (y < 0 || y >= K)) {
+      ++bad;
+      atomicAdd(&hist[am * K1 + K], 1u);
+      if (WITH_CE) for (int k = 0; k < K; ++k) dx[v * K + k] = 0.f;
+      continue;
+    }
+    if (valid) atomicAdd(&hist[am * K1 + (int)y], 1u);
+    if (WITH_CE) {
+      float* dv = dx + v * K;
+      if (valid) {
+        float ssum = 0.f;
+        for (int k = 0; k < K; ++k) ssum += expf(xs[k] - m);
+        const float lse = m + logf(ssum);
+        ce += (double)(lse - xs[(int)y]);
+        const float inv = 1.f / ssum;
+        for (int k = 0; k < K; ++k) {
+          const float p = expf(xs[k] - m) * inv;
+          dv[k] = (p - (k == (int)y ? 1.f : 0.f)) * invN;
+        }
+      } else {
+        for (int k = 0; k < K; ++k) dv[k] = 0.f;
+      }
+    }
+  }
+  if (WITH_CE) {
+    red[threadIdx.x] = ce;
+    __syncthreads();
+    for (int s = LOSS_T / 2; s > 0; s >>= 1) {
+      if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < K * K1; i += LOSS_T)
+    if (hist[i]) atomicAdd(&conf[i], (unsigned long long)hist[i]);
+  if (bad && nbad) atomicAdd(nbad, (unsigned long long)bad);
+}
+
+// out4 = [ce, loss, dice_loss_part, n_valid]; dice per helpers.py:782-795 in fp64;
+// loss = fp32(ce) + fp32(0.5*dice) as torch adds a python float to a fp32 tensor.
+__global__ void k_loss_final(const double* __restrict__ part, int nparts,
+                             const int64_t* __restrict__ count,
+                             const unsigned long long* __restrict__ conf, int K, double smooth,
+                             float* __restrict__ out4) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  double s = 0.0;
+  for (int i = 0; i < nparts; ++i) s += part[i];
+  const double N = (double)(*count);
+  const float ce = (float)(s / N);
+  double dsum = 0.0;
+  const int K1 = K + 1;
+  for (int c = 1; c < K; ++c) {
+    double tp = (double)conf[c * K1 + c], rowp = 0.0, coll = 0.0;
+    for (int j = 0; j < K1; ++j) rowp += (double)conf[c * K1 + j];
+    for (int j = 0; j < K; ++j) coll += (double)conf[j * K1 + c];
+    const double fp = rowp - tp, fn = coll - tp;
+    dsum += (2.0 * tp + smooth) / (2.0 * tp + fp + fn + smooth);
+  }
+  const double macro = K > 1 ? dsum / (double)(K - 1) : 1.0;
+  const double dice_loss = 1.0 - macro;
+  out4[0] = ce;
+  out4[1] = ce + (float)(0.5 * dice_loss);
+  out4[2] = (float)dice_loss;
+  out4[3] = (float)N;
+}
+
+size_t loss_ws_bytes(int64_t V, int K) {
+  (void)V; (void)K;
+  return LOSS_GRID * sizeof(double) + 64;
+}
+
+hipError_t count_valid(const int64_t* labels, int64_t V, int ignore, int64_t* count,
+                       hipStream_t s) {
+  hipError_t e = hipMemsetAsync(count, 0, sizeof(int64_t), s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_count_valid, dim3(LOSS_GRID), dim3(LOSS_T), 0, s, labels, V, ignore,
+                     reinterpret_cast<unsigned long long*>(count));
+  return hipGetLastError();
+}
+
+// ws: [LOSS_GRID doubles][int64 count][uint64 nbad]
+hipError_t loss_fwd(const float* logits, const int64_t* labels, int64_t V, int K, int ignore,
+                    double smooth, const int64_t* count_override, float* out4, float* dlogits,
+                    int64_t* conf, float* ws, hipStream_t s) {
+  if (K > KMAX || K < 1) return hipErrorInvalidValue;
+  double* part = reinterpret_cast<double*>(ws);
+  int64_t* cnt = reinterpret_cast<int64_t*>(part + LOSS_GRID);
+  unsigned long long* nbad = reinterpret_cast<unsigned long long*>(cnt + 1);
+  hipError_t e;
+  const int64_t* cptr = count_override;
+  if (!cptr) {
+    if ((e = count_valid(labels, V, ignore, cnt, s)) != hipSuccess) return e;
+    cptr = cnt;
+  }
+  if ((e = hipMemsetAsync(conf, 0, sizeof(int64_t) * K * (K + 1), s)) != hipSuccess) return e;
+  if ((e = hipMemsetAsync(nbad, 0, sizeof(unsigned long long), s)) != hipSuccess) return e;
+  hipLaunchKernelGGL(k_loss<true>, dim3(LOSS_GRID), dim3(LOSS_T), 0, s, logits, labels, V, K,
+                     ignore, cptr, dlogits, reinterpret_cast<unsigned long long*>(conf), part,
+                     nbad);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(k_loss_final, dim3(1), dim3(64), 0, s, part, LOSS_GRID, cptr,
+                     reinterpret_cast<unsigned long long*>(conf), K, smooth, out4);
+  return hipGetLastError();
+}
+
+hipError_t confusion_only(const float* logits, const int64_t* labels, int64_t V, int K, int ignore,
+                          int64_t* conf, hipStream_t s) {
+  if (K > KMAX || K < 1) return hipErrorInvalidValue;
+  hipError_t e = hipMemsetAsync(conf, 0, sizeof(int64_t) * K * (K + 1), s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_loss<false>, dim3(LOSS_GRID), dim3(LOSS_T), 0, s, logits, labels, V, K,
+                     ignore, nullptr, nullptr, reinterpret_cast<unsigned long long*>(conf),
+                     nullptr, nullptr);
+  return hipGetLastError();
+}
+
+}  // namespace spff

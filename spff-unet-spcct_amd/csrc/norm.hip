@@ -1,0 +1,311 @@
+// InstanceNorm3d(affine, eps=1e-5) + LeakyReLU(0.01) forward/backward and the
+// per-(b, c, d) hw-reductions the gate algebra needs (reference models.py:168-181,
+// 1453-1469).  All HBM-bound: one float4 (4 channels) per lane, channel-last
+// [B][D][H][W][C] rows, per-thread register accumulation over voxels, then a
+// fixed-order LDS tree -> deterministic sums, no float atomics.
+//
+// Naming: y = raw conv output, al = gamma*rstd, de = beta - mean*al (so the
+// normalised+affine value is r = y*al + de, exactly the CPU batch-norm
+// transform form), a = lrelu(r).
+#include "spff_internal.h"
+
+namespace spff {
+
+static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+__device__ __forceinline__ float lrelu(float r) { return r > 0.f ? r : 0.01f * r; }
+__device__ __forceinline__ float slope(float r) { return r > 0.f ? 1.f : 0.01f; }
+
+namespace {
+struct RedPlan {
+  int tpv, vpp, chunk, nsplit, HW;
+};
+RedPlan red_plan(Vol vol, int C) {
+  RedPlan p;
+  p.HW = vol.H * vol.W;
+  p.tpv = C / 4;
+  p.vpp = 256 / p.tpv;
+  p.chunk = p.vpp * 16;
+  p.nsplit = cdiv(p.HW, p.chunk);
+  return p;
+}
+}  // namespace
+
+template <int OP, int NQ>
+__global__ __launch_bounds__(256) void k_slab_reduce(RedArgs a, Vol vol, int C, float* __restrict__ ws,
+                                                     int nsplit, int chunk) {
+  const int bd = blockIdx.y;  // b*D + d
+  const int split = blockIdx.x;
+  const int b = bd / vol.D, d = bd % vol.D;
+  const int HW = vol.H * vol.W;
+  const int tpv = C >> 2, vpp = 256 / tpv;
+  const int cq = threadIdx.x % tpv, vo = threadIdx.x / tpv;
+  const int c = 4 * cq;
+  float acc[NQ][4];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[q][j] = 0.f;
+  if (vo < vpp) {
+    float p0[4], p1[4], p2[4], p3[4];  // per-channel params
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int bc = b * C + c + j;
+      p0[j] = 0.f; p1[j] = 0.f; p2[j] = 1.f; p3[j] = 0.f;
+      if (OP == RED_SQDEV) p0[j] = a.mean[bc];
+      if (OP == RED_ACT || OP == RED_BWD_TAIL || OP == RED_BWD_IN) { p0[j] = a.al[bc]; p1[j] = a.de[bc]; }
+      if (OP == RED_BWD_IN) {
+        if (a.A) { p2[j] = a.A[(int64_t)bc * vol.D + d]; p3[j] = a.Bc[(int64_t)bc * vol.D + d]; }
+      }
+    }
+    float mu[4], rs[4];
+    if (OP == RED_BWD_IN) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { mu[j] = a.mean[b * C + c + j]; rs[j] = a.rstd[b * C + c + j]; }
+    }
+    const int hb = split * chunk, he = min(HW, hb + chunk);
+    const int64_t base = (int64_t)bd * HW;
+    for (int hw = hb + vo; hw < he; hw += vpp) {
+      const int64_t off = (base + hw) * C + c;
+      const float4 yv = *reinterpret_cast<const float4*>(a.y + off);
+      const float ys[4] = {yv.x, yv.y, yv.z, yv.w};
+      float gs[4] = {0.f, 0.f, 0.f, 0.f};
+      if (OP == RED_BWD_TAIL || OP == RED_BWD_IN) {
+        const float4 gv = *reinterpret_cast<const float4*>(a.g + off);
+        gs[0] = gv.x; gs[1] = gv.y; gs[2] = gv.z; gs[3] = gv.w;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (OP == RED_SUM) {
+          acc[0][j] += ys[j];
+        } else if (OP == RED_SQDEV) {
+          const float t = ys[j] - p0[j];
+          acc[0][j] += t * t;
+        } else if (OP == RED_ACT) {
+          acc[0][j] += lrelu(ys[j] * p0[j] + p1[j]);
+        } else if (OP == RED_BWD_TAIL) {
+          acc[0][j] += gs[j];
+          acc[NQ - 1][j] += gs[j] * lrelu(ys[j] * p0[j] + p1[j]);
+        } else {  // RED_BWD_IN
+          const float r = ys[j] * p0[j] + p1[j];
+          const float dr = (gs[j] * p2[j] + p3[j]) * slope(r);
+          const float xh = (ys[j] - mu[j]) * rs[j];
+          acc[0][j] += dr;
+          acc[NQ - 1][j] += dr * xh;
+        }
+      }
+    }
+  }
+  // fixed-order LDS tree over the vpp voxel lanes
+  __shared__ float red[256 * 4];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) red[threadIdx.x * 4 + j] = acc[q][j];
+    __syncthreads();
+    for (int st = vpp / 2; st >= 1; st >>= 1) {
+      if (vo < st) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) red[threadIdx.x * 4 + j] += red[(threadIdx.x + st * tpv) * 4 + j];
+      }
+      __syncthreads();
+    }
+    if (vo == 0) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        ws[(((int64_t)bd * nsplit + split) * C + c + j) * NQ + q] = red[threadIdx.x * 4 + j];
+    }
+    __syncthreads();
+  }
+}
+
+// combine splits: out[b][c][d][q] = sum_split ws[bd][split][c][q]
+__global__ void k_slab_combine(const float* __restrict__ ws, float* __restrict__ out, Vol vol,
+                               int C, int nq, int nsplit) {
+  const int total = vol.B * vol.D * C * nq;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int q = i % nq;
+    const int c = (i / nq) % C;
+    const int bd = i / (nq * C);
+    const int b = bd / vol.D, d = bd % vol.D;
+    float s = 0.f;
+    for (int k = 0; k < nsplit; ++k) s += ws[(((int64_t)bd * nsplit + k) * C + c) * nq + q];
+    out[(((int64_t)b * C + c) * vol.D + d) * nq + q] = s;
+  }
+}
+
+size_t slab_reduce_ws_bytes(Vol vol, int C, int nq) {
+  RedPlan p = red_plan(vol, C);
+  return (size_t)vol.B * vol.D * p.nsplit * C * nq * sizeof(float);
+}
+
+hipError_t slab_reduce(RedOp op, const RedArgs& a, Vol vol, int C, float* out, float* ws,
+                       hipStream_t s) {
+  if (C % 4 || C > 1024) return hipErrorInvalidValue;
+  RedPlan p = red_plan(vol, C);
+  dim3 grid(p.nsplit, vol.B * vol.D);
+  int nq = 1;
+  switch (op) {
+    case RED_SUM: hipLaunchKernelGGL((k_slab_reduce<RED_SUM, 1>), grid, dim3(256), 0, s, a, vol, C, ws, p.nsplit, p.chunk); break;
+    case RED_SQDEV: hipLaunchKernelGGL((k_slab_reduce<RED_SQDEV, 1>), grid, dim3(256), 0, s, a, vol, C, ws, p.nsplit, p.chunk); break;
+    case RED_ACT: hipLaunchKernelGGL((k_slab_reduce<RED_ACT, 1>), grid, dim3(256), 0, s, a, vol, C, ws, p.nsplit, p.chunk); break;
+    case RED_BWD_TAIL: nq = 2; hipLaunchKernelGGL((k_slab_reduce<RED_BWD_TAIL, 2>), grid, dim3(256), 0, s, a, vol, C, ws, p.nsplit, p.chunk); break;
+    case RED_BWD_IN: nq = 2; hipLaunchKernelGGL((k_slab_reduce<RED_BWD_IN, 2>), grid, dim3(256), 0, s, a, vol, C, ws, p.nsplit, p.chunk); break;
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const int total = vol.B * vol.D * C * nq;
+  hipLaunchKernelGGL(k_slab_combine, dim3(std::min(cdiv(total, 256), 4096)), dim3(256), 0, s, ws,
+                     out, vol, C, nq, p.nsplit);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------ finalizers --
+__global__ void k_in_mean(const float* __restrict__ sums, float* __restrict__ mean, Vol vol, int C) {
+  const int bc = blockIdx.x * blockDim.x + threadIdx.x;
+  if (bc >= vol.B * C) return;
+  double s = 0.0;
+  for (int d = 0; d < vol.D; ++d) s += sums[(int64_t)bc * vol.D + d];
+  mean[bc] = (float)(s / ((double)vol.D * vol.H * vol.W));
+}
+
+__global__ void k_in_rstd(const float* __restrict__ sq, const float* __restrict__ gamma,
+                          const float* __restrict__ beta, const float* __restrict__ mean,
+                          float* __restrict__ rstd, float* __restrict__ al, float* __restrict__ de,
+                          Vol vol, int C) {
+  const int bc = blockIdx.x * blockDim.x + threadIdx.x;
+  if (bc >= vol.B * C) return;
+  const int c = bc % C;
+  double s = 0.0;
+  for (int d = 0; d < vol.D; ++d) s += sq[(int64_t)bc * vol.D + d];
+  const double var = s / ((double)vol.D * vol.H * vol.W);
+  const float rs = (float)(1.0 / sqrt(var + 1e-5));
+  rstd[bc] = rs;
+  const float a = gamma[c] * rs;
+  al[bc] = a;
+  de[bc] = beta[c] - mean[bc] * a;
+}
+
+hipError_t in_mean(const float* sums, float* mean, Vol vol, int C, hipStream_t s) {
+  hipLaunchKernelGGL(k_in_mean, dim3(cdiv(vol.B * C, 256)), dim3(256), 0, s, sums, mean, vol, C);
+  return hipGetLastError();
+}
+
+hipError_t in_rstd(const float* sq, const float* gamma, const float* beta, const float* mean,
+                   float* rstd, float* al, float* de, Vol vol, int C, hipStream_t s) {
+  hipLaunchKernelGGL(k_in_rstd, dim3(cdiv(vol.B * C, 256)), dim3(256), 0, s, sq, gamma, beta,
+                     mean, rstd, al, de, vol, C);
+  return hipGetLastError();
+}
+
+__global__ void k_in_bwd_stats(const float* __restrict__ sums, float* __restrict__ dgamma,
+                               float* __restrict__ dbeta, float* __restrict__ k1,
+                               float* __restrict__ k2, Vol vol, int C) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const double N = (double)vol.D * vol.H * vol.W;
+  double tg = 0.0, tb = 0.0;
+  for (int b = 0; b < vol.B; ++b) {
+    const int64_t bc = (int64_t)b * C + c;
+    double s0 = 0.0, s1 = 0.0;
+    for (int d = 0; d < vol.D; ++d) {
+      s0 += sums[(bc * vol.D + d) * 2 + 0];
+      s1 += sums[(bc * vol.D + d) * 2 + 1];
+    }
+    k1[bc] = (float)(s0 / N);
+    k2[bc] = (float)(s1 / N);
+    tb += s0;
+    tg += s1;
+  }
+  if (dgamma) dgamma[c] = (float)tg;
+  if (dbeta) dbeta[c] = (float)tb;
+}
+
+hipError_t in_bwd_stats(const float* sums, const float* gamma, float* dgamma, float* dbeta,
+                        float* k1, float* k2, Vol vol, int C, hipStream_t s) {
+  (void)gamma;
+  hipLaunchKernelGGL(k_in_bwd_stats, dim3(cdiv(C, 64)), dim3(64), 0, s, sums, dgamma, dbeta, k1,
+                     k2, vol, C);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------ elementwise --
+// grid.y = b*D + d ; grid.x strides over the (h,w,c/4) float4s of that slab.
+__global__ __launch_bounds__(256) void k_act_apply(const float* __restrict__ y, float* __restrict__ out,
+                                                   const float* __restrict__ al, const float* __restrict__ de,
+                                                   const float* __restrict__ P, const float* __restrict__ Q,
+                                                   Vol vol, int C) {
+  const int bd = blockIdx.y, b = bd / vol.D, d = bd % vol.D;
+  const int n4 = vol.H * vol.W * (C >> 2);
+  const int64_t base = (int64_t)bd * vol.H * vol.W * C;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += gridDim.x * blockDim.x) {
+    const int c = (i % (C >> 2)) * 4;
+    const float4 v = *reinterpret_cast<const float4*>(y + base + 4 * (int64_t)i);
+    float r[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int bc = b * C + c + j;
+      float a = lrelu(r[j] * al[bc] + de[bc]);
+      if (P) {
+        const int64_t k = (int64_t)bc * vol.D + d;
+        a = a * P[k] + Q[k];
+      }
+      r[j] = a;
+    }
+    *reinterpret_cast<float4*>(out + base + 4 * (int64_t)i) = make_float4(r[0], r[1], r[2], r[3]);
+  }
+}
+
+static dim3 ew_grid(Vol vol, int C) {
+  const int n4 = vol.H * vol.W * (C / 4);
+  int gx = std::min(cdiv(n4, 256), 64);
+  return dim3(gx, vol.B * vol.D);
+}
+
+hipError_t act_apply(const float* y, float* out, const float* al, const float* de, const float* P,
+                     const float* Q, Vol vol, int C, hipStream_t s) {
+  hipLaunchKernelGGL(k_act_apply, ew_grid(vol, C), dim3(256), 0, s, y, out, al, de, P, Q, vol, C);
+  return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void k_in_bwd_apply(
+    const float* __restrict__ y, const float* g, float* dy, const float* __restrict__ mean,
+    const float* __restrict__ rstd, const float* __restrict__ al, const float* __restrict__ de,
+    const float* __restrict__ gamma, const float* __restrict__ A, const float* __restrict__ Bc,
+    const float* __restrict__ k1, const float* __restrict__ k2, Vol vol, int C) {
+  const int bd = blockIdx.y, b = bd / vol.D, d = bd % vol.D;
+  const int n4 = vol.H * vol.W * (C >> 2);
+  const int64_t base = (int64_t)bd * vol.H * vol.W * C;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += gridDim.x * blockDim.x) {
+    const int c = (i % (C >> 2)) * 4;
+    const float4 yv = *reinterpret_cast<const float4*>(y + base + 4 * (int64_t)i);
+    const float4 gv = *reinterpret_cast<const float4*>(g + base + 4 * (int64_t)i);
+    const float ys[4] = {yv.x, yv.y, yv.z, yv.w};
+    const float gs[4] = {gv.x, gv.y, gv.z, gv.w};
+    float o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int bc = b * C + c + j;
+      const float r = ys[j] * al[bc] + de[bc];
+      float gg = gs[j];
+      if (A) {
+        const int64_t k = (int64_t)bc * vol.D + d;
+        gg = gg * A[k] + Bc[k];
+      }
+      const float dr = gg * slope(r);
+      const float xh = (ys[j] - mean[bc]) * rstd[bc];
+      o[j] = rstd[bc] * gamma[c + j] * (dr - k1[bc] - xh * k2[bc]);
+    }
+    *reinterpret_cast<float4*>(dy + base + 4 * (int64_t)i) = make_float4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+hipError_t in_bwd_apply(const float* y, const float* g, float* dy, const float* mean,
+                        const float* rstd, const float* al, const float* de, const float* gamma,
+                        const float* A, const float* Bc, const float* k1, const float* k2, Vol vol,
+                        int C, hipStream_t s) {
+  hipLaunchKernelGGL(k_in_bwd_apply, ew_grid(vol, C), dim3(256), 0, s, y, g, dy, mean, rstd, al,
+                     de, gamma, A, Bc, k1, k2, vol, C);
+  return hipGetLastError();
+}
+
+}  // namespace spff

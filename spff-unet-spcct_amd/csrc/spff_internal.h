@@ -1,0 +1,155 @@
+// Internal declarations shared by the SPFF HIP translation units.
+// Layout convention everywhere: activations are channel-last [B][D][H][W][C]
+// fp32 ("NDHWC"), voxel index v = ((b*D + d)*H + h)*W + w.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+namespace spff {
+
+// Two-source channel view: channel c < split reads p0[v*ld0 + c], otherwise
+// p1[v*ld1 + c - split].  Lets the decoder's first conv read [up | skip]
+// without materialising torch.cat (reference _cat, models.py:687-691).
+struct Src2 {
+  const float* p0; const float* p1; int ld0, ld1, split;
+};
+struct Dst2 {
+  float* p0; float* p1; int ld0, ld1, split;
+};
+inline Src2 src1(const float* p, int ld) { return Src2{p, p, ld, ld, 1 << 30}; }
+inline Dst2 dst1(float* p, int ld) { return Dst2{p, p, ld, ld, 1 << 30}; }
+
+struct Vol { int B, D, H, W; };
+inline int64_t nvox(const Vol& v) { return (int64_t)v.B * v.D * v.H * v.W; }
+
+// ---------------------------------------------------------------- conv3d --
+// Weight repack: reference layout W[Cout][Cin][KD][3][3] ->
+//   fwd:   Wt[tap][ci(pad cin_pad)][co(pad cout_pad)]
+//   dgrad: Wt[tap][co(pad cout_pad)][ci(pad cin_pad)] with taps flipped.
+hipError_t conv_pack_weights(const float* w, float* wt, int Cout, int Cin, int KD,
+                             int kpad, int npad, bool dgrad, hipStream_t s);
+// y = conv3d(x, W) 'same' padding (KD/2,1,1); x: Cin channels (kpad: padded
+// reduction channels, multiple of 8), y: Cout channels (npad: multiple of BN).
+hipError_t conv3d_fwd(const Src2& x, const float* wt, const Dst2& y, Vol vol, int KD,
+                      int Cin, int kpad, int Cout, int npad, hipStream_t s);
+int conv3d_bn(int Cout);        // output-channel tile the fwd kernel uses
+// dW partials + reduction into reference layout dw[Cout][Cin][KD][3][3].
+size_t conv3d_wgrad_ws_bytes(Vol vol, int KD, int Cin, int Cout);
+hipError_t conv3d_wgrad(const Src2& x, const float* dy, int lddy, float* dw, Vol vol, int KD,
+                        int Cin, int Cout, float* ws, hipStream_t s);
+
+// ---------------------------------------------------------------- gemms --
+// ConvTranspose3d(Cin->Cout, k=(1,2,2), s=(1,2,2)) + bias, low-res x [Vlow][Cin],
+// high-res y [Vhigh][Cout] (Vhigh: H*2, W*2).  Reference weight W[Cin][Cout][1][2][2].
+hipError_t upconv_pack(const float* w, float* wf, float* wd, int Cin, int Cout, hipStream_t s);
+hipError_t upconv_fwd(const float* x, const float* wf, const float* bias, float* y,
+                      Vol low, int Cin, int Cout, hipStream_t s);
+hipError_t upconv_dgrad(const float* dy, int lddy, const float* wd, float* dx, Vol low,
+                        int Cin, int Cout, hipStream_t s);
+size_t upconv_wgrad_ws_bytes(Vol low, int Cin, int Cout);
+hipError_t upconv_wgrad(const float* x, const float* dy, int lddy, float* dw, float* db,
+                        Vol low, int Cin, int Cout, float* ws, hipStream_t s);
+size_t upconv_pack_floats(int Cin, int Cout);
+size_t upconv_pack_dgrad_offset(int Cin, int Cout);
+// 1x1x1 conv head: y[v][K] = x[v][:Cin] . W[K][Cin] + b  (wf/wd from head_pack)
+hipError_t head_pack(const float* w, float* wf, float* wd, int Cin, int K, hipStream_t s);
+size_t head_pack_floats(int Cin, int K);
+size_t head_pack_dgrad_offset(int Cin, int K);
+hipError_t head_fwd(const float* x, const float* wf, const float* b, float* y, int64_t V,
+                    int Cin, int K, hipStream_t s);
+hipError_t head_dgrad(const float* dy, const float* wd, float* dx, int64_t V, int Cin, int K,
+                      hipStream_t s);
+size_t head_wgrad_ws_bytes(int64_t V, int Cin, int K);
+hipError_t head_wgrad(const float* x, const float* dy, float* dw, float* db, int64_t V,
+                      int Cin, int K, float* ws, hipStream_t s);
+
+// ------------------------------------------------------------- norm/gates --
+// Per-(b,d,c) reductions over (h,w) with per-(b,c) affine/recompute ops.
+enum RedOp {
+  RED_SUM = 0,        // q0 = y
+  RED_SQDEV = 1,      // q0 = (y - mean[b,c])^2            (aux0 = mean)
+  RED_ACT = 2,        // q0 = lrelu(y*al + de)              (aux0 = alpha, aux1 = delta)
+  RED_BWD_TAIL = 3,   // q0 = g, q1 = g*lrelu(y*al+de)      (g = dout)
+  RED_BWD_IN = 4,     // r = y*al+de; dr = (g*A+Bc)*slope(r); q0 = dr, q1 = dr*xhat
+};
+struct RedArgs {
+  const float* y; const float* g;     // y: [V][C] (ld = C), g: [V][C] (ld = C)
+  const float* mean; const float* rstd; // [B][C]
+  const float* al; const float* de;   // [B][C]
+  const float* A; const float* Bc;    // [B][C][D] or null (identity)
+};
+// out: [B][C][D][nq] fp32, summed over h,w in a fixed order.
+size_t slab_reduce_ws_bytes(Vol vol, int C, int nq);
+hipError_t slab_reduce(RedOp op, const RedArgs& a, Vol vol, int C, float* out, float* ws,
+                       hipStream_t s);
+// stats: from per-(b,c,d) sums -> mean[b,c] ; from sqdev sums -> rstd, alpha, delta
+hipError_t in_mean(const float* sums, float* mean, Vol vol, int C, hipStream_t s);
+hipError_t in_rstd(const float* sqsums, const float* gamma, const float* beta,
+                   const float* mean, float* rstd, float* al, float* de, Vol vol, int C,
+                   hipStream_t s);
+// out = lrelu(y*al[b,c]+de[b,c]) * P[b,c,d] + Q[b,c,d]   (P/Q null -> identity)
+hipError_t act_apply(const float* y, float* out, const float* al, const float* de,
+                     const float* P, const float* Q, Vol vol, int C, hipStream_t s);
+// IN backward finalize: from per-(b,c,d) [sum dr, sum dr*xhat] -> dgamma, dbeta (over b),
+// k1[b,c] = mean dr, k2[b,c] = mean dr*xhat
+hipError_t in_bwd_stats(const float* sums, const float* gamma, float* dgamma, float* dbeta,
+                        float* k1, float* k2, Vol vol, int C, hipStream_t s);
+// dy = rstd*gamma*(dr - k1 - xhat*k2), dr = (g*A+Bc)*slope(y*al+de) ; may alias g
+hipError_t in_bwd_apply(const float* y, const float* g, float* dy, const float* mean,
+                        const float* rstd, const float* al, const float* de, const float* gamma,
+                        const float* A, const float* Bc, const float* k1, const float* k2,
+                        Vol vol, int C, hipStream_t s);
+
+struct GateParams {
+  const float* pe;   // sinusoidal code [16][D] (models.py:1495-1503)
+  // EnergyFiLM (models.py:1479-1512)
+  const float* fw0; const float* fb0; const float* fw2; const float* fb2;  // null if off
+  // FourierGate (models.py:1515-1544)
+  const float* mask; const float* mag;                                      // null if off
+  // SE (models.py:600-609)
+  const float* sw0; const float* sb0; const float* sw2; const float* sb2;   // null if off
+  int specse;
+};
+struct GateSaved {
+  float* t; float* bt; float* hid;    // EFiLM: t=tanh(gamma)[C][D], beta[C][D], hid_pre[32][D]
+  float* s1; float* g1; float* sg2;   // [B][D]
+  float* p; float* h; float* e;       // SE: p[B][C], h[B][Hse] (pre-ReLU), e[B][C]
+  float* P; float* Q;                 // [B][C][D] apply coefficients
+};
+int se_hidden(int C);
+// forward gate algebra from Sa[b,c,d] = sum_hw lrelu(IN(y2))
+hipError_t gates_fwd(const GateParams& gp, const float* Sa, GateSaved& sv, Vol vol, int C,
+                     float* scratch, hipStream_t s);
+struct GateGrads {
+  float* fw0; float* fb0; float* fw2; float* fb2;
+  float* mask; float* mag;
+  float* sw0; float* sb0; float* sw2; float* sb2;
+};
+// backward gate algebra: from per-(b,c,d) [sum dout, sum dout*a2] -> A,Bc with
+// da2 = dout*A + Bc, plus parameter grads.
+hipError_t gates_bwd(const GateParams& gp, const GateSaved& sv, const float* Sa,
+                     const float* Sg, GateGrads& gg, float* A, float* Bc, Vol vol, int C,
+                     float* scratch, hipStream_t s);
+size_t gates_scratch_bytes(Vol vol, int C);
+
+// ------------------------------------------------------------------ misc --
+hipError_t ncdhw_to_ndhwc(const float* x, float* y, Vol vol, int C, int ldy, hipStream_t s);
+hipError_t maxpool_fwd(const float* x, float* y, uint8_t* idx, Vol in, int C, hipStream_t s);
+// dx = dskip(ld) + unpool(dp, idx)
+hipError_t maxpool_bwd_add(const float* dp, const uint8_t* idx, const float* dskip, int ldskip,
+                           float* dx, Vol in, int C, hipStream_t s);
+hipError_t scale_by_dev(float* x, int64_t n, const float* scale, hipStream_t s);
+
+// ------------------------------------------------------------------ loss --
+size_t loss_ws_bytes(int64_t V, int K);
+// conf: K x (K+1) int64, conf[pred*(K+1) + label], column K = label outside [0,K)
+hipError_t loss_fwd(const float* logits, const int64_t* labels, int64_t V, int K, int ignore,
+                    double smooth, const int64_t* count_override, float* out4, float* dlogits,
+                    int64_t* conf, float* ws, hipStream_t s);
+hipError_t count_valid(const int64_t* labels, int64_t V, int ignore, int64_t* count,
+                       hipStream_t s);
+hipError_t confusion_only(const float* logits, const int64_t* labels, int64_t V, int K,
+                          int ignore, int64_t* conf, hipStream_t s);
+
+}  // namespace spff

@@ -1,0 +1,289 @@
+"""ctypes binding of libspff_hip.so (include/spff.h) + the torch glue around it.
+
+There is deliberately no CPU / PyTorch fallback: if the HIP library is
+missing or the tensors are not on a ROCm device, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import pathlib
+import threading
+from typing import Dict, List, Optional, Tuple
+
+import torch
+
+_LIB_PATH = pathlib.Path(__file__).resolve().parent / "_lib" / "libspff_hip.so"
+_lib = None
+_lib_lock = threading.Lock()
+
+
+class SpffError(RuntimeError):
+    pass
+
+
+class spff_cfg(ctypes.Structure):
+    _fields_ = [
+        ("batch", ctypes.c_int), ("in_ch", ctypes.c_int), ("depth", ctypes.c_int),
+        ("height", ctypes.c_int), ("width", ctypes.c_int), ("num_classes", ctypes.c_int),
+        ("base", ctypes.c_int), ("ksd", ctypes.c_int), ("use_efilm", ctypes.c_int),
+        ("use_fgate", ctypes.c_int), ("use_se", ctypes.c_int), ("use_specse", ctypes.c_int),
+        ("reserved", ctypes.c_int * 8),
+    ]
+
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_L = ctypes.c_int64
+_S = ctypes.c_size_t
+
+_SIGS = {
+    "spff_plan_create": (_I, [ctypes.POINTER(spff_cfg), ctypes.POINTER(_P)]),
+    "spff_plan_destroy": (None, [_P]),
+    "spff_last_error": (ctypes.c_char_p, []),
+    "spff_num_params": (_I, [_P]),
+    "spff_param_info": (_I, [_P, _I, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(_I),
+                             ctypes.POINTER(_L), ctypes.POINTER(_L), ctypes.POINTER(_L)]),
+    "spff_param_floats": (_L, [_P]),
+    "spff_workspace_bytes": (_S, [_P]),
+    "spff_forward": (_I, [_P, _P, _P, _P, _P, _P]),
+    "spff_backward": (_I, [_P, _P, _P, _P, _P, _P]),
+    "spff_saved_tensor": (_I, [_P, _P, ctypes.c_char_p, ctypes.POINTER(_P), ctypes.POINTER(_L),
+                               ctypes.POINTER(_I)]),
+    "spff_prof_enable": (_I, [_P, _I]),
+    "spff_prof_collect": (_I, [_P, ctypes.POINTER(ctypes.c_double), _I]),
+    "spff_loss_ws_bytes": (_S, [_L, _I]),
+    "spff_loss": (_I, [_P, _P, _L, _I, _I, ctypes.c_double, _P, _P, _P, _P, _P, _P]),
+    "spff_confusion": (_I, [_P, _P, _L, _I, _I, _P, _P]),
+    "spff_count_valid": (_I, [_P, _L, _I, _P, _P]),
+    "spff_scale": (_I, [_P, _L, _P, _P]),
+    "spff_conv3d_ws_bytes": (_S, [_I, _I, _I, _I, _I, _I, _I]),
+    "spff_conv3d_fwd": (_I, [_P, _I, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
+    "spff_conv3d_dgrad": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
+    "spff_conv3d_wgrad": (_I, [_P, _I, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
+}
+EXPORTED = tuple(_SIGS)
+
+
+def lib_path() -> pathlib.Path:
+    return pathlib.Path(os.environ.get("SPFF_LIB", str(_LIB_PATH)))
+
+
+def lib():
+    """Load libspff_hip.so (raises if it is missing -- no fallback path)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lib_lock:
+        if _lib is None:
+            p = lib_path()
+            if not p.exists():
+                raise SpffError(
+                    f"libspff_hip.so not found at {p}; build it with "
+                    f"`python spff-unet-spcct_amd/build_ext.py` (hipcc, gfx950)")
+            L = ctypes.CDLL(str(p))
+            for name, (res, args) in _SIGS.items():
+                fn = getattr(L, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = L
+    return _lib
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = lib().spff_last_error()
+        raise SpffError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream(device: torch.device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def require_device(t: torch.Tensor, what: str):
+    if not (t.is_cuda and torch.version.hip is not None):
+        raise SpffError(f"{what}: the SPFF engine runs only on a ROCm (HIP) device; got a tensor "
+                        f"on {t.device}. There is no CPU fallback.")
+
+
+class Plan:
+    """One engine plan (shape + flags) and its device workspace.
+
+    The workspace holds the saved activations of the most recent forward until
+    the matching backward (``generation`` guards against interleaving)."""
+
+    def __init__(self, batch, in_ch, depth, height, width, num_classes, base=32, ksd=3,
+                 efilm=True, fgate=True, se=True, specse=True, device=None):
+        cfg = spff_cfg()
+        cfg.batch, cfg.in_ch, cfg.depth, cfg.height, cfg.width = batch, in_ch, depth, height, width
+        cfg.num_classes, cfg.base, cfg.ksd = num_classes, base, ksd
+        cfg.use_efilm, cfg.use_fgate, cfg.use_se, cfg.use_specse = (int(bool(efilm)), int(bool(fgate)),
+                                                                    int(bool(se)), int(bool(specse)))
+        self.cfg = cfg
+        self.key = (batch, in_ch, depth, height, width, num_classes, base, ksd, bool(efilm),
+                    bool(fgate), bool(se), bool(specse))
+        L = lib()
+        h = ctypes.c_void_p()
+        check(L.spff_plan_create(ctypes.byref(cfg), ctypes.byref(h)), "spff_plan_create")
+        self._h = h
+        self.params: List[Tuple[str, Tuple[int, ...], int, int]] = []
+        for i in range(L.spff_num_params(h)):
+            name = ctypes.c_char_p()
+            nd = ctypes.c_int()
+            shape = (ctypes.c_int64 * 5)()
+            off = ctypes.c_int64()
+            n = ctypes.c_int64()
+            check(L.spff_param_info(h, i, ctypes.byref(name), ctypes.byref(nd), shape,
+                                    ctypes.byref(off), ctypes.byref(n)), "spff_param_info")
+            self.params.append((name.value.decode(), tuple(shape[k] for k in range(nd.value)),
+                                off.value, n.value))
+        self.nfloats = int(L.spff_param_floats(h))
+        self.ws_bytes = int(L.spff_workspace_bytes(h))
+        self.device = device
+        self._ws: Optional[torch.Tensor] = None
+        self.generation = 0
+
+    def __del__(self):
+        try:
+            if getattr(self, "_h", None) is not None and _lib is not None:
+                _lib.spff_plan_destroy(self._h)
+        except Exception:
+            pass
+
+    def workspace(self, device) -> torch.Tensor:
+        if self._ws is None or self._ws.device != device:
+            self._ws = torch.empty(self.ws_bytes, dtype=torch.uint8, device=device)
+        return self._ws
+
+    def forward(self, x: torch.Tensor, flat: torch.Tensor, out: Optional[torch.Tensor] = None):
+        """x [B,Cin,D,H,W] contiguous fp32 -> logits channel-last [B,D,H,W,K]."""
+        c = self.cfg
+        require_device(x, "SPFF forward")
+        if tuple(x.shape) != (c.batch, c.in_ch, c.depth, c.height, c.width):
+            raise SpffError(f"input shape {tuple(x.shape)} does not match plan")
+        x = x.contiguous()
+        if x.dtype != torch.float32:
+            raise SpffError("SPFF engine computes in fp32; got " + str(x.dtype))
+        if out is None:
+            out = torch.empty((c.batch, c.depth, c.height, c.width, c.num_classes),
+                              dtype=torch.float32, device=x.device)
+        ws = self.workspace(x.device)
+        self.generation += 1
+        check(lib().spff_forward(self._h, _ptr(x), _ptr(flat), _ptr(out), _ptr(ws),
+                                 _stream(x.device)), "spff_forward")
+        return out
+
+    def backward(self, dlogits_cl: torch.Tensor, flat: torch.Tensor,
+                 dflat: Optional[torch.Tensor] = None) -> torch.Tensor:
+        dlogits_cl = dlogits_cl.contiguous()
+        if dflat is None:
+            dflat = torch.empty(self.nfloats, dtype=torch.float32, device=dlogits_cl.device)
+        ws = self.workspace(dlogits_cl.device)
+        check(lib().spff_backward(self._h, _ptr(dlogits_cl), _ptr(flat), _ptr(dflat), _ptr(ws),
+                                  _stream(dlogits_cl.device)), "spff_backward")
+        return dflat
+
+    PROF_CLASSES = ("conv_fwd", "conv_dgrad", "conv_wgrad", "gemm")
+
+    def prof_enable(self, on: bool = True):
+        check(lib().spff_prof_enable(self._h, int(bool(on))), "spff_prof_enable")
+
+    def prof_collect(self) -> Dict[str, Tuple[float, float, int]]:
+        """{class: (total_ms, algorithmic_flops, launches)} since the last collect."""
+        n = len(self.PROF_CLASSES)
+        buf = (ctypes.c_double * (3 * n))()
+        check(lib().spff_prof_collect(self._h, buf, n), "spff_prof_collect")
+        return {c: (buf[3 * i], buf[3 * i + 1], int(buf[3 * i + 2]))
+                for i, c in enumerate(self.PROF_CLASSES)}
+
+    def saved(self, name: str) -> torch.Tensor:
+        """Copy of a saved intermediate as a channel-last [V, C] tensor (debug/tests)."""
+        ws = self._ws
+        if ws is None:
+            raise SpffError("no forward has run")
+        ptr = ctypes.c_void_p()
+        nv = ctypes.c_int64()
+        ch = ctypes.c_int()
+        check(lib().spff_saved_tensor(self._h, _ptr(ws), name.encode(), ctypes.byref(ptr),
+                                      ctypes.byref(nv), ctypes.byref(ch)), "spff_saved_tensor")
+        off = ptr.value - ws.data_ptr()
+        n = nv.value * ch.value
+        return ws[off:off + 4 * n].view(torch.float32).view(nv.value, ch.value).clone()
+
+
+_PLANS: Dict[tuple, Plan] = {}
+
+
+def get_plan(**kw) -> Plan:
+    """Plans are cached per (shape, flags, tag); the tag keeps one workspace per model."""
+    key = (kw["batch"], kw["in_ch"], kw["depth"], kw["height"], kw["width"], kw["num_classes"],
+           kw.get("base", 32), kw.get("ksd", 3), bool(kw.get("efilm", True)),
+           bool(kw.get("fgate", True)), bool(kw.get("se", True)), bool(kw.get("specse", True)),
+           kw.get("tag", ""))
+    if key not in _PLANS:
+        kk = dict(kw)
+        kk.pop("tag", None)
+        _PLANS[key] = Plan(**kk)
+    return _PLANS[key]
+
+
+# ------------------------------------------------------------------ loss ops --
+def loss_ws(device) -> torch.Tensor:
+    n = int(lib().spff_loss_ws_bytes(0, 1))
+    return torch.empty(n, dtype=torch.uint8, device=device)
+
+
+def ce_dice_forward(logits_cl: torch.Tensor, labels: torch.Tensor, K: int, ignore_index: int,
+                    smooth: float, count_override: Optional[torch.Tensor] = None):
+    """Returns (out4, dlogits_cl, conf[K, K+1])."""
+    require_device(logits_cl, "ce_plus_macro_dice_loss")
+    logits_cl = logits_cl.contiguous()
+    labels = labels.to(device=logits_cl.device, dtype=torch.int64).contiguous()
+    V = labels.numel()
+    if logits_cl.numel() != V * K:
+        raise SpffError(f"logits ({tuple(logits_cl.shape)}) / labels ({tuple(labels.shape)}) mismatch")
+    dev = logits_cl.device
+    out4 = torch.empty(4, dtype=torch.float32, device=dev)
+    dl = torch.empty_like(logits_cl)
+    conf = torch.empty(K * (K + 1), dtype=torch.int64, device=dev)
+    ws = loss_ws(dev)
+    check(lib().spff_loss(_ptr(logits_cl), _ptr(labels), V, K, int(ignore_index), float(smooth),
+                          _ptr(count_override), _ptr(out4), _ptr(dl), _ptr(conf), _ptr(ws),
+                          _stream(dev)), "spff_loss")
+    return out4, dl, conf.view(K, K + 1)
+
+
+def confusion(logits_cl: torch.Tensor, labels: torch.Tensor, K: int,
+              ignore_index: Optional[int]) -> torch.Tensor:
+    require_device(logits_cl, "per_class_metrics_3d")
+    logits_cl = logits_cl.contiguous()
+    labels = labels.to(device=logits_cl.device, dtype=torch.int64).contiguous()
+    conf = torch.empty(K * (K + 1), dtype=torch.int64, device=logits_cl.device)
+    ign = -(2 ** 31) if ignore_index is None else int(ignore_index)
+    check(lib().spff_confusion(_ptr(logits_cl), _ptr(labels), labels.numel(), K, ign, _ptr(conf),
+                               _stream(logits_cl.device)), "spff_confusion")
+    return conf.view(K, K + 1)
+
+
+def count_valid(labels: torch.Tensor, ignore_index: int) -> torch.Tensor:
+    require_device(labels, "count_valid")
+    labels = labels.to(torch.int64).contiguous()
+    cnt = torch.empty(1, dtype=torch.int64, device=labels.device)
+    check(lib().spff_count_valid(_ptr(labels), labels.numel(), int(ignore_index), _ptr(cnt),
+                                 _stream(labels.device)), "spff_count_valid")
+    return cnt
+
+
+def scale_(x: torch.Tensor, scale: torch.Tensor) -> torch.Tensor:
+    check(lib().spff_scale(_ptr(x), x.numel(), _ptr(scale.to(torch.float32).contiguous()),
+                           _stream(x.device)), "spff_scale")
+    return x
+
+
+def to_channels_last(t: torch.Tensor) -> torch.Tensor:
+    """[B,C,D,H,W] -> contiguous [B,D,H,W,C] (a free view for channels_last_3d)."""
+    return t.permute(0, 2, 3, 4, 1).contiguous()

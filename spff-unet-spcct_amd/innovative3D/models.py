@@ -1,0 +1,467 @@
+"""SPFF-UNet model family -- drop-in mirror of innovative3D/models.py whose
+forward/backward run on the MI355X HIP engine (libspff_hip.so).
+
+The module tree (names, parameter shapes, registration order, the lazily
+created and aliased FourierGate mask) is identical to the reference, so
+state_dicts / checkpoints move between the two unchanged.  The nn.Conv3d /
+nn.InstanceNorm3d / ... children are parameter containers only: their
+forward is never called.  ``UNet3D_SpectralCore.forward`` hands the input and
+one flat fp32 parameter buffer (the Parameters are views into it) to the
+engine through a torch.autograd.Function; autograd receives the engine's
+flat gradient back as per-parameter views.
+
+Reference map (models.py): _SEChannelLite 600-609, _SpectralSE 611-614,
+_conv3x3xk 616-618, _DoubleConvSpectral 620-625, UNet3D_SpectralCore 647-701,
+_LitSPCT_Base 703-712, upgrade_spct_with_novel_blocks 1416-1446,
+_DoubleConvSpectral_Novel 1448-1478, EnergyFiLM3D 1479-1512, FourierGate3D
+1515-1544, build_spct_energyfilm_fourier 1547-1555, LitSPCT_* 1558-1607,
+BaseLitModel 466-594.
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Optional, Tuple
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _engine as E
+from .config import BEST_LR, IGNORE_INDEX, NUM_CLASSES, NUM_FRAMES  # noqa: F401
+from .helpers import (LOSS_REGISTRY, ce_plus_macro_dice_loss, ce_dice_with_confusion,  # noqa: F401
+                      metrics_from_confusion, per_class_metrics_2d, per_class_metrics_3d)
+from .lightning_compat import pl
+
+# ----------------------------------------------------------------- utilities --
+
+
+def _pick_first_if_seq(x):
+    return x[0] if isinstance(x, (list, tuple)) else x
+
+
+def _canonicalize_targets_2d(lbls):
+    lbls = _pick_first_if_seq(lbls)
+    if not torch.is_tensor(lbls):
+        lbls = torch.as_tensor(lbls)
+    if lbls.ndim == 4:
+        lbls = lbls.max(dim=1).values
+    elif lbls.ndim == 2:
+        lbls = lbls.unsqueeze(0)
+    return lbls.long()
+
+
+def _canonicalize_targets_3d(lbls):
+    """(B,1,F,H,W)/(B,F,H,W,1)/(F,H,W) -> (B,F,H,W) long (models.py:69-84)."""
+    lbls = _pick_first_if_seq(lbls)
+    if not torch.is_tensor(lbls):
+        lbls = torch.as_tensor(lbls)
+    if lbls.ndim == 5 and lbls.size(1) == 1:
+        lbls = lbls[:, 0]
+    if lbls.ndim == 5 and lbls.size(-1) == 1:
+        lbls = lbls[..., 0]
+    if lbls.ndim == 3:
+        lbls = lbls.unsqueeze(0)
+    assert lbls.ndim == 4, f"Need (B,F,H,W) labels, got {tuple(lbls.shape)}"
+    return lbls.long()
+
+
+def _next_mult(n: int, m: int = 16) -> int:
+    return ((n + m - 1) // m) * m
+
+
+def _pad_to_mult_3d(x: torch.Tensor, m: int = 16):
+    """Replicate-pad D/H/W to multiples of m (models.py:109-120)."""
+    B, C, D, H, W = x.shape
+    Dn, Hn, Wn = _next_mult(D, m), _next_mult(H, m), _next_mult(W, m)
+    pd, ph, pw = Dn - D, Hn - H, Wn - W
+    if not (pd or ph or pw):
+        return x, None
+    x = F.pad(x, (pw // 2, pw - pw // 2, ph // 2, ph - ph // 2, pd // 2, pd - pd // 2),
+              mode="replicate")
+    return x, (D, H, W)
+
+
+def _center_crop_to_3d(x: torch.Tensor, orig_dhw):
+    if orig_dhw is None:
+        return x
+    D, H, W = orig_dhw
+    _, _, Dn, Hn, Wn = x.shape
+    sd, sh, sw = (Dn - D) // 2, (Hn - H) // 2, (Wn - W) // 2
+    return x[:, :, sd:sd + D, sh:sh + H, sw:sw + W]
+
+
+_pad_to_mult16_3d = lambda x, multiple=16: _pad_to_mult_3d(x, m=int(multiple))  # noqa: E731
+_center_crop_3d = _center_crop_to_3d
+
+
+def _norm3d(c: int, kind: str = "instance") -> nn.Module:
+    if not (kind or "instance").lower().startswith("inst"):
+        raise NotImplementedError("SPFF engine implements InstanceNorm3d(affine) only "
+                                  "(models.py:168-173; SPFF never selects another norm)")
+    return nn.InstanceNorm3d(c, affine=True, eps=1e-5)
+
+
+def _act(kind: str = "lrelu") -> nn.Module:
+    if not (kind or "lrelu").lower().startswith("lrel"):
+        raise NotImplementedError("SPFF engine implements LeakyReLU(0.01) only (models.py:175-181)")
+    return nn.LeakyReLU(1e-2, inplace=True)
+
+
+def _conv3x3xk(cin, cout, ksd=1, bias=False):
+    return nn.Conv3d(cin, cout, kernel_size=(ksd, 3, 3), padding=(ksd // 2, 1, 1), bias=bias)
+
+
+# ------------------------------------------------------- parameter containers --
+class _SEChannelLite(nn.Module):
+    def __init__(self, c, r=16):
+        super().__init__()
+        h = max(4, c // r)
+        self.pool = nn.AdaptiveAvgPool3d(1)
+        self.fc = nn.Sequential(nn.Conv3d(c, h, 1, bias=True), nn.ReLU(inplace=True),
+                                nn.Conv3d(h, c, 1, bias=True), nn.Sigmoid())
+
+
+class _SpectralSE(nn.Module):
+    pass
+
+
+class _DoubleConvSpectral(nn.Module):
+    def __init__(self, cin, cout, ksd=1, norm="instance", act="lrelu"):
+        super().__init__()
+        self.b1 = nn.Sequential(_conv3x3xk(cin, cout, ksd, bias=False), _norm3d(cout, norm), _act(act))
+        self.b2 = nn.Sequential(_conv3x3xk(cout, cout, ksd, bias=False), _norm3d(cout, norm), _act(act))
+
+
+class EnergyFiLM3D(nn.Module):
+    def __init__(self, channels: int, hidden: int = 32, pe_dims: int = 16):
+        super().__init__()
+        if hidden != 32 or pe_dims != 16:
+            raise NotImplementedError("engine EnergyFiLM uses hidden=32, pe_dims=16 (models.py:1485)")
+        self.channels = int(channels)
+        self.pe_dims = int(pe_dims)
+        self.mlp = nn.Sequential(nn.Conv1d(self.pe_dims, hidden, 1, bias=True), nn.ReLU(inplace=True),
+                                 nn.Conv1d(hidden, 2 * self.channels, 1, bias=True))
+
+
+class FourierGate3D(nn.Module):
+    """Same lazy mask semantics as the reference (models.py:1527-1535):
+    ``_mask``/``freq_mask`` (one tensor, two names) appear at the first forward."""
+
+    def __init__(self, learn_phase: bool = False):
+        super().__init__()
+        if learn_phase:
+            raise NotImplementedError("learn_phase=True is not on the SPFF path")
+        self.learn_phase = False
+        self.mag_scale = nn.Parameter(torch.ones(1))
+        self._mask = None
+
+    def _ensure_mask(self, Fdim: int, device):
+        L = Fdim // 2 + 1
+        if (self._mask is None) or (self._mask.shape[2] != L):
+            self._mask = nn.Parameter(torch.ones(1, 1, L, 1, 1, device=device,
+                                                 dtype=self.mag_scale.dtype))
+            self.register_parameter("freq_mask", self._mask)
+
+
+class _DoubleConvSpectral_Novel(nn.Module):
+    def __init__(self, cin, cout, ksd=1, norm="instance", act="lrelu", use_efilm: bool = False,
+                 use_fouriergate: bool = False, use_moe: bool = False, moe_K: int = 3):
+        super().__init__()
+        if use_moe:
+            # SpectralMoE3D is referenced but never defined in the reference (models.py:1464)
+            raise NotImplementedError("use_moe: SpectralMoE3D does not exist in the reference")
+        self.pre = nn.Sequential(_conv3x3xk(cin, cout, ksd, bias=False), _norm3d(cout, norm), _act(act))
+        self.body = nn.Sequential(_conv3x3xk(cout, cout, ksd, bias=False), _norm3d(cout, norm), _act(act))
+        self.efilm = EnergyFiLM3D(cout) if use_efilm else nn.Identity()
+        self.fgate = FourierGate3D() if use_fouriergate else nn.Identity()
+
+
+# --------------------------------------------------------- engine autograd op --
+class _SPFFFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, core, flat, *params):
+        plan = core._plan
+        logits_cl = plan.forward(x, flat)
+        ctx.plan = plan
+        ctx.gen = plan.generation
+        ctx.flat = flat
+        ctx.slices = [(off, n, shape) for (_name, shape, off, n) in plan.params]
+        return logits_cl.permute(0, 4, 1, 2, 3)
+
+    @staticmethod
+    def backward(ctx, g):
+        plan = ctx.plan
+        if plan.generation != ctx.gen:
+            raise E.SpffError("SPFF engine: another forward ran on this model before the backward "
+                              "of this one; the engine keeps one forward's activations per model")
+        g_cl = g.permute(0, 2, 3, 4, 1)
+        if not g_cl.is_contiguous():
+            g_cl = g_cl.contiguous()
+        dflat = plan.backward(g_cl, ctx.flat)
+        grads = [dflat[o:o + n].view(s) for (o, n, s) in ctx.slices]
+        return (None, None, None, *grads)
+
+
+# -------------------------------------------------------------------- core ----
+class UNet3D_SpectralCore(nn.Module):
+    """Depth-preserving 3-level UNet (models.py:647-701).  forward runs on the
+    HIP engine; pool/upsample act in (H,W) only, so D is arbitrary while H, W
+    must be multiples of 8."""
+
+    def __init__(self, in_channels=1, num_classes=2, base=32, ksd=3, use_se=False,
+                 use_specse=False, use_spatial=False, use_skip_gate=False, norm="instance",
+                 act="lrelu"):
+        super().__init__()
+        if use_spatial or use_skip_gate:
+            raise NotImplementedError("use_spatial/use_skip_gate are off on every SPCT registry "
+                                      "entry (config.py:417-418) and not on the engine path")
+        f = int(base)
+        P = (1, 2, 2)
+        self.in_channels, self.num_classes, self.base, self.ksd = int(in_channels), int(num_classes), f, int(ksd)
+        self.use_se, self.use_specse = bool(use_se), bool(use_specse)
+        self.enc1 = _DoubleConvSpectral(in_channels, f, ksd, norm, act)
+        self.pool1 = nn.MaxPool3d(P)
+        self.enc2 = _DoubleConvSpectral(f, 2 * f, ksd, norm, act)
+        self.pool2 = nn.MaxPool3d(P)
+        self.enc3 = _DoubleConvSpectral(2 * f, 4 * f, ksd, norm, act)
+        self.pool3 = nn.MaxPool3d(P)
+        self.bott = _DoubleConvSpectral(4 * f, 8 * f, ksd, norm, act)
+        self.up3 = nn.ConvTranspose3d(8 * f, 4 * f, kernel_size=P, stride=P)
+        self.dec3 = _DoubleConvSpectral(8 * f, 4 * f, ksd, norm, act)
+        self.up2 = nn.ConvTranspose3d(4 * f, 2 * f, kernel_size=P, stride=P)
+        self.dec2 = _DoubleConvSpectral(4 * f, 2 * f, ksd, norm, act)
+        self.up1 = nn.ConvTranspose3d(2 * f, f, kernel_size=P, stride=P)
+        self.dec1 = _DoubleConvSpectral(2 * f, f, ksd, norm, act)
+        self.out = nn.Conv3d(f, num_classes, 1)
+        self.se = nn.ModuleList([_SEChannelLite(c) if use_se else nn.Identity() for c in (f, 2 * f, 4 * f, 8 * f)])
+        self.sp = nn.ModuleList([_SpectralSE() if use_specse else nn.Identity() for _ in range(4)])
+        self.sa = nn.ModuleList([nn.Identity() for _ in range(4)])
+        self.g3 = self.g2 = self.g1 = None
+        self._plan = None
+        self._flat = None
+        self._infer_plan = None
+
+    # ---- flags derived from the (possibly upgraded) module tree ----
+    def _blocks(self):
+        return [self.enc1, self.enc2, self.enc3, self.bott, self.dec3, self.dec2, self.dec1]
+
+    def _flags(self) -> Tuple[bool, bool]:
+        kinds = set()
+        for b in self._blocks():
+            if isinstance(b, _DoubleConvSpectral_Novel):
+                kinds.add((isinstance(b.efilm, EnergyFiLM3D), isinstance(b.fgate, FourierGate3D)))
+            else:
+                kinds.add((False, False))
+        if len(kinds) != 1:
+            raise NotImplementedError("mixed block kinds; upgrade_spct_with_novel_blocks upgrades all")
+        return next(iter(kinds))
+
+    def _engine_plan(self, x: torch.Tensor, tag: str):
+        B, C, D, H, W = x.shape
+        if C != self.in_channels:
+            raise ValueError(f"expected {self.in_channels} input channels, got {C}")
+        efilm, fgate = self._flags()
+        if fgate:
+            for b in self._blocks():
+                b.fgate._ensure_mask(D, x.device)
+        return E.get_plan(batch=B, in_ch=C, depth=D, height=H, width=W,
+                          num_classes=self.num_classes, base=self.base, ksd=self.ksd,
+                          efilm=efilm, fgate=fgate, se=self.use_se, specse=self.use_specse,
+                          device=x.device, tag=f"{id(self)}:{tag}")
+
+    def _engine_params(self, plan) -> List[nn.Parameter]:
+        named = dict(self.named_parameters(remove_duplicate=False))
+        out = []
+        for name, shape, _off, _n in plan.params:
+            p = named.get(name)
+            if p is None or tuple(p.shape) != tuple(shape):
+                raise E.SpffError(f"parameter {name} {shape} missing or mis-shaped in the module")
+            out.append(p)
+        return out
+
+    def _ensure_flat(self, plan, params, device) -> torch.Tensor:
+        flat = self._flat
+        ok = flat is not None and flat.device == device and flat.numel() == plan.nfloats
+        if ok:
+            base = flat.data_ptr()
+            for p, (_name, _shape, off, _n) in zip(params, plan.params):
+                if p.data_ptr() != base + 4 * off or p.dtype != torch.float32:
+                    ok = False
+                    break
+        if ok:
+            return flat
+        flat = torch.empty(plan.nfloats, dtype=torch.float32, device=device)
+        with torch.no_grad():
+            for p, (_name, shape, off, n) in zip(params, plan.params):
+                flat[off:off + n].copy_(p.detach().reshape(-1).to(device=device, dtype=torch.float32))
+                p.data = flat[off:off + n].view(shape)
+        self._flat = flat
+        return flat
+
+    def forward(self, x):
+        x = _pick_first_if_seq(x)
+        E.require_device(x, "UNet3D_SpectralCore.forward")
+        need_grad = torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
+        plan = self._engine_plan(x, "train" if need_grad else "infer")
+        params = self._engine_params(plan)
+        flat = self._ensure_flat(plan, params, x.device)
+        if need_grad:
+            self._plan = plan
+            return _SPFFFunction.apply(x.float(), self, flat, *params)
+        logits_cl = plan.forward(x.float(), flat)
+        return logits_cl.permute(0, 4, 1, 2, 3)
+
+
+def upgrade_spct_with_novel_blocks(m: nn.Module, use_efilm: bool = True, use_fouriergate: bool = True,
+                                   use_moe: bool = False, moe_K: int = 3):
+    """models.py:1416-1446: replace every _DoubleConvSpectral by the novel block."""
+    for name, child in list(m.named_children()):
+        if isinstance(child, _DoubleConvSpectral):
+            conv1, conv2 = child.b1[0], child.b2[0]
+            new_block = _DoubleConvSpectral_Novel(int(conv1.in_channels), int(conv2.out_channels),
+                                                  ksd=int(conv1.kernel_size[0]), use_efilm=use_efilm,
+                                                  use_fouriergate=use_fouriergate, use_moe=use_moe,
+                                                  moe_K=moe_K)
+            setattr(m, name, new_block)
+        else:
+            upgrade_spct_with_novel_blocks(child, use_efilm, use_fouriergate, use_moe, moe_K)
+    return m
+
+
+def build_spct_energyfilm_fourier(num_classes=NUM_CLASSES, base=32, ksd=3, use_se=True, use_specse=True,
+                                  use_spatial=False, use_skip_gate=False, in_channels=1, **kw):
+    """models.py:1547-1555 (``in_channels`` added for the Cin=5 north-star layout)."""
+    core = UNet3D_SpectralCore(in_channels=in_channels, num_classes=num_classes, base=base, ksd=ksd,
+                               use_se=use_se, use_specse=use_specse, use_spatial=use_spatial,
+                               use_skip_gate=use_skip_gate, **kw)
+    return upgrade_spct_with_novel_blocks(core, use_efilm=True, use_fouriergate=True, use_moe=False)
+
+
+# ----------------------------------------------------------- Lightning layer --
+class BaseLitModel(pl.LightningModule):
+    """models.py:466-594.  The loss is the fused HIP ce_plus_macro_dice kernel;
+    metrics come from its confusion matrix (one host copy instead of ~100
+    .item() syncs).  The test-only sklearn PR/ROC block (models.py:510-584) is
+    host-side analytics outside the hot path and is not reproduced."""
+
+    def __init__(self, num_classes=NUM_CLASSES, lr=BEST_LR, is_3d=True, **kwargs):
+        super().__init__()
+        self.is_3d = bool(is_3d)
+        self.save_hyperparameters({"num_classes": num_classes, "lr": float(lr), "is_3d": bool(is_3d),
+                                   **kwargs})
+        self.lambda_esc = float(kwargs.get("lambda_esc", 0.0))
+        self.lambda_smooth = float(kwargs.get("lambda_smooth", 0.0))
+
+    def _normalize_input(self, x):
+        return _pick_first_if_seq(x)
+
+    def forward(self, x):
+        return self.model(self._normalize_input(x))
+
+    def compute_loss(self, logits, labels):
+        return ce_plus_macro_dice_loss(logits, labels, self.hparams.num_classes, ignore_index=IGNORE_INDEX)
+
+    def _shared_step(self, batch, prefix):
+        imgs, lbls = batch if isinstance(batch, (list, tuple)) else (batch["image"], batch["label"])
+        imgs = _pick_first_if_seq(imgs)
+        lbls = _pick_first_if_seq(lbls)
+        if not self.is_3d:
+            lbls = _canonicalize_targets_2d(lbls)
+        logits = self(imgs)
+        lbls = lbls.to(logits.device).long()
+        K = int(self.hparams.num_classes)
+        loss, conf = ce_dice_with_confusion(logits, lbls, K, IGNORE_INDEX)
+        # per_class_metrics_3d(logits, lbls, K, ignore_index=IGNORE_INDEX) from the same counts
+        (dice_list, sens_list, spec_list, macro_dice, macro_sens, macro_spec,
+         micro_dice, micro_sens, micro_spec) = metrics_from_confusion(conf.cpu().numpy(), K,
+                                                                      int(lbls.numel()))
+        self.log(f"{prefix}_loss", loss, on_step=False, on_epoch=True, prog_bar=(prefix == "train"),
+                 sync_dist=True)
+        self.log(f"{prefix}_macro_dice", macro_dice, on_step=False, on_epoch=True,
+                 prog_bar=(prefix != "test"), sync_dist=True)
+        for k, v in (("micro_dice", micro_dice), ("macro_sens", macro_sens), ("macro_spec", macro_spec),
+                     ("micro_sens", micro_sens), ("micro_spec", micro_spec)):
+            self.log(f"{prefix}_{k}", v, on_step=False, on_epoch=True, prog_bar=True, sync_dist=True)
+        for i, (d, s, sp) in enumerate(zip(dice_list, sens_list, spec_list)):
+            self.log(f"{prefix}_dice_class_{i}", d, on_step=False, on_epoch=True, prog_bar=False, sync_dist=True)
+            self.log(f"{prefix}_sens_class_{i}", s, on_step=False, on_epoch=True, prog_bar=False, sync_dist=True)
+            self.log(f"{prefix}_spec_class_{i}", sp, on_step=False, on_epoch=True, prog_bar=False, sync_dist=True)
+        return loss
+
+    def training_step(self, batch, batch_idx, dataloader_idx=0):
+        return self._shared_step(batch, "train")
+
+    def validation_step(self, batch, batch_idx, dataloader_idx=0):
+        return {"val_loss": self._shared_step(batch, "val")}
+
+    def test_step(self, batch, batch_idx):
+        return self._shared_step(batch, "test")
+
+    def configure_optimizers(self):
+        opt = torch.optim.Adam(self.parameters(), lr=self.hparams.lr)
+        sch = torch.optim.lr_scheduler.ReduceLROnPlateau(opt, mode="max", factor=0.5, patience=5)
+        return {"optimizer": opt, "lr_scheduler": {"scheduler": sch, "monitor": "val_macro_dice"}}
+
+
+class _LitSPCT_Base(BaseLitModel):
+    def __init__(self, num_classes=NUM_CLASSES, lr=BEST_LR, pad_multiple: int = 16):
+        super().__init__(num_classes=num_classes, lr=lr, is_3d=True)
+        self._pad_multiple = int(pad_multiple)
+
+    def forward(self, x):
+        x = _pick_first_if_seq(x)
+        if x.ndim == 4:
+            x = x.unsqueeze(1)
+        x_pad, orig = _pad_to_mult16_3d(x, multiple=self._pad_multiple)
+        return _center_crop_3d(self.model(x_pad), orig)
+
+
+class LitSPCT_EFiLM_FourierGate(BaseLitModel):
+    """The north-star model: registry entry "SPFF-UNet" (config.py:423-428)."""
+
+    def __init__(self, num_classes=NUM_CLASSES, lr=BEST_LR, base=32, ksd=3, use_se=True, use_specse=True,
+                 use_spatial=False, use_skip_gate=False, **kw):
+        super().__init__(num_classes=num_classes, lr=lr, is_3d=True)
+        self.model = build_spct_energyfilm_fourier(num_classes=num_classes, base=base, ksd=ksd,
+                                                   use_se=use_se, use_specse=use_specse,
+                                                   use_spatial=use_spatial, use_skip_gate=use_skip_gate, **kw)
+
+
+class LitSPCT_EnergyFiLM(BaseLitModel):
+    def __init__(self, num_classes=NUM_CLASSES, lr=BEST_LR, base=32, ksd=3, use_se=True, use_specse=True,
+                 use_spatial=False, use_skip_gate=False, in_channels=1, **kw):
+        super().__init__(num_classes=num_classes, lr=lr, is_3d=True, **kw)
+        core = UNet3D_SpectralCore(in_channels=in_channels, num_classes=num_classes, base=base, ksd=ksd,
+                                   use_se=use_se, use_specse=use_specse, use_spatial=use_spatial,
+                                   use_skip_gate=use_skip_gate)
+        self.model = upgrade_spct_with_novel_blocks(core, use_efilm=True, use_fouriergate=False)
+
+
+class LitSPCT_FourierGate(BaseLitModel):
+    def __init__(self, num_classes=NUM_CLASSES, lr=BEST_LR, base=32, ksd=3, use_se=True, use_specse=True,
+                 use_spatial=False, use_skip_gate=False, in_channels=1, **kw):
+        super().__init__(num_classes=num_classes, lr=lr, is_3d=True, **kw)
+        core = UNet3D_SpectralCore(in_channels=in_channels, num_classes=num_classes, base=base, ksd=ksd,
+                                   use_se=use_se, use_specse=use_specse, use_spatial=use_spatial,
+                                   use_skip_gate=use_skip_gate)
+        self.model = upgrade_spct_with_novel_blocks(core, use_efilm=False, use_fouriergate=True)
+
+
+class LitSPCT_SEspec(_LitSPCT_Base):
+    """Channel-SE + Spectral-SE at all stages (models.py:1585-1592)."""
+
+    def __init__(self, num_classes=NUM_CLASSES, lr=BEST_LR, base=32, pad_multiple=16):
+        super().__init__(num_classes=num_classes, lr=lr, pad_multiple=pad_multiple)
+        self.model = UNet3D_SpectralCore(in_channels=1, num_classes=num_classes, base=base, ksd=3,
+                                         use_se=True, use_specse=True, use_spatial=False,
+                                         use_skip_gate=False)
+
+
+class LitSPCT_ControlUNet(BaseLitModel):
+    def __init__(self, num_classes=NUM_CLASSES, lr=BEST_LR, base=32, ksd=3, use_se=False, use_specse=False,
+                 use_spatial=False, use_skip_gate=False, in_channels=1, **kw):
+        super().__init__(num_classes=num_classes, lr=lr, is_3d=True, **kw)
+        self.model = UNet3D_SpectralCore(in_channels=in_channels, num_classes=num_classes, base=base,
+                                         ksd=ksd, use_se=use_se, use_specse=use_specse,
+                                         use_spatial=use_spatial, use_skip_gate=use_skip_gate)

@@ -1,0 +1,63 @@
+"""CPU-only checks of the C-ABI library and the host-side mirror (no GPU calls)."""
+import ctypes
+import pathlib
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from _golden import cfg_of, fixture_names, load
+from innovative3D import _engine as E
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+
+
+def _header_symbols():
+    src = (ROOT / "include" / "spff.h").read_text()
+    return sorted(set(re.findall(r"\b(spff_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_header_symbol():
+    L = E.lib()
+    syms = _header_symbols()
+    assert len(syms) >= 15
+    for s in syms:
+        assert hasattr(L, s), s
+    assert set(syms) == set(E.EXPORTED)
+
+
+def test_plan_layout_matches_reference_state_dict():
+    for name in fixture_names():
+        d = load(name)
+        m = d["meta"]
+        cfg = cfg_of(m)
+        x = d["x"]
+        B, Cin, D, H, W = x.shape
+        plan = E.Plan(B, Cin, D, H, W, cfg.num_classes, base=cfg.base, ksd=3, efilm=cfg.efilm,
+                      fgate=cfg.fgate, se=cfg.se, specse=cfg.specse)
+        prefix = "model." if m.get("lit") else ""
+        ref = {k[len(prefix):]: tuple(v) for k, v in d["state_shapes"].items()}
+        ref_order = [k for k in ref if not k.endswith("._mask")]
+        assert [p[0] for p in plan.params] == ref_order, name
+        for pname, shape, off, n in plan.params:
+            assert tuple(shape) == ref[pname]
+            assert n == int(np.prod(shape))
+        offs = [p[2] for p in plan.params]
+        assert offs == sorted(offs) and plan.nfloats == offs[-1] + plan.params[-1][3]
+
+
+def test_plan_rejects_bad_shapes():
+    with pytest.raises(E.SpffError):
+        E.Plan(1, 1, 5, 60, 64, 13)   # H not a multiple of 8
+    with pytest.raises(E.SpffError):
+        E.Plan(1, 1, 5, 64, 64, 40)   # K > 32
+    with pytest.raises(E.SpffError):
+        E.Plan(1, 1, 5, 64, 64, 13, base=24)
+
+
+def test_workspace_size_headline_config_fits_hbm():
+    p = E.Plan(2, 5, 128, 128, 128, 13)
+    assert 5e9 < p.ws_bytes < 40e9
+    # 5 491 284 (registry, Cin=1) + 27*32*4 (Cin=5 first conv) + 7 lazy masks of L=65
+    assert p.nfloats == 5491284 + 27 * 32 * 4 + 7 * 65

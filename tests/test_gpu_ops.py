@@ -1,0 +1,108 @@
+"""Per-op parity of the HIP kernels vs the CPU oracle (torch-CPU fp32 ops that
+the reference itself calls).  Marked gpu: run on the MI355X box."""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from innovative3D import _engine as E
+import innovative3D.helpers as Hh
+from oracle import spff_oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _cl(t):  # [B,C,D,H,W] -> [B,D,H,W,C]
+    return t.permute(0, 2, 3, 4, 1).contiguous()
+
+
+def _ncdhw(t):  # [B,D,H,W,C] -> [B,C,D,H,W]
+    return t.permute(0, 4, 1, 2, 3).contiguous()
+
+
+CONV_CASES = [
+    # B, D, H, W, cin, cout, ksd
+    (2, 5, 16, 32, 8, 32, 3),
+    (1, 3, 8, 16, 5, 32, 3),     # first layer, Cin=5 padded to ld 8
+    (1, 4, 16, 16, 32, 64, 3),
+    (1, 2, 8, 8, 64, 128, 3),
+    (1, 3, 8, 16, 16, 8, 3),     # base-8 nets: Cout < 32
+    (2, 4, 8, 16, 32, 32, 1),    # ksd = 1
+    (1, 5, 24, 40, 16, 16, 3),   # ragged tiles (H, W not multiples of the tile)
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv3d_fwd_dgrad_wgrad(case):
+    B, D, H, W, cin, cout, ksd = case
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(B, cin, D, H, W, generator=g)
+    w = torch.randn(cout, cin, ksd, 3, 3, generator=g) / math.sqrt(cin * ksd * 9)
+    dy = torch.randn(B, cout, D, H, W, generator=g)
+    xr = x.clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    y = F.conv3d(xr, wr, None, padding=(ksd // 2, 1, 1))
+    y.backward(dy)
+    ldx = (cin + 7) // 8 * 8
+    xcl = torch.zeros(B, D, H, W, ldx)
+    xcl[..., :cin] = _cl(x)
+    xcl = xcl.to(DEV)
+    wd = w.to(DEV)
+    ws = torch.empty(E.lib().spff_conv3d_ws_bytes(B, D, H, W, cin, cout, ksd), dtype=torch.uint8,
+                     device=DEV)
+    L, p, st = E.lib(), E._ptr, E._stream(torch.device(DEV))
+    yg = torch.empty(B, D, H, W, cout, device=DEV)
+    E.check(L.spff_conv3d_fwd(p(xcl), ldx, p(wd), p(yg), B, D, H, W, cin, cout, ksd, p(ws), st), "fwd")
+    dyg = _cl(dy).to(DEV)
+    dwg = torch.empty_like(wd)
+    E.check(L.spff_conv3d_wgrad(p(xcl), ldx, p(dyg), p(dwg), B, D, H, W, cin, cout, ksd, p(ws), st),
+            "wgrad")
+    torch.cuda.synchronize()
+    ref = _cl(y.detach())
+    assert float((yg.cpu() - ref).abs().max()) <= 2e-5 * float(ref.abs().max()) + 1e-6
+    assert float((dwg.cpu() - wr.grad).abs().max()) <= 2e-5 * float(wr.grad.abs().max()) + 1e-6
+    if cin % 4 == 0:
+        dxg = torch.empty(B, D, H, W, cin, device=DEV)
+        E.check(L.spff_conv3d_dgrad(p(dyg), p(wd), p(dxg), B, D, H, W, cin, cout, ksd, p(ws), st), "dgrad")
+        torch.cuda.synchronize()
+        refx = _cl(xr.grad)
+        assert float((dxg.cpu() - refx).abs().max()) <= 2e-5 * float(refx.abs().max()) + 1e-6
+
+
+@pytest.mark.parametrize("K,shape", [(13, (2, 5, 16, 16)), (9, (1, 16, 32, 32)), (2, (1, 3, 8, 8))])
+def test_loss_matches_oracle(K, shape):
+    g = torch.Generator().manual_seed(K)
+    logits = torch.randn(shape[0], K, *shape[1:], generator=g) * 2
+    y = torch.randint(0, K, shape, generator=g)
+    y[torch.rand(shape, generator=g) < 0.05] = 255
+    if K > 3:
+        y[y == 2] = 3  # an absent class
+    lr = logits.clone().requires_grad_(True)
+    loss_ref, ce_ref, dice_ref = O.ce_plus_macro_dice(lr, y, K)
+    loss_ref.backward()
+    lg = logits.to(DEV).requires_grad_(True)
+    loss, conf = Hh.ce_dice_with_confusion(lg, y.to(DEV), K, 255)
+    loss.backward()
+    torch.cuda.synchronize()
+    assert math.isclose(float(loss), float(loss_ref), rel_tol=2e-6)
+    np.testing.assert_array_equal(conf.cpu().numpy()[:, :K], O.confusion(logits, y, K, 255))
+    assert float((lg.grad.cpu() - lr.grad).abs().max()) <= 1e-7
+    # standalone helpers
+    assert math.isclose(Hh.macro_dice_loss(lg, y.to(DEV), K), dice_ref, abs_tol=1e-12)
+    met = Hh.per_class_metrics_3d(lg.detach(), y.to(DEV), K, ignore_index=255)
+    ref = O.per_class_metrics_3d(logits, y, K, ignore_index=255)
+    np.testing.assert_allclose(np.array(met[0]), np.array(ref[0]), rtol=1e-12, equal_nan=True)
+    np.testing.assert_allclose(np.array(met[3:]), np.array(ref[3:]), rtol=1e-12, equal_nan=True)
+
+
+def test_loss_all_ignored_is_nan_with_zero_grad():
+    K = 4
+    lg = torch.randn(1, K, 2, 4, 4, device=DEV, requires_grad=True)
+    y = torch.full((1, 2, 4, 4), 255, dtype=torch.long, device=DEV)
+    loss = Hh.ce_plus_macro_dice_loss(lg, y, K)
+    loss.backward()
+    assert math.isnan(float(loss))
+    assert float(lg.grad.abs().max()) == 0.0

@@ -1,0 +1,158 @@
+"""Whole-network parity of the HIP engine against the golden fixtures produced
+by the reference itself (tests/golden/make_golden.py), plus stage-wise
+localisation against the CPU oracle.  Marked gpu.
+
+Tolerances (north star, BASELINE.json): logits within 1e-3 of the reference
+PyTorch-CPU forward, identical argmax (voxels whose reference top-2 margin is
+below 2 x the observed max |dlogit| are reported as near-ties, not failures);
+gradients within 1e-3 of max|g| per tensor; loss within 1e-5 relative."""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from _golden import cfg_of, fixture_names, load, state_of
+from oracle import spff_oracle as O
+import innovative3D.models as M
+import innovative3D.helpers as Hh
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def build_core(meta):
+    fl = {k: meta.get(k, True) for k in ("efilm", "fgate", "se", "specse")}
+    core = M.UNet3D_SpectralCore(in_channels=meta["in_ch"], num_classes=meta["K"], base=meta["base"],
+                                 ksd=3, use_se=fl["se"], use_specse=fl["specse"])
+    if fl["efilm"] or fl["fgate"]:
+        core = M.upgrade_spct_with_novel_blocks(core, use_efilm=fl["efilm"], use_fouriergate=fl["fgate"])
+    return core
+
+
+def load_core(d):
+    meta = d["meta"]
+    core = build_core(meta)
+    D = d["x"].shape[2]
+    for b in core._blocks():
+        if isinstance(getattr(b, "fgate", None), M.FourierGate3D):
+            b.fgate._ensure_mask(D, "cpu")
+    st = state_of(d)
+    core.load_state_dict({k: torch.from_numpy(v) for k, v in st.items()}, strict=True)
+    return core.to(DEV)
+
+
+def near_tie_mask(ref_logits, tol):
+    top2 = np.sort(ref_logits, axis=1)[:, -2:]
+    return (top2[:, 1] - top2[:, 0]) < tol
+
+
+@pytest.mark.parametrize("name", fixture_names())
+def test_network_matches_reference(name):
+    d = load(name)
+    meta = d["meta"]
+    K = meta["K"]
+    core = load_core(d)
+    x = torch.from_numpy(d["x"]).to(DEV)
+    y = torch.from_numpy(d["labels"]).to(DEV)
+    logits = core(x)
+    loss, conf = Hh.ce_dice_with_confusion(logits, y, K, 255)
+    loss.backward()
+    torch.cuda.synchronize()
+    lg = logits.detach().cpu().numpy()
+    ref = d["logits"]
+    err = float(np.abs(lg - ref).max())
+    print(f"{name}: max|dlogit| = {err:.3e}  loss {float(loss):.7f} vs {float(d['loss']):.7f}")
+    assert err <= 1e-3
+    am, am_ref = lg.argmax(1), ref.argmax(1)
+    flips = am != am_ref
+    if flips.any():
+        ties = near_tie_mask(ref, 2 * err)
+        assert not (flips & ~ties).any(), f"{int(flips.sum())} argmax flips outside near-ties"
+    assert math.isclose(float(loss), float(d["loss"]), rel_tol=1e-5)
+    met = M.metrics_from_confusion(conf.cpu().numpy(), K, int(y.numel()))
+    if not flips.any():
+        np.testing.assert_allclose(np.array(met[0]), d["met_dice"], rtol=1e-12, equal_nan=True)
+        np.testing.assert_allclose(np.array(met[3:]), d["met_scalars"], rtol=1e-12, equal_nan=True)
+    prefix = "model." if meta.get("lit") else ""
+    named = dict(core.named_parameters(remove_duplicate=False))
+    worst = 0.0
+    for k in d["param_names"]:
+        k = str(k)
+        kk = k[len(prefix):].replace("._mask", ".freq_mask")
+        g = named[kk].grad
+        assert g is not None, kk
+        g = g.detach().cpu().numpy()
+        if "grad/" + k in d:
+            r = d["grad/" + k]
+            scale = max(float(np.abs(r).max()), 1e-8)
+            rel = float(np.abs(g - r).max()) / scale
+        else:
+            flat = g.reshape(-1)
+            r = d["gradhead/" + k]
+            scale = max(float(np.abs(r).max()), 1e-8)
+            rel = max(float(np.abs(flat[:64] - r).max()), float(np.abs(flat[-64:] - d["gradtail/" + k]).max())) / scale
+            nrm = float(np.sqrt((flat.astype(np.float64) ** 2).sum()))
+            assert math.isclose(nrm, float(d["gradsum/" + k][1]), rel_tol=1e-3, abs_tol=1e-9), kk
+        worst = max(worst, rel)
+        assert rel <= 1e-3, f"{kk}: rel grad err {rel:.3e}"
+    print(f"{name}: worst rel grad err {worst:.3e}")
+
+
+def _oracle_stages(P, x, cfg):
+    """Intermediates of the oracle forward (channel-first), keyed like spff_saved_tensor."""
+    S = {}
+
+    def blk(name, inp):
+        a, b = ("pre", "body") if cfg.novel else ("b1", "b2")
+        y1 = F.conv3d(inp, P[f"{name}.{a}.0.weight"], None, padding=(1, 1, 1))
+        a1 = F.leaky_relu(F.instance_norm(y1, weight=P[f"{name}.{a}.1.weight"],
+                                          bias=P[f"{name}.{a}.1.bias"], eps=1e-5), 0.01)
+        y2 = F.conv3d(a1, P[f"{name}.{b}.0.weight"], None, padding=(1, 1, 1))
+        z = F.leaky_relu(F.instance_norm(y2, weight=P[f"{name}.{b}.1.weight"],
+                                         bias=P[f"{name}.{b}.1.bias"], eps=1e-5), 0.01)
+        if cfg.novel and cfg.efilm:
+            z = O.energy_film(P, name + ".efilm", z)
+        if cfg.novel and cfg.fgate:
+            z = O.fourier_gate(P, name + ".fgate", z)
+        S[name + ".y1"], S[name + ".a1"], S[name + ".y2"] = y1, a1, y2
+        return z
+
+    pool = lambda t: F.max_pool3d(t, (1, 2, 2))  # noqa: E731
+    up = lambda t, n: F.conv_transpose3d(t, P[n + ".weight"], P[n + ".bias"], stride=(1, 2, 2))  # noqa: E731
+    e1 = O._post(P, blk("enc1", x), 0, cfg); S["enc1.out"] = e1; S["pool1"] = pool(e1)
+    e2 = O._post(P, blk("enc2", S["pool1"]), 1, cfg); S["enc2.out"] = e2; S["pool2"] = pool(e2)
+    e3 = O._post(P, blk("enc3", S["pool2"]), 2, cfg); S["enc3.out"] = e3; S["pool3"] = pool(e3)
+    b = O._post(P, blk("bott", S["pool3"]), 3, cfg); S["bott.out"] = b
+    S["up3"] = up(b, "up3"); d3 = blk("dec3", torch.cat([S["up3"], e3], 1)); S["dec3.out"] = d3
+    S["up2"] = up(d3, "up2"); d2 = blk("dec2", torch.cat([S["up2"], e2], 1)); S["dec2.out"] = d2
+    S["up1"] = up(d2, "up1"); d1 = blk("dec1", torch.cat([S["up1"], e1], 1)); S["dec1.out"] = d1
+    return S
+
+
+@pytest.mark.parametrize("name", ["fx2_ns_base8", "fx3_fgate_even_b2", "fx3b_fgate_odd_b2"])
+def test_stagewise_forward(name):
+    """Localises a forward mismatch to the first diverging stage."""
+    d = load(name)
+    cfg = cfg_of(d["meta"])
+    P = O.params_from_state(state_of(d), requires_grad=False)
+    x = torch.from_numpy(d["x"])
+    with torch.no_grad():
+        S = _oracle_stages(P, x, cfg)
+    core = load_core(d)
+    core(x.to(DEV)).sum().backward()  # grad-mode forward -> training plan holds the stages
+    plan = core._plan
+    order = ["enc1.y1", "enc1.a1", "enc1.y2", "enc1.out", "pool1", "enc2.out", "pool2", "enc3.out",
+             "pool3", "bott.y1", "bott.out", "up3", "dec3.y1", "dec3.out", "up2", "dec2.out", "up1",
+             "dec1.y1", "dec1.out"]
+    report = []
+    for k in order:
+        r = S[k]
+        mine = plan.saved(k).numpy()
+        rr = r.permute(0, 2, 3, 4, 1).reshape(-1, r.shape[1]).numpy()
+        e = float(np.abs(mine - rr).max()) / max(1e-6, float(np.abs(rr).max()))
+        report.append((k, e))
+    print("\n".join(f"  {k:10s} rel {e:.2e}" for k, e in report))
+    bad = [(k, e) for k, e in report if e > 1e-4]
+    assert not bad, f"first diverging stage: {bad[0]}"
