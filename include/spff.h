@@ -71,6 +71,9 @@ int spff_backward(spff_plan* plan, const float* dlogits, const float* params, fl
 int spff_saved_tensor(const spff_plan* plan, void* workspace, const char* name,
                       const float** ptr, int64_t* nvox, int* channels);
 
+/* debug knobs (tests): key 0 = stop the backward after N decoder blocks (-1 off) */
+int spff_debug_set(spff_plan* plan, int key, int value);
+
 /* optional HIP-event timing of the MFMA kernels on the plan's stream (bench.py):
  * classes 0 = conv3d fwd, 1 = conv3d dgrad (same kernel), 2 = conv3d wgrad,
  * 3 = ConvTranspose / 1x1 head GEMMs.  collect() syncs on the recorded events

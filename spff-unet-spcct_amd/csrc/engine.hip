@@ -114,6 +114,7 @@ struct spff_plan {
   std::vector<ProfRec> prof;
   size_t prof_n = 0;
   bool prof_on = false;
+  int dbg_stop = -1;  // debug: stop backward after this many blocks (-1 = off)
   // per call
   char* ws = nullptr;
   const float* prm = nullptr;
@@ -558,6 +559,7 @@ int backward(spff_plan* p, const float* dl) {
     const int lvl = d.lvl;
     Dst2 dx{p->F(p->G_dx), p->F(p->dskip[lvl]), C, C, C};
     CK(bwd_block(p, d, p->F(p->G_out), &dx, src2(p->F(U.out), p->F(B[lvl].out), C)));
+    if (p->dbg_stop == k + 1) return SPFF_OK;
     const float* upin = (ui == 0) ? p->F(B[3].out) : p->F(B[bi - 1].out);
     const Vol& low = p->vol[U.lvl_low];
     PROF(p, 3, 2.0 * nvox(low) * U.Cin * 4.0 * U.Cout,
@@ -669,6 +671,11 @@ int spff_saved_tensor(const spff_plan* p, void* ws, const char* name, const floa
     return SPFF_OK;
   };
   if (n == "x_cl") return ret(p->x_cl, p->vol[0], p->ldx);
+  if (n.rfind("grad.", 0) == 0) {  // backward scratch, sized as level-0 [V0][f]
+    const size_t off = n == "grad.out" ? p->G_out : n == "grad.dy2" ? p->G_dy2 :
+                       n == "grad.da1" ? p->G_da1 : n == "grad.dx" ? p->G_dx : 0;
+    if (off) return ret(off, p->vol[0], p->f);
+  }
   for (int i = 0; i < 7; ++i) {
     const Blk& b = p->blk[i];
     const Vol& v = p->vol[b.lvl];
@@ -683,6 +690,12 @@ int spff_saved_tensor(const spff_plan* p, void* ws, const char* name, const floa
   for (int u = 0; u < 3; ++u)
     if (n == upn[u]) return ret(p->up[u].out, p->vol[p->up[u].lvl_low - 1], p->up[u].Cout);
   return fail(SPFF_EINVAL, "unknown saved tensor " + n);
+}
+
+int spff_debug_set(spff_plan* p, int key, int value) {
+  if (!p) return fail(SPFF_EINVAL, "null plan");
+  if (key == 0) p->dbg_stop = value;
+  return SPFF_OK;
 }
 
 int spff_prof_enable(spff_plan* p, int on) {

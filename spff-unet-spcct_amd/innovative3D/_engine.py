@@ -50,6 +50,7 @@ _SIGS = {
     "spff_backward": (_I, [_P, _P, _P, _P, _P, _P]),
     "spff_saved_tensor": (_I, [_P, _P, ctypes.c_char_p, ctypes.POINTER(_P), ctypes.POINTER(_L),
                                ctypes.POINTER(_I)]),
+    "spff_debug_set": (_I, [_P, _I, _I]),
     "spff_prof_enable": (_I, [_P, _I]),
     "spff_prof_collect": (_I, [_P, ctypes.POINTER(ctypes.c_double), _I]),
     "spff_loss_ws_bytes": (_S, [_L, _I]),
