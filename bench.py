@@ -102,35 +102,17 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=device)
 
-    import innovative3D.helpers as Hh
-    from innovative3D import _engine as E
+    from innovative3D.distributed import DataParallelSPFF
     from innovative3D.synthetic import synthetic_batch
 
     B, S, K = args.batch, args.size, args.classes
     core, st = build_model(K, args.base, args.in_ch, S, device)
     x, y = synthetic_batch(B, args.in_ch, S, S, S, K, ignore_frac=0.01, seed=1000 + rank,
                            device=device)
-    params = [p for p in core.parameters()]
+    dp = DataParallelSPFF(core, K, 255)
 
     def step():
-        for p in params:
-            p.grad = None
-        logits = core(x)
-        cnt = None
-        if world > 1:
-            cnt = E.count_valid(y, 255)
-            dist.all_reduce(cnt)
-        loss, _conf = Hh.ce_dice_with_confusion(logits, y, K, 255, count_override=cnt)
-        loss.backward()
-        if world > 1:
-            gs = [p.grad for p in params if p.grad is not None]
-            flat = torch.cat([g.reshape(-1) for g in gs])
-            dist.all_reduce(flat)
-            o = 0
-            for g in gs:
-                n = g.numel()
-                g.copy_(flat[o:o + n].view_as(g))
-                o += n
+        loss, _conf = dp.step(x, y)
         return loss
 
     for _ in range(args.warmup):
