@@ -13,10 +13,12 @@
 //    re-fetched from L2.  MFMA is v_mfma_f32_32x32x2_f32 (exact fp32, k-ordered
 //    fma chain) -- the parity-safe precision.
 //  * dgrad = the same kernel on dy with the flipped / transposed weight pack.
-//  * wgrad: rows = (tap, ci) pairs, cols = co, reduction over voxels; each
-//    workgroup owns all taps x 16 ci x 32 co and a contiguous range of
-//    1x8x16 voxel tiles, writes an fp32 partial slab; a second kernel sums the
-//    slabs in a fixed order (deterministic, no float atomics).
+//  * wgrad: per tap an MFMA block (rows = 32 ci, cols = 32 co, reduction over
+//    voxels); a workgroup owns all taps of a 32x32 (ci, co) tile and a
+//    contiguous range of 1x8x16 voxel tiles, register-prefetching the next
+//    tile while computing the current one; it writes an fp32 partial slab and
+//    a second kernel sums the slabs in a fixed order (deterministic, no float
+//    atomics).
 #include "spff_internal.h"
 
 namespace spff {
@@ -198,8 +200,17 @@ hipError_t conv3d_fwd(const Src2& x, const float* wt, const Dst2& y, Vol vol, in
 }
 
 // ------------------------------------------------------------------ wgrad --
+// dW[co][ci][tap] = sum_v x[v + off(tap)][ci] * dy[v][co].
+// One workgroup (4 waves, 1 per SIMD) owns ALL taps x 32 ci x 32 co: MFMA block
+// j of wave w is tap w + 4j (7/7/7/6 blocks for 27 taps), row = ci, col = co,
+// reduction = voxels (2 per MFMA k-step).  It walks a contiguous range of
+// 1 x 8 x 16 voxel tiles; the next tile's halo (3 x 10 x 18 x 32 ch) and dy tile
+// (128 x 32) are prefetched into registers while the current tile is computed
+// out of LDS, then written to LDS after the compute (loads never exposed).
+// Each workgroup writes one fp32 partial slab; k_wgrad_reduce sums the slabs
+// in a fixed order (deterministic).
 namespace {
-constexpr int WG_CI = 16, WG_CO = 32, WG_TH = 8, WG_TW = 16, WG_TV = WG_TH * WG_TW;
+constexpr int WG_CI = 32, WG_CO = 32, WG_TH = 8, WG_TW = 16, WG_TV = WG_TH * WG_TW;
 struct WgradPlan {
   int kpad, npad, tilesD, tilesH, tilesW, ntiles, nsplit, tps;
 };
@@ -212,8 +223,9 @@ WgradPlan wgrad_plan(Vol vol, int Cin, int Cout) {
   p.tilesW = cdiv(vol.W, WG_TW);
   p.ntiles = vol.B * p.tilesD * p.tilesH * p.tilesW;
   const int nout = (p.kpad / WG_CI) * (p.npad / WG_CO);
-  int nsplit = std::max(1, cdiv(2048, nout));
-  nsplit = std::min(nsplit, std::max(1, p.ntiles / 2));
+  // one workgroup per CU: aim at 2 rounds of 256 CUs, >= 4 tiles per workgroup
+  int nsplit = std::max(1, cdiv(512, nout));
+  nsplit = std::min(nsplit, std::max(1, p.ntiles / 4));
   p.tps = cdiv(p.ntiles, nsplit);
   p.nsplit = cdiv(p.ntiles, p.tps);
   return p;
@@ -221,44 +233,36 @@ WgradPlan wgrad_plan(Vol vol, int Cin, int Cout) {
 }  // namespace
 
 template <int KD>
-__global__ __launch_bounds__(256) void k_conv3d_wgrad(Src2 x, const float* __restrict__ dy,
-                                                      int lddy, float* __restrict__ part, Vol vol,
-                                                      int Cin, int kpad, int Cout, int npad,
-                                                      int tilesH, int tilesW, int ntiles,
-                                                      int tps) {
+__global__ __launch_bounds__(256, 1) void k_conv3d_wgrad(Src2 x, const float* __restrict__ dy,
+                                                         int lddy, float* __restrict__ part,
+                                                         Vol vol, int Cin, int kpad, int Cout,
+                                                         int npad, int tilesH, int tilesW,
+                                                         int ntiles, int tps) {
   constexpr int HD = KD, HH = WG_TH + 2, HWD = WG_TW + 2;
-  constexpr int P = WG_CI + 1;
-  constexpr int XS = HD * HH * HWD * P;
+  constexpr int P = WG_CI + 1;  // odd pitch: a wave's 32 ci of one voxel hit 32 banks
+  constexpr int NPOS = HD * HH * HWD;
+  constexpr int XS = NPOS * P;
   constexpr int T = KD * 9;
-  constexpr int R = T * WG_CI;
-  constexpr int NBLK = (R + 31) / 32;
-  constexpr int NJ = (NBLK + 3) / 4;
-  __shared__ float lds[XS + WG_TV * WG_CO + 4];
+  constexpr int NJ = (T + 3) / 4;
+  constexpr int HQ = WG_CI / 4;                     // float4 per halo voxel
+  constexpr int NH = (NPOS * HQ + 255) / 256;        // halo float4 per thread
+  constexpr int NY = WG_TV * (WG_CO / 4) / 256;      // dy float4 per thread (= 4)
+  __shared__ float lds[XS + WG_TV * WG_CO];
   float* Xs = lds;
   float* Ys = lds + XS;
-  const int ZERO = XS + WG_TV * WG_CO;  // index of a 0.0 slot
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int khalf = lane >> 5, l32 = lane & 31;
   const int split = blockIdx.x, ci0 = blockIdx.y * WG_CI, co0 = blockIdx.z * WG_CO;
   const int D = vol.D, H = vol.H, W = vol.W;
-  if (threadIdx.x == 0) lds[ZERO] = 0.f;
 
-  // per-lane row -> (tap, ci) lds offset; invalid rows read the zero slot.
-  int off[NJ], mul[NJ];
+  int off[NJ];
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
-    const int rb = wave + 4 * j;
-    const int rr = rb * 32 + l32;
-    if (rb < NBLK && rr < R) {
-      const int tap = rr / WG_CI, ci = rr % WG_CI;
-      const int kd = tap / 9, kh = (tap / 3) % 3, kw = tap % 3;
-      off[j] = ((kd * HH + kh) * HWD + kw) * P + ci;
-      mul[j] = P;
-    } else {
-      off[j] = ZERO;
-      mul[j] = 0;
-    }
+    const int tap = wave + 4 * j;
+    const int t = tap < T ? tap : 0;
+    const int kd = t / 9, kh = (t / 3) % 3, kw = t % 3;
+    off[j] = ((kd * HH + kh) * HWD + kw) * P + l32;
   }
   f32x16 acc[NJ];
 #pragma unroll
@@ -266,70 +270,112 @@ __global__ __launch_bounds__(256) void k_conv3d_wgrad(Src2 x, const float* __res
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
 
-  const int tbeg = split * tps;
-  const int tend = min(ntiles, tbeg + tps);
-  for (int tile = tbeg; tile < tend; ++tile) {
+  float4 hreg[NH], yreg[NY];
+  auto fetch = [&](int tile) {
     int t = tile;
     const int twi = t % tilesW; t /= tilesW;
     const int thi = t % tilesH; t /= tilesH;
     const int d0 = t % D;
     const int b = t / D;
     const int h0 = thi * WG_TH, w0 = twi * WG_TW;
-    __syncthreads();
-    // halo of x: HD x 10 x 18 voxels x 16 channels
-    for (int i = threadIdx.x; i < HD * HH * HWD * (WG_CI / 4); i += 256) {
-      const int q = i % (WG_CI / 4), pos = i / (WG_CI / 4);
-      const int hw = pos % HWD, t2 = pos / HWD, hh = t2 % HH, hd = t2 / HH;
-      const int gd = d0 + hd - KD / 2, gh = h0 + hh - 1, gw = w0 + hw - 1;
-      const int c = ci0 + 4 * q;
+#pragma unroll
+    for (int k = 0; k < NH; ++k) {
+      const int i = threadIdx.x + 256 * k;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if ((unsigned)gd < (unsigned)D && (unsigned)gh < (unsigned)H &&
-          (unsigned)gw < (unsigned)W && c < Cin) {
-        const int64_t vox = (((int64_t)b * D + gd) * H + gh) * W + gw;
-        const float* p = c < x.split ? x.p0 + vox * x.ld0 + c : x.p1 + vox * x.ld1 + (c - x.split);
-        v = *reinterpret_cast<const float4*>(p);
+      if (i < NPOS * HQ) {
+        const int q = i % HQ, pos = i / HQ;
+        const int hw = pos % HWD, t2 = pos / HWD, hh = t2 % HH, hd = t2 / HH;
+        const int gd = d0 + hd - KD / 2, gh = h0 + hh - 1, gw = w0 + hw - 1;
+        const int c = ci0 + 4 * q;
+        if ((unsigned)gd < (unsigned)D && (unsigned)gh < (unsigned)H &&
+            (unsigned)gw < (unsigned)W && c < Cin) {
+          const int64_t vox = (((int64_t)b * D + gd) * H + gh) * W + gw;
+          const float* p =
+              c < x.split ? x.p0 + vox * x.ld0 + c : x.p1 + vox * x.ld1 + (c - x.split);
+          v = *reinterpret_cast<const float4*>(p);
+        }
       }
-      float* dd = Xs + pos * P + 4 * q;
-      dd[0] = v.x; dd[1] = v.y; dd[2] = v.z; dd[3] = v.w;
+      hreg[k] = v;
     }
-    // dy tile: 128 voxels x 32 channels
-    for (int i = threadIdx.x; i < WG_TV * (WG_CO / 4); i += 256) {
-      const int q = i % (WG_CO / 4), k = i / (WG_CO / 4);
-      const int gh = h0 + k / WG_TW, gw = w0 + k % WG_TW;
+#pragma unroll
+    for (int k = 0; k < NY; ++k) {
+      const int i = threadIdx.x + 256 * k;
+      const int q = i % (WG_CO / 4), kv = i / (WG_CO / 4);
+      const int gh = h0 + kv / WG_TW, gw = w0 + kv % WG_TW;
       const int c = co0 + 4 * q;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       if (gh < H && gw < W && c < Cout) {
         const int64_t vox = (((int64_t)b * D + d0) * H + gh) * W + gw;
         v = *reinterpret_cast<const float4*>(dy + vox * lddy + c);
       }
-      *reinterpret_cast<float4*>(Ys + k * WG_CO + 4 * q) = v;
+      yreg[k] = v;
     }
-    __syncthreads();
-#pragma unroll 4
-    for (int s = 0; s < WG_TV / 2; ++s) {
-      const int k = 2 * s + khalf;
-      const int hp = (k / WG_TW) * HWD + (k % WG_TW);
-      const float bv = Ys[k * WG_CO + l32];
+  };
+  auto stash = [&]() {
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        if (wave + 4 * j < NBLK) {
-          const float av = lds[hp * mul[j] + off[j]];
-          acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[j], 0, 0, 0);
-        }
+    for (int k = 0; k < NH; ++k) {
+      const int i = threadIdx.x + 256 * k;
+      if (i < NPOS * HQ) {
+        const int q = i % HQ, pos = i / HQ;
+        float* d = Xs + pos * P + 4 * q;
+        d[0] = hreg[k].x; d[1] = hreg[k].y; d[2] = hreg[k].z; d[3] = hreg[k].w;
       }
     }
+#pragma unroll
+    for (int k = 0; k < NY; ++k) {
+      const int i = threadIdx.x + 256 * k;
+      *reinterpret_cast<float4*>(Ys + 4 * i) = yreg[k];
+    }
+  };
+
+  const int tbeg = split * tps;
+  const int tend = min(ntiles, tbeg + tps);
+  if (tbeg < tend) fetch(tbeg);
+  for (int tile = tbeg; tile < tend; ++tile) {
+    __syncthreads();  // previous compute done reading LDS
+    stash();
+    __syncthreads();
+    if (tile + 1 < tend) fetch(tile + 1);  // in flight during the MFMA loop
+    // Operands of k-step s+1 are read from LDS while the MFMAs of step s run
+    // (two named register sets, static indices).  No per-block guard: a wave
+    // with fewer than NJ taps runs a dummy block (tap 0, never stored) -- it
+    // would idle on its SIMD anyway, and a divergent-looking branch here
+    // de-pipelines the whole MFMA chain.
+    float a0[NJ], a1[NJ], b0, b1;
+    auto ldk = [&](int s, float (&a)[NJ], float& b) {
+      const int k = 2 * s + khalf;
+      const int hp = ((k / WG_TW) * HWD + (k % WG_TW)) * P;
+      b = Ys[k * WG_CO + l32];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) a[j] = Xs[hp + off[j]];
+    };
+    ldk(0, a0, b0);
+#pragma unroll 2
+    for (int s = 0; s < WG_TV / 2; s += 2) {
+      // sched_barrier pins the order: without it hipcc sinks the prefetch
+      // reads back in front of their own MFMAs (lgkmcnt stall per MFMA).
+      ldk(s + 1, a1, b1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[j], b0, acc[j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (s + 2 < WG_TV / 2) ldk(s + 2, a0, b0);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[j], b1, acc[j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
   }
-  // write partial slab [split][tap][kpad][npad]
+  // partial slab [split][tap][kpad][npad]: row = ci, col = co
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
-    const int rb = wave + 4 * j;
-    if (rb >= NBLK) continue;
+    const int tap = wave + 4 * j;
+    if (tap >= T) continue;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int i = (r & 3) + 8 * (r >> 2) + 4 * khalf;
-      const int rr = rb * 32 + i;
-      if (rr >= R) continue;
-      const int tap = rr / WG_CI, ci = rr % WG_CI;
+      const int ci = (r & 3) + 8 * (r >> 2) + 4 * khalf;
       part[(((int64_t)split * T + tap) * kpad + ci0 + ci) * npad + co0 + l32] = acc[j][r];
     }
   }
@@ -358,6 +404,7 @@ size_t conv3d_wgrad_ws_bytes(Vol vol, int KD, int Cin, int Cout) {
 
 hipError_t conv3d_wgrad(const Src2& x, const float* dy, int lddy, float* dw, Vol vol, int KD,
                         int Cin, int Cout, float* ws, hipStream_t s) {
+  if (lddy % 4) return hipErrorInvalidValue;
   WgradPlan p = wgrad_plan(vol, Cin, Cout);
   dim3 grid(p.nsplit, p.kpad / WG_CI, p.npad / WG_CO);
   if (KD == 3)
