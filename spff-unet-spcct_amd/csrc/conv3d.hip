@@ -201,28 +201,32 @@ hipError_t conv3d_fwd(const Src2& x, const float* wt, const Dst2& y, Vol vol, in
 
 // ------------------------------------------------------------------ wgrad --
 // dW[co][ci][tap] = sum_v x[v + off(tap)][ci] * dy[v][co].
-// One workgroup (4 waves, 1 per SIMD) owns ALL taps x 32 ci x 32 co: MFMA block
-// j of wave w is tap w + 4j (7/7/7/6 blocks for 27 taps), row = ci, col = co,
-// reduction = voxels (2 per MFMA k-step).  It walks a contiguous range of
+// One workgroup (4 waves, 1 per SIMD) owns ALL taps x CI ci x 32 co.  MFMA
+// rows enumerate (tap, ci) pairs r = tap*CI + ci in blocks of 32 (block j of
+// wave w is w + 4j); with CI = 32 a block is one tap (7/7/7/6 blocks for 27
+// taps), with CI = 8 (first layer, Cin = 5) four taps.  col = co, reduction =
+// voxels (2 per MFMA k-step).  It walks a contiguous range of
 // 1 x 8 x 16 voxel tiles; the next tile's halo (3 x 10 x 18 x 32 ch) and dy tile
 // (128 x 32) are prefetched into registers while the current tile is computed
 // out of LDS, then written to LDS after the compute (loads never exposed).
 // Each workgroup writes one fp32 partial slab; k_wgrad_reduce sums the slabs
 // in a fixed order (deterministic).
 namespace {
-constexpr int WG_CI = 32, WG_CO = 32, WG_TH = 8, WG_TW = 16, WG_TV = WG_TH * WG_TW;
+constexpr int WG_CO = 32, WG_TH = 8, WG_TW = 16, WG_TV = WG_TH * WG_TW;
+inline int wgrad_ci(int Cin) { return Cin <= 8 ? 8 : 32; }
 struct WgradPlan {
-  int kpad, npad, tilesD, tilesH, tilesW, ntiles, nsplit, tps;
+  int ci, kpad, npad, tilesD, tilesH, tilesW, ntiles, nsplit, tps;
 };
 WgradPlan wgrad_plan(Vol vol, int Cin, int Cout) {
   WgradPlan p;
-  p.kpad = cdiv(Cin, WG_CI) * WG_CI;
+  p.ci = wgrad_ci(Cin);
+  p.kpad = cdiv(Cin, p.ci) * p.ci;
   p.npad = cdiv(Cout, WG_CO) * WG_CO;
   p.tilesD = vol.D;
   p.tilesH = cdiv(vol.H, WG_TH);
   p.tilesW = cdiv(vol.W, WG_TW);
   p.ntiles = vol.B * p.tilesD * p.tilesH * p.tilesW;
-  const int nout = (p.kpad / WG_CI) * (p.npad / WG_CO);
+  const int nout = (p.kpad / p.ci) * (p.npad / WG_CO);
   // one workgroup per CU: aim at 2 rounds of 256 CUs, >= 4 tiles per workgroup
   int nsplit = std::max(1, cdiv(512, nout));
   nsplit = std::min(nsplit, std::max(1, p.ntiles / 4));
@@ -232,19 +236,21 @@ WgradPlan wgrad_plan(Vol vol, int Cin, int Cout) {
 }
 }  // namespace
 
-template <int KD>
+template <int KD, int CI>
 __global__ __launch_bounds__(256, 1) void k_conv3d_wgrad(Src2 x, const float* __restrict__ dy,
                                                          int lddy, float* __restrict__ part,
                                                          Vol vol, int Cin, int kpad, int Cout,
                                                          int npad, int tilesH, int tilesW,
                                                          int ntiles, int tps) {
   constexpr int HD = KD, HH = WG_TH + 2, HWD = WG_TW + 2;
-  constexpr int P = WG_CI + 1;  // odd pitch: a wave's 32 ci of one voxel hit 32 banks
+  constexpr int P = CI + 1;  // odd pitch: 32 lanes reading distinct (tap, ci) avoid conflicts
   constexpr int NPOS = HD * HH * HWD;
   constexpr int XS = NPOS * P;
   constexpr int T = KD * 9;
-  constexpr int NJ = (T + 3) / 4;
-  constexpr int HQ = WG_CI / 4;                     // float4 per halo voxel
+  constexpr int R = T * CI;                          // (tap, ci) rows
+  constexpr int NBLK = (R + 31) / 32;
+  constexpr int NJ = (NBLK + 3) / 4;
+  constexpr int HQ = CI / 4;                         // float4 per halo voxel
   constexpr int NH = (NPOS * HQ + 255) / 256;        // halo float4 per thread
   constexpr int NY = WG_TV * (WG_CO / 4) / 256;      // dy float4 per thread (= 4)
   __shared__ float lds[XS + WG_TV * WG_CO];
@@ -253,16 +259,17 @@ __global__ __launch_bounds__(256, 1) void k_conv3d_wgrad(Src2 x, const float* __
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int khalf = lane >> 5, l32 = lane & 31;
-  const int split = blockIdx.x, ci0 = blockIdx.y * WG_CI, co0 = blockIdx.z * WG_CO;
+  const int split = blockIdx.x, ci0 = blockIdx.y * CI, co0 = blockIdx.z * WG_CO;
   const int D = vol.D, H = vol.H, W = vol.W;
 
   int off[NJ];
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
-    const int tap = wave + 4 * j;
-    const int t = tap < T ? tap : 0;
+    const int r = (wave + 4 * j) * 32 + l32;
+    const int rr = r < R ? r : 0;  // rows past R: dummy reads of (tap 0, ci 0), never stored
+    const int t = rr / CI, ci = rr % CI;
     const int kd = t / 9, kh = (t / 3) % 3, kw = t % 3;
-    off[j] = ((kd * HH + kh) * HWD + kw) * P + l32;
+    off[j] = ((kd * HH + kh) * HWD + kw) * P + ci;
   }
   f32x16 acc[NJ];
 #pragma unroll
@@ -371,29 +378,45 @@ __global__ __launch_bounds__(256, 1) void k_conv3d_wgrad(Src2 x, const float* __
   // partial slab [split][tap][kpad][npad]: row = ci, col = co
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
-    const int tap = wave + 4 * j;
-    if (tap >= T) continue;
+    const int blk = wave + 4 * j;
+    if (blk >= NBLK) continue;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int ci = (r & 3) + 8 * (r >> 2) + 4 * khalf;
+      const int row = blk * 32 + (r & 3) + 8 * (r >> 2) + 4 * khalf;
+      if (row >= R) continue;
+      const int tap = row / CI, ci = row % CI;
       part[(((int64_t)split * T + tap) * kpad + ci0 + ci) * npad + co0 + l32] = acc[j][r];
     }
   }
 }
 
-__global__ void k_wgrad_reduce(const float* __restrict__ part, float* __restrict__ dw, int nsplit,
-                               int T, int kpad, int npad, int Cin, int Cout) {
+// 256 threads = 32 consecutive outputs (co fastest -> coalesced slab reads) x 8
+// split groups; group g sums splits g, g+8, ... in order, then a fixed-order LDS
+// combine: deterministic, and 8x more loads in flight than one thread per output.
+__global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ part,
+                                                      float* __restrict__ dw, int nsplit, int T,
+                                                      int kpad, int npad, int Cin, int Cout) {
+  __shared__ float red[8][33];
   const int64_t total = (int64_t)T * Cin * Cout;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int co = (int)(i % Cout);
-    const int ci = (int)((i / Cout) % Cin);
-    const int tap = (int)(i / ((int64_t)Cout * Cin));
+  const int o = threadIdx.x & 31, g = threadIdx.x >> 5;
+  const int64_t i = (int64_t)blockIdx.x * 32 + o;
+  float s = 0.f;
+  int co = 0, ci = 0, tap = 0;
+  if (i < total) {
+    co = (int)(i % Cout);
+    ci = (int)((i / Cout) % Cin);
+    tap = (int)(i / ((int64_t)Cout * Cin));
     const int64_t stride = (int64_t)T * kpad * npad;
     const float* p = part + ((int64_t)tap * kpad + ci) * npad + co;
-    float s = 0.f;
-    for (int k = 0; k < nsplit; ++k) s += p[k * stride];
-    dw[((int64_t)co * Cin + ci) * T + tap] = s;
+    for (int k = g; k < nsplit; k += 8) s += p[k * stride];
+  }
+  red[g][o] = s;
+  __syncthreads();
+  if (g == 0 && i < total) {
+    float t = red[0][o];
+#pragma unroll
+    for (int q = 1; q < 8; ++q) t += red[q][o];
+    dw[((int64_t)co * Cin + ci) * T + tap] = t;
   }
 }
 
@@ -406,20 +429,22 @@ hipError_t conv3d_wgrad(const Src2& x, const float* dy, int lddy, float* dw, Vol
                         int Cin, int Cout, float* ws, hipStream_t s) {
   if (lddy % 4) return hipErrorInvalidValue;
   WgradPlan p = wgrad_plan(vol, Cin, Cout);
-  dim3 grid(p.nsplit, p.kpad / WG_CI, p.npad / WG_CO);
-  if (KD == 3)
-    hipLaunchKernelGGL(k_conv3d_wgrad<3>, grid, dim3(256), 0, s, x, dy, lddy, ws, vol, Cin, p.kpad,
-                       Cout, p.npad, p.tilesH, p.tilesW, p.ntiles, p.tps);
-  else
-    hipLaunchKernelGGL(k_conv3d_wgrad<1>, grid, dim3(256), 0, s, x, dy, lddy, ws, vol, Cin, p.kpad,
-                       Cout, p.npad, p.tilesH, p.tilesW, p.ntiles, p.tps);
+  dim3 grid(p.nsplit, p.kpad / p.ci, p.npad / WG_CO);
+#define SPFF_WG(KD_, CI_)                                                                  \
+  hipLaunchKernelGGL((k_conv3d_wgrad<KD_, CI_>), grid, dim3(256), 0, s, x, dy, lddy, ws, vol, \
+                     Cin, p.kpad, Cout, p.npad, p.tilesH, p.tilesW, p.ntiles, p.tps)
+  if (KD == 3) {
+    if (p.ci == 8) SPFF_WG(3, 8); else SPFF_WG(3, 32);
+  } else {
+    if (p.ci == 8) SPFF_WG(1, 8); else SPFF_WG(1, 32);
+  }
+#undef SPFF_WG
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const int T = KD * 9;
-  int64_t total = (int64_t)T * Cin * Cout;
-  int g = (int)std::min<int64_t>((total + 255) / 256, 8192);
-  hipLaunchKernelGGL(k_wgrad_reduce, dim3(g), dim3(256), 0, s, ws, dw, p.nsplit, T, p.kpad,
-                     p.npad, Cin, Cout);
+  const int64_t total = (int64_t)T * Cin * Cout;
+  hipLaunchKernelGGL(k_wgrad_reduce, dim3((unsigned)((total + 31) / 32)), dim3(256), 0, s, ws, dw,
+                     p.nsplit, T, p.kpad, p.npad, Cin, Cout);
   return hipGetLastError();
 }
 

@@ -230,6 +230,9 @@ hipError_t in_bwd_stats(const float* sums, const float* gamma, float* dgamma, fl
 
 // ------------------------------------------------------------ elementwise --
 // grid.y = b*D + d ; grid.x strides over the (h,w,c/4) float4s of that slab.
+// The stride (gridDim.x * 256) is a multiple of C/4 (C/4 <= 64, power of two),
+// so a thread's channel quad is fixed: its per-(b,c[,d]) parameters are loaded
+// once into registers, and the loop is pure float4 streaming.
 __global__ __launch_bounds__(256) void k_act_apply(const float* __restrict__ y, float* __restrict__ out,
                                                    const float* __restrict__ al, const float* __restrict__ de,
                                                    const float* __restrict__ P, const float* __restrict__ Q,
@@ -237,20 +240,22 @@ __global__ __launch_bounds__(256) void k_act_apply(const float* __restrict__ y, 
   const int bd = blockIdx.y, b = bd / vol.D, d = bd % vol.D;
   const int n4 = vol.H * vol.W * (C >> 2);
   const int64_t base = (int64_t)bd * vol.H * vol.W * C;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += gridDim.x * blockDim.x) {
-    const int c = (i % (C >> 2)) * 4;
+  const int i0 = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = (i0 % (C >> 2)) * 4;
+  float pa[4], pd[4], pp[4], pq[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int bc = b * C + c + j;
+    pa[j] = al[bc];
+    pd[j] = de[bc];
+    pp[j] = P ? P[(int64_t)bc * vol.D + d] : 1.f;
+    pq[j] = P ? Q[(int64_t)bc * vol.D + d] : 0.f;
+  }
+  for (int i = i0; i < n4; i += gridDim.x * blockDim.x) {
     const float4 v = *reinterpret_cast<const float4*>(y + base + 4 * (int64_t)i);
     float r[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int bc = b * C + c + j;
-      float a = lrelu(r[j] * al[bc] + de[bc]);
-      if (P) {
-        const int64_t k = (int64_t)bc * vol.D + d;
-        a = a * P[k] + Q[k];
-      }
-      r[j] = a;
-    }
+    for (int j = 0; j < 4; ++j) r[j] = lrelu(r[j] * pa[j] + pd[j]) * pp[j] + pq[j];
     *reinterpret_cast<float4*>(out + base + 4 * (int64_t)i) = make_float4(r[0], r[1], r[2], r[3]);
   }
 }
@@ -275,8 +280,18 @@ __global__ __launch_bounds__(256) void k_in_bwd_apply(
   const int bd = blockIdx.y, b = bd / vol.D, d = bd % vol.D;
   const int n4 = vol.H * vol.W * (C >> 2);
   const int64_t base = (int64_t)bd * vol.H * vol.W * C;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += gridDim.x * blockDim.x) {
-    const int c = (i % (C >> 2)) * 4;
+  const int i0 = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = (i0 % (C >> 2)) * 4;
+  float pal[4], pde[4], pmu[4], prs[4], psc[4], pk1[4], pk2[4], pA[4], pB[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int bc = b * C + c + j;
+    pal[j] = al[bc]; pde[j] = de[bc]; pmu[j] = mean[bc]; prs[j] = rstd[bc];
+    psc[j] = rstd[bc] * gamma[c + j]; pk1[j] = k1[bc]; pk2[j] = k2[bc];
+    pA[j] = A ? A[(int64_t)bc * vol.D + d] : 1.f;
+    pB[j] = A ? Bc[(int64_t)bc * vol.D + d] : 0.f;
+  }
+  for (int i = i0; i < n4; i += gridDim.x * blockDim.x) {
     const float4 yv = *reinterpret_cast<const float4*>(y + base + 4 * (int64_t)i);
     const float4 gv = *reinterpret_cast<const float4*>(g + base + 4 * (int64_t)i);
     const float ys[4] = {yv.x, yv.y, yv.z, yv.w};
@@ -284,16 +299,10 @@ __global__ __launch_bounds__(256) void k_in_bwd_apply(
     float o[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int bc = b * C + c + j;
-      const float r = ys[j] * al[bc] + de[bc];
-      float gg = gs[j];
-      if (A) {
-        const int64_t k = (int64_t)bc * vol.D + d;
-        gg = gg * A[k] + Bc[k];
-      }
-      const float dr = gg * slope(r);
-      const float xh = (ys[j] - mean[bc]) * rstd[bc];
-      o[j] = rstd[bc] * gamma[c + j] * (dr - k1[bc] - xh * k2[bc]);
+      const float r = ys[j] * pal[j] + pde[j];
+      const float dr = (gs[j] * pA[j] + pB[j]) * slope(r);
+      const float xh = (ys[j] - pmu[j]) * prs[j];
+      o[j] = psc[j] * (dr - pk1[j] - xh * pk2[j]);
     }
     *reinterpret_cast<float4*>(dy + base + 4 * (int64_t)i) = make_float4(o[0], o[1], o[2], o[3]);
   }
