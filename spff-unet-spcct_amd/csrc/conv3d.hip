@@ -104,34 +104,74 @@ __global__ __launch_bounds__(256) void k_conv3d_fwd(Src2 x, const float* __restr
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[mb][nb][r] = 0.f;
 
+  // Register-prefetch pipeline: chunk c0+CK's halo and weight slab are loaded
+  // into registers while chunk c0 is computed out of LDS, and written to LDS
+  // after the next barrier -- the global-load latency is never on the
+  // critical path (the 3 co-resident workgroups then only cover barriers).
+  constexpr int Q = CK / 4;
+  constexpr int NHX = HD * HH * HWD * Q;            // halo float4 per chunk
+  constexpr int NWX = T * CK * (BN / 4);             // weight float4 per chunk
+  constexpr int RH = (NHX + 255) / 256, RW = (NWX + 255) / 256;
+  float4 hreg[RH], wreg[RW];
+  auto fetch = [&](int c0) {
+#pragma unroll
+    for (int k = 0; k < RH; ++k) {
+      const int i = threadIdx.x + 256 * k;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (i < NHX) {
+        const int q = i % Q, pos = i / Q;
+        const int hw = pos % HWD, t2 = pos / HWD, hh = t2 % HH, hd = t2 / HH;
+        const int gd = d0 + hd - KD / 2, gh = h0 + hh - 1, gw = w0 + hw - 1;
+        const int c = c0 + 4 * q;
+        if ((unsigned)gd < (unsigned)D && (unsigned)gh < (unsigned)H &&
+            (unsigned)gw < (unsigned)W && c < Cin) {
+          const int64_t vox = (((int64_t)b * D + gd) * H + gh) * W + gw;
+          const float* p =
+              c < x.split ? x.p0 + vox * x.ld0 + c : x.p1 + vox * x.ld1 + (c - x.split);
+          v = *reinterpret_cast<const float4*>(p);
+        }
+      }
+      hreg[k] = v;
+    }
+#pragma unroll
+    for (int k = 0; k < RW; ++k) {
+      const int i = threadIdx.x + 256 * k;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (i < NWX) {
+        const int j = i % (BN / 4), row = i / (BN / 4);
+        const int tap = row / CK, ci = row % CK;
+        v = *reinterpret_cast<const float4*>(wt + ((int64_t)(tap * kpad + c0 + ci)) * npad + n0 +
+                                             4 * j);
+      }
+      wreg[k] = v;
+    }
+  };
+  auto stash = [&]() {
+#pragma unroll
+    for (int k = 0; k < RH; ++k) {
+      const int i = threadIdx.x + 256 * k;
+      if (i < NHX) {
+        const int q = i % Q, pos = i / Q;
+        float* d = Xs + pos * P + 4 * q;
+        d[0] = hreg[k].x; d[1] = hreg[k].y; d[2] = hreg[k].z; d[3] = hreg[k].w;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < RW; ++k) {
+      const int i = threadIdx.x + 256 * k;
+      if (i < NWX) {
+        const int j = i % (BN / 4), row = i / (BN / 4);
+        *reinterpret_cast<float4*>(Ws + row * BN + 4 * j) = wreg[k];
+      }
+    }
+  };
+
+  fetch(0);
   for (int c0 = 0; c0 < kpad; c0 += CK) {
     if (c0) __syncthreads();
-    // ---- stage input halo (zero padded) ----
-    constexpr int Q = CK / 4;
-    for (int i = threadIdx.x; i < HD * HH * HWD * Q; i += 256) {
-      const int q = i % Q, pos = i / Q;
-      const int hw = pos % HWD, t2 = pos / HWD, hh = t2 % HH, hd = t2 / HH;
-      const int gd = d0 + hd - KD / 2, gh = h0 + hh - 1, gw = w0 + hw - 1;
-      const int c = c0 + 4 * q;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if ((unsigned)gd < (unsigned)D && (unsigned)gh < (unsigned)H &&
-          (unsigned)gw < (unsigned)W && c < Cin) {
-        const int64_t vox = (((int64_t)b * D + gd) * H + gh) * W + gw;
-        const float* p = c < x.split ? x.p0 + vox * x.ld0 + c : x.p1 + vox * x.ld1 + (c - x.split);
-        v = *reinterpret_cast<const float4*>(p);
-      }
-      float* d = Xs + pos * P + 4 * q;
-      d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
-    }
-    // ---- stage weight slab [T][CK][BN] ----
-    for (int i = threadIdx.x; i < T * CK * (BN / 4); i += 256) {
-      const int j = i % (BN / 4), row = i / (BN / 4);
-      const int tap = row / CK, ci = row % CK;
-      const float4 v = *reinterpret_cast<const float4*>(
-          wt + ((int64_t)(tap * kpad + c0 + ci)) * npad + n0 + 4 * j);
-      *reinterpret_cast<float4*>(Ws + row * BN + 4 * j) = v;
-    }
+    stash();
     __syncthreads();
+    if (c0 + CK < kpad) fetch(c0 + CK);
 #pragma unroll 3
     for (int tap = 0; tap < T; ++tap) {
       const int kd = tap / 9, kh = (tap / 3) % 3, kw = tap % 3;
