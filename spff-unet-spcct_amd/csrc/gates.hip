@@ -10,7 +10,10 @@
 // The FourierGate's rfft -> real mask -> irfft(n=D) is a real circulant
 // operator w = A s1 with A[d,d'] = (1/D) sum_k c_k M_k cos(2 pi k (d-d') / D)
 // (c_0 = 1, c_{D/2} = 1 for even D, else 2); it is evaluated as an explicit
-// double-precision DFT (D <= 512, negligible work).
+// double-precision DFT from an LDS twiddle table (D <= 512, negligible work).
+//
+// One 1024-thread workgroup per sample; every sum is a fixed-order
+// (thread-slice partials in LDS, then an ordered combine) -> deterministic.
 #include "spff_internal.h"
 #include <math.h>
 
@@ -21,13 +24,51 @@ __device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); 
 __device__ __forceinline__ double ck_coef(int k, int D) {
   return (k == 0 || (D % 2 == 0 && k == D / 2)) ? 1.0 : 2.0;
 }
-__device__ __forceinline__ void cis(int k, int d, int D, double& c, double& s) {
-  const int m = (int)(((int64_t)k * d) % D);
-  const double ang = 6.283185307179586476925286766559 * (double)m / (double)D;
-  sincos(ang, &s, &c);
-}
 
 int se_hidden(int C) { return C / 16 > 4 ? C / 16 : 4; }
+
+constexpr int GT = 1024;  // threads per gate workgroup
+
+// twiddles: twc[m] = cos(2 pi m / D), tws[m] = sin(2 pi m / D)
+__device__ void make_twiddles(double* twc, double* tws, int D) {
+  for (int m = threadIdx.x; m < D; m += blockDim.x) {
+    double s, c;
+    sincos(6.283185307179586476925286766559 * (double)m / (double)D, &s, &c);
+    twc[m] = c;
+    tws[m] = s;
+  }
+}
+
+// out[i] = scale * sum_{j<NJ} f(i, j) for i < NI, computed by slices of threads
+// (partials in `part`, combined in slice order).  Ends with __syncthreads().
+template <class Fn>
+__device__ void rowsum(int NI, int NJ, Fn f, double* part, double scale, double* out) {
+  const int t = threadIdx.x;
+  if (NI >= (int)blockDim.x) {  // one thread per row
+    for (int i = t; i < NI; i += blockDim.x) {
+      double s = 0.0;
+      for (int j = 0; j < NJ; ++j) s += f(i, j);
+      out[i] = s * scale;
+    }
+    __syncthreads();
+    return;
+  }
+  const int S = (int)blockDim.x / NI;
+  double acc = 0.0;
+  if (t < NI * S) {
+    const int i = t / S, sl = t % S;
+    for (int j = sl; j < NJ; j += S) acc += f(i, j);
+  }
+  __syncthreads();
+  if (t < NI * S) part[t] = acc;
+  __syncthreads();
+  for (int i = t; i < NI; i += blockDim.x) {
+    double s = 0.0;
+    for (int q = 0; q < S; ++q) s += part[i * S + q];
+    out[i] = s * scale;
+  }
+  __syncthreads();
+}
 
 // ------------------------------------------------------------- EFiLM fwd --
 // hid[j][d] = fw0[j] . pe[:,d] + fb0[j]; gb[o][d] = fw2[o] . relu(hid[:,d]) + fb2[o]
@@ -58,106 +99,108 @@ __global__ void k_efilm_fwd(const float* __restrict__ pe, const float* __restric
 }
 
 // ------------------------------------------------------------- gates fwd --
-__global__ void k_gates_fwd(GateParams gp, const float* __restrict__ Sa, GateSaved sv, Vol vol,
-                            int C, int Hse, int efilm) {
+struct GFShm {
+  double *twc, *tws, *Sre, *Sim, *part, *tmp;
+  float *s1, *g1, *sg2, *p, *h, *e;
+};
+__device__ GFShm gf_carve(void* base, int C, int D, int Hse) {
+  const int L = D / 2 + 1;
+  GFShm m;
+  double* dp = reinterpret_cast<double*>(base);
+  m.twc = dp; dp += D;
+  m.tws = dp; dp += D;
+  m.Sre = dp; dp += L;
+  m.Sim = dp; dp += L;
+  m.part = dp; dp += GT;
+  m.tmp = dp; dp += (C > D ? C : D) + 1;
+  float* fp = reinterpret_cast<float*>(dp);
+  m.s1 = fp; fp += D;
+  m.g1 = fp; fp += D;
+  m.sg2 = fp; fp += D;
+  m.p = fp; fp += C;
+  m.h = fp; fp += Hse;
+  m.e = fp;
+  return m;
+}
+static size_t gates_fwd_shmem(int C, int D, int Hse) {
+  const int L = D / 2 + 1;
+  return (2 * (size_t)D + 2 * L + GT + (C > D ? C : D) + 1) * sizeof(double) +
+         (3 * (size_t)D + 2 * C + Hse) * sizeof(float);
+}
+
+__global__ __launch_bounds__(GT) void k_gates_fwd(GateParams gp, const float* __restrict__ Sa,
+                                                  GateSaved sv, Vol vol, int C, int Hse,
+                                                  int efilm) {
   const int b = blockIdx.x;
   const int D = vol.D, HW = vol.H * vol.W, L = D / 2 + 1;
   extern __shared__ double shd[];
-  double* Sre = shd;                        // [L]
-  double* Sim = Sre + L;                    // [L]
-  float* s1 = reinterpret_cast<float*>(Sim + L);  // [D]
-  float* g1 = s1 + D;                       // [D]
-  float* sg2 = g1 + D;                      // [D]
-  float* p = sg2 + D;                       // [C]
-  float* h = p + C;                         // [Hse]
-  float* e = h + Hse;                       // [C]
+  GFShm m = gf_carve(shd, C, D, Hse);
   const float* Sab = Sa + (int64_t)b * C * D;
   auto Z = [&](int c, int d) -> float {
     const float sa = Sab[c * D + d];
     return efilm ? (1.f + sv.t[c * D + d]) * sa + sv.bt[c * D + d] * (float)HW : sa;
   };
+  make_twiddles(m.twc, m.tws, D);
   // s1[d] = mean_{c,hw} z
-  for (int d = threadIdx.x; d < D; d += blockDim.x) {
-    double s = 0.0;
-    for (int c = 0; c < C; ++c) s += (double)Z(c, d);
-    s1[d] = (float)(s / ((double)C * HW));
-  }
+  rowsum(D, C, [&](int d, int c) { return (double)Z(c, d); }, m.part, 1.0 / ((double)C * HW),
+         m.tmp);
+  for (int d = threadIdx.x; d < D; d += blockDim.x) m.s1[d] = (float)m.tmp[d];
   __syncthreads();
   if (gp.mask) {
-    for (int k = threadIdx.x; k < L; k += blockDim.x) {
-      double re = 0.0, im = 0.0;
-      for (int d = 0; d < D; ++d) {
-        double c, s;
-        cis(k, d, D, c, s);
-        re += (double)s1[d] * c;
-        im -= (double)s1[d] * s;
-      }
-      Sre[k] = re;
-      Sim[k] = im;
-    }
-    __syncthreads();
-    const double mag = (double)gp.mag[0];
-    for (int d = threadIdx.x; d < D; d += blockDim.x) {
-      double w = 0.0;
-      for (int k = 0; k < L; ++k) {
-        double c, s;
-        cis(k, d, D, c, s);
-        const double Mk = (double)(gp.mask[k] * gp.mag[0]);
-        (void)mag;
-        w += ck_coef(k, D) * Mk * (Sre[k] * c - Sim[k] * s);
-      }
-      g1[d] = sigm((float)(w / D));
-    }
+    rowsum(L, D, [&](int k, int d) { return (double)m.s1[d] * m.twc[(k * d) % D]; }, m.part, 1.0,
+           m.Sre);
+    rowsum(L, D, [&](int k, int d) { return -(double)m.s1[d] * m.tws[(k * d) % D]; }, m.part, 1.0,
+           m.Sim);
+    rowsum(D, L, [&](int d, int k) {
+      const int q = (k * d) % D;
+      const double Mk = (double)(gp.mask[k] * gp.mag[0]);
+      return ck_coef(k, D) * Mk * (m.Sre[k] * m.twc[q] - m.Sim[k] * m.tws[q]);
+    }, m.part, 1.0 / D, m.tmp);
+    for (int d = threadIdx.x; d < D; d += blockDim.x) m.g1[d] = sigm((float)m.tmp[d]);
   } else {
-    for (int d = threadIdx.x; d < D; d += blockDim.x) g1[d] = 1.f;
+    for (int d = threadIdx.x; d < D; d += blockDim.x) m.g1[d] = 1.f;
   }
   __syncthreads();
-  for (int d = threadIdx.x; d < D; d += blockDim.x) sg2[d] = gp.specse ? sigm(g1[d] * s1[d]) : 1.f;
+  for (int d = threadIdx.x; d < D; d += blockDim.x)
+    m.sg2[d] = gp.specse ? sigm(m.g1[d] * m.s1[d]) : 1.f;
   __syncthreads();
   if (gp.sw0) {
-    for (int c = threadIdx.x; c < C; c += blockDim.x) {
-      double s = 0.0;
-      for (int d = 0; d < D; ++d) s += (double)(g1[d] * sg2[d]) * (double)Z(c, d);
-      p[c] = (float)(s / ((double)D * HW));
-    }
+    rowsum(C, D, [&](int c, int d) { return (double)(m.g1[d] * m.sg2[d]) * (double)Z(c, d); },
+           m.part, 1.0 / ((double)D * HW), m.tmp);
+    for (int c = threadIdx.x; c < C; c += blockDim.x) m.p[c] = (float)m.tmp[c];
     __syncthreads();
     for (int j = threadIdx.x; j < Hse; j += blockDim.x) {
       float s = 0.f;
-      for (int c = 0; c < C; ++c) s += gp.sw0[j * C + c] * p[c];
-      h[j] = s + gp.sb0[j];
+      for (int c = 0; c < C; ++c) s += gp.sw0[j * C + c] * m.p[c];
+      m.h[j] = s + gp.sb0[j];
     }
     __syncthreads();
     for (int c = threadIdx.x; c < C; c += blockDim.x) {
       float s = 0.f;
-      for (int j = 0; j < Hse; ++j) s += gp.sw2[c * Hse + j] * fmaxf(h[j], 0.f);
-      e[c] = sigm(s + gp.sb2[c]);
+      for (int j = 0; j < Hse; ++j) s += gp.sw2[c * Hse + j] * fmaxf(m.h[j], 0.f);
+      m.e[c] = sigm(s + gp.sb2[c]);
     }
   } else {
-    for (int c = threadIdx.x; c < C; c += blockDim.x) e[c] = 1.f;
+    for (int c = threadIdx.x; c < C; c += blockDim.x) m.e[c] = 1.f;
   }
   __syncthreads();
   for (int d = threadIdx.x; d < D; d += blockDim.x) {
-    sv.s1[b * D + d] = s1[d];
-    sv.g1[b * D + d] = g1[d];
-    sv.sg2[b * D + d] = sg2[d];
+    sv.s1[b * D + d] = m.s1[d];
+    sv.g1[b * D + d] = m.g1[d];
+    sv.sg2[b * D + d] = m.sg2[d];
   }
   if (gp.sw0) {
-    for (int c = threadIdx.x; c < C; c += blockDim.x) { sv.p[b * C + c] = p[c]; sv.e[b * C + c] = e[c]; }
-    for (int j = threadIdx.x; j < Hse; j += blockDim.x) sv.h[b * Hse + j] = h[j];
+    for (int c = threadIdx.x; c < C; c += blockDim.x) { sv.p[b * C + c] = m.p[c]; sv.e[b * C + c] = m.e[c]; }
+    for (int j = threadIdx.x; j < Hse; j += blockDim.x) sv.h[b * Hse + j] = m.h[j];
   }
   for (int i = threadIdx.x; i < C * D; i += blockDim.x) {
     const int c = i / D, d = i % D;
-    const float G = g1[d] * sg2[d] * e[c];
+    const float G = m.g1[d] * m.sg2[d] * m.e[c];
     const float onept = efilm ? (1.f + sv.t[i]) : 1.f;
     const float btv = efilm ? sv.bt[i] : 0.f;
     sv.P[(int64_t)b * C * D + i] = onept * G;
     sv.Q[(int64_t)b * C * D + i] = btv * G;
   }
-}
-
-static size_t gates_fwd_shmem(int C, int D, int Hse) {
-  const int L = D / 2 + 1;
-  return 2 * L * sizeof(double) + (3 * D + 2 * C + Hse) * sizeof(float);
 }
 
 hipError_t gates_fwd(const GateParams& gp, const float* Sa, GateSaved& sv, Vol vol, int C,
@@ -171,7 +214,7 @@ hipError_t gates_fwd(const GateParams& gp, const float* Sa, GateSaved& sv, Vol v
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(k_gates_fwd, dim3(vol.B), dim3(256), gates_fwd_shmem(C, D, Hse), s, gp, Sa,
+  hipLaunchKernelGGL(k_gates_fwd, dim3(vol.B), dim3(GT), gates_fwd_shmem(C, D, Hse), s, gp, Sa,
                      sv, vol, C, Hse, efilm);
   return hipGetLastError();
 }
@@ -203,26 +246,50 @@ size_t gates_scratch_bytes(Vol vol, int C) {
   return n * sizeof(float) + 256;
 }
 
-__global__ void k_gates_bwd(GateParams gp, GateSaved sv, const float* __restrict__ Sa,
-                            const float* __restrict__ Sg, GScr gs, float* __restrict__ Aout,
-                            float* __restrict__ Bout, Vol vol, int C, int Hse, int efilm) {
+struct GBShm {
+  double *twc, *tws, *Sre, *Sim, *Tre, *Tim, *part, *tmp;
+  float *e, *c0, *dq, *dh, *g1, *sg2, *ds2, *dw, *ds1;
+};
+__device__ GBShm gb_carve(void* base, int C, int D, int Hse) {
+  const int L = D / 2 + 1;
+  GBShm m;
+  double* dp = reinterpret_cast<double*>(base);
+  m.twc = dp; dp += D;
+  m.tws = dp; dp += D;
+  m.Sre = dp; dp += L;
+  m.Sim = dp; dp += L;
+  m.Tre = dp; dp += L;
+  m.Tim = dp; dp += L;
+  m.part = dp; dp += GT;
+  m.tmp = dp; dp += (C > D ? C : D) + 1;
+  float* fp = reinterpret_cast<float*>(dp);
+  m.e = fp; fp += C;
+  m.c0 = fp; fp += C;
+  m.dq = fp; fp += C;
+  m.dh = fp; fp += Hse;
+  m.g1 = fp; fp += D;
+  m.sg2 = fp; fp += D;
+  m.ds2 = fp; fp += D;
+  m.dw = fp; fp += D;
+  m.ds1 = fp;
+  return m;
+}
+static size_t gates_bwd_shmem(int C, int D, int Hse) {
+  const int L = D / 2 + 1;
+  return (2 * (size_t)D + 4 * L + GT + (C > D ? C : D) + 1) * sizeof(double) +
+         (3 * (size_t)C + Hse + 5 * (size_t)D) * sizeof(float);
+}
+
+__global__ __launch_bounds__(GT) void k_gates_bwd(GateParams gp, GateSaved sv,
+                                                  const float* __restrict__ Sa,
+                                                  const float* __restrict__ Sg, GScr gs,
+                                                  float* __restrict__ Aout,
+                                                  float* __restrict__ Bout, Vol vol, int C,
+                                                  int Hse, int efilm) {
   const int b = blockIdx.x;
   const int D = vol.D, HW = vol.H * vol.W, L = D / 2 + 1;
   extern __shared__ double shd[];
-  double* Sre = shd;
-  double* Sim = Sre + L;
-  double* Tre = Sim + L;
-  double* Tim = Tre + L;
-  float* fb = reinterpret_cast<float*>(Tim + L);
-  float* e = fb;            // [C]
-  float* c0 = e + C;        // [C]
-  float* dq = c0 + C;       // [C]
-  float* dh = dq + C;       // [Hse]
-  float* g1 = dh + Hse;     // [D]
-  float* sg2 = g1 + D;      // [D]
-  float* ds2 = sg2 + D;     // [D]
-  float* dw = ds2 + D;      // [D]
-  float* ds1 = dw + D;      // [D]
+  GBShm m = gb_carve(shd, C, D, Hse);
   const int64_t bo = (int64_t)b * C * D;
   auto Zf = [&](int c, int d) -> float {
     const float sa = Sa[bo + c * D + d];
@@ -232,101 +299,94 @@ __global__ void k_gates_bwd(GateParams gp, GateSaved sv, const float* __restrict
     const float sgd = Sg[(bo + c * D + d) * 2 + 0], sda = Sg[(bo + c * D + d) * 2 + 1];
     return efilm ? (1.f + sv.t[c * D + d]) * sda + sv.bt[c * D + d] * sgd : sda;
   };
+  make_twiddles(m.twc, m.tws, D);
   for (int d = threadIdx.x; d < D; d += blockDim.x) {
-    g1[d] = sv.g1[b * D + d];
-    sg2[d] = sv.sg2[b * D + d];
+    m.g1[d] = sv.g1[b * D + d];
+    m.sg2[d] = sv.sg2[b * D + d];
   }
   __syncthreads();
-  // ---- channel SE ----
+  // ---- channel SE: out = v * e[c] ----
   if (gp.sw0) {
+    rowsum(C, D, [&](int c, int d) { return (double)(m.g1[d] * m.sg2[d]) * (double)R1(c, d); },
+           m.part, 1.0, m.tmp);
     for (int c = threadIdx.x; c < C; c += blockDim.x) {
-      double de = 0.0;
-      for (int d = 0; d < D; ++d) de += (double)(g1[d] * sg2[d]) * (double)R1(c, d);
       const float ev = sv.e[b * C + c];
-      e[c] = ev;
-      dq[c] = (float)de * ev * (1.f - ev);
-      gs.sb2p[b * C + c] = dq[c];
-      for (int j = 0; j < Hse; ++j)
-        gs.sw2p[((int64_t)b * C + c) * Hse + j] = dq[c] * fmaxf(sv.h[b * Hse + j], 0.f);
+      m.e[c] = ev;
+      m.dq[c] = (float)m.tmp[c] * ev * (1.f - ev);
+      gs.sb2p[b * C + c] = m.dq[c];
     }
     __syncthreads();
+    for (int i = threadIdx.x; i < C * Hse; i += blockDim.x) {
+      const int c = i / Hse, j = i % Hse;
+      gs.sw2p[(int64_t)b * C * Hse + i] = m.dq[c] * fmaxf(sv.h[b * Hse + j], 0.f);
+    }
     for (int j = threadIdx.x; j < Hse; j += blockDim.x) {
       float s = 0.f;
-      for (int c = 0; c < C; ++c) s += gp.sw2[c * Hse + j] * dq[c];
+      for (int c = 0; c < C; ++c) s += gp.sw2[c * Hse + j] * m.dq[c];
       const float dhv = sv.h[b * Hse + j] > 0.f ? s : 0.f;
-      dh[j] = dhv;
+      m.dh[j] = dhv;
       gs.sb0p[b * Hse + j] = dhv;
-      for (int c = 0; c < C; ++c) gs.sw0p[((int64_t)b * Hse + j) * C + c] = dhv * sv.p[b * C + c];
     }
     __syncthreads();
+    for (int i = threadIdx.x; i < Hse * C; i += blockDim.x) {
+      const int j = i / C, c = i % C;
+      gs.sw0p[(int64_t)b * Hse * C + i] = m.dh[j] * sv.p[b * C + c];
+    }
     for (int c = threadIdx.x; c < C; c += blockDim.x) {
       float s = 0.f;
-      for (int j = 0; j < Hse; ++j) s += gp.sw0[j * C + c] * dh[j];
-      c0[c] = s / ((float)D * (float)HW);
+      for (int j = 0; j < Hse; ++j) s += gp.sw0[j * C + c] * m.dh[j];
+      m.c0[c] = s / ((float)D * (float)HW);
     }
   } else {
-    for (int c = threadIdx.x; c < C; c += blockDim.x) { e[c] = 1.f; c0[c] = 0.f; }
+    for (int c = threadIdx.x; c < C; c += blockDim.x) { m.e[c] = 1.f; m.c0[c] = 0.f; }
   }
   __syncthreads();
   // ---- spectral SE: v = u * sg2[d] ----
-  for (int d = threadIdx.x; d < D; d += blockDim.x) {
-    if (gp.specse) {
-      double acc = 0.0;
-      for (int c = 0; c < C; ++c) acc += (double)e[c] * R1(c, d) + (double)c0[c] * Zf(c, d);
-      ds2[d] = sg2[d] * (1.f - sg2[d]) * g1[d] * (float)acc;
-    } else {
-      ds2[d] = 0.f;
-    }
+  if (gp.specse) {
+    rowsum(D, C, [&](int d, int c) {
+      return (double)m.e[c] * R1(c, d) + (double)m.c0[c] * Zf(c, d);
+    }, m.part, 1.0, m.tmp);
+    for (int d = threadIdx.x; d < D; d += blockDim.x)
+      m.ds2[d] = m.sg2[d] * (1.f - m.sg2[d]) * m.g1[d] * (float)m.tmp[d];
+  } else {
+    for (int d = threadIdx.x; d < D; d += blockDim.x) m.ds2[d] = 0.f;
   }
   __syncthreads();
   const float invCHW = 1.f / ((float)C * (float)HW);
   // du = dout*a + bb, a = e[c]*sg2[d], bb = c0[c]*sg2[d] + ds2[d]/(C*HW)
   // ---- FourierGate: u = z * g1[d] ----
   if (gp.mask) {
-    for (int d = threadIdx.x; d < D; d += blockDim.x) {
-      double acc = 0.0;
-      for (int c = 0; c < C; ++c) {
-        const float a = e[c] * sg2[d];
-        const float bb = c0[c] * sg2[d] + ds2[d] * invCHW;
-        acc += (double)a * R1(c, d) + (double)bb * Zf(c, d);
-      }
-      dw[d] = (float)acc * g1[d] * (1.f - g1[d]);
-    }
+    rowsum(D, C, [&](int d, int c) {
+      const float a = m.e[c] * m.sg2[d];
+      const float bb = m.c0[c] * m.sg2[d] + m.ds2[d] * invCHW;
+      return (double)a * R1(c, d) + (double)bb * Zf(c, d);
+    }, m.part, 1.0, m.tmp);
+    for (int d = threadIdx.x; d < D; d += blockDim.x)
+      m.dw[d] = (float)m.tmp[d] * m.g1[d] * (1.f - m.g1[d]);
     __syncthreads();
-    for (int k = threadIdx.x; k < L; k += blockDim.x) {
-      double sre = 0.0, sim = 0.0, tre = 0.0, tim = 0.0;
-      for (int d = 0; d < D; ++d) {
-        double cc, ss;
-        cis(k, d, D, cc, ss);
-        const double s1 = (double)sv.s1[b * D + d];
-        sre += s1 * cc;
-        sim -= s1 * ss;
-        tre += (double)dw[d] * cc;
-        tim += (double)dw[d] * ss;
-      }
-      Sre[k] = sre; Sim[k] = sim; Tre[k] = tre; Tim[k] = tim;
-      gs.dMr[b * L + k] = (float)(ck_coef(k, D) / D * (sre * tre - sim * tim));
-    }
-    __syncthreads();
-    for (int d = threadIdx.x; d < D; d += blockDim.x) {
-      double acc = 0.0;
-      for (int k = 0; k < L; ++k) {
-        double cc, ss;
-        cis(k, d, D, cc, ss);
-        const double Mk = (double)(gp.mask[k] * gp.mag[0]);
-        acc += ck_coef(k, D) * Mk * (cc * Tre[k] + ss * Tim[k]);
-      }
-      ds1[d] = (float)(acc / D);
-    }
+    const float* s1 = sv.s1 + b * D;
+    rowsum(L, D, [&](int k, int d) { return (double)s1[d] * m.twc[(k * d) % D]; }, m.part, 1.0, m.Sre);
+    rowsum(L, D, [&](int k, int d) { return -(double)s1[d] * m.tws[(k * d) % D]; }, m.part, 1.0, m.Sim);
+    rowsum(L, D, [&](int k, int d) { return (double)m.dw[d] * m.twc[(k * d) % D]; }, m.part, 1.0, m.Tre);
+    rowsum(L, D, [&](int k, int d) { return (double)m.dw[d] * m.tws[(k * d) % D]; }, m.part, 1.0, m.Tim);
+    for (int k = threadIdx.x; k < L; k += blockDim.x)
+      gs.dMr[b * L + k] =
+          (float)(ck_coef(k, D) / D * (m.Sre[k] * m.Tre[k] - m.Sim[k] * m.Tim[k]));
+    rowsum(D, L, [&](int d, int k) {
+      const int q = (k * d) % D;
+      const double Mk = (double)(gp.mask[k] * gp.mag[0]);
+      return ck_coef(k, D) * Mk * (m.twc[q] * m.Tre[k] + m.tws[q] * m.Tim[k]);
+    }, m.part, 1.0 / D, m.tmp);
+    for (int d = threadIdx.x; d < D; d += blockDim.x) m.ds1[d] = (float)m.tmp[d];
   }
   __syncthreads();
   for (int i = threadIdx.x; i < C * D; i += blockDim.x) {
     const int c = i / D, d = i % D;
-    float al = e[c] * sg2[d];
-    float be = c0[c] * sg2[d] + ds2[d] * invCHW;
+    float al = m.e[c] * m.sg2[d];
+    float be = m.c0[c] * m.sg2[d] + m.ds2[d] * invCHW;
     if (gp.mask) {
-      al = al * g1[d];
-      be = be * g1[d] + ds1[d] * invCHW;
+      al = al * m.g1[d];
+      be = be * m.g1[d] + m.ds1[d] * invCHW;
     }
     if (efilm) {
       const float sgd = Sg[(bo + i) * 2 + 0], sda = Sg[(bo + i) * 2 + 1];
@@ -431,18 +491,13 @@ __global__ void k_efilm_bwd3(GateParams gp, GateGrads gg, GScr gs, int D) {
   }
 }
 
-static size_t gates_bwd_shmem(int C, int D, int Hse) {
-  const int L = D / 2 + 1;
-  return 4 * L * sizeof(double) + (3 * C + Hse + 5 * D) * sizeof(float);
-}
-
 hipError_t gates_bwd(const GateParams& gp, const GateSaved& sv, const float* Sa, const float* Sg,
                      GateGrads& gg, float* A, float* Bc, Vol vol, int C, float* scratch,
                      hipStream_t s) {
   const int D = vol.D, B = vol.B, Hse = se_hidden(C);
   const int efilm = gp.fw0 != nullptr;
   GScr g = gscr(scratch, B, C, D, Hse);
-  hipLaunchKernelGGL(k_gates_bwd, dim3(B), dim3(256), gates_bwd_shmem(C, D, Hse), s, gp, sv, Sa,
+  hipLaunchKernelGGL(k_gates_bwd, dim3(B), dim3(GT), gates_bwd_shmem(C, D, Hse), s, gp, sv, Sa,
                      Sg, g, A, Bc, vol, C, Hse, efilm);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
@@ -454,10 +509,10 @@ hipError_t gates_bwd(const GateParams& gp, const GateSaved& sv, const float* Sa,
     hipLaunchKernelGGL(k_efilm_bwd1, dim3(std::min(cdiv(2 * C * D, 256), 1024)), dim3(256), 0, s,
                        g, sv.t, B, C, D);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_efilm_bwd2, dim3(cdiv(2 * C * 33 + 32 * D, 256)), dim3(256), 0, s, gp, gg,
+    hipLaunchKernelGGL(k_efilm_bwd2, dim3(cdiv(2 * C * 33 + 32 * D, 64)), dim3(64), 0, s, gp, gg,
                        g, sv.hid, C, D);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_efilm_bwd3, dim3(cdiv(32 * 17, 256)), dim3(256), 0, s, gp, gg, g, D);
+    hipLaunchKernelGGL(k_efilm_bwd3, dim3(cdiv(32 * 17, 64)), dim3(64), 0, s, gp, gg, g, D);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   return hipSuccess;

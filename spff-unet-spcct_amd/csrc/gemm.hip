@@ -192,34 +192,50 @@ __global__ __launch_bounds__(256) void k_atb(XL X, YL Y, float* __restrict__ par
 
 // dW layouts: mode 0 = upconv W[Cin][Cout][1][2][2] from C[ci][ij*Cout+co]
 //             mode 1 = head   W[K][Cin]           from C[ci][k]
-__global__ void k_atb_reduce(const float* __restrict__ part, const float* __restrict__ csum,
-                             float* __restrict__ dw, float* __restrict__ db, int nsplit, int k1pad,
-                             int npad, int K1, int N, int Cout, int mode) {
-  const int total = K1 * N;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total + npad;
-       i += gridDim.x * blockDim.x) {
-    if (i < total) {
-      const int n = i % N, k1 = i / N;
-      const float* p = part + (int64_t)k1 * npad + n;
-      float s = 0.f;
-      for (int k = 0; k < nsplit; ++k) s += p[(int64_t)k * k1pad * npad];
-      if (mode == 0) {
-        const int ij = n / Cout, co = n % Cout;
-        dw[((int64_t)k1 * Cout + co) * 4 + ij] = s;
-      } else {
-        dw[(int64_t)n * K1 + k1] = s;
-      }
-    } else {
-      const int co = i - total;  // bias: sum over splits (and over ij for upconv)
-      if (co >= Cout) continue;
-      float s = 0.f;
+// One block = 32 outputs x 8 split groups; each group sums its splits in order,
+// then the 8 group sums are combined in order (deterministic).  Blocks past
+// nwb reduce the bias (column sums, also summed over ij for the upconv).
+__global__ __launch_bounds__(256) void k_atb_reduce(const float* __restrict__ part,
+                                                    const float* __restrict__ csum,
+                                                    float* __restrict__ dw, float* __restrict__ db,
+                                                    int nsplit, int k1pad, int npad, int K1, int N,
+                                                    int Cout, int mode, int nwb) {
+  __shared__ float red[8][33];
+  const int jl = threadIdx.x & 31, g = threadIdx.x >> 5;
+  float s = 0.f;
+  bool valid;
+  int k1 = 0, n = 0, co = 0;
+  if ((int)blockIdx.x < nwb) {
+    const int j = blockIdx.x * 32 + jl;
+    k1 = j / npad;
+    n = j % npad;
+    valid = k1 < K1 && n < N;
+    if (valid) {
+      const int64_t stride = (int64_t)k1pad * npad;
+      for (int k = g; k < nsplit; k += 8) s += part[k * stride + j];
+    }
+  } else {
+    co = (blockIdx.x - nwb) * 32 + jl;
+    valid = co < Cout;
+    if (valid) {
       const int nij = (mode == 0) ? 4 : 1;
-      for (int ij = 0; ij < nij; ++ij) {
-        float t = 0.f;
-        for (int k = 0; k < nsplit; ++k) t += csum[(int64_t)k * npad + ij * Cout + co];
-        s += t;
-      }
-      db[co] = s;
+      for (int k = g; k < nsplit; k += 8)
+        for (int ij = 0; ij < nij; ++ij) s += csum[(int64_t)k * npad + ij * Cout + co];
+    }
+  }
+  red[g][jl] = s;
+  __syncthreads();
+  if (g == 0 && valid) {
+    float t = 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) t += red[q][jl];
+    if ((int)blockIdx.x >= nwb) {
+      db[co] = t;
+    } else if (mode == 0) {
+      const int ij = n / Cout, c = n % Cout;
+      dw[((int64_t)k1 * Cout + c) * 4 + ij] = t;
+    } else {
+      dw[(int64_t)n * K1 + k1] = t;
     }
   }
 }
@@ -240,9 +256,9 @@ static hipError_t launch_atb(const XL& X, const YL& Y, int64_t M, int K1, int N,
                      npad);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  const int total = K1 * N + npad;
-  hipLaunchKernelGGL(k_atb_reduce, dim3(cdiv(total, 256)), dim3(256), 0, s, part, csum, dw, db,
-                     (int)nsplit, k1pad, npad, K1, N, Cout, mode);
+  const int nwb = cdiv(k1pad * npad, 32);
+  hipLaunchKernelGGL(k_atb_reduce, dim3(nwb + cdiv(Cout, 32)), dim3(256), 0, s, part, csum, dw,
+                     db, (int)nsplit, k1pad, npad, K1, N, Cout, mode, nwb);
   return hipGetLastError();
 }
 
