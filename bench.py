@@ -33,6 +33,17 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 = f32 vector peak
+# dense bf16 MFMA: 256 CUs x 4 SIMDs x 1024 flop/clk (32x32x16 in 32 cycles) x 2.4 GHz
+BF16_MFMA_PEAK_TFLOPS = 256 * 4 * 1024 * 2.4e9 / 1e12
+# fp32-equivalent peak of each conv arithmetic: bf16x6 runs 6 bf16 MFMA products per
+# fp32 multiply-add, bf16x3 runs 3
+MATH_PEAK = {"f32": FP32_MFMA_PEAK_TFLOPS, "bf16x6": BF16_MFMA_PEAK_TFLOPS / 6,
+             "bf16x3": BF16_MFMA_PEAK_TFLOPS / 3}
+MATH_KERNEL = {"f32": "k_conv3d_fwd (fp32 MFMA 3x3x3 implicit GEMM, fwd+dgrad)",
+               "bf16x6": "k_conv3d_fwd_x<.,.,3> (3-plane split-bf16 MFMA 3x3x3 implicit GEMM, "
+                         "fwd+dgrad)",
+               "bf16x3": "k_conv3d_fwd_x<.,.,2> (2-plane split-bf16 MFMA 3x3x3 implicit GEMM, "
+                         "fwd+dgrad)"}
 HBM_PEAK_GBS = 8000.0
 
 
@@ -88,6 +99,9 @@ def main():
     ap.add_argument("--classes", type=int, default=13)
     ap.add_argument("--base", type=int, default=32)
     ap.add_argument("--cpu-baseline", choices=("auto", "skip"), default="auto")
+    ap.add_argument("--math", choices=("f32", "bf16x6", "bf16x3"), default="bf16x6",
+                    help="conv arithmetic: bf16x6 = fp32 operands split exactly into 3 bf16 "
+                         "planes, 6 products, fp32 accumulate (fp32 accuracy class; default)")
     ap.add_argument("--cpu-depth", type=int, default=32)
     ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--pmc", default=str(ROOT / "profiles" / "r01_pmc_conv.json"),
@@ -107,6 +121,7 @@ def main():
 
     B, S, K = args.batch, args.size, args.classes
     core, st = build_model(K, args.base, args.in_ch, S, device)
+    core.math = args.math
     x, y = synthetic_batch(B, args.in_ch, S, S, S, K, ignore_frac=0.01, seed=1000 + rank,
                            device=device)
     dp = DataParallelSPFF(core, K, 255)
@@ -140,7 +155,7 @@ def main():
     vox_step = B * S * S * S
     value = world * vox_step * args.steps / elapsed
 
-    # dominant kernel: k_conv3d_fwd (forward + dgrad convs, fp32 MFMA), timed live
+    # dominant kernel: the fwd/dgrad conv kernel (forward + input-grad convs), timed live
     ms = prof["conv_fwd"][0] + prof["conv_dgrad"][0]
     fl = prof["conv_fwd"][1] + prof["conv_dgrad"][1]
     nl = prof["conv_fwd"][2] + prof["conv_dgrad"][2]
@@ -151,9 +166,16 @@ def main():
         traffic = pm.get("hbm_bytes_per_launch")
     except Exception:
         traffic = None
-    roof = {"bound": "mfma", "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": (achieved / FP32_MFMA_PEAK_TFLOPS) if achieved else None, "traffic": traffic,
-            "kernel": "k_conv3d_fwd (3x3x3 implicit GEMM, fwd+dgrad)",
+    peak = MATH_PEAK[args.math]
+    roof = {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+            "frac": (achieved / peak) if achieved else None, "traffic": traffic,
+            "kernel": MATH_KERNEL[args.math],
+            "peak_note": ("algorithmic fp32 flops (2*V*Cin*Cout*27 per conv); peak = the "
+                          f"{args.math} arithmetic's fp32-equivalent MFMA peak"
+                          + ("" if args.math == "f32" else
+                             f" = dense bf16 MFMA {BF16_MFMA_PEAK_TFLOPS:.0f} / "
+                             f"{6 if args.math == 'bf16x6' else 3} products")),
+            "frac_of_fp32_mfma_peak": (achieved / FP32_MFMA_PEAK_TFLOPS) if achieved else None,
             "avg_launch_ms": ms / max(1, nl), "launches": int(nl),
             "algorithmic_flops_per_launch": fl / max(1, nl),
             "per_class_ms_per_step": {k: v[0] / args.steps for k, v in prof.items()},
@@ -165,6 +187,7 @@ def main():
         "value": value, "unit": "voxels/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "conv_math": args.math,
         "data": "synthetic (x~N(0,1), labels U[0,K) with 1% ignore=255; weights from weightgen seed 0)",
         "config": {"workload": f"SPFF-UNet fwd+ce_plus_macro_dice+bwd, batch {B} x {args.in_ch}ch x "
                                f"{S}^3 per GPU, K={K}, base {args.base}",

@@ -36,6 +36,16 @@ extern "C" {
 #define SPFF_EHIP (-2)
 #define SPFF_ESHAPE (-3)
 
+/* arithmetic of the 3x3x3 conv contractions (spff_cfg.math):
+ *   SPFF_MATH_F32     fp32 MFMA (v_mfma_f32_32x32x2_f32, an exact fp32 fma chain)
+ *   SPFF_MATH_BF16X6  fp32 operands split exactly into 3 bf16 planes, 6 cross
+ *                     products on the bf16 MFMA, fp32 accumulate: dropped terms
+ *                     < 2^-24 |xy| per product (fp32 accuracy class), ~2.7x the rate
+ *   SPFF_MATH_BF16X3  2 planes, 3 products: ~2^-17 relative per product (opt-in) */
+#define SPFF_MATH_F32 0
+#define SPFF_MATH_BF16X6 1
+#define SPFF_MATH_BF16X3 2
+
 typedef struct spff_cfg {
   int batch, in_ch, depth, height, width;  /* input [B][Cin][D][H][W] */
   int num_classes;                          /* K (<= 32) */
@@ -43,7 +53,8 @@ typedef struct spff_cfg {
   int ksd;                                  /* spectral kernel depth: 1 or 3 */
   int use_efilm, use_fgate;                 /* novel block (models.py:1448) */
   int use_se, use_specse;                   /* encoder post (models.py:684) */
-  int reserved[8];                          /* zero */
+  int math;                                 /* SPFF_MATH_* (0 = fp32 MFMA) */
+  int reserved[7];                          /* zero */
 } spff_cfg;
 
 typedef struct spff_plan spff_plan;
@@ -108,6 +119,11 @@ int spff_conv3d_fwd(const float* x, int ldx, const float* w, float* y, int B, in
                     int cin, int cout, int ksd, void* ws, void* stream);
 int spff_conv3d_dgrad(const float* dy, const float* w, float* dx, int B, int D, int H, int W,
                       int cin, int cout, int ksd, void* ws, void* stream);
+/* the same with an explicit SPFF_MATH_* arithmetic (the two above use SPFF_MATH_F32) */
+int spff_conv3d_fwd_ex(const float* x, int ldx, const float* w, float* y, int B, int D, int H,
+                       int W, int cin, int cout, int ksd, int math, void* ws, void* stream);
+int spff_conv3d_dgrad_ex(const float* dy, const float* w, float* dx, int B, int D, int H, int W,
+                         int cin, int cout, int ksd, int math, void* ws, void* stream);
 int spff_conv3d_wgrad(const float* x, int ldx, const float* dy, float* dw, int B, int D, int H,
                       int W, int cin, int cout, int ksd, void* ws, void* stream);
 

@@ -3,6 +3,7 @@
 headline shapes (batch 2, 128^3, base 32).  Prints ms and TFLOP/s per op.
 
     python scripts/kbench.py [--ops fwd,dgrad,wgrad] [--iters 5] [--layers all|l0|...]
+                             [--math f32|bf16x6|bf16x3]
 """
 import argparse
 import pathlib
@@ -30,11 +31,14 @@ def main():
     ap.add_argument("--batch", type=int, default=2)
     ap.add_argument("--size", type=int, default=128)
     ap.add_argument("--layers", default="all")
+    ap.add_argument("--math", default="f32", choices=sorted(E.MATH_NAMES))
     args = ap.parse_args()
     L, p = E.lib(), E._ptr
     dev = torch.device("cuda", 0)
     st = E._stream(dev)
     ops = args.ops.split(",")
+    m = E.MATH_NAMES[args.math]
+    print(f"math={args.math}")
     tot = {o: [0.0, 0.0] for o in ops}
     for name, lvl, cin, cout in LAYERS:
         if args.layers != "all" and not name.startswith(args.layers):
@@ -50,8 +54,10 @@ def main():
                          device=dev)
         flops = 2.0 * B * D * H * W * cin * cout * 27
         calls = {
-            "fwd": lambda: L.spff_conv3d_fwd(p(x), ldx, p(w), p(y), B, D, H, W, cin, cout, 3, p(ws), st),
-            "dgrad": (lambda: L.spff_conv3d_dgrad(p(y), p(w), p(dx), B, D, H, W, cin, cout, 3, p(ws), st))
+            "fwd": lambda: L.spff_conv3d_fwd_ex(p(x), ldx, p(w), p(y), B, D, H, W, cin, cout, 3, m,
+                                                p(ws), st),
+            "dgrad": (lambda: L.spff_conv3d_dgrad_ex(p(y), p(w), p(dx), B, D, H, W, cin, cout, 3, m,
+                                                     p(ws), st))
             if dx is not None else None,
             "wgrad": lambda: L.spff_conv3d_wgrad(p(x), ldx, p(y), p(dw), B, D, H, W, cin, cout, 3, p(ws), st),
         }

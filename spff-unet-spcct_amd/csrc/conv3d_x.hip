@@ -1,0 +1,379 @@
+// 3x3x3 convolution forward / input-gradient on the bf16 matrix cores with an
+// fp32-faithful operand split ("bf16x6"), plus the layer-level dispatcher.
+//
+// Replaces nn.Conv3d(cin, cout, (ksd,3,3), padding=(ksd//2,1,1), bias=False)
+// (reference models.py:616-618) forward and its input gradient, like
+// k_conv3d_fwd in conv3d.hip, but at the bf16 MFMA rate (16x the f32 rate).
+//
+// Numerics.  Every fp32 operand is split exactly into three bf16 planes,
+//   x = h + m + l (+ e),  h = bf16(x), m = bf16(x - h), l = bf16(x - h - m),
+// |m| <= 2^-8 |x|, |l| <= 2^-16 |x|, |e| <= 2^-25 |x|; both subtractions are exact
+// in fp32.  The six products hh, hm, mh, hl, lh, mm are accumulated by the
+// MFMA in fp32; the dropped terms ml + lm + ll + e are below 2^-24 |xy|, i.e.
+// under half an fp32 ulp of each product -- the same accuracy class as the f32
+// MFMA (an fp32 fma chain).  math = SPFF_MATH_BF16X3 keeps only h, l
+// (x = h + l, |err| <= 2^-17) and hh, hl, lh: 2x faster, ~1e-5 relative.
+//
+// Structure (gfx950, 8 waves = 512 threads, one workgroup per CU):
+//  * output tile 2 x 16 x 16 = 512 voxels x BN out channels; MFMA
+//    v_mfma_f32_32x32x16_bf16, rows = voxels, cols = out channels,
+//    k = (tap parity, 8 input channels): per input-channel chunk of 8 the 27
+//    taps are walked as 14 tap pairs (lane half h takes tap 2j+h; tap 27 is a
+//    zero weight row).
+//  * LDS: halo [plane][pos][8ch] and weight slab [plane][tap][co][8ch], 16-byte
+//    units read with ds_read_b128.  Lanes of one ds_read_b128 group must hit
+//    distinct pos mod 16: a 32-row block covers two W-rows of 16 voxels and the
+//    second row is rotated by 2 (tw = (r + 14) mod 16), which cancels the halo
+//    row pitch 18 = 2 mod 16 -- conflict-free without padding.
+//  * register-prefetch pipeline as in k_conv3d_fwd: chunk c+1's halo (fp32)
+//    and weight slab (both fp32) are in flight during chunk c's MFMAs, and
+//    are split into bf16 planes on their way into LDS.
+#include "spff_internal.h"
+
+#include <cstdlib>
+#include <cstring>
+
+namespace spff {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+static inline int rup(int a, int b) { return cdiv(a, b) * b; }
+
+__device__ __forceinline__ unsigned short bfbits(__bf16 v) {
+  return __builtin_bit_cast(unsigned short, v);
+}
+// exact split of x into NS bf16 planes (planes past NS-1 get the remainder)
+template <int NS>
+__device__ __forceinline__ void split_bf16(float x, unsigned short (&o)[NS]) {
+  float r = x;
+#pragma unroll
+  for (int p = 0; p < NS; ++p) {
+    const __bf16 b = (__bf16)r;
+    o[p] = bfbits(b);
+    r = r - (float)b;
+  }
+}
+
+// ------------------------------------------------------------ weight pack --
+// wp[kc][T2][npad][8] fp32: gemm k = kc*8 + e, gemm n; fwd: k = ci, n = co;
+// dgrad: k = co, n = ci with the tap flipped.  Taps >= T are zero.  The kernel
+// splits it into bf16 planes on its way into LDS.
+__global__ void k_conv_pack_x(const float* __restrict__ w, float* __restrict__ wp, int Cout,
+                              int Cin, int T, int T2, int nkc, int npad, int dgrad) {
+  const int64_t total = (int64_t)nkc * T2 * npad * 8;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int e = (int)(i & 7);
+    const int n = (int)((i >> 3) % npad);
+    const int tap = (int)((i / (8 * (int64_t)npad)) % T2);
+    const int kc = (int)(i / (8 * (int64_t)npad * T2));
+    const int k = kc * 8 + e;
+    float v = 0.f;
+    if (tap < T) {
+      if (!dgrad) {
+        if (k < Cin && n < Cout) v = w[((int64_t)n * Cin + k) * T + tap];
+      } else {
+        if (k < Cout && n < Cin) v = w[((int64_t)k * Cin + n) * T + (T - 1 - tap)];
+      }
+    }
+    wp[i] = v;
+  }
+}
+
+// ------------------------------------------------------------ fwd / dgrad --
+namespace {
+constexpr int XT_D = 2, XT_H = 16, XT_W = 16, XT_THREADS = 512, XT_MB = 2;
+template <int KD>
+__host__ __device__ constexpr int xt_npos() {
+  return (XT_D + KD - 1) * (XT_H + 2) * (XT_W + 2);
+}
+template <int KD>
+__host__ __device__ constexpr int xt_t2() {
+  return (KD * 9 + 1) & ~1;
+}
+template <int BN, int KD, int NS>
+constexpr size_t xt_lds_bytes() {
+  return (size_t)NS * (xt_npos<KD>() + xt_t2<KD>() * BN) * 16;
+}
+}  // namespace
+
+template <int BN, int KD, int NS>
+__global__ __launch_bounds__(XT_THREADS, 1) void k_conv3d_fwd_x(
+    Src2 x, const float4* __restrict__ wp, Dst2 y, Vol vol, int Cin, int nkc, int Cout, int npad,
+    int tilesD, int tilesH, int tilesW) {
+  constexpr int TD = XT_D, TH = XT_H, TW = XT_W;
+  constexpr int HD = TD + KD - 1, HH = TH + 2, HWD = TW + 2;
+  constexpr int NPOS = xt_npos<KD>();
+  constexpr int T = KD * 9, T2 = xt_t2<KD>(), NJ = T2 / 2;
+  constexpr int NB = BN / 32, MB = XT_MB;
+  constexpr int NHX = NPOS * 2;  // halo float4 per chunk (8 channels = 2 float4)
+  constexpr int RH = (NHX + XT_THREADS - 1) / XT_THREADS;
+  constexpr int NWX = T2 * BN * 2;  // weight float4 per chunk (fp32, split at stash)
+  constexpr int RW = (NWX + XT_THREADS - 1) / XT_THREADS;
+  extern __shared__ uint4 lds4[];
+  uint4* Xs = lds4;               // [NS][NPOS]
+  uint4* Ws = lds4 + NS * NPOS;   // [NS][T2][BN]
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int khalf = lane >> 5, l32 = lane & 31;
+  int t = blockIdx.x;
+  const int twi = t % tilesW; t /= tilesW;
+  const int thi = t % tilesH; t /= tilesH;
+  const int tdi = t % tilesD;
+  const int b = t / tilesD;
+  const int d0 = tdi * TD, h0 = thi * TH, w0 = twi * TW;
+  const int n0 = blockIdx.y * BN;
+  const int D = vol.D, H = vol.H, W = vol.W;
+
+  // voxel of MFMA row r in 32-row block q (q = wave*MB + mb)
+  auto vrow = [](int q, int r, int& td, int& th, int& tw) {
+    td = q >> 3;
+    th = 2 * (q & 7) + (r >> 4);
+    tw = r < 16 ? r : ((r + 14) & 15);
+  };
+  int hpos[MB];
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) {
+    int td, th, tw;
+    vrow(wave * MB + mb, l32, td, th, tw);
+    hpos[mb] = (td * HH + th) * HWD + tw;
+  }
+
+  f32x16 acc[MB][NB];
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[mb][nb][r] = 0.f;
+
+  float4 hreg[RH], wreg[RW];
+  auto fetch = [&](int kc) {
+#pragma unroll
+    for (int k = 0; k < RH; ++k) {
+      const int i = tid + XT_THREADS * k;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (i < NHX) {
+        const int q = i & 1, pos = i >> 1;
+        const int hw = pos % HWD, t2 = pos / HWD, hh = t2 % HH, hd = t2 / HH;
+        const int gd = d0 + hd - KD / 2, gh = h0 + hh - 1, gw = w0 + hw - 1;
+        const int c = kc * 8 + 4 * q;
+        if ((unsigned)gd < (unsigned)D && (unsigned)gh < (unsigned)H &&
+            (unsigned)gw < (unsigned)W && c < Cin) {
+          const int64_t vox = (((int64_t)b * D + gd) * H + gh) * W + gw;
+          const float* p =
+              c < x.split ? x.p0 + vox * x.ld0 + c : x.p1 + vox * x.ld1 + (c - x.split);
+          v = *reinterpret_cast<const float4*>(p);
+        }
+      }
+      hreg[k] = v;
+    }
+#pragma unroll
+    for (int k = 0; k < RW; ++k) {
+      const int i = tid + XT_THREADS * k;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (i < NWX) {
+        const int q = i & 1, u = i >> 1;  // unit u = tap * BN + co
+        const int co = u % BN, tap = u / BN;
+        v = wp[(((int64_t)kc * T2 + tap) * npad + n0 + co) * 2 + q];
+      }
+      wreg[k] = v;
+    }
+  };
+  // split 4 consecutive channels into NS planes: 8 bytes per plane at dst[p*pitch]
+  auto put4 = [&](const float4& v, uint4* dst, int pitch, int q) {
+    unsigned short s0[NS], s1[NS], s2[NS], s3[NS];
+    split_bf16<NS>(v.x, s0);
+    split_bf16<NS>(v.y, s1);
+    split_bf16<NS>(v.z, s2);
+    split_bf16<NS>(v.w, s3);
+#pragma unroll
+    for (int p = 0; p < NS; ++p) {
+      uint2 u;
+      u.x = (unsigned)s0[p] | ((unsigned)s1[p] << 16);
+      u.y = (unsigned)s2[p] | ((unsigned)s3[p] << 16);
+      reinterpret_cast<uint2*>(dst + p * pitch)[q] = u;
+    }
+  };
+  auto stash = [&]() {
+#pragma unroll
+    for (int k = 0; k < RH; ++k) {
+      const int i = tid + XT_THREADS * k;
+      if (i < NHX) put4(hreg[k], Xs + (i >> 1), NPOS, i & 1);
+    }
+#pragma unroll
+    for (int k = 0; k < RW; ++k) {
+      const int i = tid + XT_THREADS * k;
+      if (i < NWX) put4(wreg[k], Ws + (i >> 1), T2 * BN, i & 1);
+    }
+  };
+
+  fetch(0);
+  for (int kc = 0; kc < nkc; ++kc) {
+    if (kc) __syncthreads();
+    stash();
+    __syncthreads();
+    if (kc + 1 < nkc) fetch(kc + 1);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      // lane half h takes tap 2j+h; the padding tap (>= T) reads a valid
+      // position against a zero weight row
+      const int tp0 = 2 * j, tp1 = (2 * j + 1 < T) ? 2 * j + 1 : T - 1;
+      const int toff0 = ((tp0 / 9) * HH + (tp0 / 3) % 3) * HWD + tp0 % 3;
+      const int toff1 = ((tp1 / 9) * HH + (tp1 / 3) % 3) * HWD + tp1 % 3;
+      const int toff = khalf ? toff1 : toff0;
+      const int wtap = 2 * j + khalf;
+      bf16x8 a[MB][NS], bm[NB][NS];
+#pragma unroll
+      for (int p = 0; p < NS; ++p) {
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb)
+          a[mb][p] = __builtin_bit_cast(bf16x8, Xs[p * NPOS + hpos[mb] + toff]);
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb)
+          bm[nb][p] = __builtin_bit_cast(bf16x8, Ws[(p * T2 + wtap) * BN + nb * 32 + l32]);
+      }
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) {
+          f32x16 c = acc[mb][nb];
+          if constexpr (NS == 3) {
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mb][1], bm[nb][1], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mb][0], bm[nb][2], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mb][2], bm[nb][0], c, 0, 0, 0);
+          }
+          if constexpr (NS >= 2) {
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mb][0], bm[nb][1], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mb][1], bm[nb][0], c, 0, 0, 0);
+          }
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mb][0], bm[nb][0], c, 0, 0, 0);
+          acc[mb][nb] = c;
+        }
+    }
+  }
+
+  // ---- epilogue: C[i][j], row i = voxel (vrow mapping), col j = out channel ----
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int i = (r & 3) + 8 * (r >> 2) + 4 * khalf;
+      int td, th, tw;
+      vrow(wave * MB + mb, i, td, th, tw);
+      const int gd = d0 + td, gh = h0 + th, gw = w0 + tw;
+      if (gd >= D || gh >= H || gw >= W) continue;
+      const int64_t vox = (((int64_t)b * D + gd) * H + gh) * W + gw;
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) {
+        const int n = n0 + nb * 32 + l32;
+        if (n >= Cout) continue;
+        float* p = n < y.split ? y.p0 + vox * y.ld0 + n : y.p1 + vox * y.ld1 + (n - y.split);
+        *p = acc[mb][nb][r];
+      }
+    }
+  }
+}
+
+template <int BN, int KD, int NS>
+static hipError_t launch_fwd_x(const Src2& x, const float4* wx, const Dst2& y, Vol vol, int K,
+                               int nkc, int N, int npad, hipStream_t s) {
+  constexpr size_t shm = xt_lds_bytes<BN, KD, NS>();
+  static_assert(shm <= 160 * 1024, "LDS budget");
+  auto kern = k_conv3d_fwd_x<BN, KD, NS>;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  const int tilesD = cdiv(vol.D, XT_D), tilesH = cdiv(vol.H, XT_H), tilesW = cdiv(vol.W, XT_W);
+  dim3 grid(vol.B * tilesD * tilesH * tilesW, npad / BN);
+  hipLaunchKernelGGL(kern, grid, dim3(XT_THREADS), shm, s, x, wx, y, vol, K, nkc, N, npad, tilesD,
+                     tilesH, tilesW);
+  return hipGetLastError();
+}
+
+namespace {
+struct XDims {
+  int K, N, BN, nkc, npad, T, T2;
+};
+XDims xdims(int KD, int Cin_w, int Cout_w, bool dgrad) {
+  XDims d;
+  d.K = dgrad ? Cout_w : Cin_w;
+  d.N = dgrad ? Cin_w : Cout_w;
+  d.BN = d.N >= 64 ? 64 : 32;
+  d.nkc = cdiv(d.K, 8);
+  d.npad = rup(d.N, d.BN);
+  d.T = KD * 9;
+  d.T2 = (d.T + 1) & ~1;
+  return d;
+}
+// SPFF_DEBUG_SPLIT=fwd|dgrad (diagnostics only) limits the split path to one direction
+int debug_split_dir() {
+  static int v = [] {
+    const char* e = getenv("SPFF_DEBUG_SPLIT");
+    if (!e) return 0;
+    return strcmp(e, "fwd") == 0 ? 1 : strcmp(e, "dgrad") == 0 ? 2 : 0;
+  }();
+  return v;
+}
+bool use_split(Vol vol, int math, bool dgrad) {
+  const int dbg = debug_split_dir();
+  if (dbg && dbg != (dgrad ? 2 : 1)) return false;
+  return math != SPFF_MATH_F32 && vol.H >= XT_H && vol.W >= XT_W;
+}
+}  // namespace
+
+// ----------------------------------------------------------- dispatcher --
+size_t conv3d_pack_bytes(int KD, int Cin, int Cout) {
+  size_t f32 = 0, x = 0;
+  for (int dg = 0; dg < 2; ++dg) {
+    const XDims d = xdims(KD, Cin, Cout, dg != 0);
+    f32 = std::max(f32, (size_t)d.T * rup(d.K, 8) * rup(d.N, conv3d_bn(d.N)) * sizeof(float));
+    x = std::max(x, (size_t)d.T2 * d.nkc * 8 * d.npad * sizeof(float));
+  }
+  return std::max(f32, x);
+}
+
+hipError_t conv3d_pack(const float* w, void* wpack, Vol vol, int KD, int Cin_w, int Cout_w,
+                       bool dgrad, int math, hipStream_t s) {
+  const XDims d = xdims(KD, Cin_w, Cout_w, dgrad);
+  if (use_split(vol, math, dgrad)) {
+    const int64_t total = (int64_t)d.nkc * d.T2 * d.npad * 8;
+    const int grid = (int)std::min<int64_t>((total + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_conv_pack_x, dim3(grid), dim3(256), 0, s, w, static_cast<float*>(wpack),
+                       Cout_w, Cin_w, d.T, d.T2, d.nkc, d.npad, dgrad ? 1 : 0);
+    return hipGetLastError();
+  }
+  return conv_pack_weights(w, static_cast<float*>(wpack), Cout_w, Cin_w, KD, rup(d.K, 8),
+                           rup(d.N, conv3d_bn(d.N)), dgrad, s);
+}
+
+template <int NS>
+static hipError_t run_x(const Src2& x, const float4* wu, const Dst2& y, Vol vol, int KD,
+                        const XDims& d, hipStream_t s) {
+  if (d.BN == 64)
+    return KD == 3 ? launch_fwd_x<64, 3, NS>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s)
+                   : launch_fwd_x<64, 1, NS>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s);
+  return KD == 3 ? launch_fwd_x<32, 3, NS>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s)
+                 : launch_fwd_x<32, 1, NS>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s);
+}
+
+hipError_t conv3d_run(const Src2& x, const void* wpack, const Dst2& y, Vol vol, int KD,
+                      int Cin_w, int Cout_w, bool dgrad, int math, hipStream_t s) {
+  const XDims d = xdims(KD, Cin_w, Cout_w, dgrad);
+  if (use_split(vol, math, dgrad)) {
+    const float4* wu = static_cast<const float4*>(wpack);
+    return math == SPFF_MATH_BF16X3 ? run_x<2>(x, wu, y, vol, KD, d, s)
+                                    : run_x<3>(x, wu, y, vol, KD, d, s);
+  }
+  return conv3d_fwd(x, static_cast<const float*>(wpack), y, vol, KD, d.K, rup(d.K, 8), d.N,
+                    rup(d.N, conv3d_bn(d.N)), s);
+}
+
+}  // namespace spff

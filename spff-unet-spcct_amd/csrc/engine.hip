@@ -183,10 +183,7 @@ void conv_dims(ConvL& c, int Cin, int Cout) {
   c.npad_d = rup(Cin, conv3d_bn(Cin));
 }
 
-size_t conv_pack_bytes(const ConvL& c, int KD) {
-  size_t a = (size_t)KD * 9 * c.kpad_f * c.npad_f, b = (size_t)KD * 9 * c.kpad_d * c.npad_d;
-  return (a > b ? a : b) * sizeof(float);
-}
+size_t conv_pack_bytes(const ConvL& c, int KD) { return conv3d_pack_bytes(KD, c.Cin, c.Cout); }
 
 void host_pe(int D, std::vector<float>& pe) {
   // models.py:1495-1503 in fp32: denom = exp(i * (-ln(1e4)/8)), pe = [sin(pos*denom); cos(...)]
@@ -214,6 +211,8 @@ int build_plan(spff_plan* p) {
                 "H and W must be multiples of 8 (three (1,2,2) pools without the trilinear _cat "
                 "fallback of models.py:689-690)");
   if (c.in_ch > 64) return fail(SPFF_EINVAL, "in_ch > 64 not supported");
+  if (c.math < SPFF_MATH_F32 || c.math > SPFF_MATH_BF16X3)
+    return fail(SPFF_EINVAL, "math must be one of SPFF_MATH_*");
   p->f = c.base;
   p->KD = c.ksd;
   p->K = c.num_classes;
@@ -394,20 +393,18 @@ int in_stats(spff_plan* p, const Vol& v, int C, size_t y, size_t mean, size_t rs
 int fwd_block(spff_plan* p, Blk& b, const Src2& in) {
   const Vol& v = p->vol[b.lvl];
   const int C = b.C, KD = p->KD;
-  HIPCK(conv_pack_weights(p->P(b.c1.w), p->F(p->wt), C, b.Cin, KD, b.c1.kpad_f, b.c1.npad_f,
-                          false, p->st));
+  const int math = p->cfg.math;
+  HIPCK(conv3d_pack(p->P(b.c1.w), p->F(p->wt), v, KD, b.Cin, C, false, math, p->st));
   const double V = (double)nvox(v), T = 9.0 * KD;
   PROF(p, 0, 2.0 * V * b.Cin * C * T,
-       conv3d_fwd(in, p->F(p->wt), dst1(p->F(b.y1), C), v, KD, b.Cin, b.c1.kpad_f, C,
-                  b.c1.npad_f, p->st));
+       conv3d_run(in, p->F(p->wt), dst1(p->F(b.y1), C), v, KD, b.Cin, C, false, math, p->st));
   CK(in_stats(p, v, C, b.y1, b.mean1, b.rstd1, b.al1, b.de1, b.g1, b.b1));
   HIPCK(act_apply(p->F(b.y1), p->F(b.a1), p->F(b.al1), p->F(b.de1), nullptr, nullptr, v, C,
                   p->st));
-  HIPCK(conv_pack_weights(p->P(b.c2.w), p->F(p->wt), C, C, KD, b.c2.kpad_f, b.c2.npad_f, false,
-                          p->st));
+  HIPCK(conv3d_pack(p->P(b.c2.w), p->F(p->wt), v, KD, C, C, false, math, p->st));
   PROF(p, 0, 2.0 * V * C * C * T,
-       conv3d_fwd(src1(p->F(b.a1), C), p->F(p->wt), dst1(p->F(b.y2), C), v, KD, C,
-                  b.c2.kpad_f, C, b.c2.npad_f, p->st));
+       conv3d_run(src1(p->F(b.a1), C), p->F(p->wt), dst1(p->F(b.y2), C), v, KD, C, C, false,
+                  math, p->st));
   CK(in_stats(p, v, C, b.y2, b.mean2, b.rstd2, b.al2, b.de2, b.g2, b.b2));
   if (b.tail()) {
     RedArgs a{};
@@ -473,11 +470,10 @@ int bwd_block(spff_plan* p, Blk& b, const float* dout, const Dst2* dx, const Src
   PROF(p, 2, 2.0 * V * C * C * T,
        conv3d_wgrad(src1(p->F(b.a1), C), dy2, C, p->DP(b.c2.w), v, KD, C, C, p->F(p->wg_ws),
                     p->st));
-  HIPCK(conv_pack_weights(p->P(b.c2.w), p->F(p->wt), C, C, KD, b.c2.kpad_d, b.c2.npad_d, true,
-                          p->st));
+  const int math = p->cfg.math;
+  HIPCK(conv3d_pack(p->P(b.c2.w), p->F(p->wt), v, KD, C, C, true, math, p->st));
   PROF(p, 1, 2.0 * V * C * C * T,
-       conv3d_fwd(src1(dy2, C), p->F(p->wt), dst1(da1, C), v, KD, C, b.c2.kpad_d, C,
-                  b.c2.npad_d, p->st));
+       conv3d_run(src1(dy2, C), p->F(p->wt), dst1(da1, C), v, KD, C, C, true, math, p->st));
   {
     RedArgs a{};
     a.y = p->F(b.y1); a.g = da1; a.mean = p->F(b.mean1); a.rstd = p->F(b.rstd1);
@@ -492,11 +488,9 @@ int bwd_block(spff_plan* p, Blk& b, const float* dout, const Dst2* dx, const Src
   PROF(p, 2, 2.0 * V * b.Cin * C * T,
        conv3d_wgrad(in, da1, C, p->DP(b.c1.w), v, KD, b.Cin, C, p->F(p->wg_ws), p->st));
   if (dx) {
-    HIPCK(conv_pack_weights(p->P(b.c1.w), p->F(p->wt), C, b.Cin, KD, b.c1.kpad_d, b.c1.npad_d,
-                            true, p->st));
+    HIPCK(conv3d_pack(p->P(b.c1.w), p->F(p->wt), v, KD, b.Cin, C, true, math, p->st));
     PROF(p, 1, 2.0 * V * b.Cin * C * T,
-         conv3d_fwd(src1(da1, C), p->F(p->wt), *dx, v, KD, C, b.c1.kpad_d, b.Cin, b.c1.npad_d,
-                    p->st));
+         conv3d_run(src1(da1, C), p->F(p->wt), *dx, v, KD, b.Cin, C, true, math, p->st));
   }
   return SPFF_OK;
 }
@@ -675,6 +669,8 @@ int spff_saved_tensor(const spff_plan* p, void* ws, const char* name, const floa
     const size_t off = n == "grad.out" ? p->G_out : n == "grad.dy2" ? p->G_dy2 :
                        n == "grad.da1" ? p->G_da1 : n == "grad.dx" ? p->G_dx : 0;
     if (off) return ret(off, p->vol[0], p->f);
+    for (int l = 0; l < 3; ++l)  // total gradient at encoder output l after a backward
+      if (n == "grad.dskip" + std::to_string(l)) return ret(p->dskip[l], p->vol[l], p->f << l);
   }
   for (int i = 0; i < 7; ++i) {
     const Blk& b = p->blk[i];
@@ -771,33 +767,39 @@ size_t spff_conv3d_ws_bytes(int B, int D, int H, int W, int cin, int cout, int k
          conv3d_wgrad_ws_bytes(v, ksd, cin, cout);
 }
 
-int spff_conv3d_fwd(const float* x, int ldx, const float* w, float* y, int B, int D, int H, int W,
-                    int cin, int cout, int ksd, void* ws, void* stream) {
+int spff_conv3d_fwd_ex(const float* x, int ldx, const float* w, float* y, int B, int D, int H,
+                       int W, int cin, int cout, int ksd, int math, void* ws, void* stream) {
   if (!x || !w || !y || !ws) return fail(SPFF_EINVAL, "null argument");
   if (ldx % 4 || ldx < cin) return fail(SPFF_EINVAL, "ldx must be >= cin and a multiple of 4");
   if (cout % 4) return fail(SPFF_EINVAL, "cout must be a multiple of 4");
+  if (math < SPFF_MATH_F32 || math > SPFF_MATH_BF16X3) return fail(SPFF_EINVAL, "bad math");
   hipStream_t s = static_cast<hipStream_t>(stream);
-  ConvL c;
-  conv_dims(c, cin, cout);
-  float* wt = static_cast<float*>(ws);
-  HIPCK(conv_pack_weights(w, wt, cout, cin, ksd, c.kpad_f, c.npad_f, false, s));
-  HIPCK(conv3d_fwd(src1(x, ldx), wt, dst1(y, cout), Vol{B, D, H, W}, ksd, cin, c.kpad_f, cout,
-                   c.npad_f, s));
+  const Vol v{B, D, H, W};
+  HIPCK(conv3d_pack(w, ws, v, ksd, cin, cout, false, math, s));
+  HIPCK(conv3d_run(src1(x, ldx), ws, dst1(y, cout), v, ksd, cin, cout, false, math, s));
+  return SPFF_OK;
+}
+
+int spff_conv3d_fwd(const float* x, int ldx, const float* w, float* y, int B, int D, int H, int W,
+                    int cin, int cout, int ksd, void* ws, void* stream) {
+  return spff_conv3d_fwd_ex(x, ldx, w, y, B, D, H, W, cin, cout, ksd, SPFF_MATH_F32, ws, stream);
+}
+
+int spff_conv3d_dgrad_ex(const float* dy, const float* w, float* dx, int B, int D, int H, int W,
+                         int cin, int cout, int ksd, int math, void* ws, void* stream) {
+  if (!dy || !w || !dx || !ws) return fail(SPFF_EINVAL, "null argument");
+  if (cout % 4 || cin % 4) return fail(SPFF_EINVAL, "channels must be multiples of 4");
+  if (math < SPFF_MATH_F32 || math > SPFF_MATH_BF16X3) return fail(SPFF_EINVAL, "bad math");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const Vol v{B, D, H, W};
+  HIPCK(conv3d_pack(w, ws, v, ksd, cin, cout, true, math, s));
+  HIPCK(conv3d_run(src1(dy, cout), ws, dst1(dx, cin), v, ksd, cin, cout, true, math, s));
   return SPFF_OK;
 }
 
 int spff_conv3d_dgrad(const float* dy, const float* w, float* dx, int B, int D, int H, int W,
                       int cin, int cout, int ksd, void* ws, void* stream) {
-  if (!dy || !w || !dx || !ws) return fail(SPFF_EINVAL, "null argument");
-  if (cout % 4 || cin % 4) return fail(SPFF_EINVAL, "channels must be multiples of 4");
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  ConvL c;
-  conv_dims(c, cin, cout);
-  float* wt = static_cast<float*>(ws);
-  HIPCK(conv_pack_weights(w, wt, cout, cin, ksd, c.kpad_d, c.npad_d, true, s));
-  HIPCK(conv3d_fwd(src1(dy, cout), wt, dst1(dx, cin), Vol{B, D, H, W}, ksd, cout, c.kpad_d, cin,
-                   c.npad_d, s));
-  return SPFF_OK;
+  return spff_conv3d_dgrad_ex(dy, w, dx, B, D, H, W, cin, cout, ksd, SPFF_MATH_F32, ws, stream);
 }
 
 int spff_conv3d_wgrad(const float* x, int ldx, const float* dy, float* dw, int B, int D, int H,

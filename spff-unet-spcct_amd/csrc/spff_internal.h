@@ -3,6 +3,7 @@
 // fp32 ("NDHWC"), voxel index v = ((b*D + d)*H + h)*W + w.
 #pragma once
 #include <hip/hip_runtime.h>
+#include "spff.h"
 #include <stdint.h>
 #include <stddef.h>
 
@@ -34,6 +35,16 @@ hipError_t conv_pack_weights(const float* w, float* wt, int Cout, int Cin, int K
 hipError_t conv3d_fwd(const Src2& x, const float* wt, const Dst2& y, Vol vol, int KD,
                       int Cin, int kpad, int Cout, int npad, hipStream_t s);
 int conv3d_bn(int Cout);        // output-channel tile the fwd kernel uses
+// Layer-level conv (conv3d_x.hip): pack W[Cout_w][Cin_w][KD][3][3] for the
+// forward (dgrad = false: x has Cin_w channels, y Cout_w) or the input gradient
+// (dgrad = true: x = dy with Cout_w channels, y = dx with Cin_w) in the layout
+// the chosen arithmetic (SPFF_MATH_*) runs on, then run it.  Volumes smaller
+// than one 16 x 16 H/W tile take the fp32 kernel whatever the math.
+size_t conv3d_pack_bytes(int KD, int Cin_w, int Cout_w);
+hipError_t conv3d_pack(const float* w, void* wpack, Vol vol, int KD, int Cin_w, int Cout_w,
+                       bool dgrad, int math, hipStream_t s);
+hipError_t conv3d_run(const Src2& x, const void* wpack, const Dst2& y, Vol vol, int KD,
+                      int Cin_w, int Cout_w, bool dgrad, int math, hipStream_t s);
 // dW partials + reduction into reference layout dw[Cout][Cin][KD][3][3].
 size_t conv3d_wgrad_ws_bytes(Vol vol, int KD, int Cin, int Cout);
 hipError_t conv3d_wgrad(const Src2& x, const float* dy, int lddy, float* dw, Vol vol, int KD,

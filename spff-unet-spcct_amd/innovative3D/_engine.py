@@ -28,8 +28,21 @@ class spff_cfg(ctypes.Structure):
         ("height", ctypes.c_int), ("width", ctypes.c_int), ("num_classes", ctypes.c_int),
         ("base", ctypes.c_int), ("ksd", ctypes.c_int), ("use_efilm", ctypes.c_int),
         ("use_fgate", ctypes.c_int), ("use_se", ctypes.c_int), ("use_specse", ctypes.c_int),
-        ("reserved", ctypes.c_int * 8),
+        ("math", ctypes.c_int), ("reserved", ctypes.c_int * 7),
     ]
+
+
+# conv arithmetic (include/spff.h SPFF_MATH_*)
+MATH_F32, MATH_BF16X6, MATH_BF16X3 = 0, 1, 2
+MATH_NAMES = {"f32": MATH_F32, "bf16x6": MATH_BF16X6, "bf16x3": MATH_BF16X3}
+
+
+def default_math() -> str:
+    """Conv arithmetic for new plans: $SPFF_MATH, else "bf16x6" (fp32-faithful split)."""
+    m = os.environ.get("SPFF_MATH", "bf16x6")
+    if m not in MATH_NAMES:
+        raise SpffError(f"SPFF_MATH={m!r}: expected one of {sorted(MATH_NAMES)}")
+    return m
 
 
 _P = ctypes.c_void_p
@@ -61,6 +74,8 @@ _SIGS = {
     "spff_conv3d_ws_bytes": (_S, [_I, _I, _I, _I, _I, _I, _I]),
     "spff_conv3d_fwd": (_I, [_P, _I, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
     "spff_conv3d_dgrad": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
+    "spff_conv3d_fwd_ex": (_I, [_P, _I, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
+    "spff_conv3d_dgrad_ex": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
     "spff_conv3d_wgrad": (_I, [_P, _I, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
 }
 EXPORTED = tuple(_SIGS)
@@ -118,15 +133,20 @@ class Plan:
     the matching backward (``generation`` guards against interleaving)."""
 
     def __init__(self, batch, in_ch, depth, height, width, num_classes, base=32, ksd=3,
-                 efilm=True, fgate=True, se=True, specse=True, device=None):
+                 efilm=True, fgate=True, se=True, specse=True, device=None, math=None):
+        math = default_math() if math is None else math
+        if math not in MATH_NAMES:
+            raise SpffError(f"math={math!r}: expected one of {sorted(MATH_NAMES)}")
         cfg = spff_cfg()
+        cfg.math = MATH_NAMES[math]
+        self.math = math
         cfg.batch, cfg.in_ch, cfg.depth, cfg.height, cfg.width = batch, in_ch, depth, height, width
         cfg.num_classes, cfg.base, cfg.ksd = num_classes, base, ksd
         cfg.use_efilm, cfg.use_fgate, cfg.use_se, cfg.use_specse = (int(bool(efilm)), int(bool(fgate)),
                                                                     int(bool(se)), int(bool(specse)))
         self.cfg = cfg
         self.key = (batch, in_ch, depth, height, width, num_classes, base, ksd, bool(efilm),
-                    bool(fgate), bool(se), bool(specse))
+                    bool(fgate), bool(se), bool(specse), math)
         L = lib()
         h = ctypes.c_void_p()
         check(L.spff_plan_create(ctypes.byref(cfg), ctypes.byref(h)), "spff_plan_create")
@@ -224,7 +244,7 @@ def get_plan(**kw) -> Plan:
     key = (kw["batch"], kw["in_ch"], kw["depth"], kw["height"], kw["width"], kw["num_classes"],
            kw.get("base", 32), kw.get("ksd", 3), bool(kw.get("efilm", True)),
            bool(kw.get("fgate", True)), bool(kw.get("se", True)), bool(kw.get("specse", True)),
-           kw.get("tag", ""))
+           kw.get("math") or default_math(), kw.get("tag", ""))
     if key not in _PLANS:
         kk = dict(kw)
         kk.pop("tag", None)

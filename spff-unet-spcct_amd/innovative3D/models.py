@@ -268,7 +268,8 @@ class UNet3D_SpectralCore(nn.Module):
         return E.get_plan(batch=B, in_ch=C, depth=D, height=H, width=W,
                           num_classes=self.num_classes, base=self.base, ksd=self.ksd,
                           efilm=efilm, fgate=fgate, se=self.use_se, specse=self.use_specse,
-                          device=x.device, tag=f"{id(self)}:{tag}")
+                          device=x.device, math=getattr(self, "math", None),
+                          tag=f"{id(self)}:{tag}")
 
     def _engine_params(self, plan) -> List[nn.Parameter]:
         named = dict(self.named_parameters(remove_duplicate=False))

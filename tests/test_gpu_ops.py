@@ -72,6 +72,62 @@ def test_conv3d_fwd_dgrad_wgrad(case):
         assert float((dxg.cpu() - refx).abs().max()) <= 2e-5 * float(refx.abs().max()) + 1e-6
 
 
+SPLIT_CASES = [
+    # B, D, H, W, cin, cout, ksd  (H, W >= 16: the split-bf16 kernel's tile)
+    (2, 5, 16, 32, 8, 32, 3),
+    (1, 3, 16, 16, 5, 32, 3),     # first layer, Cin=5 padded to ld 8
+    (1, 4, 16, 16, 32, 64, 3),
+    (1, 3, 32, 48, 64, 128, 3),
+    (1, 3, 16, 16, 16, 8, 3),     # Cout < 32
+    (2, 4, 16, 16, 32, 32, 1),    # ksd = 1
+    (1, 5, 24, 40, 16, 16, 3),    # ragged tiles
+]
+
+
+@pytest.mark.parametrize("math_mode", ["bf16x6", "bf16x3"])
+@pytest.mark.parametrize("case", SPLIT_CASES)
+def test_conv3d_split_bf16(case, math_mode):
+    """fwd / dgrad on the bf16 matrix cores with the exact 3-plane (2-plane)
+    operand split, against an fp64 conv.  bf16x6 must be as accurate as the fp32
+    MFMA path (error within 4x of it); bf16x3 within 3e-5 of max|ref|."""
+    B, D, H, W, cin, cout, ksd = case
+    mth = E.MATH_NAMES[math_mode]
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(B, cin, D, H, W, generator=g)
+    w = torch.randn(cout, cin, ksd, 3, 3, generator=g) / math.sqrt(cin * ksd * 9)
+    dy = torch.randn(B, cout, D, H, W, generator=g)
+    y64 = F.conv3d(x.double(), w.double(), None, padding=(ksd // 2, 1, 1))
+    dx64 = torch.nn.grad.conv3d_input(x.shape, w.double(), dy.double(), padding=(ksd // 2, 1, 1))
+    ldx = (cin + 7) // 8 * 8
+    xcl = torch.zeros(B, D, H, W, ldx)
+    xcl[..., :cin] = _cl(x)
+    xcl, wd, dyg = xcl.to(DEV), w.to(DEV), _cl(dy).to(DEV)
+    L, p, st = E.lib(), E._ptr, E._stream(torch.device(DEV))
+    ws = torch.empty(L.spff_conv3d_ws_bytes(B, D, H, W, cin, cout, ksd), dtype=torch.uint8,
+                     device=DEV)
+    out = {}
+    for m in (E.MATH_F32, mth):
+        yg = torch.empty(B, D, H, W, cout, device=DEV)
+        E.check(L.spff_conv3d_fwd_ex(p(xcl), ldx, p(wd), p(yg), B, D, H, W, cin, cout, ksd, m,
+                                     p(ws), st), "fwd")
+        dxg = None
+        if cin % 4 == 0:
+            dxg = torch.empty(B, D, H, W, cin, device=DEV)
+            E.check(L.spff_conv3d_dgrad_ex(p(dyg), p(wd), p(dxg), B, D, H, W, cin, cout, ksd, m,
+                                           p(ws), st), "dgrad")
+        torch.cuda.synchronize()
+        out[m] = (yg.cpu().double(), None if dxg is None else dxg.cpu().double())
+    pairs = [(0, _cl(y64))] + ([(1, _cl(dx64))] if cin % 4 == 0 else [])
+    for k, ref in pairs:
+        e32 = float((out[E.MATH_F32][k] - ref).abs().max())
+        ex = float((out[mth][k] - ref).abs().max())
+        scale = float(ref.abs().max())
+        if math_mode == "bf16x6":
+            assert ex <= 4 * e32 + 1e-7 * scale, (k, ex, e32)
+        else:
+            assert ex <= 3e-5 * scale, (k, ex, scale)
+
+
 @pytest.mark.parametrize("K,shape", [(13, (2, 5, 16, 16)), (9, (1, 16, 32, 32)), (2, (1, 3, 8, 8))])
 def test_loss_matches_oracle(K, shape):
     g = torch.Generator().manual_seed(K)

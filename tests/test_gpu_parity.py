@@ -51,12 +51,17 @@ def near_tie_mask(ref_logits, tol):
     return (top2[:, 1] - top2[:, 0]) < tol
 
 
+@pytest.mark.parametrize("mth", ["f32", "bf16x6", "bf16x3"])
 @pytest.mark.parametrize("name", fixture_names())
-def test_network_matches_reference(name):
+def test_network_matches_reference(name, mth):
+    """f32 and bf16x6 (the fp32-faithful split) are held to the same bar;
+    bf16x3 (opt-in, ~2^-17 per product) to the same logits / argmax bar, loss
+    within 1e-4 and gradients within max(5e-3, 64 x the fp32 oracle's error)."""
     d = load(name)
     meta = d["meta"]
     K = meta["K"]
     core = load_core(d)
+    core.math = mth
     x = torch.from_numpy(d["x"]).to(DEV)
     y = torch.from_numpy(d["labels"]).to(DEV)
     logits = core(x)
@@ -66,14 +71,14 @@ def test_network_matches_reference(name):
     lg = logits.detach().cpu().numpy()
     ref = d["logits"]
     err = float(np.abs(lg - ref).max())
-    print(f"{name}: max|dlogit| = {err:.3e}  loss {float(loss):.7f} vs {float(d['loss']):.7f}")
+    print(f"{name}/{mth}: max|dlogit| = {err:.3e}  loss {float(loss):.7f} vs {float(d['loss']):.7f}")
     assert err <= 1e-3
     am, am_ref = lg.argmax(1), ref.argmax(1)
     flips = am != am_ref
     if flips.any():
         ties = near_tie_mask(ref, 2 * err)
         assert not (flips & ~ties).any(), f"{int(flips.sum())} argmax flips outside near-ties"
-    assert math.isclose(float(loss), float(d["loss"]), rel_tol=1e-5)
+    assert math.isclose(float(loss), float(d["loss"]), rel_tol=1e-4 if mth == "bf16x3" else 1e-5)
     met = M.metrics_from_confusion(conf.cpu().numpy(), K, int(y.numel()))
     if not flips.any():
         np.testing.assert_allclose(np.array(met[0]), d["met_dice"], rtol=1e-12, equal_nan=True)
@@ -93,7 +98,7 @@ def test_network_matches_reference(name):
         scale = max(float(absb[kk].max()), 1e-12)
         e_gpu = float(np.abs(g - g64).max()) / scale
         e_32 = float(np.abs(ref32[kk] - g64).max()) / scale
-        tol = max(1e-3, 8 * e_32)
+        tol = max(5e-3, 64 * e_32) if mth == "bf16x3" else max(1e-3, 8 * e_32)
         rows.append((e_gpu, e_32, kk))
         if e_gpu > tol:
             bad.append(f"{kk}: gpu {e_gpu:.2e} vs fp32-oracle {e_32:.2e}")
@@ -109,7 +114,9 @@ def _block_names(cfg):
 
 
 def engine_lrelu_masks(core, d):
-    """Sign pattern of every LeakyReLU input as the ENGINE saw it: the engine's
+    """Sign pattern of every LeakyReLU input, and the argmax of every max-pool
+    window, as the ENGINE saw them (the pools: from its saved pool inputs; ties
+    resolved first-max like the engine and torch).  The LeakyReLUs: the engine's
     saved conv outputs y1/y2, normalised in fp64.  A fp32 conv differs from the
     reference's by ~1e-6 relative, so an input sitting within that of the kink
     (|r| ~ 0) can take the other slope (1 vs 0.01) -- a legitimate fp32 outcome
@@ -131,6 +138,15 @@ def engine_lrelu_masks(core, d):
             g = torch.from_numpy(st[f"{blk}.{tag}.1.weight"]).double()
             bb = torch.from_numpy(st[f"{blk}.{tag}.1.bias"]).double()
             masks[f"{blk}.{tag}"] = F.instance_norm(y, weight=g, bias=bb, eps=1e-5) > 0
+    # max-pool windows: the engine's own first-max argmax over its pool inputs
+    Dd = d["x"].shape[2]
+    for k, blk in enumerate(("enc1", "enc2", "enc3")):
+        Hh_, Ww = d["x"].shape[3] >> k, d["x"].shape[4] >> k
+        y = plan.saved(f"{blk}.out").double().cpu()
+        C = y.shape[1]
+        y = y.view(B, Dd, Hh_, Ww, C).permute(0, 4, 1, 2, 3)
+        v = y.reshape(B, C, Dd, Hh_ // 2, 2, Ww // 2, 2).permute(0, 1, 2, 3, 5, 4, 6)
+        masks[f"pool{k + 1}"] = v.reshape(B, C, Dd, Hh_ // 2, Ww // 2, 4).argmax(-1)
     return masks
 
 
@@ -144,7 +160,19 @@ def oracle_grads(d, masks):
     st = state_of(d)
     out = []
     nflip = [0]
-    orig = O.conv_in_lrelu
+    orig, orig_pool = O.conv_in_lrelu, O.maxpool
+    npool = [0]
+
+    def pool_hooked(t):
+        k = npool[0] % 3
+        npool[0] += 1
+        idx = masks[f"pool{k + 1}"]
+        B_, C_, D_, H_, W_ = t.shape
+        v = t.reshape(B_, C_, D_, H_ // 2, 2, W_ // 2, 2).permute(0, 1, 2, 3, 5, 4, 6)
+        v = v.reshape(B_, C_, D_, H_ // 2, W_ // 2, 4)
+        if t.dtype == torch.float64:
+            nflip[0] += int((v.detach().argmax(-1) != idx).sum())
+        return v.gather(-1, idx.unsqueeze(-1)).squeeze(-1)
 
     def hooked(P_, pre, inp, ksd):
         y = F.conv3d(inp, P_[pre + ".0.weight"], None, padding=(ksd // 2, 1, 1))
@@ -155,6 +183,7 @@ def oracle_grads(d, masks):
         return torch.where(m, r, 0.01 * r)
 
     O.conv_in_lrelu = hooked
+    O.maxpool = pool_hooked
     try:
         for dt in (torch.float64, torch.float32):
             P = O.params_from_state(st, dtype=dt)
@@ -175,9 +204,11 @@ def oracle_grads(d, masks):
                 (F.cross_entropy(lg, yall[b:b + 1], ignore_index=255, reduction="sum") / N).backward()
                 gb = {k: np.abs(v.grad.numpy()) for k, v in P.items()}
                 absb = gb if absb is None else {k: absb[k] + gb[k] for k in absb}
+            for k in full:
+                masks[k] = full[k]
             masks.update(full)
     finally:
-        O.conv_in_lrelu = orig
+        O.conv_in_lrelu, O.maxpool = orig, orig_pool
     return out[0], out[1], nflip[0], absb
 
 
