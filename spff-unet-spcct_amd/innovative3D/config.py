@@ -69,8 +69,11 @@ def build_from_models(func_name: str, **fixed_kwargs):
 
 
 def build_class(class_name: str, **ctor_kwargs):
-    """Factory that filters kwargs by the constructor signature (config.py:159-182)."""
-    def _factory():
+    """Factory that filters kwargs by the constructor signature (config.py:159-182).
+    Call-time keyword overrides (e.g. ``in_channels=5`` for the north-star
+    5-bin-as-channels layout) are merged over the registered ones."""
+    def _factory(**overrides):
+        ctor = {**ctor_kwargs, **overrides}
         mod = import_module("innovative3D.models")
         cls = getattr(mod, class_name, None)
         if cls is None:
@@ -78,12 +81,12 @@ def build_class(class_name: str, **ctor_kwargs):
         try:
             sig = inspect.signature(cls.__init__)
             if any(p.kind == inspect.Parameter.VAR_KEYWORD for p in sig.parameters.values()):
-                filtered = dict(ctor_kwargs)
+                filtered = dict(ctor)
             else:
                 allowed = {n for n in sig.parameters if n != "self"}
-                filtered = {k: v for k, v in ctor_kwargs.items() if k in allowed}
+                filtered = {k: v for k, v in ctor.items() if k in allowed}
         except (TypeError, ValueError):
-            filtered = dict(ctor_kwargs)
+            filtered = dict(ctor)
         return cls(**filtered)
     return _factory
 
