@@ -105,6 +105,7 @@ def main():
     ap.add_argument("--fixture", default="fx1_registry_k13")
     ap.add_argument("--no-stats", action="store_true")
     ap.add_argument("--dskip", action="store_true")
+    ap.add_argument("--perturb", action="store_true")
     args = ap.parse_args()
     if not args.no_stats:
         print("conv error statistics vs fp64 (relative to max / rms / mean|ref|):")
@@ -113,6 +114,10 @@ def main():
             conv_stats(*shp)
     if args.dskip:
         dskip_compare(args.fixture)
+        return
+    if args.perturb:
+        perturb_sensitivity(args.fixture, math_mode="f32")
+        perturb_sensitivity(args.fixture, math_mode="bf16x6")
         return
     import os
     print(f"SPFF_DEBUG_SPLIT={os.environ.get('SPFF_DEBUG_SPLIT', '')}")
@@ -180,6 +185,39 @@ def dskip_compare(name="fx1_registry_k13"):
             print(f"  {name} {m:7s} dskip{l}: max {float(e.abs().max() / sc):.2e} "
                   f"rms {float(e.pow(2).mean().sqrt() / sc):.2e}  per-d rms "
                   + " ".join(f"{float(v):.1e}" for v in per_d), flush=True)
+
+
+
+def perturb_sensitivity(name="fx1_registry_k13", eps=(1e-7, 3e-7), math_mode="f32"):
+    """How far each gradient moves when the INPUT is perturbed at fp32-rounding
+    scale: the conditioning every fp32 implementation is subject to."""
+    from _golden import load
+    from test_gpu_parity import load_core
+    import innovative3D.helpers as Hh
+    d = load(name)
+    K = d["meta"]["K"]
+
+    def grads(x_np):
+        core = load_core(d)
+        core.math = math_mode
+        x = torch.from_numpy(x_np).to(DEV)
+        y = torch.from_numpy(d["labels"]).to(DEV)
+        logits = core(x)
+        loss, _ = Hh.ce_dice_with_confusion(logits, y, K, 255)
+        loss.backward()
+        torch.cuda.synchronize()
+        return {k: v.grad.detach().double().cpu() for k, v in core.named_parameters() if v.grad is not None}
+    g0 = grads(d["x"])
+    import numpy as np
+    for e in eps:
+        for seed in (1, 2, 3):
+            rng = np.random.default_rng(seed)
+            xp = (d["x"] * (1 + e * rng.standard_normal(d["x"].shape))).astype(np.float32)
+            g1 = grads(xp)
+            rows = sorted(((float((g1[k] - g0[k]).abs().max() / g0[k].abs().max()), k) for k in g0),
+                          reverse=True)[:4]
+            print(f"  {math_mode} input eps {e:.0e} seed {seed}: "
+                  + ", ".join(f"{k} {v:.1e}" for v, k in rows), flush=True)
 
 
 if __name__ == "__main__":

@@ -31,6 +31,7 @@ import torch  # noqa: E402
 
 from innovative3D import config as C  # noqa: E402
 from innovative3D import helpers as Hh  # noqa: E402
+from innovative3D import models as M  # noqa: E402
 from innovative3D.synthetic import SyntheticSPCCT  # noqa: E402
 from train import Settings, _build_lit  # noqa: E402
 
@@ -59,6 +60,15 @@ def align_state_dict_keys(ckpt_sd: Dict, model_sd: Dict) -> Dict:
         elif have and not want:
             ckpt_sd = {(k[len(p):] if k.startswith(p) else k): v for k, v in ckpt_sd.items()}
     return ckpt_sd
+
+
+def materialize_lazy(model, depth, device):
+    """FourierGate masks are created lazily at the first forward (models.py:1527-
+    1533); create them at the run's depth so a checkpoint that holds
+    them loads strictly."""
+    for m in model.modules():
+        if isinstance(m, M.FourierGate3D):
+            m._ensure_mask(depth, device)
 
 
 def evaluate(model, dataset, K, device):
@@ -92,6 +102,7 @@ def main(argv=None):
                 print(f"[test] {name} seed{seed}: no checkpoint under {S.ckpt_dir}")
                 continue
             model = _build_lit(builder, S.in_ch).to(device)
+            materialize_lazy(model, S.depth, device)
             sd = torch.load(ck, map_location="cpu", weights_only=True)
             sd = sd.get("state_dict", sd)
             model.load_state_dict(align_state_dict_keys(sd, model.state_dict()))

@@ -8,7 +8,10 @@ below 2 x the observed max |dlogit| are reported as near-ties, not failures);
 gradients vs a kink-consistent fp64 oracle (engine_lrelu_masks) within
 max(1e-3, 8 x the fp32 oracle's own error) of max|g| per tensor (some
 gate-parameter gradients are cancelling sums the fp32 reference itself only
-gets to ~5e-2); loss within 1e-5 relative."""
+gets to ~5e-2; FourierGate mag_scale, whose gradient sum_k mask_k dL/dM_k cancels
+almost completely, is judged against the sum of its absolute terms); loss within
+1e-5 relative.  Max-pool windows route the oracle's gradient through the
+engine's own argmax, like the LeakyReLU signs."""
 import math
 
 import numpy as np
@@ -96,6 +99,16 @@ def test_network_matches_reference(name, mth):
         # scale: sum over samples of |per-sample gradient| (= max|g| for B=1); the batch
         # gradient is a sum of per-sample terms that can cancel (e.g. SE biases)
         scale = max(float(absb[kk].max()), 1e-12)
+        if kk.endswith("fgate.mag_scale"):
+            # d/d(mag) = sum_k mask_k dL/dM_k (M = mask * mag): a sum over the rfft
+            # bins that can cancel almost completely; judge it against the sum of
+            # its absolute terms, sum_k |mask_k dL/dM_k| = sum_k |mask_k g_mask_k| / |mag|
+            pre = kk[: -len("mag_scale")]
+            mk = pre + ("freq_mask" if pre + "freq_mask" in ref64 else "_mask")
+            st_ = state_of(d)
+            mag = abs(float(st_[kk].reshape(-1)[0]))
+            terms = np.abs(st_[pre + "freq_mask"].reshape(-1) * absb[mk].reshape(-1)).sum()
+            scale = max(scale, float(terms) / max(mag, 1e-12))
         e_gpu = float(np.abs(g - g64).max()) / scale
         e_32 = float(np.abs(ref32[kk] - g64).max()) / scale
         tol = max(5e-3, 64 * e_32) if mth == "bf16x3" else max(1e-3, 8 * e_32)
