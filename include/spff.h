@@ -126,6 +126,9 @@ int spff_conv3d_dgrad_ex(const float* dy, const float* w, float* dx, int B, int 
                          int cin, int cout, int ksd, int math, void* ws, void* stream);
 int spff_conv3d_wgrad(const float* x, int ldx, const float* dy, float* dw, int B, int D, int H,
                       int W, int cin, int cout, int ksd, void* ws, void* stream);
+int spff_conv3d_wgrad_ex(const float* x, int ldx, const float* dy, float* dw, int B, int D,
+                         int H, int W, int cin, int cout, int ksd, int math, void* ws,
+                         void* stream);
 
 #ifdef __cplusplus
 }

@@ -59,7 +59,8 @@ def main():
             "dgrad": (lambda: L.spff_conv3d_dgrad_ex(p(y), p(w), p(dx), B, D, H, W, cin, cout, 3, m,
                                                      p(ws), st))
             if dx is not None else None,
-            "wgrad": lambda: L.spff_conv3d_wgrad(p(x), ldx, p(y), p(dw), B, D, H, W, cin, cout, 3, p(ws), st),
+            "wgrad": lambda: L.spff_conv3d_wgrad_ex(p(x), ldx, p(y), p(dw), B, D, H, W, cin, cout, 3, m,
+                                                    p(ws), st),
         }
         row = []
         for o in ops:

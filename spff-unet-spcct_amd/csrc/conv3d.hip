@@ -462,11 +462,22 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ 
 
 size_t conv3d_wgrad_ws_bytes(Vol vol, int KD, int Cin, int Cout) {
   WgradPlan p = wgrad_plan(vol, Cin, Cout);
-  return (size_t)p.nsplit * KD * 9 * p.kpad * p.npad * sizeof(float);
+  return std::max((size_t)p.nsplit * KD * 9 * p.kpad * p.npad * sizeof(float),
+                  conv3d_wgrad_x_ws_bytes(vol, KD, Cin, Cout));
+}
+
+hipError_t conv3d_wgrad_reduce(const float* part, float* dw, int nsplit, int T, int kpad,
+                               int npad, int Cin, int Cout, hipStream_t s) {
+  const int64_t total = (int64_t)T * Cin * Cout;
+  hipLaunchKernelGGL(k_wgrad_reduce, dim3((unsigned)((total + 31) / 32)), dim3(256), 0, s, part,
+                     dw, nsplit, T, kpad, npad, Cin, Cout);
+  return hipGetLastError();
 }
 
 hipError_t conv3d_wgrad(const Src2& x, const float* dy, int lddy, float* dw, Vol vol, int KD,
-                        int Cin, int Cout, float* ws, hipStream_t s) {
+                        int Cin, int Cout, int math, float* ws, hipStream_t s) {
+  if (math != SPFF_MATH_F32)
+    return conv3d_wgrad_x(x, dy, lddy, dw, vol, KD, Cin, Cout, math, ws, s);
   if (lddy % 4) return hipErrorInvalidValue;
   WgradPlan p = wgrad_plan(vol, Cin, Cout);
   dim3 grid(p.nsplit, p.kpad / p.ci, p.npad / WG_CO);
@@ -481,11 +492,7 @@ hipError_t conv3d_wgrad(const Src2& x, const float* dy, int lddy, float* dw, Vol
 #undef SPFF_WG
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  const int T = KD * 9;
-  const int64_t total = (int64_t)T * Cin * Cout;
-  hipLaunchKernelGGL(k_wgrad_reduce, dim3((unsigned)((total + 31) / 32)), dim3(256), 0, s, ws, dw,
-                     p.nsplit, T, p.kpad, p.npad, Cin, Cout);
-  return hipGetLastError();
+  return conv3d_wgrad_reduce(ws, dw, p.nsplit, KD * 9, p.kpad, p.npad, Cin, Cout, s);
 }
 
 }  // namespace spff

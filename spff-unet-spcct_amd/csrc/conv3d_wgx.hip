@@ -1,0 +1,349 @@
+// 3x3x3 convolution weight gradient on the bf16 matrix cores with the exact
+// 3-plane (bf16x6) or 2-plane (bf16x3) operand split of conv3d_x.hip.
+//
+// Replaces the weight gradient of nn.Conv3d(cin, cout, (ksd,3,3),
+// padding=(ksd//2,1,1), bias=False) (reference models.py:616-618):
+//   dW[co][ci][tap] = sum_v x[v + off(tap)][ci] * dy[v][co].
+//
+// MFMA v_mfma_f32_32x32x16_bf16: rows = (tap, ci) -- a 32-row block is 8 chunks
+// of 4 input channels, each chunk at its own tap -- cols = 32 out channels,
+// k = 16 voxels (one W-row of the 1 x 8 x 16 voxel tile).  Both operands need
+// the voxel axis in their k slots while the LDS images are channel-last
+// ([plane][pos][CI] halo, [plane][voxel][32] dy tile, exactly as global memory):
+// ds_read_b64_tr_b16 gathers them transposed -- every lane supplies the address
+// of 4 contiguous channels of one voxel, so each row's tap offset and each
+// chunk's channel base are free per lane and no shifted copies are needed.
+// Blocks pair taps whose halo offsets differ by 4 (mod 8) positions, so the
+// two 16-lane groups of a 32-lane half read disjoint bank ranges.
+//
+// 256 threads (4 waves), two workgroups per CU (76 KB LDS each) so one
+// workgroup's staging (fp32 loads, exact split, LDS stores) overlaps the other's
+// MFMAs; the next tile's halo / dy are register-prefetched during the current
+// tile's MFMAs.  Output: the fp32 partial slabs of conv3d.hip's wgrad
+// ([split][tap][kpad][npad]), summed in fixed order by k_wgrad_reduce.
+#include "spff_internal.h"
+
+#include <type_traits>
+#include <vector>
+
+namespace spff {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short i16x4 __attribute__((ext_vector_type(4)));
+
+static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+static inline int rup(int a, int b) { return cdiv(a, b) * b; }
+
+namespace {
+constexpr int WX_TH = 8, WX_TW = 16, WX_TV = WX_TH * WX_TW, WX_CO = 32, WX_MAXBLK = 16;
+
+// (tap, channel base) of the 8 four-channel chunks of each 32-row block
+struct WxTable {
+  signed char tap[WX_MAXBLK][8];   // -1: padding chunk (computed, never stored)
+  signed char ci0[WX_MAXBLK][8];
+  int nblk;
+};
+
+__device__ __forceinline__ unsigned short bfbits(__bf16 v) {
+  return __builtin_bit_cast(unsigned short, v);
+}
+template <int NS>
+__device__ __forceinline__ void split4(const float4& v, uint2 (&o)[NS]) {
+  float r[4] = {v.x, v.y, v.z, v.w};
+  unsigned short s[4][NS];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+#pragma unroll
+    for (int p = 0; p < NS; ++p) {
+      const __bf16 b = (__bf16)r[e];
+      s[e][p] = bfbits(b);
+      r[e] = r[e] - (float)b;
+    }
+  }
+#pragma unroll
+  for (int p = 0; p < NS; ++p) {
+    o[p].x = (unsigned)s[0][p] | ((unsigned)s[1][p] << 16);
+    o[p].y = (unsigned)s[2][p] | ((unsigned)s[3][p] << 16);
+  }
+}
+
+typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
+__device__ __forceinline__ i16x4 tr_read(const unsigned short* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(p));
+}
+__device__ __forceinline__ bf16x8 frag(const i16x4& lo, const i16x4& hi) {
+  typedef short i16x8 __attribute__((ext_vector_type(8)));
+  i16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+}  // namespace
+
+template <int KD, int CI, int NS, int NJMAX>
+__global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x(
+    Src2 x, const float* __restrict__ dy, int lddy, float* __restrict__ part, Vol vol, int Cin,
+    int kpad, int Cout, int npad, int tilesH, int tilesW, int ntiles, int tps, WxTable tb) {
+  constexpr int HD = KD, HH = WX_TH + 2, HWD = WX_TW + 2;
+  constexpr int NPOS = HD * HH * HWD;
+  constexpr int T = KD * 9;
+  constexpr int CQ = CI / 4;                              // float4 per halo position
+  constexpr int NH = (NPOS * CQ + 255) / 256;              // halo float4 per thread
+  constexpr int NY = WX_TV * (WX_CO / 4) / 256;            // dy float4 per thread (= 4)
+  __shared__ __attribute__((aligned(16))) unsigned short Xs[NS * NPOS * CI];
+  __shared__ __attribute__((aligned(16))) unsigned short Ys[NS * WX_TV * WX_CO];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, h = g >> 1, q = (lane & 15) >> 2, pq = lane & 3;
+  const int split = blockIdx.x, ci_base = blockIdx.y * CI, co0 = blockIdx.z * WX_CO;
+  const int D = vol.D, H = vol.H, W = vol.W;
+
+  // blocks of this wave: wave, wave + 4, ...; nj of them (uniform per wave)
+  const int nj = (tb.nblk - wave + 3) / 4;
+  // lane-constant A addresses (elements, plane 0, k-step 0, read 0) per block
+  int aoff[NJMAX];
+#pragma unroll
+  for (int j = 0; j < NJMAX; ++j) {
+    const int blk = wave + 4 * j;
+    const int c4 = 4 * (g & 1) + pq;
+    int t = blk < tb.nblk ? tb.tap[blk][c4] : -1;
+    const int ci0 = blk < tb.nblk ? tb.ci0[blk][c4] : 0;
+    if (t < 0) t = 0;  // padding chunk: any valid address
+    const int kd = t / 9, kh = (t / 3) % 3, kw = t % 3;
+    aoff[j] = ((kd * HH + kh) * HWD + kw + 8 * h + q) * CI + ci0;
+  }
+  // B: row q of the read = voxel 8h + 4s + q of k-step j; cols co 16(g&1) + 4pq
+  const int boff = (8 * h + q) * WX_CO + 16 * (g & 1) + 4 * pq;
+
+  f32x16 acc[NJMAX];
+#pragma unroll
+  for (int j = 0; j < NJMAX; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+
+  float4 hreg[NH], yreg[NY];
+  auto fetch = [&](int tile) {
+    int t = tile;
+    const int twi = t % tilesW; t /= tilesW;
+    const int thi = t % tilesH; t /= tilesH;
+    const int d0 = t % D;
+    const int b = t / D;
+    const int h0 = thi * WX_TH, w0 = twi * WX_TW;
+#pragma unroll
+    for (int k = 0; k < NH; ++k) {
+      const int i = tid + 256 * k;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (i < NPOS * CQ) {
+        const int c4 = i % CQ, pos = i / CQ;
+        const int hw = pos % HWD, t2 = pos / HWD, hh = t2 % HH, hd = t2 / HH;
+        const int gd = d0 + hd - KD / 2, gh = h0 + hh - 1, gw = w0 + hw - 1;
+        const int c = ci_base + 4 * c4;
+        if ((unsigned)gd < (unsigned)D && (unsigned)gh < (unsigned)H &&
+            (unsigned)gw < (unsigned)W && c < Cin) {
+          const int64_t vox = (((int64_t)b * D + gd) * H + gh) * W + gw;
+          const float* p =
+              c < x.split ? x.p0 + vox * x.ld0 + c : x.p1 + vox * x.ld1 + (c - x.split);
+          v = *reinterpret_cast<const float4*>(p);
+        }
+      }
+      hreg[k] = v;
+    }
+#pragma unroll
+    for (int k = 0; k < NY; ++k) {
+      const int i = tid + 256 * k;
+      const int c4 = i % (WX_CO / 4), kv = i / (WX_CO / 4);
+      const int gh = h0 + kv / WX_TW, gw = w0 + kv % WX_TW;
+      const int c = co0 + 4 * c4;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (gh < H && gw < W && c < Cout) {
+        const int64_t vox = (((int64_t)b * D + d0) * H + gh) * W + gw;
+        v = *reinterpret_cast<const float4*>(dy + vox * lddy + c);
+      }
+      yreg[k] = v;
+    }
+  };
+  auto stash = [&]() {
+#pragma unroll
+    for (int k = 0; k < NH; ++k) {
+      const int i = tid + 256 * k;
+      if (i < NPOS * CQ) {
+        uint2 o[NS];
+        split4<NS>(hreg[k], o);
+#pragma unroll
+        for (int p = 0; p < NS; ++p)
+          *reinterpret_cast<uint2*>(Xs + p * NPOS * CI + 4 * i) = o[p];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NY; ++k) {
+      const int i = tid + 256 * k;
+      uint2 o[NS];
+      split4<NS>(yreg[k], o);
+#pragma unroll
+      for (int p = 0; p < NS; ++p)
+        *reinterpret_cast<uint2*>(Ys + p * WX_TV * WX_CO + 4 * i) = o[p];
+    }
+  };
+
+  auto compute = [&](auto NJc) {
+    constexpr int NJ = decltype(NJc)::value;
+#pragma unroll 2
+    for (int ks = 0; ks < WX_TH; ++ks) {
+      bf16x8 bq[NS];
+#pragma unroll
+      for (int p = 0; p < NS; ++p) {
+        const unsigned short* yb = Ys + p * WX_TV * WX_CO + ks * WX_TW * WX_CO + boff;
+        bq[p] = frag(tr_read(yb), tr_read(yb + 4 * WX_CO));
+      }
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        bf16x8 aq[NS];
+#pragma unroll
+        for (int p = 0; p < NS; ++p) {
+          const unsigned short* xb = Xs + p * NPOS * CI + ks * HWD * CI + aoff[j];
+          aq[p] = frag(tr_read(xb), tr_read(xb + 4 * CI));
+        }
+        f32x16 c = acc[j];
+        if constexpr (NS == 3) {
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aq[1], bq[1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aq[0], bq[2], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aq[2], bq[0], c, 0, 0, 0);
+        }
+        if constexpr (NS >= 2) {
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aq[0], bq[1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aq[1], bq[0], c, 0, 0, 0);
+        }
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aq[0], bq[0], c, 0, 0, 0);
+        acc[j] = c;
+      }
+    }
+  };
+
+  const int tbeg = split * tps;
+  const int tend = min(ntiles, tbeg + tps);
+  if (tbeg < tend) fetch(tbeg);
+  for (int tile = tbeg; tile < tend; ++tile) {
+    __syncthreads();  // previous compute done reading LDS
+    stash();
+    __syncthreads();
+    if (tile + 1 < tend) fetch(tile + 1);
+    if (nj == NJMAX) compute(std::integral_constant<int, NJMAX>{});
+    else if constexpr (NJMAX > 1) compute(std::integral_constant<int, NJMAX - 1>{});
+  }
+
+  // partial slab [split][tap][kpad][npad]: row i = chunk (i/4) channel i%4, col = co
+#pragma unroll
+  for (int j = 0; j < NJMAX; ++j) {
+    const int blk = wave + 4 * j;
+    if (j >= nj || blk >= tb.nblk) continue;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int i = (r & 3) + 8 * (r >> 2) + 4 * h;  // h = lane >> 5
+      const int c4 = i >> 2;
+      const int t = tb.tap[blk][c4];
+      if (t < 0) continue;
+      const int ci = ci_base + tb.ci0[blk][c4] + (i & 3);
+      part[(((int64_t)split * T + t) * kpad + ci) * npad + co0 + (lane & 31)] = acc[j][r];
+    }
+  }
+}
+
+// ------------------------------------------------------------------ host --
+namespace {
+// halo position offset of a tap inside the 1 x 8 x 16 tile's halo
+int tap_pos(int t) {
+  const int kd = t / 9, kh = (t / 3) % 3, kw = t % 3;
+  return (kd * (WX_TH + 2) + kh) * (WX_TW + 2) + kw;
+}
+
+WxTable make_table(int KD, int CI) {
+  WxTable tb{};
+  const int T = KD * 9;
+  std::vector<int> taps;
+  if (CI == 16) {
+    // pair taps 2 per block, preferring halo offsets 4 apart (mod 8): the two
+    // 16-lane groups of a half then cover disjoint 32-bank ranges
+    std::vector<bool> used(T, false);
+    for (int a = 0; a < T; ++a) {
+      if (used[a]) continue;
+      used[a] = true;
+      int best = -1;
+      for (int b = a + 1; b < T; ++b)
+        if (!used[b] && (((tap_pos(b) - tap_pos(a)) % 8) + 8) % 8 == 4) { best = b; break; }
+      if (best < 0)
+        for (int b = a + 1; b < T; ++b)
+          if (!used[b]) { best = b; break; }
+      taps.push_back(a);
+      taps.push_back(best);  // -1: half-empty block
+      if (best >= 0) used[best] = true;
+    }
+    tb.nblk = (int)taps.size() / 2;
+    for (int b = 0; b < tb.nblk; ++b)
+      for (int c = 0; c < 8; ++c) {
+        tb.tap[b][c] = (signed char)taps[2 * b + c / 4];
+        tb.ci0[b][c] = (signed char)(4 * (c % 4));
+      }
+  } else {  // CI == 8: 4 taps per block
+    tb.nblk = cdiv(T, 4);
+    for (int b = 0; b < tb.nblk; ++b)
+      for (int c = 0; c < 8; ++c) {
+        const int t = 4 * b + c / 2;
+        tb.tap[b][c] = (signed char)(t < T ? t : -1);
+        tb.ci0[b][c] = (signed char)(4 * (c % 2));
+      }
+  }
+  return tb;
+}
+
+struct WxPlan {
+  int ci, kpad, npad, tilesH, tilesW, ntiles, nsplit, tps;
+};
+WxPlan wx_plan(Vol vol, int Cin, int Cout) {
+  WxPlan p;
+  p.ci = Cin <= 8 ? 8 : 16;
+  p.kpad = rup(Cin, p.ci);
+  p.npad = rup(Cout, WX_CO);
+  p.tilesH = cdiv(vol.H, WX_TH);
+  p.tilesW = cdiv(vol.W, WX_TW);
+  p.ntiles = vol.B * vol.D * p.tilesH * p.tilesW;
+  const int nout = (p.kpad / p.ci) * (p.npad / WX_CO);
+  // two workgroups per CU: aim at 2 rounds of 512, >= 4 tiles per workgroup
+  int nsplit = std::max(1, cdiv(1024, nout));
+  nsplit = std::min(nsplit, std::max(1, p.ntiles / 4));
+  p.tps = cdiv(p.ntiles, nsplit);
+  p.nsplit = cdiv(p.ntiles, p.tps);
+  return p;
+}
+}  // namespace
+
+size_t conv3d_wgrad_x_ws_bytes(Vol vol, int KD, int Cin, int Cout) {
+  WxPlan p = wx_plan(vol, Cin, Cout);
+  return (size_t)p.nsplit * KD * 9 * p.kpad * p.npad * sizeof(float);
+}
+
+hipError_t conv3d_wgrad_x(const Src2& x, const float* dy, int lddy, float* dw, Vol vol, int KD,
+                          int Cin, int Cout, int math, float* ws, hipStream_t s) {
+  if (lddy % 4) return hipErrorInvalidValue;
+  WxPlan p = wx_plan(vol, Cin, Cout);
+  const WxTable tb = make_table(KD, p.ci);
+  dim3 grid(p.nsplit, p.kpad / p.ci, p.npad / WX_CO);
+#define SPFF_WX(KD_, CI_, NS_, NJ_)                                                            \
+  hipLaunchKernelGGL((k_conv3d_wgrad_x<KD_, CI_, NS_, NJ_>), grid, dim3(256), 0, s, x, dy,     \
+                     lddy, ws, vol, Cin, p.kpad, Cout, p.npad, p.tilesH, p.tilesW, p.ntiles,   \
+                     p.tps, tb)
+  const bool x3 = math == SPFF_MATH_BF16X3;
+  // NJMAX = ceil(nblk / 4): KD3/CI16 14 blocks -> 4, KD3/CI8 7 -> 2, KD1/CI16 5 -> 2, KD1/CI8 3 -> 1
+  if (KD == 3) {
+    if (p.ci == 16) { if (x3) SPFF_WX(3, 16, 2, 4); else SPFF_WX(3, 16, 3, 4); }
+    else            { if (x3) SPFF_WX(3, 8, 2, 2);  else SPFF_WX(3, 8, 3, 2); }
+  } else {
+    if (p.ci == 16) { if (x3) SPFF_WX(1, 16, 2, 2); else SPFF_WX(1, 16, 3, 2); }
+    else            { if (x3) SPFF_WX(1, 8, 2, 1);  else SPFF_WX(1, 8, 3, 1); }
+  }
+#undef SPFF_WX
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const int T = KD * 9;
+  return conv3d_wgrad_reduce(ws, dw, p.nsplit, T, p.kpad, p.npad, Cin, Cout, s);
+}
+
+}  // namespace spff

@@ -468,8 +468,8 @@ int bwd_block(spff_plan* p, Blk& b, const float* dout, const Dst2* dx, const Src
   }
   const double V = (double)nvox(v), T = 9.0 * KD;
   PROF(p, 2, 2.0 * V * C * C * T,
-       conv3d_wgrad(src1(p->F(b.a1), C), dy2, C, p->DP(b.c2.w), v, KD, C, C, p->F(p->wg_ws),
-                    p->st));
+       conv3d_wgrad(src1(p->F(b.a1), C), dy2, C, p->DP(b.c2.w), v, KD, C, C, p->cfg.math,
+                    p->F(p->wg_ws), p->st));
   const int math = p->cfg.math;
   HIPCK(conv3d_pack(p->P(b.c2.w), p->F(p->wt), v, KD, C, C, true, math, p->st));
   PROF(p, 1, 2.0 * V * C * C * T,
@@ -486,7 +486,8 @@ int bwd_block(spff_plan* p, Blk& b, const float* dout, const Dst2* dx, const Src
                        C, p->st));
   }
   PROF(p, 2, 2.0 * V * b.Cin * C * T,
-       conv3d_wgrad(in, da1, C, p->DP(b.c1.w), v, KD, b.Cin, C, p->F(p->wg_ws), p->st));
+       conv3d_wgrad(in, da1, C, p->DP(b.c1.w), v, KD, b.Cin, C, p->cfg.math, p->F(p->wg_ws),
+                    p->st));
   if (dx) {
     HIPCK(conv3d_pack(p->P(b.c1.w), p->F(p->wt), v, KD, b.Cin, C, true, math, p->st));
     PROF(p, 1, 2.0 * V * b.Cin * C * T,
@@ -802,14 +803,23 @@ int spff_conv3d_dgrad(const float* dy, const float* w, float* dx, int B, int D, 
   return spff_conv3d_dgrad_ex(dy, w, dx, B, D, H, W, cin, cout, ksd, SPFF_MATH_F32, ws, stream);
 }
 
-int spff_conv3d_wgrad(const float* x, int ldx, const float* dy, float* dw, int B, int D, int H,
-                      int W, int cin, int cout, int ksd, void* ws, void* stream) {
+int spff_conv3d_wgrad_ex(const float* x, int ldx, const float* dy, float* dw, int B, int D,
+                         int H, int W, int cin, int cout, int ksd, int math, void* ws,
+                         void* stream) {
   if (!x || !dy || !dw || !ws) return fail(SPFF_EINVAL, "null argument");
   if (ldx % 4 || ldx < cin || cout % 4) return fail(SPFF_EINVAL, "bad channel strides");
+  if (math < SPFF_MATH_F32 || math > SPFF_MATH_BF16X3) return fail(SPFF_EINVAL, "bad math");
   hipStream_t s = static_cast<hipStream_t>(stream);
   float* part = static_cast<float*>(ws) + conv_op_pack_floats(cin, cout, ksd) + 64;
-  HIPCK(conv3d_wgrad(src1(x, ldx), dy, cout, dw, Vol{B, D, H, W}, ksd, cin, cout, part, s));
+  HIPCK(conv3d_wgrad(src1(x, ldx), dy, cout, dw, Vol{B, D, H, W}, ksd, cin, cout, math, part,
+                     s));
   return SPFF_OK;
+}
+
+int spff_conv3d_wgrad(const float* x, int ldx, const float* dy, float* dw, int B, int D, int H,
+                      int W, int cin, int cout, int ksd, void* ws, void* stream) {
+  return spff_conv3d_wgrad_ex(x, ldx, dy, dw, B, D, H, W, cin, cout, ksd, SPFF_MATH_F32, ws,
+                              stream);
 }
 
 }  // extern "C"

@@ -46,9 +46,17 @@ hipError_t conv3d_pack(const float* w, void* wpack, Vol vol, int KD, int Cin_w, 
 hipError_t conv3d_run(const Src2& x, const void* wpack, const Dst2& y, Vol vol, int KD,
                       int Cin_w, int Cout_w, bool dgrad, int math, hipStream_t s);
 // dW partials + reduction into reference layout dw[Cout][Cin][KD][3][3].
+// math = SPFF_MATH_F32: fp32 MFMA kernel (conv3d.hip); otherwise the split-bf16
+// kernel of conv3d_wgx.hip.  ws >= conv3d_wgrad_ws_bytes (covers both).
 size_t conv3d_wgrad_ws_bytes(Vol vol, int KD, int Cin, int Cout);
 hipError_t conv3d_wgrad(const Src2& x, const float* dy, int lddy, float* dw, Vol vol, int KD,
-                        int Cin, int Cout, float* ws, hipStream_t s);
+                        int Cin, int Cout, int math, float* ws, hipStream_t s);
+size_t conv3d_wgrad_x_ws_bytes(Vol vol, int KD, int Cin, int Cout);
+hipError_t conv3d_wgrad_x(const Src2& x, const float* dy, int lddy, float* dw, Vol vol, int KD,
+                          int Cin, int Cout, int math, float* ws, hipStream_t s);
+// fixed-order sum of the [nsplit][T][kpad][npad] partial slabs into dw[Cout][Cin][T]
+hipError_t conv3d_wgrad_reduce(const float* part, float* dw, int nsplit, int T, int kpad,
+                               int npad, int Cin, int Cout, hipStream_t s);
 
 // ---------------------------------------------------------------- gemms --
 // ConvTranspose3d(Cin->Cout, k=(1,2,2), s=(1,2,2)) + bias, low-res x [Vlow][Cin],

@@ -76,6 +76,7 @@ _SIGS = {
     "spff_conv3d_dgrad": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
     "spff_conv3d_fwd_ex": (_I, [_P, _I, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
     "spff_conv3d_dgrad_ex": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
+    "spff_conv3d_wgrad_ex": (_I, [_P, _I, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
     "spff_conv3d_wgrad": (_I, [_P, _I, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
 }
 EXPORTED = tuple(_SIGS)

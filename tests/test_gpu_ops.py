@@ -87,7 +87,7 @@ SPLIT_CASES = [
 @pytest.mark.parametrize("math_mode", ["bf16x6", "bf16x3"])
 @pytest.mark.parametrize("case", SPLIT_CASES)
 def test_conv3d_split_bf16(case, math_mode):
-    """fwd / dgrad on the bf16 matrix cores with the exact 3-plane (2-plane)
+    """fwd / dgrad / wgrad on the bf16 matrix cores with the exact 3-plane (2-plane)
     operand split, against an fp64 conv.  bf16x6 must be as accurate as the fp32
     MFMA path (error within 4x of it); bf16x3 within 3e-5 of max|ref|."""
     B, D, H, W, cin, cout, ksd = case
@@ -98,6 +98,7 @@ def test_conv3d_split_bf16(case, math_mode):
     dy = torch.randn(B, cout, D, H, W, generator=g)
     y64 = F.conv3d(x.double(), w.double(), None, padding=(ksd // 2, 1, 1))
     dx64 = torch.nn.grad.conv3d_input(x.shape, w.double(), dy.double(), padding=(ksd // 2, 1, 1))
+    dw64 = torch.nn.grad.conv3d_weight(x.double(), w.shape, dy.double(), padding=(ksd // 2, 1, 1))
     ldx = (cin + 7) // 8 * 8
     xcl = torch.zeros(B, D, H, W, ldx)
     xcl[..., :cin] = _cl(x)
@@ -115,9 +116,13 @@ def test_conv3d_split_bf16(case, math_mode):
             dxg = torch.empty(B, D, H, W, cin, device=DEV)
             E.check(L.spff_conv3d_dgrad_ex(p(dyg), p(wd), p(dxg), B, D, H, W, cin, cout, ksd, m,
                                            p(ws), st), "dgrad")
+        dwg = torch.empty_like(wd)
+        E.check(L.spff_conv3d_wgrad_ex(p(xcl), ldx, p(dyg), p(dwg), B, D, H, W, cin, cout, ksd, m,
+                                       p(ws), st), "wgrad")
         torch.cuda.synchronize()
-        out[m] = (yg.cpu().double(), None if dxg is None else dxg.cpu().double())
-    pairs = [(0, _cl(y64))] + ([(1, _cl(dx64))] if cin % 4 == 0 else [])
+        out[m] = (yg.cpu().double(), None if dxg is None else dxg.cpu().double(),
+                  dwg.cpu().double())
+    pairs = [(0, _cl(y64)), (2, dw64)] + ([(1, _cl(dx64))] if cin % 4 == 0 else [])
     for k, ref in pairs:
         e32 = float((out[E.MATH_F32][k] - ref).abs().max())
         ex = float((out[mth][k] - ref).abs().max())
