@@ -54,14 +54,39 @@ typedef struct spff_cfg {
   int use_efilm, use_fgate;                 /* novel block (models.py:1448) */
   int use_se, use_specse;                   /* encoder post (models.py:684) */
   int math;                                 /* SPFF_MATH_* (0 = fp32 MFMA) */
-  int reserved[7];                          /* zero */
+  /* depth sharding (BASELINE config 4): this plan holds global depths
+   * [shard_rank * depth, (shard_rank + 1) * depth) of a volume of depth
+   * shard_world * depth; requires batch == 1 and a collectives table, see spff_coll below.
+   * shard_world <= 1: unsharded. */
+  int shard_world, shard_rank;
+  int reserved[5];                          /* zero */
 } spff_cfg;
+
+/* The shard group's collectives, implemented by the caller (e.g. RCCL through
+ * torch.distributed) and called by the engine in stream order on the stream of
+ * the current spff_forward / spff_backward.  Return 0 on success.
+ *   allreduce: in-place sum over the group of n elements at device pointer buf
+ *              (dtype 0 = fp32, 1 = fp64).
+ *   halo:      interior points at slice 0 of a [d_local][slice_floats] slab
+ *              that has one writable slice before it and one after it: send
+ *              slice 0 to rank - 1 and slice d_local - 1 to rank + 1, and receive
+ *              rank - 1's last slice into interior[-slice_floats ..) and
+ *              rank + 1's first slice into interior[d_local * slice_floats ..).
+ *              Slices beyond the global ends are zeroed by the engine. */
+typedef struct spff_coll {
+  void* ctx;
+  int (*allreduce)(void* ctx, void* buf, int64_t n, int dtype, void* stream);
+  int (*halo)(void* ctx, float* interior, int64_t slice_floats, int d_local, void* stream);
+} spff_coll;
 
 typedef struct spff_plan spff_plan;
 
 /* plan lifetime (replaces build_class(...)() -> module construction, config.py:159-182) */
 int spff_plan_create(const spff_cfg* cfg, spff_plan** out);
 void spff_plan_destroy(spff_plan* plan);
+/* attach the shard group's collectives (required before the first forward of a
+ * plan with shard_world > 1; the table is copied) */
+int spff_plan_set_coll(spff_plan* plan, const spff_coll* coll);
 const char* spff_last_error(void);
 
 /* flat parameter layout (reference state-dict order, models.py:655-681) */

@@ -161,7 +161,7 @@ __global__ __launch_bounds__(XT_THREADS, 1) void k_conv3d_fwd_x(
         const int hw = pos % HWD, t2 = pos / HWD, hh = t2 % HH, hd = t2 / HH;
         const int gd = d0 + hd - KD / 2, gh = h0 + hh - 1, gw = w0 + hw - 1;
         const int c = kc * 8 + 4 * q;
-        if ((unsigned)gd < (unsigned)D && (unsigned)gh < (unsigned)H &&
+        if ((unsigned)(gd + vol.dh) < (unsigned)(D + 2 * vol.dh) && (unsigned)gh < (unsigned)H &&
             (unsigned)gw < (unsigned)W && c < Cin) {
           const int64_t vox = (((int64_t)b * D + gd) * H + gh) * W + gw;
           const float* p =

@@ -81,6 +81,7 @@ struct Blk {
   size_t y1, a1, y2, out;
   size_t mean1, rstd1, al1, de1, mean2, rstd2, al2, de2;
   size_t Sa, t, bt, hid, s1, g1s, sg2, p, h, e, P, Q;
+  size_t spec = 0;  // sharded plans: full-depth s1 spectrum [B][L][2] (fp64)
   bool tail() const { return efilm || fgate || post_se || post_spec; }
 };
 
@@ -106,7 +107,10 @@ struct spff_plan {
   size_t red_ws = 0, red_out = 0, gscr = 0, Abuf = 0, Bbuf = 0, kk1 = 0, kk2 = 0, wg_ws = 0,
          wt = 0;
   size_t G_out = 0, G_dy2 = 0, G_da1 = 0, G_dx = 0, dskip[3] = {0, 0, 0};
+  size_t part_d = 0;  // sharded plans: fp64 IN partials [B][C][2]
   size_t total = 0;
+  Coll co;             // depth-sharding group (world 1: unsharded)
+  bool coll_set = false;
   float* pe_dev = nullptr;
   std::vector<float> pe_host;
   // optional HIP-event timing of the MFMA kernels (bench.py roofline)
@@ -129,6 +133,13 @@ struct spff_plan {
     total += (bytes + 255) / 256 * 256;
     return o;
   }
+  // a conv input of a halo'd (depth-sharded) plan: one neighbour slice of up to
+  // slice_bytes before and after the interior; returns the interior offset
+  size_t alloc_halo(size_t bytes, size_t slice_bytes) {
+    if (!vol[0].dh) return alloc(bytes);
+    return alloc(bytes + 2 * slice_bytes) + slice_bytes;
+  }
+  double* D64(size_t off) const { return reinterpret_cast<double*>(ws + off); }
   int64_t reg(const std::string& name, std::vector<int64_t> shape) {
     int64_t n = 1;
     for (auto s : shape) n *= s;
@@ -170,7 +181,7 @@ void reg_block(spff_plan* p, Blk& b) {
   }
   if (b.fgate) {
     b.mag = p->reg(b.name + ".fgate.mag_scale", {1});
-    b.mask = p->reg(b.name + ".fgate.freq_mask", {1, 1, p->vol[0].D / 2 + 1, 1, 1});
+    b.mask = p->reg(b.name + ".fgate.freq_mask", {1, 1, p->co.D_glob / 2 + 1, 1, 1});
   }
 }
 
@@ -213,11 +224,24 @@ int build_plan(spff_plan* p) {
   if (c.in_ch > 64) return fail(SPFF_EINVAL, "in_ch > 64 not supported");
   if (c.math < SPFF_MATH_F32 || c.math > SPFF_MATH_BF16X3)
     return fail(SPFF_EINVAL, "math must be one of SPFF_MATH_*");
+  const int world = c.shard_world > 1 ? c.shard_world : 1;
+  if (world > 1) {
+    if (c.batch != 1) return fail(SPFF_EINVAL, "depth-sharded plans take batch == 1");
+    if (c.shard_rank < 0 || c.shard_rank >= world) return fail(SPFF_EINVAL, "bad shard_rank");
+  }
+  p->co.world = world;
+  p->co.rank = world > 1 ? c.shard_rank : 0;
+  p->co.D_glob = c.depth * world;
+  p->co.d_off = p->co.rank * c.depth;
   p->f = c.base;
   p->KD = c.ksd;
   p->K = c.num_classes;
   p->ldx = rup(c.in_ch, 8);
-  for (int l = 0; l < 4; ++l) p->vol[l] = Vol{c.batch, c.depth, c.height >> l, c.width >> l};
+  const int dh = (world > 1 && c.ksd == 3) ? 1 : 0;
+  for (int l = 0; l < 4; ++l) {
+    p->vol[l] = Vol{c.batch, c.depth, c.height >> l, c.width >> l};
+    p->vol[l].dh = dh;
+  }
   const int f = p->f;
   const char* names[7] = {"enc1", "enc2", "enc3", "bott", "dec3", "dec2", "dec1"};
   const int lvl[7] = {0, 1, 2, 3, 2, 1, 0};
@@ -271,16 +295,17 @@ int build_plan(spff_plan* p) {
   // ---- workspace layout ----
   const int B = c.batch, D = c.depth;
   const Vol& v0 = p->vol[0];
-  p->x_cl = p->alloc(nvox(v0) * p->ldx * sizeof(float));
+  const auto slice = [&](const Vol& v, int C) { return (size_t)v.H * v.W * C * sizeof(float); };
+  p->x_cl = p->alloc_halo(nvox(v0) * p->ldx * sizeof(float), slice(v0, p->ldx));
   size_t red_ws = 0, red_out = 0, gs = 0, bcd = 0, wg = 0, wt = 0;
   for (int i = 0; i < 7; ++i) {
     Blk& b = p->blk[i];
     const Vol& v = p->vol[b.lvl];
     const size_t act = nvox(v) * b.C * sizeof(float);
     b.y1 = p->alloc(act);
-    b.a1 = p->alloc(act);
+    b.a1 = p->alloc_halo(act, slice(v, b.C));
     b.y2 = p->alloc(act);
-    b.out = p->alloc(act);
+    b.out = p->alloc_halo(act, slice(v, b.C));
     const size_t bc = (size_t)B * b.C * sizeof(float);
     b.mean1 = p->alloc(bc); b.rstd1 = p->alloc(bc); b.al1 = p->alloc(bc); b.de1 = p->alloc(bc);
     b.mean2 = p->alloc(bc); b.rstd2 = p->alloc(bc); b.al2 = p->alloc(bc); b.de2 = p->alloc(bc);
@@ -298,10 +323,12 @@ int build_plan(spff_plan* p) {
       b.t = p->alloc((size_t)b.C * D * 4);
       b.bt = p->alloc((size_t)b.C * D * 4);
       b.hid = p->alloc((size_t)32 * D * 4);
+      if (world > 1) b.spec = p->alloc((size_t)B * (p->co.D_glob / 2 + 1) * 2 * sizeof(double));
     }
     red_ws = std::max(red_ws, slab_reduce_ws_bytes(v, b.C, 2));
     red_out = std::max(red_out, (size_t)B * b.C * D * 2 * sizeof(float));
-    gs = std::max(gs, gates_scratch_bytes(v, b.C));
+    gs = std::max(gs, world > 1 ? gates_sh_scratch_bytes(v, b.C, p->co.D_glob)
+                                : gates_scratch_bytes(v, b.C));
     bcd = std::max(bcd, bcdz);
     wg = std::max(wg, conv3d_wgrad_ws_bytes(v, p->KD, b.Cin, b.C));
     wg = std::max(wg, conv3d_wgrad_ws_bytes(v, p->KD, b.C, b.C));
@@ -311,13 +338,13 @@ int build_plan(spff_plan* p) {
   for (int l = 0; l < 3; ++l) {
     const Vol& vl = p->vol[l + 1];
     const int C = f << l;  // channels of e_{l+1} pooled
-    p->pool[l] = p->alloc(nvox(vl) * C * sizeof(float));
+    p->pool[l] = p->alloc_halo(nvox(vl) * C * sizeof(float), slice(vl, C));
     p->pidx[l] = p->alloc(nvox(vl) * C);
   }
   for (int u = 0; u < 3; ++u) {
     UpL& U = p->up[u];
     const Vol& vh = p->vol[U.lvl_low - 1];
-    U.out = p->alloc(nvox(vh) * U.Cout * sizeof(float));
+    U.out = p->alloc_halo(nvox(vh) * U.Cout * sizeof(float), slice(vh, U.Cout));
     U.pk = p->alloc(upconv_pack_floats(U.Cin, U.Cout) * sizeof(float));
     wg = std::max(wg, upconv_wgrad_ws_bytes(p->vol[U.lvl_low], U.Cin, U.Cout));
   }
@@ -334,12 +361,13 @@ int build_plan(spff_plan* p) {
   p->wt = p->alloc(wt);
   const size_t gbytes = nvox(v0) * f * sizeof(float);  // max over levels of V_l * C_l
   p->G_out = p->alloc(gbytes);
-  p->G_dy2 = p->alloc(gbytes);
-  p->G_da1 = p->alloc(gbytes);
+  p->G_dy2 = p->alloc_halo(gbytes, slice(v0, f));  // level-0 slice = the largest
+  p->G_da1 = p->alloc_halo(gbytes, slice(v0, f));
   p->G_dx = p->alloc(gbytes);
   for (int l = 0; l < 3; ++l) p->dskip[l] = p->alloc(nvox(p->vol[l]) * (f << l) * sizeof(float));
+  if (world > 1) p->part_d = p->alloc((size_t)B * 8 * f * 2 * sizeof(double));
 
-  host_pe(D, p->pe_host);  // uploaded on the first forward (plan creation needs no GPU)
+  host_pe(p->co.D_glob, p->pe_host);  // global depths; a slab reads columns d_off + d  // uploaded on the first forward (plan creation needs no GPU)
   return SPFF_OK;
 }
 
@@ -354,6 +382,8 @@ int ensure_pe(spff_plan* p) {
 GateParams gate_params(const spff_plan* p, const Blk& b) {
   GateParams g;
   g.pe = p->pe_dev;
+  g.pe_pitch = p->co.D_glob;
+  g.d_off = p->co.d_off;
   g.fw0 = b.efilm ? p->P(b.fw0) : nullptr;
   g.fb0 = b.efilm ? p->P(b.fb0) : nullptr;
   g.fw2 = b.efilm ? p->P(b.fw2) : nullptr;
@@ -374,19 +404,69 @@ GateSaved gate_saved(const spff_plan* p, const Blk& b) {
   s.s1 = p->F(b.s1); s.g1 = p->F(b.g1s); s.sg2 = p->F(b.sg2);
   s.p = p->F(b.p); s.h = p->F(b.h); s.e = p->F(b.e);
   s.P = p->F(b.P); s.Q = p->F(b.Q);
+  s.spec = p->co.on() ? p->D64(b.spec) : nullptr;
   return s;
+}
+
+// one D-slice halo per side for a conv input of a depth-sharded plan (no-op otherwise)
+int halo(spff_plan* p, const float* interior, const Vol& v, int C) {
+  if (!v.dh) return SPFF_OK;
+  const int64_t sl = (int64_t)v.H * v.W * C;
+  float* in = const_cast<float*>(interior);
+  if (p->co.rank == 0) HIPCK(hipMemsetAsync(in - sl, 0, sl * sizeof(float), p->st));
+  if (p->co.rank == p->co.world - 1)
+    HIPCK(hipMemsetAsync(in + v.D * sl, 0, sl * sizeof(float), p->st));
+  if (p->co.halo(p->co.ctx, in, sl, v.D, p->st) != 0) return fail(SPFF_EHIP, "halo exchange failed");
+  return SPFF_OK;
+}
+int halo_src(spff_plan* p, const Src2& x, const Vol& v) {
+  CK(halo(p, x.p0, v, x.ld0));
+  if (x.p1 != x.p0) CK(halo(p, x.p1, v, x.ld1));
+  return SPFF_OK;
 }
 
 int in_stats(spff_plan* p, const Vol& v, int C, size_t y, size_t mean, size_t rstd, size_t al,
              size_t de, int64_t gamma, int64_t beta) {
   RedArgs a{};
   a.y = p->F(y);
+  const bool sh = p->co.on();
+  double* pd = sh ? p->D64(p->part_d) : nullptr;
+  const double N = (double)p->co.D_glob * v.H * v.W;
   HIPCK(slab_reduce(RED_SUM, a, v, C, p->F(p->red_out), p->F(p->red_ws), p->st));
-  HIPCK(in_mean(p->F(p->red_out), p->F(mean), v, C, p->st));
+  if (sh) {  // per-(b,c) sums over the slab -> group sum -> global mean
+    HIPCK(in_partial(p->F(p->red_out), pd, v, C, 1, p->st));
+    HIPCK(p->co.sum_f64(pd, (int64_t)v.B * C, p->st));
+    HIPCK(in_mean_fin(pd, p->F(mean), v.B * C, N, p->st));
+  } else {
+    HIPCK(in_mean(p->F(p->red_out), p->F(mean), v, C, p->st));
+  }
   a.mean = p->F(mean);
   HIPCK(slab_reduce(RED_SQDEV, a, v, C, p->F(p->red_out), p->F(p->red_ws), p->st));
-  HIPCK(in_rstd(p->F(p->red_out), p->P(gamma), p->P(beta), p->F(mean), p->F(rstd), p->F(al),
-                p->F(de), v, C, p->st));
+  if (sh) {
+    HIPCK(in_partial(p->F(p->red_out), pd, v, C, 1, p->st));
+    HIPCK(p->co.sum_f64(pd, (int64_t)v.B * C, p->st));
+    HIPCK(in_rstd_fin(pd, p->P(gamma), p->P(beta), p->F(mean), p->F(rstd), p->F(al), p->F(de),
+                      v.B, C, N, p->st));
+  } else {
+    HIPCK(in_rstd(p->F(p->red_out), p->P(gamma), p->P(beta), p->F(mean), p->F(rstd), p->F(al),
+                  p->F(de), v, C, p->st));
+  }
+  return SPFF_OK;
+}
+
+// IN backward statistics from p->red_out = per-(b,c,d) [sum dr, sum dr*xhat]
+int in_bwd(spff_plan* p, const Vol& v, int C, int64_t gamma, int64_t beta) {
+  if (!p->co.on())
+    return in_bwd_stats(p->F(p->red_out), p->P(gamma), p->DP(gamma), p->DP(beta), p->F(p->kk1),
+                        p->F(p->kk2), v, C, p->st) == hipSuccess
+               ? SPFF_OK
+               : fail(SPFF_EHIP, "in_bwd_stats");
+  double* pd = p->D64(p->part_d);
+  HIPCK(in_partial(p->F(p->red_out), pd, v, C, 2, p->st));
+  HIPCK(in_bwd_dgb(pd, p->DP(gamma), p->DP(beta), v.B, C, p->st));  // local partial grads
+  HIPCK(p->co.sum_f64(pd, (int64_t)v.B * C * 2, p->st));
+  HIPCK(in_bwd_fin(pd, p->F(p->kk1), p->F(p->kk2), v.B * C,
+                   (double)p->co.D_glob * v.H * v.W, p->st));
   return SPFF_OK;
 }
 
@@ -395,6 +475,7 @@ int fwd_block(spff_plan* p, Blk& b, const Src2& in) {
   const int C = b.C, KD = p->KD;
   const int math = p->cfg.math;
   HIPCK(conv3d_pack(p->P(b.c1.w), p->F(p->wt), v, KD, b.Cin, C, false, math, p->st));
+  CK(halo_src(p, in, v));
   const double V = (double)nvox(v), T = 9.0 * KD;
   PROF(p, 0, 2.0 * V * b.Cin * C * T,
        conv3d_run(in, p->F(p->wt), dst1(p->F(b.y1), C), v, KD, b.Cin, C, false, math, p->st));
@@ -402,6 +483,7 @@ int fwd_block(spff_plan* p, Blk& b, const Src2& in) {
   HIPCK(act_apply(p->F(b.y1), p->F(b.a1), p->F(b.al1), p->F(b.de1), nullptr, nullptr, v, C,
                   p->st));
   HIPCK(conv3d_pack(p->P(b.c2.w), p->F(p->wt), v, KD, C, C, false, math, p->st));
+  CK(halo(p, p->F(b.a1), v, C));
   PROF(p, 0, 2.0 * V * C * C * T,
        conv3d_run(src1(p->F(b.a1), C), p->F(p->wt), dst1(p->F(b.y2), C), v, KD, C, C, false,
                   math, p->st));
@@ -414,7 +496,10 @@ int fwd_block(spff_plan* p, Blk& b, const Src2& in) {
     HIPCK(slab_reduce(RED_ACT, a, v, C, p->F(b.Sa), p->F(p->red_ws), p->st));
     GateParams gp = gate_params(p, b);
     GateSaved sv = gate_saved(p, b);
-    HIPCK(gates_fwd(gp, p->F(b.Sa), sv, v, C, p->F(p->gscr), p->st));
+    if (p->co.on())
+      HIPCK(gates_fwd_sh(gp, p->F(b.Sa), sv, v, C, p->F(p->gscr), p->co, p->st));
+    else
+      HIPCK(gates_fwd(gp, p->F(b.Sa), sv, v, C, p->F(p->gscr), p->st));
     HIPCK(act_apply(p->F(b.y2), p->F(b.out), p->F(b.al2), p->F(b.de2), p->F(b.P), p->F(b.Q), v,
                     C, p->st));
   } else {
@@ -449,8 +534,12 @@ int bwd_block(spff_plan* p, Blk& b, const float* dout, const Dst2* dx, const Src
     gg.sb0 = b.post_se ? p->DP(b.sb0) : nullptr;
     gg.sw2 = b.post_se ? p->DP(b.sw2) : nullptr;
     gg.sb2 = b.post_se ? p->DP(b.sb2) : nullptr;
-    HIPCK(gates_bwd(gp, sv, p->F(b.Sa), p->F(p->red_out), gg, p->F(p->Abuf), p->F(p->Bbuf), v,
-                    C, p->F(p->gscr), p->st));
+    if (p->co.on())
+      HIPCK(gates_bwd_sh(gp, sv, p->F(b.Sa), p->F(p->red_out), gg, p->F(p->Abuf), p->F(p->Bbuf),
+                         v, C, p->F(p->gscr), p->co, p->st));
+    else
+      HIPCK(gates_bwd(gp, sv, p->F(b.Sa), p->F(p->red_out), gg, p->F(p->Abuf), p->F(p->Bbuf), v,
+                      C, p->F(p->gscr), p->st));
     A = p->F(p->Abuf);
     Bc = p->F(p->Bbuf);
   }
@@ -461,8 +550,7 @@ int bwd_block(spff_plan* p, Blk& b, const float* dout, const Dst2* dx, const Src
     a.y = p->F(b.y2); a.g = dout; a.mean = p->F(b.mean2); a.rstd = p->F(b.rstd2);
     a.al = p->F(b.al2); a.de = p->F(b.de2); a.A = A; a.Bc = Bc;
     HIPCK(slab_reduce(RED_BWD_IN, a, v, C, p->F(p->red_out), p->F(p->red_ws), p->st));
-    HIPCK(in_bwd_stats(p->F(p->red_out), p->P(b.g2), p->DP(b.g2), p->DP(b.b2), p->F(p->kk1),
-                       p->F(p->kk2), v, C, p->st));
+    CK(in_bwd(p, v, C, b.g2, b.b2));
     HIPCK(in_bwd_apply(p->F(b.y2), dout, dy2, p->F(b.mean2), p->F(b.rstd2), p->F(b.al2),
                        p->F(b.de2), p->P(b.g2), A, Bc, p->F(p->kk1), p->F(p->kk2), v, C, p->st));
   }
@@ -472,6 +560,7 @@ int bwd_block(spff_plan* p, Blk& b, const float* dout, const Dst2* dx, const Src
                     p->F(p->wg_ws), p->st));
   const int math = p->cfg.math;
   HIPCK(conv3d_pack(p->P(b.c2.w), p->F(p->wt), v, KD, C, C, true, math, p->st));
+  CK(halo(p, dy2, v, C));
   PROF(p, 1, 2.0 * V * C * C * T,
        conv3d_run(src1(dy2, C), p->F(p->wt), dst1(da1, C), v, KD, C, C, true, math, p->st));
   {
@@ -479,8 +568,7 @@ int bwd_block(spff_plan* p, Blk& b, const float* dout, const Dst2* dx, const Src
     a.y = p->F(b.y1); a.g = da1; a.mean = p->F(b.mean1); a.rstd = p->F(b.rstd1);
     a.al = p->F(b.al1); a.de = p->F(b.de1);
     HIPCK(slab_reduce(RED_BWD_IN, a, v, C, p->F(p->red_out), p->F(p->red_ws), p->st));
-    HIPCK(in_bwd_stats(p->F(p->red_out), p->P(b.g1), p->DP(b.g1), p->DP(b.b1), p->F(p->kk1),
-                       p->F(p->kk2), v, C, p->st));
+    CK(in_bwd(p, v, C, b.g1, b.b1));
     HIPCK(in_bwd_apply(p->F(b.y1), da1, da1, p->F(b.mean1), p->F(b.rstd1), p->F(b.al1),
                        p->F(b.de1), p->P(b.g1), nullptr, nullptr, p->F(p->kk1), p->F(p->kk2), v,
                        C, p->st));
@@ -490,6 +578,7 @@ int bwd_block(spff_plan* p, Blk& b, const float* dout, const Dst2* dx, const Src
                     p->st));
   if (dx) {
     HIPCK(conv3d_pack(p->P(b.c1.w), p->F(p->wt), v, KD, b.Cin, C, true, math, p->st));
+    CK(halo(p, da1, v, C));
     PROF(p, 1, 2.0 * V * b.Cin * C * T,
          conv3d_run(src1(da1, C), p->F(p->wt), *dx, v, KD, b.Cin, C, true, math, p->st));
   }
@@ -605,6 +694,16 @@ int spff_plan_create(const spff_cfg* cfg, spff_plan** out) {
   return SPFF_OK;
 }
 
+int spff_plan_set_coll(spff_plan* p, const spff_coll* coll) {
+  if (!p || !coll) return fail(SPFF_EINVAL, "null argument");
+  if (!coll->allreduce || !coll->halo) return fail(SPFF_EINVAL, "spff_coll needs allreduce and halo");
+  p->co.ctx = coll->ctx;
+  p->co.allreduce = coll->allreduce;
+  p->co.halo = coll->halo;
+  p->coll_set = true;
+  return SPFF_OK;
+}
+
 void spff_plan_destroy(spff_plan* p) {
   if (!p) return;
   for (auto& r : p->prof) {
@@ -640,6 +739,8 @@ int spff_forward(spff_plan* p, const float* x, const float* params, float* logit
   p->prm = params;
   p->dprm = nullptr;
   p->st = static_cast<hipStream_t>(stream);
+  if (p->co.on() && !p->coll_set)
+    return fail(SPFF_EINVAL, "depth-sharded plan: call spff_plan_set_coll first");
   CK(ensure_pe(p));
   return forward(p, x, logits);
 }
@@ -651,6 +752,8 @@ int spff_backward(spff_plan* p, const float* dlogits, const float* params, float
   p->prm = params;
   p->dprm = dparams;
   p->st = static_cast<hipStream_t>(stream);
+  if (p->co.on() && !p->coll_set)
+    return fail(SPFF_EINVAL, "depth-sharded plan: call spff_plan_set_coll first");
   return backward(p, dlogits);
 }
 

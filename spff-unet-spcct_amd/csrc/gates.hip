@@ -75,12 +75,13 @@ __device__ void rowsum(int NI, int NJ, Fn f, double* part, double scale, double*
 __global__ void k_efilm_fwd(const float* __restrict__ pe, const float* __restrict__ fw0,
                             const float* __restrict__ fb0, const float* __restrict__ fw2,
                             const float* __restrict__ fb2, float* __restrict__ t,
-                            float* __restrict__ bt, float* __restrict__ hid, int C, int D) {
+                            float* __restrict__ bt, float* __restrict__ hid, int C, int D,
+                            int pitch) {
   extern __shared__ float hs[];  // [32][D]
   for (int i = threadIdx.x; i < 32 * D; i += blockDim.x) {
     const int j = i / D, d = i % D;
     float s = 0.f;
-    for (int q = 0; q < 16; ++q) s += fw0[j * 16 + q] * pe[q * D + d];
+    for (int q = 0; q < 16; ++q) s += fw0[j * 16 + q] * pe[q * pitch + d];
     s += fb0[j];
     hs[i] = s;
     if (blockIdx.x == 0) hid[i] = s;
@@ -210,7 +211,8 @@ hipError_t gates_fwd(const GateParams& gp, const float* Sa, GateSaved& sv, Vol v
   const int efilm = gp.fw0 != nullptr;
   if (efilm) {
     hipLaunchKernelGGL(k_efilm_fwd, dim3(cdiv(2 * C, 32)), dim3(256), 32 * D * sizeof(float), s,
-                       gp.pe, gp.fw0, gp.fb0, gp.fw2, gp.fb2, sv.t, sv.bt, sv.hid, C, D);
+                       gp.pe + gp.d_off, gp.fw0, gp.fb0, gp.fw2, gp.fb2, sv.t, sv.bt, sv.hid, C,
+                       D, gp.pe_pitch);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
@@ -483,12 +485,35 @@ __global__ void k_efilm_bwd3(GateParams gp, GateGrads gg, GScr gs, int D) {
   const int j = i / 17, q = i % 17;
   float s = 0.f;
   if (q < 16) {
-    for (int d = 0; d < D; ++d) s += gs.dh[j * D + d] * gp.pe[q * D + d];
+    for (int d = 0; d < D; ++d) s += gs.dh[j * D + d] * gp.pe[q * gp.pe_pitch + gp.d_off + d];
     gg.fw0[j * 16 + q] = s;
   } else {
     for (int d = 0; d < D; ++d) s += gs.dh[j * D + d];
     gg.fb0[j] = s;
   }
+}
+
+// SE / FourierGate parameter grads (sums over b) and the EFiLM MLP backward.
+// Lf = the spectrum length of the FULL depth (sharded plans: D_glob / 2 + 1).
+static hipError_t gates_bwd_tail(const GateParams& gp, const GateSaved& sv, GateGrads& gg,
+                                 const GScr& g, int B, int C, int D, int Dfull, int Hse,
+                                 hipStream_t s) {
+  hipError_t e;
+  if (gp.sw0 || gp.mask) {
+    hipLaunchKernelGGL(k_gates_bwd_final, dim3(64), dim3(256), 0, s, gp, gg, g, B, C, Dfull, Hse);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
+  if (gp.fw0) {
+    hipLaunchKernelGGL(k_efilm_bwd1, dim3(std::min(cdiv(2 * C * D, 256), 1024)), dim3(256), 0, s,
+                       g, sv.t, B, C, D);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_efilm_bwd2, dim3(cdiv(2 * C * 33 + 32 * D, 64)), dim3(64), 0, s, gp, gg,
+                       g, sv.hid, C, D);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_efilm_bwd3, dim3(cdiv(32 * 17, 64)), dim3(64), 0, s, gp, gg, g, D);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 hipError_t gates_bwd(const GateParams& gp, const GateSaved& sv, const float* Sa, const float* Sg,
@@ -501,21 +526,425 @@ hipError_t gates_bwd(const GateParams& gp, const GateSaved& sv, const float* Sa,
                      Sg, g, A, Bc, vol, C, Hse, efilm);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  if (gp.sw0 || gp.mask) {
-    hipLaunchKernelGGL(k_gates_bwd_final, dim3(64), dim3(256), 0, s, gp, gg, g, B, C, D, Hse);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
+  return gates_bwd_tail(gp, sv, gg, g, B, C, D, D, Hse, s);
+}
+
+// ====================================================== depth-sharded path ==
+// The slab holds depths [d_off, d_off + D) of Dg.  s1, g1, sg2, P, Q and the
+// EFiLM coefficients are per depth (local).  The FourierGate needs the
+// spectrum of the FULL s1: each slab adds its depths' terms (at their global
+// indices) and the partial spectra are all-reduced -- likewise the SE pool p[c]
+// and, backward, sum_d g1 sg2 R1 and the spectrum of dw.  Gradients of the SE
+// and FourierGate parameters are functions of those replicated totals: rank 0
+// writes them, the others write zeros, so the flat gradient all-reduce counts
+// them once.  EFiLM gradients are sums over the local depths (partials).
+namespace {
+struct ShScr {
+  double *ppart, *depart, *Tpart;
+  float *dw, *ds2, *c0, *dMr;
+};
+size_t sh_base(Vol vol, int C) { return (gates_scratch_bytes(vol, C) + 255) / 256 * 256; }
+ShScr shscr(float* base, Vol vol, int C, int Dg) {
+  char* p = reinterpret_cast<char*>(base) + sh_base(vol, C);
+  const int B = vol.B, L = Dg / 2 + 1, D = vol.D;
+  ShScr r;
+  r.ppart = reinterpret_cast<double*>(p); p += (size_t)B * C * 8;
+  r.depart = reinterpret_cast<double*>(p); p += (size_t)B * C * 8;
+  r.Tpart = reinterpret_cast<double*>(p); p += (size_t)B * L * 16;
+  r.dw = reinterpret_cast<float*>(p); p += (size_t)B * D * 4;
+  r.ds2 = reinterpret_cast<float*>(p); p += (size_t)B * D * 4;
+  r.c0 = reinterpret_cast<float*>(p); p += (size_t)B * C * 4;
+  r.dMr = reinterpret_cast<float*>(p);
+  return r;
+}
+struct ShShm {
+  double *twc, *tws, *part, *tmp, *Sre, *Sim, *Tre, *Tim;
+  float *s1, *g1, *sg2, *e, *c0, *ds2, *dw, *ds1;
+};
+__device__ ShShm sh_carve(void* base, int C, int D, int Dg) {
+  const int L = Dg / 2 + 1, M = (C > D ? C : D) > L ? (C > D ? C : D) : L;
+  ShShm m;
+  double* dp = reinterpret_cast<double*>(base);
+  m.twc = dp; dp += Dg;
+  m.tws = dp; dp += Dg;
+  m.part = dp; dp += GT;
+  m.tmp = dp; dp += M + 1;
+  m.Sre = dp; dp += L;
+  m.Sim = dp; dp += L;
+  m.Tre = dp; dp += L;
+  m.Tim = dp; dp += L;
+  float* fp = reinterpret_cast<float*>(dp);
+  m.s1 = fp; fp += D;
+  m.g1 = fp; fp += D;
+  m.sg2 = fp; fp += D;
+  m.ds2 = fp; fp += D;
+  m.dw = fp; fp += D;
+  m.ds1 = fp; fp += D;
+  m.e = fp; fp += C;
+  m.c0 = fp;
+  return m;
+}
+size_t sh_shmem(int C, int D, int Dg) {
+  const int L = Dg / 2 + 1, M = std::max(std::max(C, D), L);
+  return (2 * (size_t)Dg + GT + M + 1 + 4 * (size_t)L) * sizeof(double) +
+         (6 * (size_t)D + 2 * (size_t)C) * sizeof(float);
+}
+}  // namespace
+
+size_t gates_sh_scratch_bytes(Vol vol, int C, int Dg) {
+  const int B = vol.B, L = Dg / 2 + 1;
+  return sh_base(vol, C) + (size_t)B * C * 16 + (size_t)B * L * 16 + (size_t)B * vol.D * 8 +
+         (size_t)B * C * 4 + (size_t)B * L * 4 + 256;
+}
+
+// fwd A: s1 (local depths) and its partial spectrum -> sv.spec
+__global__ __launch_bounds__(GT) void k_gsh_fwd_a(GateParams gp, const float* __restrict__ Sa,
+                                                  GateSaved sv, Vol vol, int C, int efilm,
+                                                  int d_off, int Dg) {
+  const int b = blockIdx.x, D = vol.D, HW = vol.H * vol.W, L = Dg / 2 + 1;
+  extern __shared__ double shd[];
+  ShShm m = sh_carve(shd, C, D, Dg);
+  const float* Sab = Sa + (int64_t)b * C * D;
+  auto Z = [&](int c, int d) -> float {
+    const float sa = Sab[c * D + d];
+    return efilm ? (1.f + sv.t[c * D + d]) * sa + sv.bt[c * D + d] * (float)HW : sa;
+  };
+  make_twiddles(m.twc, m.tws, Dg);
+  rowsum(D, C, [&](int d, int c) { return (double)Z(c, d); }, m.part, 1.0 / ((double)C * HW),
+         m.tmp);
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    m.s1[d] = (float)m.tmp[d];
+    sv.s1[b * D + d] = m.s1[d];
   }
+  __syncthreads();
+  if (gp.mask) {
+    rowsum(L, D, [&](int k, int d) { return (double)m.s1[d] * m.twc[(k * (d_off + d)) % Dg]; },
+           m.part, 1.0, m.Sre);
+    rowsum(L, D, [&](int k, int d) { return -(double)m.s1[d] * m.tws[(k * (d_off + d)) % Dg]; },
+           m.part, 1.0, m.Sim);
+    for (int k = threadIdx.x; k < L; k += blockDim.x) {
+      sv.spec[((int64_t)b * L + k) * 2 + 0] = m.Sre[k];
+      sv.spec[((int64_t)b * L + k) * 2 + 1] = m.Sim[k];
+    }
+  }
+}
+
+// fwd B: gates from the full spectrum; SE pool partial -> ppart
+__global__ __launch_bounds__(GT) void k_gsh_fwd_b(GateParams gp, const float* __restrict__ Sa,
+                                                  GateSaved sv, Vol vol, int C, int efilm,
+                                                  int d_off, int Dg, ShScr sc) {
+  const int b = blockIdx.x, D = vol.D, HW = vol.H * vol.W, L = Dg / 2 + 1;
+  extern __shared__ double shd[];
+  ShShm m = sh_carve(shd, C, D, Dg);
+  const float* Sab = Sa + (int64_t)b * C * D;
+  auto Z = [&](int c, int d) -> float {
+    const float sa = Sab[c * D + d];
+    return efilm ? (1.f + sv.t[c * D + d]) * sa + sv.bt[c * D + d] * (float)HW : sa;
+  };
+  make_twiddles(m.twc, m.tws, Dg);
+  for (int d = threadIdx.x; d < D; d += blockDim.x) m.s1[d] = sv.s1[b * D + d];
+  if (gp.mask)
+    for (int k = threadIdx.x; k < L; k += blockDim.x) {
+      m.Sre[k] = sv.spec[((int64_t)b * L + k) * 2 + 0];
+      m.Sim[k] = sv.spec[((int64_t)b * L + k) * 2 + 1];
+    }
+  __syncthreads();
+  if (gp.mask) {
+    rowsum(D, L, [&](int d, int k) {
+      const int q = (k * (d_off + d)) % Dg;
+      const double Mk = (double)(gp.mask[k] * gp.mag[0]);
+      return ck_coef(k, Dg) * Mk * (m.Sre[k] * m.twc[q] - m.Sim[k] * m.tws[q]);
+    }, m.part, 1.0 / Dg, m.tmp);
+    for (int d = threadIdx.x; d < D; d += blockDim.x) m.g1[d] = sigm((float)m.tmp[d]);
+  } else {
+    for (int d = threadIdx.x; d < D; d += blockDim.x) m.g1[d] = 1.f;
+  }
+  __syncthreads();
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    m.sg2[d] = gp.specse ? sigm(m.g1[d] * m.s1[d]) : 1.f;
+    sv.g1[b * D + d] = m.g1[d];
+    sv.sg2[b * D + d] = m.sg2[d];
+  }
+  __syncthreads();
+  if (gp.sw0) {
+    rowsum(C, D, [&](int c, int d) { return (double)(m.g1[d] * m.sg2[d]) * (double)Z(c, d); },
+           m.part, 1.0 / ((double)Dg * HW), m.tmp);
+    for (int c = threadIdx.x; c < C; c += blockDim.x) sc.ppart[(int64_t)b * C + c] = m.tmp[c];
+  }
+}
+
+// fwd C: SE MLP on the all-reduced pool; apply coefficients P, Q
+__global__ __launch_bounds__(GT) void k_gsh_fwd_c(GateParams gp, GateSaved sv, Vol vol, int C,
+                                                  int Hse, int efilm, ShScr sc) {
+  const int b = blockIdx.x, D = vol.D;
+  __shared__ float pp[1024], hh[64], ee[1024];
+  if (gp.sw0) {
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+      pp[c] = (float)sc.ppart[(int64_t)b * C + c];
+      sv.p[b * C + c] = pp[c];
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < Hse; j += blockDim.x) {
+      float s = 0.f;
+      for (int c = 0; c < C; ++c) s += gp.sw0[j * C + c] * pp[c];
+      hh[j] = s + gp.sb0[j];
+      sv.h[b * Hse + j] = hh[j];
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+      float s = 0.f;
+      for (int j = 0; j < Hse; ++j) s += gp.sw2[c * Hse + j] * fmaxf(hh[j], 0.f);
+      ee[c] = sigm(s + gp.sb2[c]);
+      sv.e[b * C + c] = ee[c];
+    }
+  } else {
+    for (int c = threadIdx.x; c < C; c += blockDim.x) ee[c] = 1.f;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < C * D; i += blockDim.x) {
+    const int c = i / D, d = i % D;
+    const float G = sv.g1[b * D + d] * sv.sg2[b * D + d] * ee[c];
+    const float onept = efilm ? (1.f + sv.t[i]) : 1.f;
+    const float btv = efilm ? sv.bt[i] : 0.f;
+    sv.P[(int64_t)b * C * D + i] = onept * G;
+    sv.Q[(int64_t)b * C * D + i] = btv * G;
+  }
+}
+
+hipError_t gates_fwd_sh(const GateParams& gp, const float* Sa, GateSaved& sv, Vol vol, int C,
+                        float* scratch, const Coll& co, hipStream_t s) {
+  const int D = vol.D, B = vol.B, Hse = se_hidden(C), Dg = co.D_glob, L = Dg / 2 + 1;
+  const int efilm = gp.fw0 != nullptr;
+  if (C > 1024 || Hse > 64) return hipErrorInvalidValue;
+  hipError_t e;
   if (efilm) {
-    hipLaunchKernelGGL(k_efilm_bwd1, dim3(std::min(cdiv(2 * C * D, 256), 1024)), dim3(256), 0, s,
-                       g, sv.t, B, C, D);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_efilm_bwd2, dim3(cdiv(2 * C * 33 + 32 * D, 64)), dim3(64), 0, s, gp, gg,
-                       g, sv.hid, C, D);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_efilm_bwd3, dim3(cdiv(32 * 17, 64)), dim3(64), 0, s, gp, gg, g, D);
+    hipLaunchKernelGGL(k_efilm_fwd, dim3(cdiv(2 * C, 32)), dim3(256), 32 * D * sizeof(float), s,
+                       gp.pe + gp.d_off, gp.fw0, gp.fb0, gp.fw2, gp.fb2, sv.t, sv.bt, sv.hid, C,
+                       D, gp.pe_pitch);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
-  return hipSuccess;
+  ShScr sc = shscr(scratch, vol, C, Dg);
+  const size_t shm = sh_shmem(C, D, Dg);
+  hipLaunchKernelGGL(k_gsh_fwd_a, dim3(B), dim3(GT), shm, s, gp, Sa, sv, vol, C, efilm, co.d_off,
+                     Dg);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  if (gp.mask && (e = co.sum_f64(sv.spec, (int64_t)B * L * 2, s)) != hipSuccess) return e;
+  hipLaunchKernelGGL(k_gsh_fwd_b, dim3(B), dim3(GT), shm, s, gp, Sa, sv, vol, C, efilm, co.d_off,
+                     Dg, sc);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  if (gp.sw0 && (e = co.sum_f64(sc.ppart, (int64_t)B * C, s)) != hipSuccess) return e;
+  hipLaunchKernelGGL(k_gsh_fwd_c, dim3(B), dim3(GT), 0, s, gp, sv, vol, C, Hse, efilm, sc);
+  return hipGetLastError();
+}
+
+// bwd A: de[c] partial = sum_{local d} g1 sg2 R1
+__global__ __launch_bounds__(GT) void k_gsh_bwd_a(GateParams gp, GateSaved sv,
+                                                  const float* __restrict__ Sa,
+                                                  const float* __restrict__ Sg, Vol vol, int C,
+                                                  int efilm, int Dg, ShScr sc) {
+  const int b = blockIdx.x, D = vol.D;
+  extern __shared__ double shd[];
+  ShShm m = sh_carve(shd, C, D, Dg);
+  const int64_t bo = (int64_t)b * C * D;
+  auto R1 = [&](int c, int d) -> float {
+    const float sgd = Sg[(bo + c * D + d) * 2 + 0], sda = Sg[(bo + c * D + d) * 2 + 1];
+    return efilm ? (1.f + sv.t[c * D + d]) * sda + sv.bt[c * D + d] * sgd : sda;
+  };
+  (void)Sa;
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    m.g1[d] = sv.g1[b * D + d];
+    m.sg2[d] = sv.sg2[b * D + d];
+  }
+  __syncthreads();
+  rowsum(C, D, [&](int c, int d) { return (double)(m.g1[d] * m.sg2[d]) * (double)R1(c, d); },
+         m.part, 1.0, m.tmp);
+  for (int c = threadIdx.x; c < C; c += blockDim.x) sc.depart[(int64_t)b * C + c] = m.tmp[c];
+}
+
+// bwd B: SE grads (owner), c0, ds2, dw (local) and the partial spectrum of dw
+__global__ __launch_bounds__(GT) void k_gsh_bwd_b(GateParams gp, GateSaved sv,
+                                                  const float* __restrict__ Sa,
+                                                  const float* __restrict__ Sg, GScr gs, Vol vol,
+                                                  int C, int Hse, int efilm, int d_off, int Dg,
+                                                  int owner, ShScr sc) {
+  const int b = blockIdx.x, D = vol.D, HW = vol.H * vol.W, L = Dg / 2 + 1;
+  extern __shared__ double shd[];
+  ShShm m = sh_carve(shd, C, D, Dg);
+  __shared__ float dq[1024], dh[64];
+  const int64_t bo = (int64_t)b * C * D;
+  auto Zf = [&](int c, int d) -> float {
+    const float sa = Sa[bo + c * D + d];
+    return efilm ? (1.f + sv.t[c * D + d]) * sa + sv.bt[c * D + d] * (float)HW : sa;
+  };
+  auto R1 = [&](int c, int d) -> float {
+    const float sgd = Sg[(bo + c * D + d) * 2 + 0], sda = Sg[(bo + c * D + d) * 2 + 1];
+    return efilm ? (1.f + sv.t[c * D + d]) * sda + sv.bt[c * D + d] * sgd : sda;
+  };
+  make_twiddles(m.twc, m.tws, Dg);
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    m.g1[d] = sv.g1[b * D + d];
+    m.sg2[d] = sv.sg2[b * D + d];
+  }
+  __syncthreads();
+  if (gp.sw0) {
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+      const float ev = sv.e[b * C + c];
+      m.e[c] = ev;
+      dq[c] = (float)sc.depart[(int64_t)b * C + c] * ev * (1.f - ev);
+      gs.sb2p[b * C + c] = owner ? dq[c] : 0.f;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < C * Hse; i += blockDim.x) {
+      const int c = i / Hse, j = i % Hse;
+      gs.sw2p[(int64_t)b * C * Hse + i] = owner ? dq[c] * fmaxf(sv.h[b * Hse + j], 0.f) : 0.f;
+    }
+    for (int j = threadIdx.x; j < Hse; j += blockDim.x) {
+      float s = 0.f;
+      for (int c = 0; c < C; ++c) s += gp.sw2[c * Hse + j] * dq[c];
+      const float dhv = sv.h[b * Hse + j] > 0.f ? s : 0.f;
+      dh[j] = dhv;
+      gs.sb0p[b * Hse + j] = owner ? dhv : 0.f;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < Hse * C; i += blockDim.x) {
+      const int j = i / C, c = i % C;
+      gs.sw0p[(int64_t)b * Hse * C + i] = owner ? dh[j] * sv.p[b * C + c] : 0.f;
+    }
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+      float s = 0.f;
+      for (int j = 0; j < Hse; ++j) s += gp.sw0[j * C + c] * dh[j];
+      m.c0[c] = s / ((float)Dg * (float)HW);
+    }
+  } else {
+    for (int c = threadIdx.x; c < C; c += blockDim.x) { m.e[c] = 1.f; m.c0[c] = 0.f; }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += blockDim.x) sc.c0[(int64_t)b * C + c] = m.c0[c];
+  if (gp.specse) {
+    rowsum(D, C, [&](int d, int c) {
+      return (double)m.e[c] * R1(c, d) + (double)m.c0[c] * Zf(c, d);
+    }, m.part, 1.0, m.tmp);
+    for (int d = threadIdx.x; d < D; d += blockDim.x)
+      m.ds2[d] = m.sg2[d] * (1.f - m.sg2[d]) * m.g1[d] * (float)m.tmp[d];
+  } else {
+    for (int d = threadIdx.x; d < D; d += blockDim.x) m.ds2[d] = 0.f;
+  }
+  __syncthreads();
+  for (int d = threadIdx.x; d < D; d += blockDim.x) sc.ds2[b * D + d] = m.ds2[d];
+  const float invCHW = 1.f / ((float)C * (float)HW);
+  if (gp.mask) {
+    rowsum(D, C, [&](int d, int c) {
+      const float a = m.e[c] * m.sg2[d];
+      const float bb = m.c0[c] * m.sg2[d] + m.ds2[d] * invCHW;
+      return (double)a * R1(c, d) + (double)bb * Zf(c, d);
+    }, m.part, 1.0, m.tmp);
+    for (int d = threadIdx.x; d < D; d += blockDim.x) {
+      m.dw[d] = (float)m.tmp[d] * m.g1[d] * (1.f - m.g1[d]);
+      sc.dw[b * D + d] = m.dw[d];
+    }
+    __syncthreads();
+    rowsum(L, D, [&](int k, int d) { return (double)m.dw[d] * m.twc[(k * (d_off + d)) % Dg]; },
+           m.part, 1.0, m.Tre);
+    rowsum(L, D, [&](int k, int d) { return (double)m.dw[d] * m.tws[(k * (d_off + d)) % Dg]; },
+           m.part, 1.0, m.Tim);
+    for (int k = threadIdx.x; k < L; k += blockDim.x) {
+      sc.Tpart[((int64_t)b * L + k) * 2 + 0] = m.Tre[k];
+      sc.Tpart[((int64_t)b * L + k) * 2 + 1] = m.Tim[k];
+    }
+  }
+}
+
+// bwd C: FourierGate mask grads (owner), ds1 and the per-(c,d) A / Bc outputs
+__global__ __launch_bounds__(GT) void k_gsh_bwd_c(GateParams gp, GateSaved sv,
+                                                  const float* __restrict__ Sa,
+                                                  const float* __restrict__ Sg, GScr gs,
+                                                  float* __restrict__ Aout,
+                                                  float* __restrict__ Bout, Vol vol, int C,
+                                                  int efilm, int d_off, int Dg, int owner,
+                                                  ShScr sc) {
+  const int b = blockIdx.x, D = vol.D, HW = vol.H * vol.W, L = Dg / 2 + 1;
+  extern __shared__ double shd[];
+  ShShm m = sh_carve(shd, C, D, Dg);
+  const int64_t bo = (int64_t)b * C * D;
+  make_twiddles(m.twc, m.tws, Dg);
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    m.g1[d] = sv.g1[b * D + d];
+    m.sg2[d] = sv.sg2[b * D + d];
+    m.ds2[d] = sc.ds2[b * D + d];
+    m.ds1[d] = 0.f;
+  }
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    m.e[c] = gp.sw0 ? sv.e[b * C + c] : 1.f;
+    m.c0[c] = sc.c0[(int64_t)b * C + c];
+  }
+  if (gp.mask)
+    for (int k = threadIdx.x; k < L; k += blockDim.x) {
+      m.Sre[k] = sv.spec[((int64_t)b * L + k) * 2 + 0];
+      m.Sim[k] = sv.spec[((int64_t)b * L + k) * 2 + 1];
+      m.Tre[k] = sc.Tpart[((int64_t)b * L + k) * 2 + 0];
+      m.Tim[k] = sc.Tpart[((int64_t)b * L + k) * 2 + 1];
+    }
+  __syncthreads();
+  if (gp.mask) {
+    for (int k = threadIdx.x; k < L; k += blockDim.x)
+      gs.dMr[b * L + k] =
+          owner ? (float)(ck_coef(k, Dg) / Dg * (m.Sre[k] * m.Tre[k] - m.Sim[k] * m.Tim[k]))
+                : 0.f;
+    rowsum(D, L, [&](int d, int k) {
+      const int q = (k * (d_off + d)) % Dg;
+      const double Mk = (double)(gp.mask[k] * gp.mag[0]);
+      return ck_coef(k, Dg) * Mk * (m.twc[q] * m.Tre[k] + m.tws[q] * m.Tim[k]);
+    }, m.part, 1.0 / Dg, m.tmp);
+    for (int d = threadIdx.x; d < D; d += blockDim.x) m.ds1[d] = (float)m.tmp[d];
+    __syncthreads();
+  }
+  const float invCHW = 1.f / ((float)C * (float)HW);
+  for (int i = threadIdx.x; i < C * D; i += blockDim.x) {
+    const int c = i / D, d = i % D;
+    float al = m.e[c] * m.sg2[d];
+    float be = m.c0[c] * m.sg2[d] + m.ds2[d] * invCHW;
+    if (gp.mask) {
+      al = al * m.g1[d];
+      be = be * m.g1[d] + m.ds1[d] * invCHW;
+    }
+    if (efilm) {
+      const float sgd = Sg[(bo + i) * 2 + 0], sda = Sg[(bo + i) * 2 + 1];
+      gs.dt[bo + i] = al * sda + be * Sa[bo + i];
+      gs.dbt[bo + i] = al * sgd + be * (float)HW;
+      const float onept = 1.f + sv.t[i];
+      al *= onept;
+      be *= onept;
+    }
+    Aout[bo + i] = al;
+    Bout[bo + i] = be;
+  }
+}
+
+hipError_t gates_bwd_sh(const GateParams& gp, const GateSaved& sv, const float* Sa,
+                        const float* Sg, GateGrads& gg, float* A, float* Bc, Vol vol, int C,
+                        float* scratch, const Coll& co, hipStream_t s) {
+  const int D = vol.D, B = vol.B, Hse = se_hidden(C), Dg = co.D_glob, L = Dg / 2 + 1;
+  const int efilm = gp.fw0 != nullptr, owner = co.rank == 0;
+  if (C > 1024 || Hse > 64) return hipErrorInvalidValue;
+  GScr g = gscr(scratch, B, C, D, Hse);
+  ShScr sc = shscr(scratch, vol, C, Dg);
+  g.dMr = sc.dMr;  // [B][L] of the full depth
+  const size_t shm = sh_shmem(C, D, Dg);
+  hipError_t e;
+  if (gp.sw0) {
+    hipLaunchKernelGGL(k_gsh_bwd_a, dim3(B), dim3(GT), shm, s, gp, sv, Sa, Sg, vol, C, efilm, Dg,
+                       sc);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = co.sum_f64(sc.depart, (int64_t)B * C, s)) != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(k_gsh_bwd_b, dim3(B), dim3(GT), shm, s, gp, sv, Sa, Sg, g, vol, C, Hse, efilm,
+                     co.d_off, Dg, owner, sc);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  if (gp.mask && (e = co.sum_f64(sc.Tpart, (int64_t)B * L * 2, s)) != hipSuccess) return e;
+  hipLaunchKernelGGL(k_gsh_bwd_c, dim3(B), dim3(GT), shm, s, gp, sv, Sa, Sg, g, A, Bc, vol, C,
+                     efilm, co.d_off, Dg, owner, sc);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  return gates_bwd_tail(gp, sv, gg, g, B, C, D, Dg, Hse, s);
 }
 
 }  // namespace spff

@@ -228,6 +228,85 @@ hipError_t in_bwd_stats(const float* sums, const float* gamma, float* dgamma, fl
   return hipGetLastError();
 }
 
+// ---------------------------------------------- depth-sharded finalizers --
+// A sharded plan's per-(b,c,d) sums cover its own D-slab only: they are
+// reduced over d into fp64 partials, summed over the shard group (spff_coll
+// allreduce) and then finalised with the GLOBAL voxel count.
+__global__ void k_in_partial(const float* __restrict__ sums, double* __restrict__ part, Vol vol,
+                             int C, int nq) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // (bc, q)
+  if (i >= vol.B * C * nq) return;
+  const int q = i % nq;
+  const int64_t bc = i / nq;
+  double s = 0.0;
+  for (int d = 0; d < vol.D; ++d) s += sums[(bc * vol.D + d) * nq + q];
+  part[i] = s;
+}
+__global__ void k_in_mean_fin(const double* __restrict__ part, float* __restrict__ mean, int BC,
+                              double N) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < BC) mean[i] = (float)(part[i] / N);
+}
+__global__ void k_in_rstd_fin(const double* __restrict__ part, const float* __restrict__ gamma,
+                              const float* __restrict__ beta, const float* __restrict__ mean,
+                              float* __restrict__ rstd, float* __restrict__ al,
+                              float* __restrict__ de, int BC, int C, double N) {
+  const int bc = blockIdx.x * blockDim.x + threadIdx.x;
+  if (bc >= BC) return;
+  const int c = bc % C;
+  const float rs = (float)(1.0 / sqrt(part[bc] / N + 1e-5));
+  rstd[bc] = rs;
+  const float a = gamma[c] * rs;
+  al[bc] = a;
+  de[bc] = beta[c] - mean[bc] * a;
+}
+// gamma / beta gradients from the LOCAL partials (summed by the gradient all-reduce)
+__global__ void k_in_bwd_dgb(const double* __restrict__ part, float* __restrict__ dgamma,
+                             float* __restrict__ dbeta, int B, int C) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double tg = 0.0, tb = 0.0;
+  for (int b = 0; b < B; ++b) {
+    tb += part[((int64_t)b * C + c) * 2 + 0];
+    tg += part[((int64_t)b * C + c) * 2 + 1];
+  }
+  if (dgamma) dgamma[c] = (float)tg;
+  if (dbeta) dbeta[c] = (float)tb;
+}
+__global__ void k_in_bwd_fin(const double* __restrict__ part, float* __restrict__ k1,
+                             float* __restrict__ k2, int BC, double N) {
+  const int bc = blockIdx.x * blockDim.x + threadIdx.x;
+  if (bc >= BC) return;
+  k1[bc] = (float)(part[2 * bc + 0] / N);
+  k2[bc] = (float)(part[2 * bc + 1] / N);
+}
+
+hipError_t in_partial(const float* sums, double* part, Vol vol, int C, int nq, hipStream_t s) {
+  hipLaunchKernelGGL(k_in_partial, dim3(cdiv(vol.B * C * nq, 256)), dim3(256), 0, s, sums, part,
+                     vol, C, nq);
+  return hipGetLastError();
+}
+hipError_t in_mean_fin(const double* part, float* mean, int BC, double N, hipStream_t s) {
+  hipLaunchKernelGGL(k_in_mean_fin, dim3(cdiv(BC, 256)), dim3(256), 0, s, part, mean, BC, N);
+  return hipGetLastError();
+}
+hipError_t in_rstd_fin(const double* part, const float* gamma, const float* beta,
+                       const float* mean, float* rstd, float* al, float* de, int B, int C,
+                       double N, hipStream_t s) {
+  hipLaunchKernelGGL(k_in_rstd_fin, dim3(cdiv(B * C, 256)), dim3(256), 0, s, part, gamma, beta,
+                     mean, rstd, al, de, B * C, C, N);
+  return hipGetLastError();
+}
+hipError_t in_bwd_dgb(const double* part, float* dgamma, float* dbeta, int B, int C,
+                      hipStream_t s) {
+  hipLaunchKernelGGL(k_in_bwd_dgb, dim3(cdiv(C, 64)), dim3(64), 0, s, part, dgamma, dbeta, B, C);
+  return hipGetLastError();
+}
+hipError_t in_bwd_fin(const double* part, float* k1, float* k2, int BC, double N, hipStream_t s) {
+  hipLaunchKernelGGL(k_in_bwd_fin, dim3(cdiv(BC, 256)), dim3(256), 0, s, part, k1, k2, BC, N);
+  return hipGetLastError();
+}
+
 // ------------------------------------------------------------ elementwise --
 // grid.y = b*D + d ; grid.x strides over the (h,w,c/4) float4s of that slab.
 // The stride (gridDim.x * 256) is a multiple of C/4 (C/4 <= 64, power of two),

@@ -21,7 +21,13 @@ struct Dst2 {
 inline Src2 src1(const float* p, int ld) { return Src2{p, p, ld, ld, 1 << 30}; }
 inline Dst2 dst1(float* p, int ld) { return Dst2{p, p, ld, ld, 1 << 30}; }
 
-struct Vol { int B, D, H, W; };
+// dh = 1: a depth-sharded plan's conv inputs carry one neighbour slice before
+// and after the interior (B = 1), and the conv kernels read d = -1 and d = D
+// from them instead of treating those as zero padding.
+struct Vol {
+  int B, D, H, W;
+  int dh = 0;
+};
 inline int64_t nvox(const Vol& v) { return (int64_t)v.B * v.D * v.H * v.W; }
 
 // ---------------------------------------------------------------- conv3d --
@@ -112,6 +118,16 @@ hipError_t act_apply(const float* y, float* out, const float* al, const float* d
                      const float* P, const float* Q, Vol vol, int C, hipStream_t s);
 // IN backward finalize: from per-(b,c,d) [sum dr, sum dr*xhat] -> dgamma, dbeta (over b),
 // k1[b,c] = mean dr, k2[b,c] = mean dr*xhat
+// depth-sharded variants: fp64 partials over the local slab, summed across the
+// shard group by the caller, finalised with the global voxel count N
+hipError_t in_partial(const float* sums, double* part, Vol vol, int C, int nq, hipStream_t s);
+hipError_t in_mean_fin(const double* part, float* mean, int BC, double N, hipStream_t s);
+hipError_t in_rstd_fin(const double* part, const float* gamma, const float* beta,
+                       const float* mean, float* rstd, float* al, float* de, int B, int C,
+                       double N, hipStream_t s);
+hipError_t in_bwd_dgb(const double* part, float* dgamma, float* dbeta, int B, int C,
+                      hipStream_t s);
+hipError_t in_bwd_fin(const double* part, float* k1, float* k2, int BC, double N, hipStream_t s);
 hipError_t in_bwd_stats(const float* sums, const float* gamma, float* dgamma, float* dbeta,
                         float* k1, float* k2, Vol vol, int C, hipStream_t s);
 // dy = rstd*gamma*(dr - k1 - xhat*k2), dr = (g*A+Bc)*slope(y*al+de) ; may alias g
@@ -120,8 +136,23 @@ hipError_t in_bwd_apply(const float* y, const float* g, float* dy, const float* 
                         const float* A, const float* Bc, const float* k1, const float* k2,
                         Vol vol, int C, hipStream_t s);
 
+// Depth sharding: the shard group's collectives, supplied by the caller through
+// spff_coll (include/spff.h).  world == 1: unsharded, every call is a no-op.
+struct Coll {
+  int world = 1, rank = 0, d_off = 0, D_glob = 0;
+  void* ctx = nullptr;
+  int (*allreduce)(void*, void*, int64_t, int, void*) = nullptr;
+  int (*halo)(void*, float*, int64_t, int, void*) = nullptr;
+  bool on() const { return world > 1; }
+  hipError_t sum_f64(double* buf, int64_t n, hipStream_t s) const {
+    if (!on()) return hipSuccess;
+    return allreduce(ctx, buf, n, 1, s) == 0 ? hipSuccess : hipErrorUnknown;
+  }
+};
+
 struct GateParams {
-  const float* pe;   // sinusoidal code [16][D] (models.py:1495-1503)
+  const float* pe;   // sinusoidal code [16][pe_pitch] (models.py:1495-1503), column d_off + d
+  int pe_pitch, d_off;
   // EnergyFiLM (models.py:1479-1512)
   const float* fw0; const float* fb0; const float* fw2; const float* fb2;  // null if off
   // FourierGate (models.py:1515-1544)
@@ -135,6 +166,7 @@ struct GateSaved {
   float* s1; float* g1; float* sg2;   // [B][D]
   float* p; float* h; float* e;       // SE: p[B][C], h[B][Hse] (pre-ReLU), e[B][C]
   float* P; float* Q;                 // [B][C][D] apply coefficients
+  double* spec;                       // sharded plans: s1 spectrum [B][L][2] (global D)
 };
 int se_hidden(int C);
 // forward gate algebra from Sa[b,c,d] = sum_hw lrelu(IN(y2))
@@ -151,6 +183,14 @@ hipError_t gates_bwd(const GateParams& gp, const GateSaved& sv, const float* Sa,
                      const float* Sg, GateGrads& gg, float* A, float* Bc, Vol vol, int C,
                      float* scratch, hipStream_t s);
 size_t gates_scratch_bytes(Vol vol, int C);
+// the same on a depth-sharded slab: vol.D = local depth, co.D_glob the full one;
+// partial spectra / channel sums are all-reduced through co between kernels
+hipError_t gates_fwd_sh(const GateParams& gp, const float* Sa, GateSaved& sv, Vol vol, int C,
+                        float* scratch, const Coll& co, hipStream_t s);
+hipError_t gates_bwd_sh(const GateParams& gp, const GateSaved& sv, const float* Sa,
+                        const float* Sg, GateGrads& gg, float* A, float* Bc, Vol vol, int C,
+                        float* scratch, const Coll& co, hipStream_t s);
+size_t gates_sh_scratch_bytes(Vol vol, int C, int D_glob);
 
 // ------------------------------------------------------------------ misc --
 hipError_t ncdhw_to_ndhwc(const float* x, float* y, Vol vol, int C, int ldy, hipStream_t s);

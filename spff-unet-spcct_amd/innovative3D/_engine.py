@@ -28,8 +28,20 @@ class spff_cfg(ctypes.Structure):
         ("height", ctypes.c_int), ("width", ctypes.c_int), ("num_classes", ctypes.c_int),
         ("base", ctypes.c_int), ("ksd", ctypes.c_int), ("use_efilm", ctypes.c_int),
         ("use_fgate", ctypes.c_int), ("use_se", ctypes.c_int), ("use_specse", ctypes.c_int),
-        ("math", ctypes.c_int), ("reserved", ctypes.c_int * 7),
+        ("math", ctypes.c_int), ("shard_world", ctypes.c_int), ("shard_rank", ctypes.c_int),
+        ("reserved", ctypes.c_int * 5),
     ]
+
+
+# spff_coll (include/spff.h): the shard group's collectives, called back by the engine
+ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                ctypes.c_int, ctypes.c_void_p)
+HALO_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                           ctypes.c_int, ctypes.c_void_p)
+
+
+class spff_coll(ctypes.Structure):
+    _fields_ = [("ctx", ctypes.c_void_p), ("allreduce", ALLREDUCE_FN), ("halo", HALO_FN)]
 
 
 # conv arithmetic (include/spff.h SPFF_MATH_*)
@@ -52,6 +64,7 @@ _S = ctypes.c_size_t
 
 _SIGS = {
     "spff_plan_create": (_I, [ctypes.POINTER(spff_cfg), ctypes.POINTER(_P)]),
+    "spff_plan_set_coll": (_I, [_P, ctypes.POINTER(spff_coll)]),
     "spff_plan_destroy": (None, [_P]),
     "spff_last_error": (ctypes.c_char_p, []),
     "spff_num_params": (_I, [_P]),
@@ -134,20 +147,23 @@ class Plan:
     the matching backward (``generation`` guards against interleaving)."""
 
     def __init__(self, batch, in_ch, depth, height, width, num_classes, base=32, ksd=3,
-                 efilm=True, fgate=True, se=True, specse=True, device=None, math=None):
+                 efilm=True, fgate=True, se=True, specse=True, device=None, math=None,
+                 shard_world=1, shard_rank=0):
         math = default_math() if math is None else math
         if math not in MATH_NAMES:
             raise SpffError(f"math={math!r}: expected one of {sorted(MATH_NAMES)}")
         cfg = spff_cfg()
         cfg.math = MATH_NAMES[math]
+        cfg.shard_world, cfg.shard_rank = int(shard_world), int(shard_rank)
         self.math = math
+        self.shard = (int(shard_world), int(shard_rank))
         cfg.batch, cfg.in_ch, cfg.depth, cfg.height, cfg.width = batch, in_ch, depth, height, width
         cfg.num_classes, cfg.base, cfg.ksd = num_classes, base, ksd
         cfg.use_efilm, cfg.use_fgate, cfg.use_se, cfg.use_specse = (int(bool(efilm)), int(bool(fgate)),
                                                                     int(bool(se)), int(bool(specse)))
         self.cfg = cfg
         self.key = (batch, in_ch, depth, height, width, num_classes, base, ksd, bool(efilm),
-                    bool(fgate), bool(se), bool(specse), math)
+                    bool(fgate), bool(se), bool(specse), math, self.shard)
         L = lib()
         h = ctypes.c_void_p()
         check(L.spff_plan_create(ctypes.byref(cfg), ctypes.byref(h)), "spff_plan_create")
@@ -175,6 +191,44 @@ class Plan:
                 _lib.spff_plan_destroy(self._h)
         except Exception:
             pass
+
+    def set_coll(self, impl) -> None:
+        """Attach a depth-sharding collective implementation: an object with
+        ``allreduce(t)`` (in-place sum of a device tensor over the group) and
+        ``halo(slab, slice, d_local)`` (``slab`` = the [d_local + 2] x slice view
+        whose first / last slices receive the neighbours' boundary slices), e.g.
+        innovative3D.sharded.TorchDepthColl.  The engine calls them in stream
+        order with pointers into this plan's workspace."""
+        def view(ptr, n, dtype):
+            ws = self._ws
+            off = ptr - ws.data_ptr()
+            esz = 8 if dtype == torch.float64 else 4
+            if off < 0 or off % esz or off + n * esz > ws.numel():
+                raise SpffError("collective buffer outside the plan workspace")
+            return ws[off:off + n * esz].view(dtype)
+
+        def _allreduce(ctx, buf, n, dt, stream):
+            try:
+                impl.allreduce(view(buf, n, torch.float64 if dt == 1 else torch.float32))
+                return 0
+            except Exception as e:  # noqa: BLE001 -- reported through the engine status
+                self.coll_error = e
+                return 1
+
+        def _halo(ctx, interior, sl, d_local, stream):
+            try:
+                ws = self._ws
+                slab = view(interior - 4 * sl, (d_local + 2) * sl, torch.float32)
+                impl.halo(slab, int(sl), int(d_local))
+                return 0
+            except Exception as e:  # noqa: BLE001
+                self.coll_error = e
+                return 1
+        self._coll_fns = (ALLREDUCE_FN(_allreduce), HALO_FN(_halo))  # keep alive
+        self._coll = spff_coll(None, self._coll_fns[0], self._coll_fns[1])
+        self.coll_impl = impl
+        self.coll_error = None
+        check(lib().spff_plan_set_coll(self._h, ctypes.byref(self._coll)), "spff_plan_set_coll")
 
     def workspace(self, device) -> torch.Tensor:
         if self._ws is None or self._ws.device != device:
@@ -245,10 +299,12 @@ def get_plan(**kw) -> Plan:
     key = (kw["batch"], kw["in_ch"], kw["depth"], kw["height"], kw["width"], kw["num_classes"],
            kw.get("base", 32), kw.get("ksd", 3), bool(kw.get("efilm", True)),
            bool(kw.get("fgate", True)), bool(kw.get("se", True)), bool(kw.get("specse", True)),
-           kw.get("math") or default_math(), kw.get("tag", ""))
+           kw.get("math") or default_math(), tuple(kw.get("shard", (1, 0))), kw.get("tag", ""))
     if key not in _PLANS:
         kk = dict(kw)
         kk.pop("tag", None)
+        sh = kk.pop("shard", (1, 0))
+        kk["shard_world"], kk["shard_rank"] = sh
         _PLANS[key] = Plan(**kk)
     return _PLANS[key]
 

@@ -82,6 +82,12 @@ def _conf_np(logits, labels, num_classes, ignore_index):
 def macro_dice_loss(logits, labels, num_classes, ignore_index=255, smooth=1e-6):
     """1 - mean_{c>=1} hard Dice, plain mean (no NaN skipping), python float."""
     conf = _conf_np(logits, labels, num_classes, ignore_index)
+    return dice_loss_from_confusion(conf, num_classes, smooth)
+
+
+def dice_loss_from_confusion(conf, num_classes, smooth=1e-6):
+    """macro_dice_loss (helpers.py:782-795) from confusion counts conf[pred, label]
+    (a column K of out-of-range labels, if present, counts as fp only)."""
     K = int(num_classes)
     vals = []
     for c in range(1, K):

@@ -262,14 +262,24 @@ class UNet3D_SpectralCore(nn.Module):
         if C != self.in_channels:
             raise ValueError(f"expected {self.in_channels} input channels, got {C}")
         efilm, fgate = self._flags()
+        # depth sharding (innovative3D.sharded): x is this rank's D-slab of a
+        # volume of depth D * world; the FourierGate acts on the full depth
+        shard = tuple(getattr(self, "shard", (1, 0)))
         if fgate:
             for b in self._blocks():
-                b.fgate._ensure_mask(D, x.device)
-        return E.get_plan(batch=B, in_ch=C, depth=D, height=H, width=W,
+                b.fgate._ensure_mask(D * shard[0], x.device)
+        plan = E.get_plan(batch=B, in_ch=C, depth=D, height=H, width=W,
                           num_classes=self.num_classes, base=self.base, ksd=self.ksd,
                           efilm=efilm, fgate=fgate, se=self.use_se, specse=self.use_specse,
-                          device=x.device, math=getattr(self, "math", None),
+                          device=x.device, math=getattr(self, "math", None), shard=shard,
                           tag=f"{id(self)}:{tag}")
+        if shard[0] > 1:
+            coll = getattr(self, "shard_coll", None)
+            if coll is None:
+                raise E.SpffError("depth-sharded module: set .shard_coll (innovative3D.sharded)")
+            if getattr(plan, "coll_impl", None) is not coll:
+                plan.set_coll(coll)
+        return plan
 
     def _engine_params(self, plan) -> List[nn.Parameter]:
         named = dict(self.named_parameters(remove_duplicate=False))

@@ -1,0 +1,127 @@
+"""Depth sharding of one volume across the GPUs of a node (BASELINE config 4:
+a 5 x 512^3 volume, 8 x 64 depth slabs).
+
+D is never pooled by the network (pools and up-convolutions act on H, W), so
+rank r owns global depths [r * D_loc, (r + 1) * D_loc) at every level.  The
+engine (include/spff.h, spff_cfg.shard_world / shard_rank) runs the path on its
+slab and calls back, in stream order, for the only cross-slab couplings:
+
+  * a one-slice halo per side before every 3x3x3 convolution (forward input,
+    backward dy) -- ``halo``;
+  * fp64 all-reduces of the InstanceNorm moments, the channel-SE pool, the
+    partial rfft spectra of the FourierGate (forward s1, backward dw) and the
+    SE gradient contraction -- ``allreduce``.
+
+The loss is normalised by the GLOBAL valid-voxel count and the flat weight
+gradient is all-reduced once per step, as in innovative3D.distributed.  The
+algorithm is pinned against the unsharded oracle by tests/test_sharded_cpu.py
+(gloo, world 2 and 4) and the engine against the unsharded engine by
+tests/test_gpu_sharded.py.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from . import distributed as Dd
+
+
+class TorchDepthColl:
+    """spff_coll over a torch.distributed group.  Device tensors go straight to
+    the backend (RCCL: all_reduce and batched point-to-point send / recv on the
+    current stream); ``host_staged`` (default for gloo) copies through host
+    memory, which lets several ranks share one GPU in tests."""
+
+    def __init__(self, group=None, host_staged=None):
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.host = (dist.get_backend(group) == "gloo") if host_staged is None else host_staged
+
+    def _peer(self, r):
+        return dist.get_global_rank(self.group, r) if self.group is not None else r
+
+    def allreduce(self, t: torch.Tensor) -> None:
+        if self.host:
+            c = t.cpu()
+            dist.all_reduce(c, group=self.group)
+            t.copy_(c)
+        else:
+            dist.all_reduce(t, group=self.group)
+
+    def halo(self, slab: torch.Tensor, sl: int, d_local: int) -> None:
+        """slab: [(d_local + 2) * sl] view -- [left halo | d_local slices | right halo]."""
+        first, last = slab[sl:2 * sl], slab[d_local * sl:(d_local + 1) * sl]
+        left, right = slab[:sl], slab[(d_local + 1) * sl:]
+        r, w = self.rank, self.world
+        if self.host:
+            first_c, last_c = first.cpu(), last.cpu()
+            left_c, right_c = torch.empty_like(first_c), torch.empty_like(first_c)
+            ops = []
+            if r > 0:
+                ops += [dist.P2POp(dist.isend, first_c, self._peer(r - 1), self.group),
+                        dist.P2POp(dist.irecv, left_c, self._peer(r - 1), self.group)]
+            if r + 1 < w:
+                ops += [dist.P2POp(dist.isend, last_c, self._peer(r + 1), self.group),
+                        dist.P2POp(dist.irecv, right_c, self._peer(r + 1), self.group)]
+            for op in dist.batch_isend_irecv(ops) if ops else []:
+                op.wait()
+            if r > 0:
+                left.copy_(left_c)
+            if r + 1 < w:
+                right.copy_(right_c)
+            return
+        ops = []
+        if r > 0:
+            ops += [dist.P2POp(dist.isend, first.contiguous(), self._peer(r - 1), self.group),
+                    dist.P2POp(dist.irecv, left, self._peer(r - 1), self.group)]
+        if r + 1 < w:
+            ops += [dist.P2POp(dist.isend, last.contiguous(), self._peer(r + 1), self.group),
+                    dist.P2POp(dist.irecv, right, self._peer(r + 1), self.group)]
+        for op in dist.batch_isend_irecv(ops) if ops else []:
+            op.wait()
+
+
+def shard_bounds(D: int, world: int, rank: int):
+    """(offset, depth) of rank's slab of a depth-D volume (D divisible by world)."""
+    if D % world:
+        raise ValueError(f"depth {D} not divisible by {world} shards")
+    d = D // world
+    return rank * d, d
+
+
+class DepthShardedSPFF:
+    """``step(x_slab, y_slab)``: forward of this rank's slab through the sharded
+    engine, the global-count loss, backward and the flat gradient all-reduce.
+    Returns (loss, confusion) with the hard-Dice term from the all-reduced
+    confusion, i.e. the values of the unsharded step."""
+
+    def __init__(self, core: torch.nn.Module, num_classes: int, ignore_index: int = 255,
+                 group=None, coll=None):
+        self.core, self.K, self.ignore, self.group = core, int(num_classes), ignore_index, group
+        self.coll = coll or TorchDepthColl(group)
+        core.shard = (self.coll.world, self.coll.rank)
+        core.shard_coll = self.coll
+        self.params = [p for p in core.parameters()]
+
+    def step(self, x: torch.Tensor, y: torch.Tensor):
+        from .helpers import ce_dice_with_confusion, dice_loss_from_confusion
+        for p in self.params:
+            p.grad = None
+        logits = self.core(x)
+        self.last_logits = logits.detach()
+        cnt = Dd.global_valid_count(y, self.ignore, self.group)
+        loss_loc, conf = ce_dice_with_confusion(logits, y, self.K, self.ignore,
+                                                count_override=cnt)
+        loss_loc.backward()
+        Dd.allreduce_gradients(self.params, self.group)
+        # local value = local CE share + 0.5 * Dice of the LOCAL confusion; rebuild
+        # the global one from the summed CE shares and the summed confusion
+        conf_loc = conf.detach().cpu().numpy()
+        ce = (loss_loc.detach().double() -
+              0.5 * dice_loss_from_confusion(conf_loc, self.K)).reshape(1)
+        if Dd.world() > 1:
+            dist.all_reduce(ce, group=self.group)
+        Dd.allreduce_confusion(conf, self.group)
+        loss = ce[0] + 0.5 * dice_loss_from_confusion(conf.cpu().numpy(), self.K)
+        return loss, conf

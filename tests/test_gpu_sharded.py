@@ -1,0 +1,106 @@
+"""Depth-sharded engine (BASELINE config 4 path, include/spff.h shard_world /
+shard_rank + spff_coll) on ONE GPU: 2 and 4 ranks, each its own process and
+plan, exchange halos and all-reduce through host-staged gloo
+(innovative3D.sharded.TorchDepthColl).  Their gathered logits, the loss and
+the all-reduced gradients must match the unsharded engine on the same volume.
+Marked gpu."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+K, BASE, SHAPE = 5, 8, (1, 5, 8, 32, 32)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _model(math_mode):
+    import innovative3D.models as M
+    from innovative3D.weightgen import synth_state
+    core = M.build_spct_energyfilm_fourier(num_classes=K, base=BASE, in_channels=SHAPE[1])
+    for b in core._blocks():
+        b.fgate._ensure_mask(SHAPE[2], "cpu")
+    st = synth_state([(k, tuple(v.shape)) for k, v in core.state_dict().items()], seed=5)
+    # a non-trivial FourierGate (mask / scale) so the sharded spectra matter
+    for k in st:
+        if k.endswith("freq_mask") or k.endswith("_mask"):
+            st[k] = (0.5 + np.linspace(0, 1, st[k].size).reshape(st[k].shape)).astype(np.float32)
+    core.load_state_dict({k: torch.from_numpy(v) for k, v in st.items()})
+    core = core.to("cuda")
+    core.math = math_mode
+    return core
+
+
+def _data():
+    from innovative3D.synthetic import synthetic_batch
+    x, y = synthetic_batch(*SHAPE, num_classes=K, ignore_frac=0.05, seed=11)
+    return x, y
+
+
+def _worker(rank, world, port, math_mode, out):
+    import pathlib
+    import sys
+    root = pathlib.Path(__file__).resolve().parents[1]
+    sys.path[:0] = [str(root), str(root / "spff-unet-spcct_amd")]
+    from innovative3D.sharded import DepthShardedSPFF, shard_bounds
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    core = _model(math_mode)
+    x, y = _data()
+    off, d = shard_bounds(SHAPE[2], world, rank)
+    step = DepthShardedSPFF(core, K, 255)
+    loss, conf = step.step(x[:, :, off:off + d].contiguous().cuda(), y[:, off:off + d].contiguous().cuda())
+    torch.cuda.synchronize()
+    np.savez(f"{out}.{rank}.npz", logits=step.last_logits.cpu().numpy(), loss=float(loss),
+             conf=conf.cpu().numpy(),
+             **{"g_" + k: p.grad.cpu().numpy() for k, p in core.named_parameters()
+                if p.grad is not None})
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("math_mode", ["f32", "bf16x6"])
+@pytest.mark.parametrize("world", [2, 4])
+def test_depth_sharded_engine_matches_unsharded(tmp_path, world, math_mode):
+    import innovative3D.helpers as Hh
+    core = _model(math_mode)
+    x, y = _data()
+    logits = core(x.cuda())
+    loss, conf = Hh.ce_dice_with_confusion(logits, y.cuda(), K, 255)
+    loss.backward()
+    ref = logits.detach().cpu().numpy()
+    grads = {k: p.grad.cpu().numpy() for k, p in core.named_parameters() if p.grad is not None}
+    out = str(tmp_path / "sh")
+    mp.spawn(_worker, args=(world, _free_port(), math_mode, out), nprocs=world, join=True)
+    parts = [np.load(f"{out}.{r}.npz") for r in range(world)]
+    lg = np.concatenate([p["logits"] for p in parts], axis=2)
+    e = float(np.abs(lg - ref).max())
+    print(f"world {world} {math_mode}: max|dlogit| {e:.2e}, loss {float(parts[0]['loss']):.7f} "
+          f"vs {float(loss):.7f}")
+    assert e <= 1e-4 * float(np.abs(ref).max())
+    assert abs(float(parts[0]["loss"]) - float(loss)) <= 1e-5 * abs(float(loss))
+    np.testing.assert_array_equal(parts[0]["conf"], conf.cpu().numpy())
+    rows = []
+    for k, g in grads.items():
+        sc = max(float(np.abs(g).max()), 1e-30)
+        eg = float(np.abs(parts[0]["g_" + k] - g).max()) / sc
+        rows.append((eg, k))
+        for p in parts[1:]:
+            np.testing.assert_array_equal(p["g_" + k], parts[0]["g_" + k])
+    rows.sort(reverse=True)
+    print("  " + ", ".join(f"{k} {v:.1e}" for v, k in rows[:5]))
+    bad = [(k, v) for v, k in rows if v > (5e-2 if k.endswith("mag_scale") else 2e-3)]
+    assert not bad, bad
