@@ -102,6 +102,12 @@ def main():
     ap.add_argument("--math", choices=("f32", "bf16x6", "bf16x3"), default="bf16x6",
                     help="conv arithmetic: bf16x6 = fp32 operands split exactly into 3 bf16 "
                          "planes, 6 products, fp32 accumulate (fp32 accuracy class; default)")
+    ap.add_argument("--workload", choices=("patch128", "volume512"), default="patch128",
+                    help="patch128 = the headline (BASELINE configs[1]): batch data parallelism; "
+                         "volume512 = BASELINE configs[3]: one 5 x (64 N) x 512 x 512 volume "
+                         "depth-sharded over the N ranks (64-slice slab per rank, RCCL halos)")
+    ap.add_argument("--slab-depth", type=int, default=64)
+    ap.add_argument("--hw", type=int, default=512)
     ap.add_argument("--cpu-depth", type=int, default=32)
     ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--pmc", default=str(ROOT / "profiles" / "r01_pmc_conv.json"),
@@ -119,15 +125,28 @@ def main():
     from innovative3D.distributed import DataParallelSPFF
     from innovative3D.synthetic import synthetic_batch
 
-    B, S, K = args.batch, args.size, args.classes
-    core, st = build_model(K, args.base, args.in_ch, S, device)
-    core.math = args.math
-    x, y = synthetic_batch(B, args.in_ch, S, S, S, K, ignore_frac=0.01, seed=1000 + rank,
-                           device=device)
-    dp = DataParallelSPFF(core, K, 255)
+    K = args.classes
+    sharded = args.workload == "volume512"
+    if sharded:  # weak scaling: a fixed slab per rank, global depth = slab * world
+        from innovative3D.sharded import DepthShardedSPFF
+        B, Dl, HW = 1, args.slab_depth, args.hw
+        core, st = build_model(K, args.base, args.in_ch, Dl * world, device)
+        core.math = args.math
+        x, y = synthetic_batch(1, args.in_ch, Dl, HW, HW, K, ignore_frac=0.01, seed=1000 + rank,
+                               device=device)
+        runner = DepthShardedSPFF(core, K, 255) if world > 1 else DataParallelSPFF(core, K, 255)
+        vox_step = Dl * HW * HW
+    else:
+        B, S = args.batch, args.size
+        core, st = build_model(K, args.base, args.in_ch, S, device)
+        core.math = args.math
+        x, y = synthetic_batch(B, args.in_ch, S, S, S, K, ignore_frac=0.01, seed=1000 + rank,
+                               device=device)
+        runner = DataParallelSPFF(core, K, 255)
+        vox_step = B * S * S * S
 
     def step():
-        loss, _conf = dp.step(x, y)
+        loss, _conf = runner.step(x, y)
         return loss
 
     for _ in range(args.warmup):
@@ -152,7 +171,6 @@ def main():
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
-    vox_step = B * S * S * S
     value = world * vox_step * args.steps / elapsed
 
     # dominant kernel: the fwd/dgrad conv kernel (forward + input-grad convs), timed live
@@ -182,22 +200,32 @@ def main():
             "per_class_tflops": {k: (v[1] / (v[0] * 1e-3) / 1e12 if v[0] > 0 else None)
                                  for k, v in prof.items()},
             "step_tflops": value / world * 2462016 / 1e12}
+    if sharded:
+        cfg = {"workload": f"SPFF-UNet fwd+ce_plus_macro_dice+bwd, one 1 x {args.in_ch}ch x "
+                           f"{Dl * world} x {HW} x {HW} volume depth-sharded into {world} x "
+                           f"{Dl}-slice slabs (BASELINE configs[3] at 8 GPUs), K={K}, base {args.base}",
+               "global_batch": 1, "shape": [1, args.in_ch, Dl * world, HW, HW],
+               "parallelism": f"depth{world}"}
+        metric = "voxels/sec fwd+bwd, SPFF-UNet 5-ch volume depth-sharded (512^3 at 8 GPUs)"
+    else:
+        cfg = {"workload": f"SPFF-UNet fwd+ce_plus_macro_dice+bwd, batch {B} x {args.in_ch}ch x "
+                           f"{S}^3 per GPU, K={K}, base {args.base}",
+               "global_batch": B * world, "shape": [B, args.in_ch, S, S, S],
+               "parallelism": f"dp{world}"}
+        metric = "voxels/sec fwd+bwd, SPFF-UNet 5-ch 128^3 patch"
     out = {
-        "metric": "voxels/sec fwd+bwd, SPFF-UNet 5-ch 128^3 patch",
+        "metric": metric,
         "value": value, "unit": "voxels/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f32",
         "conv_math": args.math,
         "data": "synthetic (x~N(0,1), labels U[0,K) with 1% ignore=255; weights from weightgen seed 0)",
-        "config": {"workload": f"SPFF-UNet fwd+ce_plus_macro_dice+bwd, batch {B} x {args.in_ch}ch x "
-                               f"{S}^3 per GPU, K={K}, base {args.base}",
-                   "global_batch": B * world, "shape": [B, args.in_ch, S, S, S],
-                   "parallelism": f"dp{world}"},
+        "config": cfg,
         "loss": float(loss.item()),
         "roofline": roof,
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1 and args.cpu_baseline == "auto":
+    if rank == 0 and world == 1 and args.cpu_baseline == "auto" and not sharded:
         threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
         threads = min(threads, os.cpu_count() or threads)
         out["cpu_baseline"] = cpu_baseline(st, K, args.base, args.in_ch, S, S, args.cpu_depth,
