@@ -137,6 +137,14 @@ int spff_count_valid(const int64_t* labels, int64_t nvox, int ignore_index, int6
 /* x[i] *= *scale (scale is a device scalar) */
 int spff_scale(float* x, int64_t n, const float* scale, void* stream);
 
+/* fused Adam / AdamW step over n contiguous fp32 elements (replaces the
+ * torch.optim.Adam of BaseLitModel.configure_optimizers, models.py:591-594, and
+ * unified_optimizer.py:5-60): decoupled = 1 is AdamW; step = the 1-based step
+ * count after this update; arithmetic in torch's fp32 operation order. */
+int spff_adam_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq,
+                   int64_t n, double lr, double beta1, double beta2, double eps,
+                   double weight_decay, int decoupled, int64_t step, void* stream);
+
 /* op-level entry points (parity tests): channel-last activations, reference
  * weight layout W[Cout][Cin][ksd][3][3].  ws >= spff_conv3d_ws_bytes(...). */
 size_t spff_conv3d_ws_bytes(int B, int D, int H, int W, int cin, int cout, int ksd);

@@ -84,30 +84,31 @@ __global__ void k_conv_pack_x(const float* __restrict__ w, float* __restrict__ w
 
 // ------------------------------------------------------------ fwd / dgrad --
 namespace {
-constexpr int XT_D = 2, XT_H = 16, XT_W = 16, XT_THREADS = 512, XT_MB = 2;
-template <int KD>
+constexpr int XT_D = 2, XT_H = 16, XT_W = 16, XT_THREADS = 512;
+// MB 32-row blocks per wave: tile 2 x (8 MB) x 16 voxels
+template <int KD, int MB>
 __host__ __device__ constexpr int xt_npos() {
-  return (XT_D + KD - 1) * (XT_H + 2) * (XT_W + 2);
+  return (XT_D + KD - 1) * (8 * MB + 2) * (XT_W + 2);
 }
 template <int KD>
 __host__ __device__ constexpr int xt_t2() {
   return (KD * 9 + 1) & ~1;
 }
-template <int BN, int KD, int NS>
+template <int BN, int KD, int NS, int MB>
 constexpr size_t xt_lds_bytes() {
-  return (size_t)NS * (xt_npos<KD>() + xt_t2<KD>() * BN) * 16;
+  return (size_t)NS * (xt_npos<KD, MB>() + xt_t2<KD>() * BN) * 16;
 }
 }  // namespace
 
-template <int BN, int KD, int NS>
+template <int BN, int KD, int NS, int MB>
 __global__ __launch_bounds__(XT_THREADS, 1) void k_conv3d_fwd_x(
     Src2 x, const float4* __restrict__ wp, Dst2 y, Vol vol, int Cin, int nkc, int Cout, int npad,
     int tilesD, int tilesH, int tilesW) {
-  constexpr int TD = XT_D, TH = XT_H, TW = XT_W;
+  constexpr int TD = XT_D, TH = 8 * MB, TW = XT_W;
   constexpr int HD = TD + KD - 1, HH = TH + 2, HWD = TW + 2;
-  constexpr int NPOS = xt_npos<KD>();
+  constexpr int NPOS = xt_npos<KD, MB>();
   constexpr int T = KD * 9, T2 = xt_t2<KD>(), NJ = T2 / 2;
-  constexpr int NB = BN / 32, MB = XT_MB;
+  constexpr int NB = BN / 32;
   constexpr int NHX = NPOS * 2;  // halo float4 per chunk (8 channels = 2 float4)
   constexpr int RH = (NHX + XT_THREADS - 1) / XT_THREADS;
   constexpr int NWX = T2 * BN * 2;  // weight float4 per chunk (fp32, split at stash)
@@ -130,8 +131,8 @@ __global__ __launch_bounds__(XT_THREADS, 1) void k_conv3d_fwd_x(
 
   // voxel of MFMA row r in 32-row block q (q = wave*MB + mb)
   auto vrow = [](int q, int r, int& td, int& th, int& tw) {
-    td = q >> 3;
-    th = 2 * (q & 7) + (r >> 4);
+    td = q / (TH / 2);
+    th = 2 * (q % (TH / 2)) + (r >> 4);
     tw = r < 16 ? r : ((r + 14) & 15);
   };
   int hpos[MB];
@@ -141,6 +142,7 @@ __global__ __launch_bounds__(XT_THREADS, 1) void k_conv3d_fwd_x(
     vrow(wave * MB + mb, l32, td, th, tw);
     hpos[mb] = (td * HH + th) * HWD + tw;
   }
+  (void)HD;
 
   f32x16 acc[MB][NB];
 #pragma unroll
@@ -278,12 +280,12 @@ __global__ __launch_bounds__(XT_THREADS, 1) void k_conv3d_fwd_x(
   }
 }
 
-template <int BN, int KD, int NS>
+template <int BN, int KD, int NS, int MB>
 static hipError_t launch_fwd_x(const Src2& x, const float4* wx, const Dst2& y, Vol vol, int K,
                                int nkc, int N, int npad, hipStream_t s) {
-  constexpr size_t shm = xt_lds_bytes<BN, KD, NS>();
+  constexpr size_t shm = xt_lds_bytes<BN, KD, NS, MB>();
   static_assert(shm <= 160 * 1024, "LDS budget");
-  auto kern = k_conv3d_fwd_x<BN, KD, NS>;
+  auto kern = k_conv3d_fwd_x<BN, KD, NS, MB>;
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
@@ -291,7 +293,7 @@ static hipError_t launch_fwd_x(const Src2& x, const float4* wx, const Dst2& y, V
     if (e != hipSuccess) return e;
     attr = true;
   }
-  const int tilesD = cdiv(vol.D, XT_D), tilesH = cdiv(vol.H, XT_H), tilesW = cdiv(vol.W, XT_W);
+  const int tilesD = cdiv(vol.D, XT_D), tilesH = cdiv(vol.H, 8 * MB), tilesW = cdiv(vol.W, XT_W);
   dim3 grid(vol.B * tilesD * tilesH * tilesW, npad / BN);
   hipLaunchKernelGGL(kern, grid, dim3(XT_THREADS), shm, s, x, wx, y, vol, K, nkc, N, npad, tilesD,
                      tilesH, tilesW);
@@ -357,11 +359,12 @@ hipError_t conv3d_pack(const float* w, void* wpack, Vol vol, int KD, int Cin_w, 
 template <int NS>
 static hipError_t run_x(const Src2& x, const float4* wu, const Dst2& y, Vol vol, int KD,
                         const XDims& d, hipStream_t s) {
+  // (MB = 4, 1024-voxel tiles for Cout <= 32, fits LDS but spills 33 VGPRs at NS = 3)
   if (d.BN == 64)
-    return KD == 3 ? launch_fwd_x<64, 3, NS>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s)
-                   : launch_fwd_x<64, 1, NS>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s);
-  return KD == 3 ? launch_fwd_x<32, 3, NS>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s)
-                 : launch_fwd_x<32, 1, NS>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s);
+    return KD == 3 ? launch_fwd_x<64, 3, NS, 2>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s)
+                   : launch_fwd_x<64, 1, NS, 2>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s);
+  return KD == 3 ? launch_fwd_x<32, 3, NS, 2>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s)
+                 : launch_fwd_x<32, 1, NS, 2>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s);
 }
 
 hipError_t conv3d_run(const Src2& x, const void* wpack, const Dst2& y, Vol vol, int KD,

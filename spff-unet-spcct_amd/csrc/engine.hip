@@ -858,6 +858,17 @@ int spff_scale(float* x, int64_t n, const float* scale, void* stream) {
   return SPFF_OK;
 }
 
+int spff_adam_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq,
+                   int64_t n, double lr, double beta1, double beta2, double eps,
+                   double weight_decay, int decoupled, int64_t step, void* stream) {
+  if (n > 0 && (!params || !grads || !exp_avg || !exp_avg_sq))
+    return fail(SPFF_EINVAL, "null argument");
+  if (step < 1) return fail(SPFF_EINVAL, "step must be >= 1");
+  HIPCK(adam_step(params, grads, exp_avg, exp_avg_sq, n, lr, beta1, beta2, eps, weight_decay,
+                  decoupled, step, static_cast<hipStream_t>(stream)));
+  return SPFF_OK;
+}
+
 // ---- op-level conv entry points ----
 static size_t conv_op_pack_floats(int cin, int cout, int ksd) {
   ConvL c;

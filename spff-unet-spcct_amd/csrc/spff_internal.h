@@ -200,6 +200,11 @@ hipError_t maxpool_bwd_add(const float* dp, const uint8_t* idx, const float* dsk
                            float* dx, Vol in, int C, hipStream_t s);
 hipError_t scale_by_dev(float* x, int64_t n, const float* scale, hipStream_t s);
 
+// ----------------------------------------------------------------- optim --
+hipError_t adam_step(float* p, const float* g, float* m, float* v, int64_t n, double lr,
+                     double beta1, double beta2, double eps, double wd, int decoupled,
+                     int64_t step, hipStream_t s);
+
 // ------------------------------------------------------------------ loss --
 size_t loss_ws_bytes(int64_t V, int K);
 // conf: K x (K+1) int64, conf[pred*(K+1) + label], column K = label outside [0,K)

@@ -87,6 +87,8 @@ _SIGS = {
     "spff_conv3d_ws_bytes": (_S, [_I, _I, _I, _I, _I, _I, _I]),
     "spff_conv3d_fwd": (_I, [_P, _I, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
     "spff_conv3d_dgrad": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
+    "spff_adam_step": (_I, [_P, _P, _P, _P, _L, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                            ctypes.c_double, ctypes.c_double, _I, _L, _P]),
     "spff_conv3d_fwd_ex": (_I, [_P, _I, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
     "spff_conv3d_dgrad_ex": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
     "spff_conv3d_wgrad_ex": (_I, [_P, _I, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P]),

@@ -20,6 +20,7 @@ BaseLitModel 466-594.
 from __future__ import annotations
 
 import math
+import os
 from typing import List, Optional, Tuple
 
 import numpy as np
@@ -410,7 +411,12 @@ class BaseLitModel(pl.LightningModule):
         return self._shared_step(batch, "test")
 
     def configure_optimizers(self):
-        opt = torch.optim.Adam(self.parameters(), lr=self.hparams.lr)
+        # SPFF_FUSED_ADAM=1: the engine's fused Adam (same arithmetic, one pass)
+        if os.environ.get("SPFF_FUSED_ADAM", "0") == "1":
+            from .optim import SPFFAdam
+            opt = SPFFAdam(self.parameters(), lr=self.hparams.lr)
+        else:
+            opt = torch.optim.Adam(self.parameters(), lr=self.hparams.lr)
         sch = torch.optim.lr_scheduler.ReduceLROnPlateau(opt, mode="max", factor=0.5, patience=5)
         return {"optimizer": opt, "lr_scheduler": {"scheduler": sch, "monitor": "val_macro_dice"}}
 

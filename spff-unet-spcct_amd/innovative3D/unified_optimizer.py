@@ -16,8 +16,10 @@ def apply_unified_optimizer(lr: float = 1e-4, opt_cls=torch.optim.Adam, betas=(0
                             poly_power: float = 0.9, disable_lr_hooks: bool = True):
     import innovative3D.models as M
 
+    from innovative3D.optim import SPFFAdam, SPFFAdamW
+
     def _cfg(self):
-        if opt_cls in (torch.optim.Adam, torch.optim.AdamW):
+        if opt_cls in (torch.optim.Adam, torch.optim.AdamW, SPFFAdam, SPFFAdamW):
             opt = opt_cls(self.parameters(), lr=lr, betas=betas, weight_decay=weight_decay)
         else:
             opt = opt_cls(self.parameters(), lr=lr)
