@@ -85,28 +85,29 @@ __global__ void k_conv_pack_x(const float* __restrict__ w, float* __restrict__ w
 // ------------------------------------------------------------ fwd / dgrad --
 namespace {
 constexpr int XT_D = 2, XT_H = 16, XT_W = 16, XT_THREADS = 512;
-// MB 32-row blocks per wave: tile 2 x (8 MB) x 16 voxels
-template <int KD, int MB>
+// NW waves x MB 32-row blocks per wave: tile 2 x (NW MB) x 16 voxels
+template <int KD, int TH>
 __host__ __device__ constexpr int xt_npos() {
-  return (XT_D + KD - 1) * (8 * MB + 2) * (XT_W + 2);
+  return (XT_D + KD - 1) * (TH + 2) * (XT_W + 2);
 }
 template <int KD>
 __host__ __device__ constexpr int xt_t2() {
   return (KD * 9 + 1) & ~1;
 }
-template <int BN, int KD, int NS, int MB>
+template <int BN, int KD, int NS, int TH>
 constexpr size_t xt_lds_bytes() {
-  return (size_t)NS * (xt_npos<KD, MB>() + xt_t2<KD>() * BN) * 16;
+  return (size_t)NS * (xt_npos<KD, TH>() + xt_t2<KD>() * BN) * 16;
 }
 }  // namespace
 
-template <int BN, int KD, int NS, int MB>
-__global__ __launch_bounds__(XT_THREADS, 1) void k_conv3d_fwd_x(
+template <int BN, int KD, int NS, int MB, int NW>
+__global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
     Src2 x, const float4* __restrict__ wp, Dst2 y, Vol vol, int Cin, int nkc, int Cout, int npad,
     int tilesD, int tilesH, int tilesW) {
-  constexpr int TD = XT_D, TH = 8 * MB, TW = XT_W;
+  constexpr int XT_THREADS = NW * 64;
+  constexpr int TD = XT_D, TH = NW * MB, TW = XT_W;
   constexpr int HD = TD + KD - 1, HH = TH + 2, HWD = TW + 2;
-  constexpr int NPOS = xt_npos<KD, MB>();
+  constexpr int NPOS = xt_npos<KD, TH>();
   constexpr int T = KD * 9, T2 = xt_t2<KD>(), NJ = T2 / 2;
   constexpr int NB = BN / 32;
   constexpr int NHX = NPOS * 2;  // halo float4 per chunk (8 channels = 2 float4)
@@ -280,12 +281,12 @@ __global__ __launch_bounds__(XT_THREADS, 1) void k_conv3d_fwd_x(
   }
 }
 
-template <int BN, int KD, int NS, int MB>
+template <int BN, int KD, int NS, int MB, int NW = 8>
 static hipError_t launch_fwd_x(const Src2& x, const float4* wx, const Dst2& y, Vol vol, int K,
                                int nkc, int N, int npad, hipStream_t s) {
-  constexpr size_t shm = xt_lds_bytes<BN, KD, NS, MB>();
-  static_assert(shm <= 160 * 1024, "LDS budget");
-  auto kern = k_conv3d_fwd_x<BN, KD, NS, MB>;
+  constexpr size_t shm = xt_lds_bytes<BN, KD, NS, NW * MB>();
+  static_assert(shm <= (NW == 8 ? 160 : 80) * 1024, "LDS budget");
+  auto kern = k_conv3d_fwd_x<BN, KD, NS, MB, NW>;
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
@@ -293,9 +294,9 @@ static hipError_t launch_fwd_x(const Src2& x, const float4* wx, const Dst2& y, V
     if (e != hipSuccess) return e;
     attr = true;
   }
-  const int tilesD = cdiv(vol.D, XT_D), tilesH = cdiv(vol.H, 8 * MB), tilesW = cdiv(vol.W, XT_W);
+  const int tilesD = cdiv(vol.D, XT_D), tilesH = cdiv(vol.H, NW * MB), tilesW = cdiv(vol.W, XT_W);
   dim3 grid(vol.B * tilesD * tilesH * tilesW, npad / BN);
-  hipLaunchKernelGGL(kern, grid, dim3(XT_THREADS), shm, s, x, wx, y, vol, K, nkc, N, npad, tilesD,
+  hipLaunchKernelGGL(kern, grid, dim3(NW * 64), shm, s, x, wx, y, vol, K, nkc, N, npad, tilesD,
                      tilesH, tilesW);
   return hipGetLastError();
 }
@@ -360,6 +361,7 @@ template <int NS>
 static hipError_t run_x(const Src2& x, const float4* wu, const Dst2& y, Vol vol, int KD,
                         const XDims& d, hipStream_t s) {
   // (MB = 4, 1024-voxel tiles for Cout <= 32, fits LDS but spills 33 VGPRs at NS = 3)
+  // (NW = 4 waves, 2 x 8 x 16 tiles, BN 32, two workgroups per CU: measured 6 % slower)
   if (d.BN == 64)
     return KD == 3 ? launch_fwd_x<64, 3, NS, 2>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s)
                    : launch_fwd_x<64, 1, NS, 2>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s);

@@ -86,4 +86,6 @@ def test_fused_adam_on_spff_training_step():
         worst = max(float((pa[k] - pb[k]).abs().max() / max(float(pb[k].abs().max()), 1e-12))
                     for k in pb)
         assert worst <= 1e-6, worst
-    assert torch.equal(a.state_dict()["enc1.fgate.freq_mask"], b.state_dict()["enc1.fgate.freq_mask"])
+    # the FourierGate masks, created lazily by the first forward (after the optimizer),
+    # are not optimised: still the ones they were created as
+    assert torch.all(a.state_dict()["enc1.fgate.freq_mask"] == 1)
