@@ -177,6 +177,7 @@ def main():
     ms = prof["conv_fwd"][0] + prof["conv_dgrad"][0]
     fl = prof["conv_fwd"][1] + prof["conv_dgrad"][1]
     nl = prof["conv_fwd"][2] + prof["conv_dgrad"][2]
+    cb = prof["conv_fwd"][3] + prof["conv_dgrad"][3]
     achieved = fl / (ms * 1e-3) / 1e12 if ms > 0 else None
     traffic = None
     try:
@@ -196,6 +197,10 @@ def main():
             "frac_of_fp32_mfma_peak": (achieved / FP32_MFMA_PEAK_TFLOPS) if achieved else None,
             "avg_launch_ms": ms / max(1, nl), "launches": int(nl),
             "algorithmic_flops_per_launch": fl / max(1, nl),
+            "compulsory_bytes_per_launch": cb / max(1, nl),
+            "traffic_over_compulsory": (traffic / (cb / nl)) if (traffic and nl and cb) else None,
+            "traffic_note": ("PMC HBM bytes per launch of this kernel (2 x FETCH_SIZE + WRITE_SIZE, "
+                             "profiles/r01_pmc_conv.json, same bench config)"),
             "per_class_ms_per_step": {k: v[0] / args.steps for k, v in prof.items()},
             "per_class_tflops": {k: (v[1] / (v[0] * 1e-3) / 1e12 if v[0] > 0 else None)
                                  for k, v in prof.items()},

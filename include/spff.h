@@ -113,7 +113,8 @@ int spff_debug_set(spff_plan* plan, int key, int value);
 /* optional HIP-event timing of the MFMA kernels on the plan's stream (bench.py):
  * classes 0 = conv3d fwd, 1 = conv3d dgrad (same kernel), 2 = conv3d wgrad,
  * 3 = ConvTranspose / 1x1 head GEMMs.  collect() syncs on the recorded events
- * and writes out[3*c + {0,1,2}] = {total ms, algorithmic FLOPs, launches}. */
+ * and writes out[4*c + {0,1,2,3}] = {total ms, algorithmic FLOPs, launches,
+ * compulsory HBM bytes (operands read once, result written once; conv classes)}. */
 int spff_prof_enable(spff_plan* plan, int on);
 int spff_prof_collect(spff_plan* plan, double* out, int nclass);
 

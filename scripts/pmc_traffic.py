@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""Per-launch HBM traffic of the dominant conv kernel from two rocprofv3 --pmc
+passes of bench.py (FETCH_SIZE, WRITE_SIZE; scripts/gpu_round.sh pmc), with
+MI355X_MICROARCH.md's gfx950 correction: FETCH_SIZE reports half the bytes of
+16-B/lane streaming reads, so traffic = 2 x FETCH_SIZE + WRITE_SIZE (both in KB).
+
+    python scripts/pmc_traffic.py gpurun_out/pmc_fetch/run_counter_collection.csv \
+        gpurun_out/pmc_write/run_counter_collection.csv profiles/r01_pmc_conv.json
+"""
+import csv
+import json
+import statistics
+import sys
+
+KERNEL = "k_conv3d_fwd_x"
+
+
+def per_dispatch(path, counter):
+    out = {}
+    for r in csv.DictReader(open(path)):
+        if KERNEL in r["Kernel_Name"] and r["Counter_Name"] == counter:
+            out[int(r["Dispatch_Id"])] = (float(r["Counter_Value"]), r["Kernel_Name"].split("(")[0])
+    return out
+
+
+fetch = per_dispatch(sys.argv[1], "FETCH_SIZE")
+write = per_dispatch(sys.argv[2], "WRITE_SIZE")
+f_kb = [v for v, _ in fetch.values()]
+w_kb = [v for v, _ in write.values()]
+fetch_b = 2 * statistics.fmean(f_kb) * 1024
+write_b = statistics.fmean(w_kb) * 1024
+res = {"kernel": KERNEL, "launches_fetch": len(f_kb), "launches_write": len(w_kb),
+       "fetch_bytes_per_launch_corrected": fetch_b, "write_bytes_per_launch": write_b,
+       "hbm_bytes_per_launch": fetch_b + write_b,
+       "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes, --kernel-trace), "
+                 "bench.py --steps 1 --warmup 1; traffic = 2 x FETCH_SIZE + WRITE_SIZE (KB -> B), "
+                 "averaged over the fwd+dgrad launches"}
+json.dump(res, open(sys.argv[3], "w"), indent=1)
+print(json.dumps(res, indent=1))
+
+# per-kernel table of the same two passes (all spff kernels): corrected HBM bytes and the
+# effective bandwidth over the traced duration -- the memory-bound kernels' evidence.
+if len(sys.argv) > 4:
+    import collections
+    agg = collections.defaultdict(lambda: [0.0, 0.0, 0, 0])
+    for path, ctr, idx in ((sys.argv[1], "FETCH_SIZE", 0), (sys.argv[2], "WRITE_SIZE", 1)):
+        for r in csv.DictReader(open(path)):
+            if "spff::" not in r["Kernel_Name"] or r["Counter_Name"] != ctr:
+                continue
+            k = r["Kernel_Name"].split("(")[0].replace("void ", "")
+            a = agg[k]
+            a[idx] += float(r["Counter_Value"]) * 1024 * (2 if idx == 0 else 1)
+            if idx == 0:
+                a[2] += 1
+                a[3] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    with open(sys.argv[4], "w") as f:
+        f.write("kernel,launches,fetch_bytes_x2,write_bytes,hbm_bytes_per_launch,ms_per_launch,GBps\n")
+        for k, (fb, wb, n, ns) in sorted(agg.items(), key=lambda kv: -kv[1][0] - kv[1][1]):
+            f.write(f"\"{k}\",{n},{fb:.0f},{wb:.0f},{(fb + wb) / max(1, n):.0f},"
+                    f"{ns / max(1, n) / 1e6:.4f},{(fb + wb) / max(1, ns):.1f}\n")

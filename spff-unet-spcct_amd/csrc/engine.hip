@@ -39,10 +39,13 @@ static int fail(int code, const std::string& m) {
       return fail(SPFF_EHIP, std::string(#expr) + " -> " + hipGetErrorString(_e));         \
   } while (0)
 // PROF: time one launch with HIP events on the plan's stream when enabled.
-#define PROF(P, CLS, FLOPS, expr)                                                        \
+// PROFB also records the launch's compulsory HBM bytes (operands read once, result
+// written once) for the roofline's traffic comparison.
+#define PROF(P, CLS, FLOPS, expr) PROFB(P, CLS, FLOPS, 0.0, expr)
+#define PROFB(P, CLS, FLOPS, BYTES, expr)                                                \
   do {                                                                                   \
     spff_plan* _p = (P);                                                                 \
-    spff_plan::ProfRec* _r = _p->prof_on ? prof_slot(_p, (CLS), (FLOPS)) : nullptr;      \
+    spff_plan::ProfRec* _r = _p->prof_on ? prof_slot(_p, (CLS), (FLOPS), (BYTES)) : nullptr; \
     if (_r) HIPCK(hipEventRecord(_r->a, _p->st));                                        \
     HIPCK(expr);                                                                         \
     if (_r) HIPCK(hipEventRecord(_r->b, _p->st));                                        \
@@ -114,7 +117,7 @@ struct spff_plan {
   float* pe_dev = nullptr;
   std::vector<float> pe_host;
   // optional HIP-event timing of the MFMA kernels (bench.py roofline)
-  struct ProfRec { hipEvent_t a, b; int cls; double flops; };
+  struct ProfRec { hipEvent_t a, b; int cls; double flops, bytes; };
   std::vector<ProfRec> prof;
   size_t prof_n = 0;
   bool prof_on = false;
@@ -150,7 +153,12 @@ struct spff_plan {
   }
 };
 
-static spff_plan::ProfRec* prof_slot(spff_plan* p, int cls, double flops) {
+// compulsory HBM bytes of one conv launch: both activations once + the fp32 weights
+static double cbytes(double V, int Cin, int Cout, int T) {
+  return 4.0 * (V * Cin + V * Cout + (double)T * Cin * Cout);
+}
+
+static spff_plan::ProfRec* prof_slot(spff_plan* p, int cls, double flops, double bytes) {
   if (p->prof_n == p->prof.size()) {
     spff_plan::ProfRec r;
     if (hipEventCreate(&r.a) != hipSuccess || hipEventCreate(&r.b) != hipSuccess) return nullptr;
@@ -159,6 +167,7 @@ static spff_plan::ProfRec* prof_slot(spff_plan* p, int cls, double flops) {
   spff_plan::ProfRec* r = &p->prof[p->prof_n++];
   r->cls = cls;
   r->flops = flops;
+  r->bytes = bytes;
   return r;
 }
 
@@ -477,14 +486,14 @@ int fwd_block(spff_plan* p, Blk& b, const Src2& in) {
   HIPCK(conv3d_pack(p->P(b.c1.w), p->F(p->wt), v, KD, b.Cin, C, false, math, p->st));
   CK(halo_src(p, in, v));
   const double V = (double)nvox(v), T = 9.0 * KD;
-  PROF(p, 0, 2.0 * V * b.Cin * C * T,
+  PROFB(p, 0, 2.0 * V * b.Cin * C * T, cbytes(V, b.Cin, C, T),
        conv3d_run(in, p->F(p->wt), dst1(p->F(b.y1), C), v, KD, b.Cin, C, false, math, p->st));
   CK(in_stats(p, v, C, b.y1, b.mean1, b.rstd1, b.al1, b.de1, b.g1, b.b1));
   HIPCK(act_apply(p->F(b.y1), p->F(b.a1), p->F(b.al1), p->F(b.de1), nullptr, nullptr, v, C,
                   p->st));
   HIPCK(conv3d_pack(p->P(b.c2.w), p->F(p->wt), v, KD, C, C, false, math, p->st));
   CK(halo(p, p->F(b.a1), v, C));
-  PROF(p, 0, 2.0 * V * C * C * T,
+  PROFB(p, 0, 2.0 * V * C * C * T, cbytes(V, C, C, T),
        conv3d_run(src1(p->F(b.a1), C), p->F(p->wt), dst1(p->F(b.y2), C), v, KD, C, C, false,
                   math, p->st));
   CK(in_stats(p, v, C, b.y2, b.mean2, b.rstd2, b.al2, b.de2, b.g2, b.b2));
@@ -555,13 +564,13 @@ int bwd_block(spff_plan* p, Blk& b, const float* dout, const Dst2* dx, const Src
                        p->F(b.de2), p->P(b.g2), A, Bc, p->F(p->kk1), p->F(p->kk2), v, C, p->st));
   }
   const double V = (double)nvox(v), T = 9.0 * KD;
-  PROF(p, 2, 2.0 * V * C * C * T,
+  PROFB(p, 2, 2.0 * V * C * C * T, cbytes(V, C, C, T),
        conv3d_wgrad(src1(p->F(b.a1), C), dy2, C, p->DP(b.c2.w), v, KD, C, C, p->cfg.math,
                     p->F(p->wg_ws), p->st));
   const int math = p->cfg.math;
   HIPCK(conv3d_pack(p->P(b.c2.w), p->F(p->wt), v, KD, C, C, true, math, p->st));
   CK(halo(p, dy2, v, C));
-  PROF(p, 1, 2.0 * V * C * C * T,
+  PROFB(p, 1, 2.0 * V * C * C * T, cbytes(V, C, C, T),
        conv3d_run(src1(dy2, C), p->F(p->wt), dst1(da1, C), v, KD, C, C, true, math, p->st));
   {
     RedArgs a{};
@@ -573,14 +582,14 @@ int bwd_block(spff_plan* p, Blk& b, const float* dout, const Dst2* dx, const Src
                        p->F(b.de1), p->P(b.g1), nullptr, nullptr, p->F(p->kk1), p->F(p->kk2), v,
                        C, p->st));
   }
-  PROF(p, 2, 2.0 * V * b.Cin * C * T,
+  PROFB(p, 2, 2.0 * V * b.Cin * C * T, cbytes(V, b.Cin, C, T),
        conv3d_wgrad(in, da1, C, p->DP(b.c1.w), v, KD, b.Cin, C, p->cfg.math, p->F(p->wg_ws),
                     p->st));
   if (dx) {
     HIPCK(conv3d_pack(p->P(b.c1.w), p->F(p->wt), v, KD, b.Cin, C, true, math, p->st));
     CK(halo(p, da1, v, C));
-    PROF(p, 1, 2.0 * V * b.Cin * C * T,
-         conv3d_run(src1(da1, C), p->F(p->wt), *dx, v, KD, b.Cin, C, true, math, p->st));
+    PROFB(p, 1, 2.0 * V * b.Cin * C * T, cbytes(V, b.Cin, C, T),
+          conv3d_run(src1(da1, C), p->F(p->wt), *dx, v, KD, b.Cin, C, true, math, p->st));
   }
   return SPFF_OK;
 }
@@ -807,16 +816,17 @@ int spff_prof_enable(spff_plan* p, int on) {
 
 int spff_prof_collect(spff_plan* p, double* out, int nclass) {
   if (!p || !out) return fail(SPFF_EINVAL, "null argument");
-  for (int i = 0; i < 3 * nclass; ++i) out[i] = 0.0;
+  for (int i = 0; i < 4 * nclass; ++i) out[i] = 0.0;
   for (size_t i = 0; i < p->prof_n; ++i) {
     spff_plan::ProfRec& r = p->prof[i];
     HIPCK(hipEventSynchronize(r.b));
     float ms = 0.f;
     HIPCK(hipEventElapsedTime(&ms, r.a, r.b));
     if (r.cls < nclass) {
-      out[3 * r.cls + 0] += ms;
-      out[3 * r.cls + 1] += r.flops;
-      out[3 * r.cls + 2] += 1.0;
+      out[4 * r.cls + 0] += ms;
+      out[4 * r.cls + 1] += r.flops;
+      out[4 * r.cls + 2] += 1.0;
+      out[4 * r.cls + 3] += r.bytes;
     }
   }
   p->prof_n = 0;

@@ -270,12 +270,13 @@ class Plan:
     def prof_enable(self, on: bool = True):
         check(lib().spff_prof_enable(self._h, int(bool(on))), "spff_prof_enable")
 
-    def prof_collect(self) -> Dict[str, Tuple[float, float, int]]:
-        """{class: (total_ms, algorithmic_flops, launches)} since the last collect."""
+    def prof_collect(self) -> Dict[str, Tuple[float, float, int, float]]:
+        """{class: (total_ms, algorithmic_flops, launches, compulsory_bytes)} since the last
+        collect."""
         n = len(self.PROF_CLASSES)
-        buf = (ctypes.c_double * (3 * n))()
+        buf = (ctypes.c_double * (4 * n))()
         check(lib().spff_prof_collect(self._h, buf, n), "spff_prof_collect")
-        return {c: (buf[3 * i], buf[3 * i + 1], int(buf[3 * i + 2]))
+        return {c: (buf[4 * i], buf[4 * i + 1], int(buf[4 * i + 2]), buf[4 * i + 3])
                 for i, c in enumerate(self.PROF_CLASSES)}
 
     def saved(self, name: str) -> torch.Tensor:
