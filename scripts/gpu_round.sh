@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 ok() { local rc=$1; [ "$rc" -eq 0 ] || [ "$rc" -eq 1 ]; }
 for step in "$@"; do
   case "$step" in
-    tests) timeout -k 10 900 python -m pytest tests -m gpu -q -s -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1; rc=$? ;;
+    tests) timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -s --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1; rc=$? ;;
     smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$? ;;
     bench) timeout -k 10 600 python bench.py --steps 3 --warmup 1 --cpu-steps 1 > gpurun_out/bench_quick.log 2>&1; rc=$? ;;
     bench512) timeout -k 10 900 python bench.py --workload volume512 --steps 3 --warmup 1 > gpurun_out/bench512.log 2>&1; rc=$? ;;
