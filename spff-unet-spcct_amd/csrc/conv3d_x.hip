@@ -136,7 +136,7 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
   constexpr int RH = (NHX + XT_THREADS - 1) / XT_THREADS;
   constexpr int NWU = NS * T2 * BN;  // pre-split weight units (16 B) per chunk
   static_assert(NWU % 64 == 0, "weight image must be whole 1 KiB DMA pieces");
-  static_assert(RH <= NJ - NJ / 2, "halo split must fit in the second half of a chunk");
+  constexpr int SPJ = (RH + (NJ - NJ / 2) - 1) / (NJ - NJ / 2);  // halo float4 split per tap pair
   constexpr int NPC = NWU / 64;
   extern __shared__ uint4 lds4[];
   uint4* Xs = lds4;               // [NS][NPOS]
@@ -256,9 +256,11 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
       // split one prefetched halo float4 per tap pair from the middle of the
       // chunk on; the fences keep this VALU (and its vmcnt wait) in place
       // while MFMAs and LDS reads may still move across
-      if (j >= NJ / 2 && j - NJ / 2 < RH) {
+      if (j >= NJ / 2 && (j - NJ / 2) * SPJ < RH) {
         __builtin_amdgcn_sched_barrier(0x10C);
-        split_one(j - NJ / 2);
+#pragma unroll
+        for (int u = 0; u < SPJ; ++u)
+          if ((j - NJ / 2) * SPJ + u < RH) split_one((j - NJ / 2) * SPJ + u);
         __builtin_amdgcn_sched_barrier(0x10C);
       }
       // lane half h takes tap 2j+h; the padding tap (>= T) reads a valid
@@ -404,7 +406,7 @@ hipError_t conv3d_pack(const float* w, void* wpack, Vol vol, int KD, int Cin_w, 
 template <int NS>
 static hipError_t run_x(const Src2& x, const uint4* wu, const Dst2& y, Vol vol, int KD,
                         const XDims& d, hipStream_t s) {
-  // (MB = 4, 1024-voxel tiles for Cout <= 32, fits LDS but spills 33 VGPRs at NS = 3)
+  // (MB = 4, 1024-voxel tiles for Cout <= 32, fits LDS but spills 91 VGPRs at NS = 3)
   // (NW = 4 waves, 2 x 8 x 16 tiles, BN 32, two workgroups per CU: measured 6 % slower)
   if (d.BN == 64)
     return KD == 3 ? launch_fwd_x<64, 3, NS, 2>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s)
