@@ -164,6 +164,62 @@ int spff_conv3d_wgrad_ex(const float* x, int ldx, const float* dy, float* dw, in
                          int H, int W, int cin, int cout, int ksd, int math, void* ws,
                          void* stream);
 
+/* ---------------------------------------------------------------------------
+ * 3D U-Net baseline variant (BASELINE config 3; registry entry "3DUNet",
+ * config.py:283-311): LitCicek3DUNet_DepthAdapter_Published (models.py:756-853)
+ * = _resize_depth_like (models.py:153-157) -> Cicek3DUNet (models.py:718-753:
+ * 4 x [Conv3d(3, bias=False) -> BatchNorm3d -> ReLU] x 2 + MaxPool3d(2) down,
+ * ConvTranspose3d(2, stride 2) + concat [up, skip] up, 1x1x1 head) ->
+ * _resize_logits_depth_like (models.py:159-163).  Same conventions as above:
+ * params flat in reference state-dict order (names without the "backbone."
+ * prefix), BatchNorm running_mean / running_var in a second flat fp32 buffer
+ * (spff_unet3d_buffer_info; num_batches_tracked stays with the caller).
+ * -------------------------------------------------------------------------- */
+typedef struct spff_unet3d_cfg {
+  int batch, in_ch, depth, height, width;  /* input [B][Cin][D][H][W] */
+  int target_depth;  /* depth adapter: D is resampled to this before the backbone and the
+                        logits back to D (trilinear, align_corners=False); 0 = none.  The
+                        backbone depth, H and W must be multiples of 16 (4 poolings). */
+  int num_classes;   /* K (<= 32) */
+  int base;          /* f (power of two, >= 8); the reference wrapper uses 32 */
+  int math;          /* SPFF_MATH_* for the 3x3x3 convolutions */
+  int reserved[7];   /* zero */
+} spff_unet3d_cfg;
+
+typedef struct spff_unet3d spff_unet3d;
+
+int spff_unet3d_create(const spff_unet3d_cfg* cfg, spff_unet3d** out);
+void spff_unet3d_destroy(spff_unet3d* net);
+int spff_unet3d_num_params(const spff_unet3d* net);
+int spff_unet3d_param_info(const spff_unet3d* net, int i, const char** name, int* ndim,
+                           int64_t shape[5], int64_t* offset, int64_t* numel);
+int64_t spff_unet3d_param_floats(const spff_unet3d* net);
+int spff_unet3d_num_buffers(const spff_unet3d* net);
+int spff_unet3d_buffer_info(const spff_unet3d* net, int i, const char** name, int64_t* offset,
+                            int64_t* numel);
+int64_t spff_unet3d_buffer_floats(const spff_unet3d* net);
+size_t spff_unet3d_workspace_bytes(const spff_unet3d* net);
+/* forward: x [B][Cin][D][H][W] -> logits [B][D][H][W][K].  training = 1:
+ * BatchNorm normalises with batch statistics and updates running_mean /
+ * running_var in `buffers` (momentum 0.1, unbiased variance); 0: normalises
+ * with the running statistics (buffers read only). */
+int spff_unet3d_forward(spff_unet3d* net, const float* x, const float* params, float* buffers,
+                        int training, float* logits, void* workspace, void* stream);
+/* backward of the last forward: dlogits [B][D][H][W][K] -> dparams (every entry written) */
+int spff_unet3d_backward(spff_unet3d* net, const float* dlogits, const float* params,
+                         float* dparams, void* workspace, void* stream);
+int spff_unet3d_saved_tensor(const spff_unet3d* net, void* workspace, const char* name,
+                             const float** ptr, int64_t* nvox, int* channels);
+
+/* the weighted softmax CE of the 3DUNet wrapper (_weighted_softmax_ce,
+ * models.py:779-799): as spff_loss, plus optional per-class weights
+ * (class_weights: K device floats or NULL) and clamp_denominator = 1 for the
+ * wrapper's sum / max(N_valid, 1). */
+int spff_loss_ex(const float* logits, const int64_t* labels, int64_t nvox, int num_classes,
+                 int ignore_index, double smooth, const int64_t* count_override,
+                 const float* class_weights, int clamp_denominator, float* out4,
+                 float* dlogits, int64_t* conf, void* ws, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -22,15 +22,14 @@
 
 using namespace spff;
 
-namespace spff {
-size_t upconv_pack_floats(int Cin, int Cout);
-size_t upconv_pack_dgrad_offset(int Cin, int Cout);
-}
 
 static thread_local std::string g_err;
 static int fail(int code, const std::string& m) {
   g_err = m;
   return code;
+}
+namespace spff {
+int set_error(int code, const char* msg) { return fail(code, msg); }
 }
 #define HIPCK(expr)                                                                        \
   do {                                                                                     \

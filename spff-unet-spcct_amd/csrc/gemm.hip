@@ -36,19 +36,24 @@ struct LoadRowsScalar {  // generic
     return v;
   }
 };
-__device__ inline int64_t up_high_vox(int64_t m, int ij, int D, int Hl, int Wl) {
+// high-res voxel of low-res voxel m's sub-lattice ij: nsub = 4 for the (1,2,2)
+// up-convs of SPFF (ij = kh*2 + kw, depth kept), nsub = 8 for the 2x2x2 ones of
+// the 3DUNet (ij = (kd*2 + kh)*2 + kw, depth doubled)
+__device__ inline int64_t up_high_vox(int64_t m, int ij, int D, int Hl, int Wl, int nsub) {
   const int w = (int)(m % Wl);
   int64_t t = m / Wl;
   const int h = (int)(t % Hl);
   t /= Hl;  // t = b*D + d
-  return (t * (2 * Hl) + 2 * h + (ij >> 1)) * (int64_t)(2 * Wl) + 2 * w + (ij & 1);
+  if (nsub == 8) t = (t / D) * (2 * D) + 2 * (t % D) + (ij >> 2);
+  const int r = ij & 3;
+  return (t * (2 * Hl) + 2 * h + (r >> 1)) * (int64_t)(2 * Wl) + 2 * w + (r & 1);
 }
 struct LoadUpGather {  // A[m][k], k = ij*Cout + co -> dy[high(m,ij)*ld + co]
-  const float* p; int ld; int Cout; int D, Hl, Wl; int64_t M;
+  const float* p; int ld; int Cout; int D, Hl, Wl; int64_t M; int nsub;
   __device__ float4 load4(int64_t m, int k) const {
-    if (m >= M || k >= 4 * Cout) return make_float4(0.f, 0.f, 0.f, 0.f);
+    if (m >= M || k >= nsub * Cout) return make_float4(0.f, 0.f, 0.f, 0.f);
     const int ij = k / Cout, co = k % Cout;
-    return *reinterpret_cast<const float4*>(p + up_high_vox(m, ij, D, Hl, Wl) * ld + co);
+    return *reinterpret_cast<const float4*>(p + up_high_vox(m, ij, D, Hl, Wl, nsub) * ld + co);
   }
 };
 struct StoreRows {  // C[m][n] -> p[m*ld + n] (+bias[n]), n < nmax
@@ -58,11 +63,11 @@ struct StoreRows {  // C[m][n] -> p[m*ld + n] (+bias[n]), n < nmax
   }
 };
 struct StoreUp {  // C[m][n], n = ij*Cout + co -> y[high(m,ij)*Cout + co] + bias[co]
-  float* p; int Cout; const float* bias; int D, Hl, Wl; int64_t M;
+  float* p; int Cout; const float* bias; int D, Hl, Wl; int64_t M; int nsub;
   __device__ void store(int64_t m, int n, float v) const {
-    if (m >= M || n >= 4 * Cout) return;
+    if (m >= M || n >= nsub * Cout) return;
     const int ij = n / Cout, co = n % Cout;
-    p[up_high_vox(m, ij, D, Hl, Wl) * Cout + co] = v + bias[co];
+    p[up_high_vox(m, ij, D, Hl, Wl, nsub) * Cout + co] = v + bias[co];
   }
 };
 
@@ -191,6 +196,7 @@ __global__ __launch_bounds__(256) void k_atb(XL X, YL Y, float* __restrict__ par
 }
 
 // dW layouts: mode 0 = upconv W[Cin][Cout][1][2][2] from C[ci][ij*Cout+co]
+//             mode 2 = upconv W[Cin][Cout][2][2][2] from C[ci][ij*Cout+co]
 //             mode 1 = head   W[K][Cin]           from C[ci][k]
 // One block = 32 outputs x 8 split groups; each group sums its splits in order,
 // then the 8 group sums are combined in order (deterministic).  Blocks past
@@ -218,7 +224,7 @@ __global__ __launch_bounds__(256) void k_atb_reduce(const float* __restrict__ pa
     co = (blockIdx.x - nwb) * 32 + jl;
     valid = co < Cout;
     if (valid) {
-      const int nij = (mode == 0) ? 4 : 1;
+      const int nij = (mode == 0) ? 4 : (mode == 2) ? 8 : 1;
       for (int k = g; k < nsplit; k += 8)
         for (int ij = 0; ij < nij; ++ij) s += csum[(int64_t)k * npad + ij * Cout + co];
     }
@@ -231,9 +237,9 @@ __global__ __launch_bounds__(256) void k_atb_reduce(const float* __restrict__ pa
     for (int q = 0; q < 8; ++q) t += red[q][jl];
     if ((int)blockIdx.x >= nwb) {
       db[co] = t;
-    } else if (mode == 0) {
+    } else if (mode == 0 || mode == 2) {
       const int ij = n / Cout, c = n % Cout;
-      dw[((int64_t)k1 * Cout + c) * 4 + ij] = t;
+      dw[((int64_t)k1 * Cout + c) * (mode == 2 ? 8 : 4) + ij] = t;
     } else {
       dw[(int64_t)n * K1 + k1] = t;
     }
@@ -273,67 +279,69 @@ static size_t atb_ws_bytes(int64_t M, int K1, int N) {
 }
 
 // ---------------------------------------------------------------- packing --
-// wf[ci][ij*Cout+co] = W[ci][co][ij] (kpad = roundup(Cin,16), npad = roundup(4Cout, 32))
-// wd[ij*Cout+co][ci] = W[ci][co][ij] (kpad = roundup(4Cout,16), npad = roundup(Cin, 32))
+// wf[ci][ij*Cout+co] = W[ci][co][ij] (kpad = roundup(Cin,16), npad = roundup(ns*Cout, 64))
+// wd[ij*Cout+co][ci] = W[ci][co][ij] (kpad = roundup(ns*Cout,16), npad = roundup(Cin, 64))
 static inline int up_f_kpad(int Cin) { return cdiv(Cin, G_BK) * G_BK; }
-static inline int up_f_npad(int Cout) { return cdiv(4 * Cout, 64) * 64; }
-static inline int up_d_kpad(int Cout) { return cdiv(4 * Cout, G_BK) * G_BK; }
+static inline int up_f_npad(int Cout, int ns) { return cdiv(ns * Cout, 64) * 64; }
+static inline int up_d_kpad(int Cout, int ns) { return cdiv(ns * Cout, G_BK) * G_BK; }
 static inline int up_d_npad(int Cin) { return cdiv(Cin, 64) * 64; }
 
 __global__ void k_up_pack(const float* __restrict__ w, float* __restrict__ wf,
-                          float* __restrict__ wd, int Cin, int Cout, int fk, int fn, int dk,
-                          int dn) {
+                          float* __restrict__ wd, int Cin, int Cout, int ns, int fk, int fn,
+                          int dk, int dn) {
   const int tf = fk * fn, td = dk * dn;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < tf + td; i += gridDim.x * blockDim.x) {
     if (i < tf) {
       const int n = i % fn, k = i / fn;
       float v = 0.f;
-      if (k < Cin && n < 4 * Cout) v = w[((int64_t)k * Cout + n % Cout) * 4 + n / Cout];
+      if (k < Cin && n < ns * Cout) v = w[((int64_t)k * Cout + n % Cout) * ns + n / Cout];
       wf[i] = v;
     } else {
       const int j = i - tf;
       const int n = j % dn, k = j / dn;
       float v = 0.f;
-      if (k < 4 * Cout && n < Cin) v = w[((int64_t)n * Cout + k % Cout) * 4 + k / Cout];
+      if (k < ns * Cout && n < Cin) v = w[((int64_t)n * Cout + k % Cout) * ns + k / Cout];
       wd[j] = v;
     }
   }
 }
 
-hipError_t upconv_pack(const float* w, float* wf, float* wd, int Cin, int Cout, hipStream_t s) {
-  const int fk = up_f_kpad(Cin), fn = up_f_npad(Cout), dk = up_d_kpad(Cout), dn = up_d_npad(Cin);
+hipError_t upconv_pack(const float* w, float* wf, float* wd, int Cin, int Cout, hipStream_t s,
+                       int ns) {
+  const int fk = up_f_kpad(Cin), fn = up_f_npad(Cout, ns), dk = up_d_kpad(Cout, ns),
+            dn = up_d_npad(Cin);
   const int total = fk * fn + dk * dn;
-  hipLaunchKernelGGL(k_up_pack, dim3(cdiv(total, 256)), dim3(256), 0, s, w, wf, wd, Cin, Cout, fk,
-                     fn, dk, dn);
+  hipLaunchKernelGGL(k_up_pack, dim3(cdiv(total, 256)), dim3(256), 0, s, w, wf, wd, Cin, Cout, ns,
+                     fk, fn, dk, dn);
   return hipGetLastError();
 }
 
 hipError_t upconv_fwd(const float* x, const float* wf, const float* bias, float* y, Vol low,
-                      int Cin, int Cout, hipStream_t s) {
+                      int Cin, int Cout, hipStream_t s, int ns) {
   const int64_t M = nvox(low);
   LoadRowsVec A{x, Cin, Cin, M};
-  StoreUp C{y, Cout, bias, low.D, low.H, low.W, M};
-  return launch_gemm(A, wf, C, M, up_f_kpad(Cin), up_f_npad(Cout), s);
+  StoreUp C{y, Cout, bias, low.D, low.H, low.W, M, ns};
+  return launch_gemm(A, wf, C, M, up_f_kpad(Cin), up_f_npad(Cout, ns), s);
 }
 
 hipError_t upconv_dgrad(const float* dy, int lddy, const float* wd, float* dx, Vol low, int Cin,
-                        int Cout, hipStream_t s) {
+                        int Cout, hipStream_t s, int ns) {
   const int64_t M = nvox(low);
-  LoadUpGather A{dy, lddy, Cout, low.D, low.H, low.W, M};
+  LoadUpGather A{dy, lddy, Cout, low.D, low.H, low.W, M, ns};
   StoreRows C{dx, Cin, Cin, nullptr, M};
-  return launch_gemm(A, wd, C, M, up_d_kpad(Cout), up_d_npad(Cin), s);
+  return launch_gemm(A, wd, C, M, up_d_kpad(Cout, ns), up_d_npad(Cin), s);
 }
 
-size_t upconv_wgrad_ws_bytes(Vol low, int Cin, int Cout) {
-  return atb_ws_bytes(nvox(low), Cin, 4 * Cout);
+size_t upconv_wgrad_ws_bytes(Vol low, int Cin, int Cout, int ns) {
+  return atb_ws_bytes(nvox(low), Cin, ns * Cout);
 }
 
 hipError_t upconv_wgrad(const float* x, const float* dy, int lddy, float* dw, float* db, Vol low,
-                        int Cin, int Cout, float* ws, hipStream_t s) {
+                        int Cin, int Cout, float* ws, hipStream_t s, int ns) {
   const int64_t M = nvox(low);
   LoadRowsVec X{x, Cin, Cin, M};
-  LoadUpGather Y{dy, lddy, Cout, low.D, low.H, low.W, M};
-  return launch_atb(X, Y, M, Cin, 4 * Cout, Cout, 0, dw, db, ws, s);
+  LoadUpGather Y{dy, lddy, Cout, low.D, low.H, low.W, M, ns};
+  return launch_atb(X, Y, M, Cin, ns * Cout, Cout, ns == 8 ? 2 : 0, dw, db, ws, s);
 }
 
 // ------------------------------------------------------------------- head --
@@ -377,11 +385,12 @@ size_t head_pack_floats(int Cin, int K) {
   return (size_t)head_fk(Cin) * head_fn(K) + (size_t)head_dk(K) * head_dn(Cin);
 }
 size_t head_pack_dgrad_offset(int Cin, int K) { return (size_t)head_fk(Cin) * head_fn(K); }
-size_t upconv_pack_floats(int Cin, int Cout) {
-  return (size_t)up_f_kpad(Cin) * up_f_npad(Cout) + (size_t)up_d_kpad(Cout) * up_d_npad(Cin);
+size_t upconv_pack_floats(int Cin, int Cout, int ns) {
+  return (size_t)up_f_kpad(Cin) * up_f_npad(Cout, ns) +
+         (size_t)up_d_kpad(Cout, ns) * up_d_npad(Cin);
 }
-size_t upconv_pack_dgrad_offset(int Cin, int Cout) {
-  return (size_t)up_f_kpad(Cin) * up_f_npad(Cout);
+size_t upconv_pack_dgrad_offset(int Cin, int Cout, int ns) {
+  return (size_t)up_f_kpad(Cin) * up_f_npad(Cout, ns);
 }
 
 hipError_t head_dgrad(const float* dy, const float* wd, float* dx, int64_t V, int Cin, int K,

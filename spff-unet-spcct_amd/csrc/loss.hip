@@ -38,13 +38,16 @@ __global__ __launch_bounds__(LOSS_T) void k_loss(const float* __restrict__ x,
                                                  float* __restrict__ dx,
                                                  unsigned long long* __restrict__ conf,
                                                  double* __restrict__ part,
-                                                 unsigned long long* __restrict__ nbad) {
+                                                 unsigned long long* __restrict__ nbad,
+                                                 const float* __restrict__ cw, int clamp1) {
   __shared__ unsigned int hist[KMAX * (KMAX + 1)];
   __shared__ double red[LOSS_T];
   const int K1 = K + 1;  // column K = label outside [0,K) (not ignored)
   for (int i = threadIdx.x; i < K * K1; i += LOSS_T) hist[i] = 0;
   __syncthreads();
-  const float invN = WITH_CE ? 1.f / (float)(*count) : 0.f;
+  // clamp1: the 3DUNet's weighted CE divides by max(N_valid, 1) (models.py:796)
+  const float invN =
+      WITH_CE ? 1.f / (float)(clamp1 && *count < 1 ? (int64_t)1 : *count) : 0.f;
   double ce = 0.0;
   unsigned int bad = 0;
   for (int64_t v = blockIdx.x * (int64_t)LOSS_T + threadIdx.x; v < V;
@@ -74,11 +77,14 @@ __global__ __launch_bounds__(LOSS_T) void k_loss(const float* __restrict__ x,
         float ssum = 0.f;
         for (int k = 0; k < K; ++k) ssum += expf(xs[k] - m);
         const float lse = m + logf(ssum);
-        ce += (double)(lse - xs[(int)y]);
+        // class weights (F.cross_entropy(weight=w), reduction='none'): w[y] * nll
+        const float wy = cw ? cw[(int)y] : 1.f;
+        ce += cw ? (double)(wy * (lse - xs[(int)y])) : (double)(lse - xs[(int)y]);
         const float inv = 1.f / ssum;
         for (int k = 0; k < K; ++k) {
           const float p = expf(xs[k] - m) * inv;
-          dv[k] = (p - (k == (int)y ? 1.f : 0.f)) * invN;
+          dv[k] = cw ? wy * (p - (k == (int)y ? 1.f : 0.f)) * invN
+                     : (p - (k == (int)y ? 1.f : 0.f)) * invN;
         }
       } else {
         for (int k = 0; k < K; ++k) dv[k] = 0.f;
@@ -105,11 +111,11 @@ __global__ __launch_bounds__(LOSS_T) void k_loss(const float* __restrict__ x,
 __global__ void k_loss_final(const double* __restrict__ part, int nparts,
                              const int64_t* __restrict__ count,
                              const unsigned long long* __restrict__ conf, int K, double smooth,
-                             float* __restrict__ out4) {
+                             float* __restrict__ out4, int clamp1) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   double s = 0.0;
   for (int i = 0; i < nparts; ++i) s += part[i];
-  const double N = (double)(*count);
+  const double N = (clamp1 && *count < 1) ? 1.0 : (double)(*count);
   const float ce = (float)(s / N);
   double dsum = 0.0;
   const int K1 = K + 1;
@@ -145,7 +151,8 @@ hipError_t count_valid(const int64_t* labels, int64_t V, int ignore, int64_t* co
 // ws: [LOSS_GRID doubles][int64 count][uint64 nbad]
 hipError_t loss_fwd(const float* logits, const int64_t* labels, int64_t V, int K, int ignore,
                     double smooth, const int64_t* count_override, float* out4, float* dlogits,
-                    int64_t* conf, float* ws, hipStream_t s) {
+                    int64_t* conf, float* ws, hipStream_t s, const float* class_w,
+                    int clamp1) {
   if (K > KMAX || K < 1) return hipErrorInvalidValue;
   double* part = reinterpret_cast<double*>(ws);
   int64_t* cnt = reinterpret_cast<int64_t*>(part + LOSS_GRID);
@@ -160,10 +167,10 @@ hipError_t loss_fwd(const float* logits, const int64_t* labels, int64_t V, int K
   if ((e = hipMemsetAsync(nbad, 0, sizeof(unsigned long long), s)) != hipSuccess) return e;
   hipLaunchKernelGGL(k_loss<true>, dim3(LOSS_GRID), dim3(LOSS_T), 0, s, logits, labels, V, K,
                      ignore, cptr, dlogits, reinterpret_cast<unsigned long long*>(conf), part,
-                     nbad);
+                     nbad, class_w, clamp1);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(k_loss_final, dim3(1), dim3(64), 0, s, part, LOSS_GRID, cptr,
-                     reinterpret_cast<unsigned long long*>(conf), K, smooth, out4);
+                     reinterpret_cast<unsigned long long*>(conf), K, smooth, out4, clamp1);
   return hipGetLastError();
 }
 
@@ -174,7 +181,7 @@ hipError_t confusion_only(const float* logits, const int64_t* labels, int64_t V,
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_loss<false>, dim3(LOSS_GRID), dim3(LOSS_T), 0, s, logits, labels, V, K,
                      ignore, nullptr, nullptr, reinterpret_cast<unsigned long long*>(conf),
-                     nullptr, nullptr);
+                     nullptr, nullptr, nullptr, 0);
   return hipGetLastError();
 }
 

@@ -113,6 +113,224 @@ hipError_t maxpool_bwd_add(const float* dp, const uint8_t* idx, const float* dsk
   return hipGetLastError();
 }
 
+// --------------------------------------------------------- maxpool 2x2x2 --
+// nn.MaxPool3d(2) (reference Cicek3DUNet pool1..pool4, models.py:728-731):
+// scan (dd, dh, dw) in row-major order, replace on strictly greater or NaN, so
+// the FIRST max wins (ATen CPU max_pool3d).  idx = (dd*2 + dh)*2 + dw.  Odd
+// extents floor like PyTorch (the trailing plane/row/column is never read).
+__global__ void k_maxpool3_fwd(const float* __restrict__ x, float* __restrict__ y,
+                               uint8_t* __restrict__ idx, Vol in, int C) {
+  const int Do = in.D / 2, Ho = in.H / 2, Wo = in.W / 2, C4 = C / 4;
+  const int64_t total = (int64_t)in.B * Do * Ho * Wo * C4;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C4) * 4;
+    int64_t t = i / C4;
+    const int wo = (int)(t % Wo); t /= Wo;
+    const int ho = (int)(t % Ho); t /= Ho;
+    const int dd = (int)(t % Do);
+    const int64_t b = t / Do;
+    const int64_t vin = ((b * in.D + 2 * dd) * in.H + 2 * ho) * in.W + 2 * wo;
+    float best[4];
+    uint8_t bi[4] = {0, 0, 0, 0};
+    {
+      const float4 v = *reinterpret_cast<const float4*>(x + vin * C + c);
+      best[0] = v.x; best[1] = v.y; best[2] = v.z; best[3] = v.w;
+    }
+#pragma unroll
+    for (int k = 1; k < 8; ++k) {
+      const int64_t vv = vin + (int64_t)(k >> 2) * in.H * in.W + ((k >> 1) & 1) * in.W + (k & 1);
+      const float4 v = *reinterpret_cast<const float4*>(x + vv * C + c);
+      const float vs[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (vs[j] > best[j] || isnan(vs[j])) { best[j] = vs[j]; bi[j] = (uint8_t)k; }
+    }
+    const int64_t vo = i / C4;
+    *reinterpret_cast<float4*>(y + vo * C + c) = make_float4(best[0], best[1], best[2], best[3]);
+    *reinterpret_cast<uchar4*>(idx + vo * C + c) = make_uchar4(bi[0], bi[1], bi[2], bi[3]);
+  }
+}
+
+hipError_t maxpool3_fwd(const float* x, float* y, uint8_t* idx, Vol in, int C, hipStream_t s) {
+  if (C % 4) return hipErrorInvalidValue;
+  const int64_t total = (int64_t)in.B * (in.D / 2) * (in.H / 2) * (in.W / 2) * (C / 4);
+  int grid = (int)std::min<int64_t>((total + 255) / 256, 16384);
+  hipLaunchKernelGGL(k_maxpool3_fwd, dim3(grid), dim3(256), 0, s, x, y, idx, in, C);
+  return hipGetLastError();
+}
+
+// dx[v_in][c] = dskip[v_in*ld + c] + (argmax hit ? dp[v_out][c] : 0)
+__global__ void k_maxpool3_bwd_add(const float* __restrict__ dp, const uint8_t* __restrict__ idx,
+                                   const float* __restrict__ dskip, int ldskip,
+                                   float* __restrict__ dx, Vol in, int C) {
+  const int Do = in.D / 2, Ho = in.H / 2, Wo = in.W / 2, C4 = C / 4;
+  const int64_t total = (int64_t)in.B * in.D * in.H * in.W * C4;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C4) * 4;
+    const int64_t v = i / C4;
+    int64_t t = v;
+    const int w = (int)(t % in.W); t /= in.W;
+    const int h = (int)(t % in.H); t /= in.H;
+    const int d = (int)(t % in.D);
+    const int64_t b = t / in.D;
+    float o[4] = {0.f, 0.f, 0.f, 0.f};
+    if (dskip) {
+      const float* p = dskip + v * ldskip + c;
+      o[0] = p[0]; o[1] = p[1]; o[2] = p[2]; o[3] = p[3];
+    }
+    const int dd = d >> 1, ho = h >> 1, wo = w >> 1;
+    if (dd < Do && ho < Ho && wo < Wo) {
+      const int64_t vo = ((b * Do + dd) * Ho + ho) * Wo + wo;
+      const uint8_t k = (uint8_t)(((d & 1) * 2 + (h & 1)) * 2 + (w & 1));
+      const uchar4 ix = *reinterpret_cast<const uchar4*>(idx + vo * C + c);
+      const float4 g = *reinterpret_cast<const float4*>(dp + vo * C + c);
+      if (ix.x == k) o[0] += g.x;
+      if (ix.y == k) o[1] += g.y;
+      if (ix.z == k) o[2] += g.z;
+      if (ix.w == k) o[3] += g.w;
+    }
+    *reinterpret_cast<float4*>(dx + v * C + c) = make_float4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+hipError_t maxpool3_bwd_add(const float* dp, const uint8_t* idx, const float* dskip, int ldskip,
+                            float* dx, Vol in, int C, hipStream_t s) {
+  if (C % 4) return hipErrorInvalidValue;
+  const int64_t total = (int64_t)in.B * in.D * in.H * in.W * (C / 4);
+  int grid = (int)std::min<int64_t>((total + 255) / 256, 16384);
+  hipLaunchKernelGGL(k_maxpool3_bwd_add, dim3(grid), dim3(256), 0, s, dp, idx, dskip, ldskip, dx,
+                     in, C);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------- depth resampling --
+// F.interpolate(x, size=(Dout, H, W), mode="trilinear", align_corners=False)
+// with H, W unchanged (reference _resize_depth_like / _resize_logits_depth_like,
+// models.py:153-163): the H/W factors are exactly 1 (source index = output
+// index, weights 1 and 0), so it is linear interpolation along D with ATen's
+// source index: src = max(0, (Din/Dout)*(d + 0.5) - 0.5) in fp32,
+// i0 = floor(src), i1 = min(i0 + 1, Din - 1), w1 = src - i0, w0 = 1 - w1.
+__device__ __forceinline__ void lin_src(int d, int Din, int Dout, int& i0, int& i1, float& w0,
+                                        float& w1) {
+  const float scale = (float)Din / (float)Dout;
+  float src = scale * ((float)d + 0.5f) - 0.5f;
+  src = src < 0.f ? 0.f : src;
+  i0 = (int)src;
+  if (i0 > Din - 1) i0 = Din - 1;
+  i1 = i0 + (i0 < Din - 1 ? 1 : 0);
+  w1 = src - (float)i0;
+  w0 = 1.f - w1;
+}
+
+// input: x [B][C][Din][H][W] (reference layout) -> y [B][Dout][H][W][ldy]
+// (channel-last, channels C..ldy-1 zero) in one pass
+__global__ void k_resize_d_ncdhw_to_ndhwc(const float* __restrict__ x, float* __restrict__ y,
+                                          int B, int C, int Din, int Dout, int HW, int ldy) {
+  const int64_t V = (int64_t)B * Dout * HW;
+  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < V;
+       v += (int64_t)gridDim.x * blockDim.x) {
+    const int hw = (int)(v % HW);
+    const int64_t t = v / HW;
+    const int d = (int)(t % Dout);
+    const int64_t b = t / Dout;
+    int i0, i1;
+    float w0, w1;
+    lin_src(d, Din, Dout, i0, i1, w0, w1);
+    float* o = y + v * ldy;
+    for (int c = 0; c < ldy; ++c) {
+      float r = 0.f;
+      if (c < C) {
+        const float* xc = x + (b * C + c) * (int64_t)Din * HW + hw;
+        r = w0 * xc[(int64_t)i0 * HW] + w1 * xc[(int64_t)i1 * HW];
+      }
+      o[c] = r;
+    }
+  }
+}
+
+hipError_t resize_d_ncdhw_to_ndhwc(const float* x, float* y, int B, int C, int Din, int Dout,
+                                   int H, int W, int ldy, hipStream_t s) {
+  const int64_t V = (int64_t)B * Dout * H * W;
+  int grid = (int)std::min<int64_t>((V + 255) / 256, 8192);
+  hipLaunchKernelGGL(k_resize_d_ncdhw_to_ndhwc, dim3(grid), dim3(256), 0, s, x, y, B, C, Din,
+                     Dout, H * W, ldy);
+  return hipGetLastError();
+}
+
+// channel-last rows of K values: y[b][d][hw][:] = w0 x[b][i0][hw][:] + w1 x[b][i1][hw][:]
+__global__ void k_resize_d_rows(const float* __restrict__ x, float* __restrict__ y, int B, int K,
+                                int Din, int Dout, int HW) {
+  const int64_t total = (int64_t)B * Dout * HW * K;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int k = (int)(i % K);
+    int64_t t = i / K;
+    const int hw = (int)(t % HW);
+    t /= HW;
+    const int d = (int)(t % Dout);
+    const int64_t b = t / Dout;
+    int i0, i1;
+    float w0, w1;
+    lin_src(d, Din, Dout, i0, i1, w0, w1);
+    const float* xb = x + b * (int64_t)Din * HW * K + (int64_t)hw * K + k;
+    y[i] = w0 * xb[(int64_t)i0 * HW * K] + w1 * xb[(int64_t)i1 * HW * K];
+  }
+}
+
+// adjoint of k_resize_d_rows (dx[b][i][hw][:] = sum over output depths d that
+// read i of their weight * dy[b][d][hw][:]), gathered per input depth in
+// increasing d order: deterministic, no atomics
+__global__ void k_resize_d_rows_bwd(const float* __restrict__ dy, float* __restrict__ dx, int B,
+                                    int K, int Din, int Dout, int HW) {
+  const int64_t total = (int64_t)B * Din * HW * K;
+  const float inv = (float)Dout / (float)Din;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int k = (int)(i % K);
+    int64_t t = i / K;
+    const int hw = (int)(t % HW);
+    t /= HW;
+    const int di = (int)(t % Din);
+    const int64_t b = t / Din;
+    // output depths whose source lies in (di - 1, di + 1), widened by one
+    int dlo = (int)floorf(((float)di - 0.5f) * inv - 0.5f) - 1;
+    int dhi = (int)ceilf(((float)di + 1.5f) * inv - 0.5f) + 1;
+    dlo = dlo < 0 ? 0 : dlo;
+    dhi = dhi > Dout - 1 ? Dout - 1 : dhi;
+    if (di == 0) dlo = 0;                 // clamped sources (src < 0) land on 0
+    if (di == Din - 1) dhi = Dout - 1;    // i1 clamps to the last input depth
+    const float* gb = dy + b * (int64_t)Dout * HW * K + (int64_t)hw * K + k;
+    float acc = 0.f;
+    for (int d = dlo; d <= dhi; ++d) {
+      int i0, i1;
+      float w0, w1;
+      lin_src(d, Din, Dout, i0, i1, w0, w1);
+      const float g = gb[(int64_t)d * HW * K];
+      if (i0 == di) acc += w0 * g;
+      if (i1 == di) acc += w1 * g;
+    }
+    dx[i] = acc;
+  }
+}
+
+hipError_t resize_d_rows(const float* x, float* y, int B, int K, int Din, int Dout, int H, int W,
+                         hipStream_t s) {
+  const int64_t total = (int64_t)B * Dout * H * W * K;
+  int grid = (int)std::min<int64_t>((total + 255) / 256, 16384);
+  hipLaunchKernelGGL(k_resize_d_rows, dim3(grid), dim3(256), 0, s, x, y, B, K, Din, Dout, H * W);
+  return hipGetLastError();
+}
+hipError_t resize_d_rows_bwd(const float* dy, float* dx, int B, int K, int Din, int Dout, int H,
+                             int W, hipStream_t s) {
+  const int64_t total = (int64_t)B * Din * H * W * K;
+  int grid = (int)std::min<int64_t>((total + 255) / 256, 16384);
+  hipLaunchKernelGGL(k_resize_d_rows_bwd, dim3(grid), dim3(256), 0, s, dy, dx, B, K, Din, Dout,
+                     H * W);
+  return hipGetLastError();
+}
+
 __global__ void k_scale(float* x, int64_t n, const float* scale) {
   const float a = *scale;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;

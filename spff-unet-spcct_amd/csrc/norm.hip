@@ -12,8 +12,9 @@
 namespace spff {
 
 static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
-__device__ __forceinline__ float lrelu(float r) { return r > 0.f ? r : 0.01f * r; }
-__device__ __forceinline__ float slope(float r) { return r > 0.f ? 1.f : 0.01f; }
+// neg = negative slope: 0.01 for LeakyReLU (SPFF), 0 for ReLU (3DUNet)
+__device__ __forceinline__ float lrelu(float r, float neg) { return r > 0.f ? r : neg * r; }
+__device__ __forceinline__ float slope(float r, float neg) { return r > 0.f ? 1.f : neg; }
 
 namespace {
 struct RedPlan {
@@ -81,13 +82,13 @@ __global__ __launch_bounds__(256) void k_slab_reduce(RedArgs a, Vol vol, int C, 
           const float t = ys[j] - p0[j];
           acc[0][j] += t * t;
         } else if (OP == RED_ACT) {
-          acc[0][j] += lrelu(ys[j] * p0[j] + p1[j]);
+          acc[0][j] += lrelu(ys[j] * p0[j] + p1[j], a.neg);
         } else if (OP == RED_BWD_TAIL) {
           acc[0][j] += gs[j];
-          acc[NQ - 1][j] += gs[j] * lrelu(ys[j] * p0[j] + p1[j]);
+          acc[NQ - 1][j] += gs[j] * lrelu(ys[j] * p0[j] + p1[j], a.neg);
         } else {  // RED_BWD_IN
           const float r = ys[j] * p0[j] + p1[j];
-          const float dr = (gs[j] * p2[j] + p3[j]) * slope(r);
+          const float dr = (gs[j] * p2[j] + p3[j]) * slope(r, a.neg);
           const float xh = (ys[j] - mu[j]) * rs[j];
           acc[0][j] += dr;
           acc[NQ - 1][j] += dr * xh;
@@ -307,6 +308,120 @@ hipError_t in_bwd_fin(const double* part, float* k1, float* k2, int BC, double N
   return hipGetLastError();
 }
 
+// ------------------------------------------------- BatchNorm3d finalizers --
+// nn.BatchNorm3d(C) (reference Cicek3DUNet, models.py:718-724): the same
+// per-(b,c,d) hw-sums, reduced over b AND d (N = B*D*H*W per channel).  The
+// per-channel results are written replicated over b ([B][C]) so act_apply /
+// in_bwd_apply / slab_reduce run unchanged.  fp64 accumulation over (b,d), as
+// ATen's CPU batch norm accumulates in double.
+__global__ void k_bn_mean(const float* __restrict__ sums, float* __restrict__ mean, Vol vol,
+                          int C) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0;
+  for (int b = 0; b < vol.B; ++b)
+    for (int d = 0; d < vol.D; ++d) s += sums[((int64_t)b * C + c) * vol.D + d];
+  const float m = (float)(s / ((double)vol.B * vol.D * vol.H * vol.W));
+  for (int b = 0; b < vol.B; ++b) mean[b * C + c] = m;
+}
+
+// train: rstd/al/de from the squared-deviation sums; running stats updated
+// in place (momentum m, unbiased variance), batch_norm_cpu_update_stats order
+__global__ void k_bn_rstd(const float* __restrict__ sq, const float* __restrict__ gamma,
+                          const float* __restrict__ beta, const float* __restrict__ mean,
+                          float* __restrict__ rstd, float* __restrict__ al, float* __restrict__ de,
+                          float* __restrict__ rmean, float* __restrict__ rvar, double mom,
+                          double eps, Vol vol, int C) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0;
+  for (int b = 0; b < vol.B; ++b)
+    for (int d = 0; d < vol.D; ++d) s += sq[((int64_t)b * C + c) * vol.D + d];
+  const double N = (double)vol.B * vol.D * vol.H * vol.W;
+  const double var = s / N;
+  const float rs = (float)(1.0 / sqrt(var + eps));
+  const float mu = mean[c];
+  const float g = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+  const float a = g * rs;
+  for (int b = 0; b < vol.B; ++b) {
+    rstd[b * C + c] = rs;
+    al[b * C + c] = a;
+    de[b * C + c] = bt - mu * a;
+  }
+  if (rmean) {
+    rmean[c] = (float)(mom * (double)mu + (1.0 - mom) * (double)rmean[c]);
+    const double uv = N > 1.0 ? s / (N - 1.0) : var;
+    rvar[c] = (float)(mom * uv + (1.0 - mom) * (double)rvar[c]);
+  }
+}
+
+// eval: normalise with the running statistics
+__global__ void k_bn_eval(const float* __restrict__ rmean, const float* __restrict__ rvar,
+                          const float* __restrict__ gamma, const float* __restrict__ beta,
+                          float* __restrict__ mean, float* __restrict__ rstd,
+                          float* __restrict__ al, float* __restrict__ de, double eps, int B,
+                          int C) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float rs = (float)(1.0 / sqrt((double)rvar[c] + eps));
+  const float g = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+  const float a = g * rs;
+  for (int b = 0; b < B; ++b) {
+    mean[b * C + c] = rmean[c];
+    rstd[b * C + c] = rs;
+    al[b * C + c] = a;
+    de[b * C + c] = bt - rmean[c] * a;
+  }
+}
+
+// backward: from per-(b,c,d) [sum dr, sum dr*xhat] -> dgamma, dbeta and the
+// batch means k1 = mean dr, k2 = mean dr*xhat (replicated over b)
+__global__ void k_bn_bwd_stats(const float* __restrict__ sums, float* __restrict__ dgamma,
+                               float* __restrict__ dbeta, float* __restrict__ k1,
+                               float* __restrict__ k2, Vol vol, int C, int eval) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s0 = 0.0, s1 = 0.0;
+  for (int b = 0; b < vol.B; ++b)
+    for (int d = 0; d < vol.D; ++d) {
+      const int64_t i = (((int64_t)b * C + c) * vol.D + d) * 2;
+      s0 += sums[i];
+      s1 += sums[i + 1];
+    }
+  const double N = (double)vol.B * vol.D * vol.H * vol.W;
+  for (int b = 0; b < vol.B; ++b) {
+    k1[b * C + c] = eval ? 0.f : (float)(s0 / N);
+    k2[b * C + c] = eval ? 0.f : (float)(s1 / N);
+  }
+  if (dgamma) dgamma[c] = (float)s1;
+  if (dbeta) dbeta[c] = (float)s0;
+}
+
+hipError_t bn_mean(const float* sums, float* mean, Vol vol, int C, hipStream_t s) {
+  hipLaunchKernelGGL(k_bn_mean, dim3(cdiv(C, 64)), dim3(64), 0, s, sums, mean, vol, C);
+  return hipGetLastError();
+}
+hipError_t bn_rstd(const float* sq, const float* gamma, const float* beta, const float* mean,
+                   float* rstd, float* al, float* de, float* rmean, float* rvar, double mom,
+                   double eps, Vol vol, int C, hipStream_t s) {
+  hipLaunchKernelGGL(k_bn_rstd, dim3(cdiv(C, 64)), dim3(64), 0, s, sq, gamma, beta, mean, rstd,
+                     al, de, rmean, rvar, mom, eps, vol, C);
+  return hipGetLastError();
+}
+hipError_t bn_eval(const float* rmean, const float* rvar, const float* gamma, const float* beta,
+                   float* mean, float* rstd, float* al, float* de, double eps, int B, int C,
+                   hipStream_t s) {
+  hipLaunchKernelGGL(k_bn_eval, dim3(cdiv(C, 64)), dim3(64), 0, s, rmean, rvar, gamma, beta, mean,
+                     rstd, al, de, eps, B, C);
+  return hipGetLastError();
+}
+hipError_t bn_bwd_stats(const float* sums, float* dgamma, float* dbeta, float* k1, float* k2,
+                        Vol vol, int C, hipStream_t s, int eval) {
+  hipLaunchKernelGGL(k_bn_bwd_stats, dim3(cdiv(C, 64)), dim3(64), 0, s, sums, dgamma, dbeta, k1,
+                     k2, vol, C, eval);
+  return hipGetLastError();
+}
+
 // ------------------------------------------------------------ elementwise --
 // grid.y = b*D + d ; grid.x strides over the (h,w,c/4) float4s of that slab.
 // The stride (gridDim.x * 256) is a multiple of C/4 (C/4 <= 64, power of two),
@@ -315,7 +430,7 @@ hipError_t in_bwd_fin(const double* part, float* k1, float* k2, int BC, double N
 __global__ __launch_bounds__(256) void k_act_apply(const float* __restrict__ y, float* __restrict__ out,
                                                    const float* __restrict__ al, const float* __restrict__ de,
                                                    const float* __restrict__ P, const float* __restrict__ Q,
-                                                   Vol vol, int C) {
+                                                   Vol vol, int C, float neg) {
   const int bd = blockIdx.y, b = bd / vol.D, d = bd % vol.D;
   const int n4 = vol.H * vol.W * (C >> 2);
   const int64_t base = (int64_t)bd * vol.H * vol.W * C;
@@ -334,7 +449,7 @@ __global__ __launch_bounds__(256) void k_act_apply(const float* __restrict__ y, 
     const float4 v = *reinterpret_cast<const float4*>(y + base + 4 * (int64_t)i);
     float r[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-    for (int j = 0; j < 4; ++j) r[j] = lrelu(r[j] * pa[j] + pd[j]) * pp[j] + pq[j];
+    for (int j = 0; j < 4; ++j) r[j] = lrelu(r[j] * pa[j] + pd[j], neg) * pp[j] + pq[j];
     *reinterpret_cast<float4*>(out + base + 4 * (int64_t)i) = make_float4(r[0], r[1], r[2], r[3]);
   }
 }
@@ -346,8 +461,9 @@ static dim3 ew_grid(Vol vol, int C) {
 }
 
 hipError_t act_apply(const float* y, float* out, const float* al, const float* de, const float* P,
-                     const float* Q, Vol vol, int C, hipStream_t s) {
-  hipLaunchKernelGGL(k_act_apply, ew_grid(vol, C), dim3(256), 0, s, y, out, al, de, P, Q, vol, C);
+                     const float* Q, Vol vol, int C, hipStream_t s, float neg) {
+  hipLaunchKernelGGL(k_act_apply, ew_grid(vol, C), dim3(256), 0, s, y, out, al, de, P, Q, vol, C,
+                     neg);
   return hipGetLastError();
 }
 
@@ -355,7 +471,7 @@ __global__ __launch_bounds__(256) void k_in_bwd_apply(
     const float* __restrict__ y, const float* g, float* dy, const float* __restrict__ mean,
     const float* __restrict__ rstd, const float* __restrict__ al, const float* __restrict__ de,
     const float* __restrict__ gamma, const float* __restrict__ A, const float* __restrict__ Bc,
-    const float* __restrict__ k1, const float* __restrict__ k2, Vol vol, int C) {
+    const float* __restrict__ k1, const float* __restrict__ k2, Vol vol, int C, float neg) {
   const int bd = blockIdx.y, b = bd / vol.D, d = bd % vol.D;
   const int n4 = vol.H * vol.W * (C >> 2);
   const int64_t base = (int64_t)bd * vol.H * vol.W * C;
@@ -379,7 +495,7 @@ __global__ __launch_bounds__(256) void k_in_bwd_apply(
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const float r = ys[j] * pal[j] + pde[j];
-      const float dr = (gs[j] * pA[j] + pB[j]) * slope(r);
+      const float dr = (gs[j] * pA[j] + pB[j]) * slope(r, neg);
       const float xh = (ys[j] - pmu[j]) * prs[j];
       o[j] = psc[j] * (dr - pk1[j] - xh * pk2[j]);
     }
@@ -390,9 +506,9 @@ __global__ __launch_bounds__(256) void k_in_bwd_apply(
 hipError_t in_bwd_apply(const float* y, const float* g, float* dy, const float* mean,
                         const float* rstd, const float* al, const float* de, const float* gamma,
                         const float* A, const float* Bc, const float* k1, const float* k2, Vol vol,
-                        int C, hipStream_t s) {
+                        int C, hipStream_t s, float neg) {
   hipLaunchKernelGGL(k_in_bwd_apply, ew_grid(vol, C), dim3(256), 0, s, y, g, dy, mean, rstd, al,
-                     de, gamma, A, Bc, k1, k2, vol, C);
+                     de, gamma, A, Bc, k1, k2, vol, C, neg);
   return hipGetLastError();
 }
 

@@ -9,6 +9,9 @@
 
 namespace spff {
 
+// records msg for spff_last_error() (calling thread) and returns code
+int set_error(int code, const char* msg);
+
 // Two-source channel view: channel c < split reads p0[v*ld0 + c], otherwise
 // p1[v*ld1 + c - split].  Lets the decoder's first conv read [up | skip]
 // without materialising torch.cat (reference _cat, models.py:687-691).
@@ -65,18 +68,20 @@ hipError_t conv3d_wgrad_reduce(const float* part, float* dw, int nsplit, int T, 
                                int npad, int Cin, int Cout, hipStream_t s);
 
 // ---------------------------------------------------------------- gemms --
-// ConvTranspose3d(Cin->Cout, k=(1,2,2), s=(1,2,2)) + bias, low-res x [Vlow][Cin],
-// high-res y [Vhigh][Cout] (Vhigh: H*2, W*2).  Reference weight W[Cin][Cout][1][2][2].
-hipError_t upconv_pack(const float* w, float* wf, float* wd, int Cin, int Cout, hipStream_t s);
+// ConvTranspose3d(Cin->Cout, k=s=(1,2,2) [ns = 4] or 2x2x2 [ns = 8]) + bias,
+// low-res x [Vlow][Cin], high-res y [Vhigh][Cout] (H, W doubled; D too for
+// ns = 8).  Reference weight W[Cin][Cout][1 or 2][2][2].
+hipError_t upconv_pack(const float* w, float* wf, float* wd, int Cin, int Cout, hipStream_t s,
+                       int ns = 4);
 hipError_t upconv_fwd(const float* x, const float* wf, const float* bias, float* y,
-                      Vol low, int Cin, int Cout, hipStream_t s);
+                      Vol low, int Cin, int Cout, hipStream_t s, int ns = 4);
 hipError_t upconv_dgrad(const float* dy, int lddy, const float* wd, float* dx, Vol low,
-                        int Cin, int Cout, hipStream_t s);
-size_t upconv_wgrad_ws_bytes(Vol low, int Cin, int Cout);
+                        int Cin, int Cout, hipStream_t s, int ns = 4);
+size_t upconv_wgrad_ws_bytes(Vol low, int Cin, int Cout, int ns = 4);
 hipError_t upconv_wgrad(const float* x, const float* dy, int lddy, float* dw, float* db,
-                        Vol low, int Cin, int Cout, float* ws, hipStream_t s);
-size_t upconv_pack_floats(int Cin, int Cout);
-size_t upconv_pack_dgrad_offset(int Cin, int Cout);
+                        Vol low, int Cin, int Cout, float* ws, hipStream_t s, int ns = 4);
+size_t upconv_pack_floats(int Cin, int Cout, int ns = 4);
+size_t upconv_pack_dgrad_offset(int Cin, int Cout, int ns = 4);
 // 1x1x1 conv head: y[v][K] = x[v][:Cin] . W[K][Cin] + b  (wf/wd from head_pack)
 hipError_t head_pack(const float* w, float* wf, float* wd, int Cin, int K, hipStream_t s);
 size_t head_pack_floats(int Cin, int K);
@@ -103,6 +108,7 @@ struct RedArgs {
   const float* mean; const float* rstd; // [B][C]
   const float* al; const float* de;   // [B][C]
   const float* A; const float* Bc;    // [B][C][D] or null (identity)
+  float neg = 0.01f;                  // activation negative slope (0: ReLU)
 };
 // out: [B][C][D][nq] fp32, summed over h,w in a fixed order.
 size_t slab_reduce_ws_bytes(Vol vol, int C, int nq);
@@ -115,7 +121,8 @@ hipError_t in_rstd(const float* sqsums, const float* gamma, const float* beta,
                    hipStream_t s);
 // out = lrelu(y*al[b,c]+de[b,c]) * P[b,c,d] + Q[b,c,d]   (P/Q null -> identity)
 hipError_t act_apply(const float* y, float* out, const float* al, const float* de,
-                     const float* P, const float* Q, Vol vol, int C, hipStream_t s);
+                     const float* P, const float* Q, Vol vol, int C, hipStream_t s,
+                     float neg = 0.01f);
 // IN backward finalize: from per-(b,c,d) [sum dr, sum dr*xhat] -> dgamma, dbeta (over b),
 // k1[b,c] = mean dr, k2[b,c] = mean dr*xhat
 // depth-sharded variants: fp64 partials over the local slab, summed across the
@@ -134,7 +141,19 @@ hipError_t in_bwd_stats(const float* sums, const float* gamma, float* dgamma, fl
 hipError_t in_bwd_apply(const float* y, const float* g, float* dy, const float* mean,
                         const float* rstd, const float* al, const float* de, const float* gamma,
                         const float* A, const float* Bc, const float* k1, const float* k2,
-                        Vol vol, int C, hipStream_t s);
+                        Vol vol, int C, hipStream_t s, float neg = 0.01f);
+// BatchNorm3d (train: batch statistics over (b,d,h,w) + running-stat update;
+// eval: running statistics).  Per-channel values replicated over b into [B][C].
+hipError_t bn_mean(const float* sums, float* mean, Vol vol, int C, hipStream_t s);
+hipError_t bn_rstd(const float* sqsums, const float* gamma, const float* beta, const float* mean,
+                   float* rstd, float* al, float* de, float* rmean, float* rvar, double mom,
+                   double eps, Vol vol, int C, hipStream_t s);
+hipError_t bn_eval(const float* rmean, const float* rvar, const float* gamma, const float* beta,
+                   float* mean, float* rstd, float* al, float* de, double eps, int B, int C,
+                   hipStream_t s);
+// eval = 1: backward of the running-statistics transform (k1 = k2 = 0)
+hipError_t bn_bwd_stats(const float* sums, float* dgamma, float* dbeta, float* k1, float* k2,
+                        Vol vol, int C, hipStream_t s, int eval = 0);
 
 // Depth sharding: the shard group's collectives, supplied by the caller through
 // spff_coll (include/spff.h).  world == 1: unsharded, every call is a no-op.
@@ -199,6 +218,17 @@ hipError_t maxpool_fwd(const float* x, float* y, uint8_t* idx, Vol in, int C, hi
 hipError_t maxpool_bwd_add(const float* dp, const uint8_t* idx, const float* dskip, int ldskip,
                            float* dx, Vol in, int C, hipStream_t s);
 hipError_t scale_by_dev(float* x, int64_t n, const float* scale, hipStream_t s);
+// MaxPool3d(2) (full 2x2x2), first-max ties; idx = (dd*2+dh)*2+dw
+hipError_t maxpool3_fwd(const float* x, float* y, uint8_t* idx, Vol in, int C, hipStream_t s);
+hipError_t maxpool3_bwd_add(const float* dp, const uint8_t* idx, const float* dskip, int ldskip,
+                            float* dx, Vol in, int C, hipStream_t s);
+// trilinear depth resampling with H, W unchanged (align_corners=False)
+hipError_t resize_d_ncdhw_to_ndhwc(const float* x, float* y, int B, int C, int Din, int Dout,
+                                   int H, int W, int ldy, hipStream_t s);
+hipError_t resize_d_rows(const float* x, float* y, int B, int K, int Din, int Dout, int H, int W,
+                         hipStream_t s);
+hipError_t resize_d_rows_bwd(const float* dy, float* dx, int B, int K, int Din, int Dout, int H,
+                             int W, hipStream_t s);
 
 // ----------------------------------------------------------------- optim --
 hipError_t adam_step(float* p, const float* g, float* m, float* v, int64_t n, double lr,
@@ -210,7 +240,8 @@ size_t loss_ws_bytes(int64_t V, int K);
 // conf: K x (K+1) int64, conf[pred*(K+1) + label], column K = label outside [0,K)
 hipError_t loss_fwd(const float* logits, const int64_t* labels, int64_t V, int K, int ignore,
                     double smooth, const int64_t* count_override, float* out4, float* dlogits,
-                    int64_t* conf, float* ws, hipStream_t s);
+                    int64_t* conf, float* ws, hipStream_t s, const float* class_w = nullptr,
+                    int clamp1 = 0);
 hipError_t count_valid(const int64_t* labels, int64_t V, int ignore, int64_t* count,
                        hipStream_t s);
 hipError_t confusion_only(const float* logits, const int64_t* labels, int64_t V, int K,

@@ -33,6 +33,15 @@ class spff_cfg(ctypes.Structure):
     ]
 
 
+class spff_unet3d_cfg(ctypes.Structure):
+    _fields_ = [
+        ("batch", ctypes.c_int), ("in_ch", ctypes.c_int), ("depth", ctypes.c_int),
+        ("height", ctypes.c_int), ("width", ctypes.c_int), ("target_depth", ctypes.c_int),
+        ("num_classes", ctypes.c_int), ("base", ctypes.c_int), ("math", ctypes.c_int),
+        ("reserved", ctypes.c_int * 7),
+    ]
+
+
 # spff_coll (include/spff.h): the shard group's collectives, called back by the engine
 ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                                 ctypes.c_int, ctypes.c_void_p)
@@ -93,6 +102,23 @@ _SIGS = {
     "spff_conv3d_dgrad_ex": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
     "spff_conv3d_wgrad_ex": (_I, [_P, _I, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
     "spff_conv3d_wgrad": (_I, [_P, _I, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
+    # 3DUNet baseline variant (BASELINE config 3)
+    "spff_unet3d_create": (_I, [ctypes.POINTER(spff_unet3d_cfg), ctypes.POINTER(_P)]),
+    "spff_unet3d_destroy": (None, [_P]),
+    "spff_unet3d_num_params": (_I, [_P]),
+    "spff_unet3d_param_info": (_I, [_P, _I, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(_I),
+                                    ctypes.POINTER(_L), ctypes.POINTER(_L), ctypes.POINTER(_L)]),
+    "spff_unet3d_param_floats": (_L, [_P]),
+    "spff_unet3d_num_buffers": (_I, [_P]),
+    "spff_unet3d_buffer_info": (_I, [_P, _I, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(_L),
+                                     ctypes.POINTER(_L)]),
+    "spff_unet3d_buffer_floats": (_L, [_P]),
+    "spff_unet3d_workspace_bytes": (_S, [_P]),
+    "spff_unet3d_forward": (_I, [_P, _P, _P, _P, _I, _P, _P, _P]),
+    "spff_unet3d_backward": (_I, [_P, _P, _P, _P, _P, _P]),
+    "spff_unet3d_saved_tensor": (_I, [_P, _P, ctypes.c_char_p, ctypes.POINTER(_P),
+                                      ctypes.POINTER(_L), ctypes.POINTER(_I)]),
+    "spff_loss_ex": (_I, [_P, _P, _L, _I, _I, ctypes.c_double, _P, _P, _I, _P, _P, _P, _P, _P]),
 }
 EXPORTED = tuple(_SIGS)
 
@@ -312,6 +338,117 @@ def get_plan(**kw) -> Plan:
     return _PLANS[key]
 
 
+class UNet3DPlan:
+    """Engine plan of the 3DUNet baseline variant (include/spff.h spff_unet3d_*):
+    Cicek3DUNet + the depth adapter of LitCicek3DUNet_DepthAdapter_Published
+    (reference models.py:718-777).  Parameters are one flat fp32 buffer in
+    reference state-dict order (``params``), BatchNorm running statistics a
+    second one (``buffers``)."""
+
+    def __init__(self, batch, in_ch, depth, height, width, num_classes, base=32, target_depth=0,
+                 device=None, math=None):
+        math = default_math() if math is None else math
+        if math not in MATH_NAMES:
+            raise SpffError(f"math={math!r}: expected one of {sorted(MATH_NAMES)}")
+        cfg = spff_unet3d_cfg()
+        cfg.batch, cfg.in_ch, cfg.depth, cfg.height, cfg.width = batch, in_ch, depth, height, width
+        cfg.target_depth, cfg.num_classes, cfg.base = int(target_depth), num_classes, base
+        cfg.math = MATH_NAMES[math]
+        self.cfg, self.math, self.device = cfg, math, device
+        L = lib()
+        h = ctypes.c_void_p()
+        check(L.spff_unet3d_create(ctypes.byref(cfg), ctypes.byref(h)), "spff_unet3d_create")
+        self._h = h
+        self.params: List[Tuple[str, Tuple[int, ...], int, int]] = []
+        for i in range(L.spff_unet3d_num_params(h)):
+            name, nd = ctypes.c_char_p(), ctypes.c_int()
+            shape, off, n = (ctypes.c_int64 * 5)(), ctypes.c_int64(), ctypes.c_int64()
+            check(L.spff_unet3d_param_info(h, i, ctypes.byref(name), ctypes.byref(nd), shape,
+                                           ctypes.byref(off), ctypes.byref(n)),
+                  "spff_unet3d_param_info")
+            self.params.append((name.value.decode(), tuple(shape[k] for k in range(nd.value)),
+                                off.value, n.value))
+        self.buffers: List[Tuple[str, int, int]] = []
+        for i in range(L.spff_unet3d_num_buffers(h)):
+            name, off, n = ctypes.c_char_p(), ctypes.c_int64(), ctypes.c_int64()
+            check(L.spff_unet3d_buffer_info(h, i, ctypes.byref(name), ctypes.byref(off),
+                                            ctypes.byref(n)), "spff_unet3d_buffer_info")
+            self.buffers.append((name.value.decode(), off.value, n.value))
+        self.nfloats = int(L.spff_unet3d_param_floats(h))
+        self.nbuf = int(L.spff_unet3d_buffer_floats(h))
+        self.ws_bytes = int(L.spff_unet3d_workspace_bytes(h))
+        self._ws: Optional[torch.Tensor] = None
+        self.generation = 0
+
+    def __del__(self):
+        try:
+            if getattr(self, "_h", None) is not None and _lib is not None:
+                _lib.spff_unet3d_destroy(self._h)
+        except Exception:
+            pass
+
+    def workspace(self, device) -> torch.Tensor:
+        if self._ws is None or self._ws.device != device:
+            self._ws = torch.empty(self.ws_bytes, dtype=torch.uint8, device=device)
+        return self._ws
+
+    def forward(self, x: torch.Tensor, flat: torch.Tensor, bufs: torch.Tensor, training: bool,
+                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """x [B,Cin,D,H,W] fp32 -> logits channel-last [B,D,H,W,K]; training updates bufs."""
+        c = self.cfg
+        require_device(x, "3DUNet forward")
+        if tuple(x.shape) != (c.batch, c.in_ch, c.depth, c.height, c.width):
+            raise SpffError(f"input shape {tuple(x.shape)} does not match plan")
+        if x.dtype != torch.float32:
+            raise SpffError("the engine computes in fp32; got " + str(x.dtype))
+        x = x.contiguous()
+        if out is None:
+            out = torch.empty((c.batch, c.depth, c.height, c.width, c.num_classes),
+                              dtype=torch.float32, device=x.device)
+        ws = self.workspace(x.device)
+        self.generation += 1
+        check(lib().spff_unet3d_forward(self._h, _ptr(x), _ptr(flat), _ptr(bufs), int(bool(training)),
+                                        _ptr(out), _ptr(ws), _stream(x.device)),
+              "spff_unet3d_forward")
+        return out
+
+    def backward(self, dlogits_cl: torch.Tensor, flat: torch.Tensor) -> torch.Tensor:
+        dlogits_cl = dlogits_cl.contiguous()
+        dflat = torch.empty(self.nfloats, dtype=torch.float32, device=dlogits_cl.device)
+        ws = self.workspace(dlogits_cl.device)
+        check(lib().spff_unet3d_backward(self._h, _ptr(dlogits_cl), _ptr(flat), _ptr(dflat),
+                                         _ptr(ws), _stream(dlogits_cl.device)),
+              "spff_unet3d_backward")
+        return dflat
+
+    def saved(self, name: str) -> torch.Tensor:
+        ws = self._ws
+        if ws is None:
+            raise SpffError("no forward has run")
+        ptr, nv, ch = ctypes.c_void_p(), ctypes.c_int64(), ctypes.c_int()
+        check(lib().spff_unet3d_saved_tensor(self._h, _ptr(ws), name.encode(), ctypes.byref(ptr),
+                                             ctypes.byref(nv), ctypes.byref(ch)),
+              "spff_unet3d_saved_tensor")
+        off = ptr.value - ws.data_ptr()
+        n = nv.value * ch.value
+        return ws[off:off + 4 * n].view(torch.float32).view(nv.value, ch.value).clone()
+
+
+_UPLANS: Dict[tuple, UNet3DPlan] = {}
+
+
+def get_unet3d_plan(**kw) -> UNet3DPlan:
+    """UNet3D plans cached per (shape, math, tag) like get_plan."""
+    key = (kw["batch"], kw["in_ch"], kw["depth"], kw["height"], kw["width"], kw["num_classes"],
+           kw.get("base", 32), kw.get("target_depth", 0), kw.get("math") or default_math(),
+           kw.get("tag", ""))
+    if key not in _UPLANS:
+        kk = dict(kw)
+        kk.pop("tag", None)
+        _UPLANS[key] = UNet3DPlan(**kk)
+    return _UPLANS[key]
+
+
 # ------------------------------------------------------------------ loss ops --
 def loss_ws(device) -> torch.Tensor:
     n = int(lib().spff_loss_ws_bytes(0, 1))
@@ -335,6 +472,33 @@ def ce_dice_forward(logits_cl: torch.Tensor, labels: torch.Tensor, K: int, ignor
     check(lib().spff_loss(_ptr(logits_cl), _ptr(labels), V, K, int(ignore_index), float(smooth),
                           _ptr(count_override), _ptr(out4), _ptr(dl), _ptr(conf), _ptr(ws),
                           _stream(dev)), "spff_loss")
+    return out4, dl, conf.view(K, K + 1)
+
+
+def weighted_ce_forward(logits_cl: torch.Tensor, labels: torch.Tensor, K: int, ignore_index: int,
+                        class_weights: Optional[torch.Tensor] = None,
+                        count_override: Optional[torch.Tensor] = None):
+    """The 3DUNet wrapper's _weighted_softmax_ce (models.py:779-799):
+    sum_v w[y_v] nll_v / max(N_valid, 1).  Returns (out4, dlogits_cl, conf)."""
+    require_device(logits_cl, "weighted softmax CE")
+    logits_cl = logits_cl.contiguous()
+    labels = labels.to(device=logits_cl.device, dtype=torch.int64).contiguous()
+    V = labels.numel()
+    if logits_cl.numel() != V * K:
+        raise SpffError(f"logits ({tuple(logits_cl.shape)}) / labels ({tuple(labels.shape)}) mismatch")
+    dev = logits_cl.device
+    cw = None
+    if class_weights is not None:
+        cw = class_weights.to(device=dev, dtype=torch.float32).contiguous()
+        if cw.numel() != K:
+            raise SpffError(f"class_weights has {cw.numel()} entries, expected {K}")
+    out4 = torch.empty(4, dtype=torch.float32, device=dev)
+    dl = torch.empty_like(logits_cl)
+    conf = torch.empty(K * (K + 1), dtype=torch.int64, device=dev)
+    ws = loss_ws(dev)
+    check(lib().spff_loss_ex(_ptr(logits_cl), _ptr(labels), V, K, int(ignore_index), 1e-6,
+                             _ptr(count_override), _ptr(cw), 1, _ptr(out4), _ptr(dl), _ptr(conf),
+                             _ptr(ws), _stream(dev)), "spff_loss_ex")
     return out4, dl, conf.view(K, K + 1)
 
 

@@ -9,8 +9,9 @@ engine implements.  Differences, all deliberate:
   and CHECKPOINT_DIR/LOG_DIR at import (config.py:19, 258-259); here
   directories are created by whoever writes to them (train.py);
 * ``INNOVATIVE3D_VARIANT`` actually selects (SURVEY F11): ``selected_variants()``;
-* the non-SPCT baselines (3DUNet, UNETR, R2UNet3D, SwinUNETR, ResUNet++) are
-  outside the SPFF hot path (SURVEY §8) and are not registered;
+* of the non-SPCT baselines only "3DUNet" is registered (BASELINE config 3,
+  SURVEY §8(f) rank 2: Cicek3DUNet + depth adapter on the engine); UNETR,
+  R2UNet3D, SwinUNETR and ResUNet++ are outside the SPFF hot path (SURVEY §8);
 * the DICOM data modules are outside the hot path: ``MultiDicomDataModule3D``
   raises with a pointer to the synthetic data path used by bench.py.
 """
@@ -113,6 +114,23 @@ _plaincore_kwargs = {**_SPCT_COMMON, "use_se": False, "use_specse": False, "use_
                      "use_skip_gate": False}
 _add_variant("PlainCore_UNet", build_class("LitSPCT_ControlUNet", **_plaincore_kwargs),
              MultiDicomDataModule3D, CHECKPOINT_DIR / "PlainCore_UNet")
+
+
+
+def make_cicek_depth_adapter_sgd_wce():
+    """config.py:283-303: Cicek 3D U-Net + depth adapter, SGD, weighted CE."""
+    from innovative3D.models import LitCicek3DUNet_DepthAdapter_Published
+    return LitCicek3DUNet_DepthAdapter_Published(
+        num_classes=NUM_CLASSES,
+        lr=1e-2, momentum=0.99, nesterov=False, weight_decay=0.0,   # SGD like the paper
+        ignore_index=255, class_weights=None, voxel_weight_key=None,  # weighted softmax CE
+        ce_weight=1.0, dice_weight=0.0,
+        use_bn=True, target_depth=16, include_bg_in_dice=False,
+    )
+
+
+_add_variant("3DUNet", make_cicek_depth_adapter_sgd_wce, MultiDicomDataModule3D,
+             CHECKPOINT_DIR / "3DUNet")
 
 VARIANT_NAMES = [v[0] for v in VARIANTS]
 SELECTED_VARIANT = os.getenv("INNOVATIVE3D_VARIANT")

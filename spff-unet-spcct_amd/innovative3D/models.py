@@ -482,3 +482,275 @@ class LitSPCT_ControlUNet(BaseLitModel):
         self.model = UNet3D_SpectralCore(in_channels=in_channels, num_classes=num_classes, base=base,
                                          ksd=ksd, use_se=use_se, use_specse=use_specse,
                                          use_spatial=use_spatial, use_skip_gate=use_skip_gate)
+
+
+# ============================================================================
+# 3DUNet baseline variant (BASELINE config 3; registry entry "3DUNet",
+# config.py:283-311): Cicek3DUNet (models.py:718-753) + the depth-adapter
+# Lightning wrapper (models.py:756-853), on the engine's spff_unet3d plan.
+# ============================================================================
+class _UNet3DFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, plan, flat, bufs, training, *params):
+        logits_cl = plan.forward(x, flat, bufs, training)
+        ctx.plan, ctx.gen, ctx.flat = plan, plan.generation, flat
+        ctx.slices = [(off, n, shape) for (_name, shape, off, n) in plan.params]
+        return logits_cl.permute(0, 4, 1, 2, 3)
+
+    @staticmethod
+    def backward(ctx, g):
+        plan = ctx.plan
+        if plan.generation != ctx.gen:
+            raise E.SpffError("3DUNet engine: another forward ran on this model before the "
+                              "backward of this one; the engine keeps one forward's activations")
+        g_cl = g.permute(0, 2, 3, 4, 1).contiguous()
+        dflat = plan.backward(g_cl, ctx.flat)
+        grads = [dflat[o:o + n].view(s) for (o, n, s) in ctx.slices]
+        return (None, None, None, None, None, *grads)
+
+
+class Cicek3DUNet(nn.Module):
+    """models.py:718-753.  Same module tree / state-dict keys as the reference
+    (enc1.0.weight, enc1.1.running_mean, ..., up4.weight, out.bias); the
+    Conv3d / BatchNorm3d children are parameter containers and forward runs on
+    the engine (BatchNorm in train mode: batch statistics + running-stat update;
+    eval mode: running statistics).  D, H, W must be multiples of 16."""
+
+    def __init__(self, num_classes: int, base: int = 32, use_bn: bool = True, in_channels: int = 1):
+        super().__init__()
+        if not use_bn:
+            raise NotImplementedError("use_bn=False (conv bias + Identity norm) is not on the "
+                                      "registry path (config.py:308 sets use_bn=True)")
+
+        def block(ci, co):
+            return nn.Sequential(
+                nn.Conv3d(ci, co, 3, padding=1, bias=False), nn.BatchNorm3d(co), nn.ReLU(inplace=True),
+                nn.Conv3d(co, co, 3, padding=1, bias=False), nn.BatchNorm3d(co), nn.ReLU(inplace=True),
+            )
+        self.num_classes, self.base, self.in_channels = int(num_classes), int(base), int(in_channels)
+        self.enc1 = block(in_channels, base); self.pool1 = nn.MaxPool3d(2)  # noqa: E702
+        self.enc2 = block(base, base * 2); self.pool2 = nn.MaxPool3d(2)  # noqa: E702
+        self.enc3 = block(base * 2, base * 4); self.pool3 = nn.MaxPool3d(2)  # noqa: E702
+        self.enc4 = block(base * 4, base * 8); self.pool4 = nn.MaxPool3d(2)  # noqa: E702
+        self.bott = block(base * 8, base * 16)
+        self.up4 = nn.ConvTranspose3d(base * 16, base * 8, 2, stride=2)
+        self.dec4 = block(base * 8 + base * 8, base * 8)
+        self.up3 = nn.ConvTranspose3d(base * 8, base * 4, 2, stride=2)
+        self.dec3 = block(base * 4 + base * 4, base * 4)
+        self.up2 = nn.ConvTranspose3d(base * 4, base * 2, 2, stride=2)
+        self.dec2 = block(base * 2 + base * 2, base * 2)
+        self.up1 = nn.ConvTranspose3d(base * 2, base, 2, stride=2)
+        self.dec1 = block(base + base, base)
+        self.out = nn.Conv3d(base, num_classes, 1)
+        self._flat = None
+        self._bufs = None
+
+    def _bn_modules(self):
+        return [m for m in self.modules() if isinstance(m, nn.BatchNorm3d)]
+
+    def _check_bn(self):
+        for m in self._bn_modules():
+            if (m.momentum != 0.1 or m.eps != 1e-5 or not m.affine or not m.track_running_stats):
+                raise NotImplementedError("engine BatchNorm3d: momentum=0.1, eps=1e-5, affine, "
+                                          "track_running_stats (the nn.BatchNorm3d defaults)")
+
+    def _plan(self, x, target_depth: int):
+        B, C, D, H, W = x.shape
+        if C != self.in_channels:
+            raise ValueError(f"expected {self.in_channels} input channels, got {C}")
+        return E.get_unet3d_plan(batch=B, in_ch=C, depth=D, height=H, width=W,
+                                 num_classes=self.num_classes, base=self.base,
+                                 target_depth=int(target_depth) if target_depth != D else 0,
+                                 device=x.device, math=getattr(self, "math", None),
+                                 tag=str(id(self)))
+
+    def _engine_params(self, plan):
+        named = dict(self.named_parameters())
+        out = []
+        for name, shape, _off, _n in plan.params:
+            p = named.get(name)
+            if p is None or tuple(p.shape) != tuple(shape):
+                raise E.SpffError(f"parameter {name} {shape} missing or mis-shaped in the module")
+            out.append(p)
+        return out
+
+    def _ensure_flat(self, plan, params, device):
+        flat = self._flat
+        ok = flat is not None and flat.device == device and flat.numel() == plan.nfloats
+        if ok:
+            base = flat.data_ptr()
+            ok = all(p.data_ptr() == base + 4 * off and p.dtype == torch.float32
+                     for p, (_n, _s, off, _k) in zip(params, plan.params))
+        if not ok:
+            flat = torch.empty(plan.nfloats, dtype=torch.float32, device=device)
+            with torch.no_grad():
+                for p, (_name, shape, off, n) in zip(params, plan.params):
+                    flat[off:off + n].copy_(p.detach().reshape(-1).to(device=device,
+                                                                     dtype=torch.float32))
+                    p.data = flat[off:off + n].view(shape)
+            self._flat = flat
+        return flat
+
+    def _ensure_bufs(self, plan, device):
+        named = dict(self.named_buffers())
+        bufs = self._bufs
+        ok = bufs is not None and bufs.device == device and bufs.numel() == plan.nbuf
+        if ok:
+            base = bufs.data_ptr()
+            ok = all(named[n].data_ptr() == base + 4 * off and named[n].dtype == torch.float32
+                     for n, off, _k in plan.buffers)
+        if not ok:
+            bufs = torch.empty(plan.nbuf, dtype=torch.float32, device=device)
+            with torch.no_grad():
+                for name, off, n in plan.buffers:
+                    b = named[name]
+                    bufs[off:off + n].copy_(b.detach().reshape(-1).to(device=device,
+                                                                      dtype=torch.float32))
+                    b.data = bufs[off:off + n].view(b.shape)
+            self._bufs = bufs
+            for m in self._bn_modules():  # keep num_batches_tracked next to its stats
+                m.num_batches_tracked.data = m.num_batches_tracked.data.to(device)
+        return bufs
+
+    def run(self, x, target_depth: int = 0):
+        """Forward with the depth adapter fused in (target_depth > 0 resamples D
+        there and back, models.py:771-777); returns [B,K,D,H,W] logits."""
+        x = _pick_first_if_seq(x)
+        E.require_device(x, "Cicek3DUNet.forward")
+        self._check_bn()
+        plan = self._plan(x, target_depth)
+        params = self._engine_params(plan)
+        flat = self._ensure_flat(plan, params, x.device)
+        bufs = self._ensure_bufs(plan, x.device)
+        training = bool(self.training)
+        if training:
+            with torch.no_grad():
+                for m in self._bn_modules():
+                    m.num_batches_tracked.add_(1)
+        need_grad = torch.is_grad_enabled() and any(p.requires_grad for p in params)
+        if need_grad:
+            return _UNet3DFunction.apply(x.float(), plan, flat, bufs, training, *params)
+        return plan.forward(x.float(), flat, bufs, training).permute(0, 4, 1, 2, 3)
+
+    def forward(self, x):
+        return self.run(x, 0)
+
+
+class _WeightedCE(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, labels, K, ignore_index, class_weights):
+        lcl = logits.permute(0, 2, 3, 4, 1).contiguous()
+        out4, dl, conf = E.weighted_ce_forward(lcl, labels, K, ignore_index, class_weights)
+        ctx.dl = dl
+        ctx.mark_non_differentiable(conf)
+        return out4[0], conf
+
+    @staticmethod
+    def backward(ctx, g, _gconf=None):
+        dl = ctx.dl
+        E.scale_(dl, g.reshape(1))
+        return dl.permute(0, 4, 1, 2, 3), None, None, None, None
+
+
+class LitCicek3DUNet_DepthAdapter_Published(pl.LightningModule):
+    """models.py:756-853 (registry "3DUNet", config.py:283-311): depth adapter
+    (resample D -> target_depth -> backbone -> back, fused into the engine),
+    weighted softmax CE with ignore_index on the fused HIP loss kernel (class
+    weights optional; denominator max(N_valid, 1)), macro-Dice logging from its
+    confusion counts, SGD(momentum) as configure_optimizers."""
+
+    def __init__(self, num_classes: int, target_depth: int = 16,
+                 lr: float = 1e-2, momentum: float = 0.99, nesterov: bool = False,
+                 weight_decay: float = 0.0, ignore_index: Optional[int] = 255,
+                 class_weights: Optional[List[float]] = None, voxel_weight_key: Optional[str] = None,
+                 ce_weight: float = 1.0, dice_weight: float = 0.0, use_bn: bool = True,
+                 include_bg_in_dice: bool = False, *args, **kwargs):
+        super().__init__()
+        self.save_hyperparameters({"num_classes": num_classes, "target_depth": target_depth,
+                                   "lr": lr, "momentum": momentum, "nesterov": nesterov,
+                                   "weight_decay": weight_decay, "ignore_index": ignore_index,
+                                   "class_weights": class_weights,
+                                   "voxel_weight_key": voxel_weight_key, "ce_weight": ce_weight,
+                                   "dice_weight": dice_weight, "use_bn": use_bn,
+                                   "include_bg_in_dice": include_bg_in_dice})
+        self.backbone = Cicek3DUNet(num_classes=num_classes, base=32, use_bn=use_bn)
+        self.target_depth = int(target_depth)
+        if class_weights is not None:
+            cw = np.asarray(class_weights, dtype="float32")
+            assert cw.shape[0] == int(num_classes)
+            self.register_buffer("class_weights", torch.from_numpy(cw), persistent=True)
+        else:
+            self.class_weights = None
+        self.voxel_weight_key = voxel_weight_key
+        self.ignore_index = ignore_index
+        self.include_bg_in_dice = include_bg_in_dice
+        self.ce_weight = float(ce_weight)
+        self.dice_weight = float(dice_weight)
+
+    def forward(self, x):
+        return self.backbone.run(_pick_first_if_seq(x), self.target_depth)
+
+    def _weighted_softmax_ce(self, logits, target, voxel_weights: Optional[torch.Tensor]):
+        if target.ndim == 5 and target.shape[1] == 1:
+            target = target[:, 0]
+        if voxel_weights is not None:
+            raise NotImplementedError("per-voxel CE weights (voxel_weight_key) are off on the "
+                                      "registry path (config.py:297)")
+        ign = self.ignore_index if self.ignore_index is not None else -1000
+        loss, conf = _WeightedCE.apply(logits, target, int(self.hparams.num_classes), int(ign),
+                                       getattr(self, "class_weights", None))
+        self._last_conf = conf
+        return loss
+
+    def _dice_loss(self, logits, y, eps=1e-6):
+        raise NotImplementedError("the soft-Dice term (dice_weight > 0) is off on the registry "
+                                  "path (config.py:300: dice_weight=0.0)")
+
+    def _loss_and_log(self, logits, y, stage: str, voxel_w: Optional[torch.Tensor],
+                      log_metrics: bool = True):
+        ce = self._weighted_softmax_ce(logits, y, voxel_w) * self.ce_weight
+        loss = ce
+        if self.dice_weight > 0.0:
+            loss = loss + self._dice_loss(logits, y) * self.dice_weight
+        self.log(f"{stage}_loss", loss, prog_bar=(stage == "train"), on_step=False, on_epoch=True,
+                 sync_dist=True)
+        if log_metrics:
+            # per_class_metrics_3d(logits, tgt, K, ignore_index) from the argmax counts the
+            # loss kernel already produced (ignore_index None <-> the loss's -1000: no label
+            # equals either, so the counts are the same)
+            tgt = _canonicalize_targets_3d(y)
+            K = int(self.hparams.num_classes)
+            met = metrics_from_confusion(self._last_conf.cpu().numpy(), K, int(tgt.numel()))
+            self.log(f"{stage}_macro_dice", met[3], on_step=False, on_epoch=True, prog_bar=True,
+                     sync_dist=True)
+        return loss
+
+    def _unpack(self, batch):
+        if isinstance(batch, (list, tuple)):
+            x, y = batch
+            voxel_w = None
+        else:
+            x, y = batch["image"], batch["label"]
+            voxel_w = batch.get(self.voxel_weight_key) if self.voxel_weight_key is not None else None
+        return x, y, voxel_w
+
+    def training_step(self, batch, _):
+        x, y, vw = self._unpack(batch)
+        logits = self(x)
+        return self._loss_and_log(logits, y.to(logits.device), "train", voxel_w=vw)
+
+    def validation_step(self, batch, _):
+        x, y, vw = self._unpack(batch)
+        logits = self(x)
+        return self._loss_and_log(logits, y.to(logits.device), "val", voxel_w=vw, log_metrics=True)
+
+    def test_step(self, batch, _):
+        x, y, vw = self._unpack(batch)
+        logits = self(x)
+        return self._loss_and_log(logits, y.to(logits.device), "test", voxel_w=vw)
+
+    def configure_optimizers(self):
+        return torch.optim.SGD(self.parameters(), lr=self.hparams.lr,
+                               momentum=self.hparams.momentum,
+                               nesterov=bool(self.hparams.nesterov),
+                               weight_decay=self.hparams.weight_decay)

@@ -18,7 +18,9 @@ tests exercise it):
 * biases (1-D): U(-0.1, 0.1);
 * ``mag_scale``: 1 + 0.1 * N(0,1)  (FourierGate, models.py:1523);
 * ``freq_mask`` / ``_mask``: all ones unless ``mask_jitter`` > 0 -- the
-  reference creates it lazily as ones and never optimises it.
+  reference creates it lazily as ones and never optimises it (SURVEY F10);
+* BatchNorm buffers (3DUNet): ``running_mean`` U(-0.1, 0.1), ``running_var``
+  U(0.5, 1.5) (a valid variance), ``num_batches_tracked`` 0.
 """
 from __future__ import annotations
 
@@ -39,6 +41,10 @@ def synth_param(name: str, shape: Tuple[int, ...], seed: int = 0,
         out = np.ones(shape, dtype=np.float64)
         if mask_jitter > 0:
             out = out + mask_jitter * rng.standard_normal(shape)
+    elif leaf == "running_var":
+        out = rng.uniform(0.5, 1.5, size=shape)
+    elif leaf == "num_batches_tracked":
+        return np.zeros(shape, dtype=np.int64)
     elif leaf == "mag_scale":
         out = 1.0 + 0.1 * rng.standard_normal(shape)
     elif len(shape) >= 2:

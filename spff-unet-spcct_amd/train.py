@@ -148,6 +148,8 @@ def train_and_log(model_name, builder, seed, S: Settings, datasets=None):
                     SyntheticSPCCT(n=S.n_test, seed=seed + 20_000, **shape))
     tr, va, te = (_loader(d, S.batch, i == 0, seed) for i, d in enumerate(datasets))
     oc = model.configure_optimizers()
+    if isinstance(oc, torch.optim.Optimizer):  # Lightning also accepts a bare optimizer (3DUNet)
+        oc = {"optimizer": oc}
     opt = oc["optimizer"]
     sch = oc.get("lr_scheduler", {}).get("scheduler")
     monitor = oc.get("lr_scheduler", {}).get("monitor", "val_macro_dice")

@@ -8,7 +8,23 @@ GOLDEN = pathlib.Path(__file__).resolve().parent / "golden"
 
 
 def fixture_names():
-    return sorted(p.stem for p in GOLDEN.glob("fx*.npz"))
+    """SPFF-family fixtures (the 3DUNet ones are fxu3d_*: unet3d_fixture_names)."""
+    return sorted(p.stem for p in GOLDEN.glob("fx*.npz") if not p.stem.startswith("fxu3d_"))
+
+
+def unet3d_fixture_names():
+    return sorted(p.stem for p in GOLDEN.glob("fxu3d_*.npz"))
+
+
+def unet3d_state_of(d):
+    """Regenerated parameters + buffers of a 3DUNet fixture (keys as in its state dict)."""
+    from innovative3D.weightgen import synth_state
+    shapes = d["state_shapes"]
+    st = synth_state([(k, tuple(v)) for k, v in shapes.items() if k != "class_weights"],
+                     d["meta"]["seed"])
+    if "class_weights" in d:
+        st["class_weights"] = d["class_weights"]
+    return st
 
 
 def load(name):

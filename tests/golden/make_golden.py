@@ -111,7 +111,10 @@ def _install_harness():
         p.write_text(textwrap.dedent(src))
     sys.path.insert(0, str(stub_dir))
     sys.path.insert(1, str(REF))
-    sys.path.insert(2, str(REPO / "spff-unet-spcct_amd"))
+    # NOT the engine package: the reference's innovative3D has no __init__.py (it
+    # ships "_init_.py"), so it is a namespace package and a regular package of
+    # the same name anywhere on sys.path would shadow it.  The weight generator
+    # is loaded by file path instead (_synth_state).
     os.environ.setdefault("CHECKPOINT_DIR", "/tmp/spff_ref_ckpt")
     os.environ.setdefault("LOG_DIR", "/tmp/spff_ref_logs")
     os.environ["PYTHONDONTWRITEBYTECODE"] = "1"
@@ -125,11 +128,21 @@ def _install_harness():
     pathlib.Path.mkdir = _guarded_mkdir
 
 
+def _synth_state(*a, **k):
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "_spff_weightgen", REPO / "spff-unet-spcct_amd" / "innovative3D" / "weightgen.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod.synth_state(*a, **k)
+
+
 def _import_reference():
     _install_harness()
     import innovative3D.config as C  # noqa: E402
     import innovative3D.models as M  # noqa: E402
     import innovative3D.helpers as Hh  # noqa: E402
+    assert pathlib.Path(M.__file__).resolve().is_relative_to(REF.resolve()), M.__file__
     return C, M, Hh
 
 
@@ -144,7 +157,7 @@ def _labels(rng, shape, K, ignore_frac=0.03, absent=None):
 
 def _run_case(torch, Hh, core_or_lit, x_np, y_np, K, seed, mask_jitter, full_grads,
               is_lit):
-    from innovative3D.weightgen import synth_state
+    synth_state = _synth_state
     x = torch.from_numpy(x_np)
     y = torch.from_numpy(y_np)
     model = core_or_lit
@@ -198,11 +211,111 @@ def _run_case(torch, Hh, core_or_lit, x_np, y_np, K, seed, mask_jitter, full_gra
     return out
 
 
+def _summ(out, key, g, full_max):
+    flat = g.reshape(-1)
+    if flat.size <= full_max:
+        out["grad/" + key] = g
+    else:
+        out["gradhead/" + key] = flat[:64].copy()
+        out["gradtail/" + key] = flat[-64:].copy()
+        out["gradsum/" + key] = np.array([flat.astype(np.float64).sum(),
+                                          np.sqrt((flat.astype(np.float64) ** 2).sum())])
+
+
+def _run_unet3d(torch, Hh, model, x_np, y_np, K, seed, full_max, lit):
+    """3DUNet variant (config.py:283-311): train-mode forward (BatchNorm batch
+    statistics + running-stat update), the wrapper's weighted CE, backward,
+    then an eval-mode forward on the updated running statistics."""
+    synth_state = _synth_state
+    x = torch.from_numpy(x_np)
+    y = torch.from_numpy(y_np)
+    sd = model.state_dict()
+    synth = synth_state([(k, tuple(v.shape)) for k, v in sd.items() if k != "class_weights"], seed)
+    new = {k: torch.from_numpy(np.asarray(v)) for k, v in synth.items()}
+    if "class_weights" in sd:
+        new["class_weights"] = sd["class_weights"]
+    model.load_state_dict(new, strict=True)
+    state0 = {k: v.detach().clone().numpy() for k, v in model.state_dict().items()}
+    model.train()
+    model.zero_grad(set_to_none=True)
+    logits = model(x)
+    if lit:
+        loss = model._weighted_softmax_ce(logits, y, None)
+    else:
+        loss = torch.nn.functional.cross_entropy(logits, y, ignore_index=255)
+    loss.backward()
+    met = Hh.per_class_metrics_3d(logits.detach(), y, K, ignore_index=255)
+    out = {"x": x_np, "labels": y_np,
+           "logits": logits.detach().numpy().astype(np.float32),
+           "loss": np.array(loss.item(), dtype=np.float64),
+           "met_dice": np.array(met[0], dtype=np.float64),
+           "met_scalars": np.array(met[3:], dtype=np.float64)}
+    names = []
+    for k, p in model.named_parameters():
+        names.append(k)
+        g = p.grad if p.grad is not None else torch.zeros_like(p)
+        _summ(out, k, g.detach().numpy().astype(np.float32), full_max)
+    for k, v in model.state_dict().items():
+        if k.endswith("running_mean") or k.endswith("running_var"):
+            out["bufafter/" + k] = v.detach().numpy().astype(np.float32)
+            out["bufbefore/" + k] = state0[k].astype(np.float32)
+        if k.endswith("num_batches_tracked"):
+            out["nbt/" + k] = np.array(int(v))
+    if "class_weights" in sd:
+        out["class_weights"] = sd["class_weights"].numpy().astype(np.float32)
+    model.eval()
+    with torch.no_grad():
+        out["logits_eval"] = model(x).numpy().astype(np.float32)
+    out["param_names"] = np.array(names)
+    out["state_keys"] = np.array(list(sd.keys()))
+    out["state_shapes"] = np.array(json.dumps({k: list(v.shape) for k, v in sd.items()}))
+    return out
+
+
+def unet3d_cases(C, M, Hh, torch):
+    """Fixtures of the 3DUNet variant (BASELINE config 3 path, small shapes)."""
+    cases = {}
+    # --- registry factory (class_weights None), base 32, depth adapter 5 -> 16 -> 5 ---
+    name, factory, _dm, _ck = [v for v in C.VARIANTS if v[0] == "3DUNet"][0]
+    torch.manual_seed(0)
+    lit = factory()
+    rng = np.random.default_rng(77)
+    x = rng.standard_normal((2, 1, 5, 32, 32)).astype(np.float32)
+    y = _labels(rng, (2, 5, 32, 32), 13)
+    cases["fxu3d_registry_k13"] = dict(
+        meta=dict(variant="3DUNet", in_ch=1, base=32, K=13, seed=8, target_depth=16, lit=True),
+        data=_run_unet3d(torch, Hh, lit, x, y, 13, 8, 4096, True))
+    # --- class-weighted CE, K=9, depth 6 -> 16 -> 6 ---
+    torch.manual_seed(0)
+    cw = [0.5, 1.5, 2.0, 1.0, 0.75, 1.25, 3.0, 0.25, 1.0]
+    lit9 = M.LitCicek3DUNet_DepthAdapter_Published(num_classes=9, class_weights=cw)
+    rng = np.random.default_rng(78)
+    x = rng.standard_normal((1, 1, 6, 32, 32)).astype(np.float32)
+    y = _labels(rng, (1, 6, 32, 32), 9, absent=5)
+    cases["fxu3d_weighted_k9"] = dict(
+        meta=dict(variant="3DUNet", in_ch=1, base=32, K=9, seed=9, target_depth=16, lit=True),
+        data=_run_unet3d(torch, Hh, lit9, x, y, 9, 9, 4096, True))
+    # --- bare backbone, base 8, no depth adapter, batch 2 ---
+    torch.manual_seed(0)
+    core = M.Cicek3DUNet(num_classes=5, base=8, use_bn=True)
+    rng = np.random.default_rng(79)
+    x = rng.standard_normal((2, 1, 16, 32, 32)).astype(np.float32)
+    y = _labels(rng, (2, 16, 32, 32), 5)
+    cases["fxu3d_core_b8"] = dict(
+        meta=dict(variant="Cicek3DUNet", in_ch=1, base=8, K=5, seed=10, target_depth=0, lit=False),
+        data=_run_unet3d(torch, Hh, core, x, y, 5, 10, 16384, False))
+    return cases
+
+
 def main():
     C, M, Hh = _import_reference()
     import torch
     torch.set_num_threads(min(8, os.cpu_count() or 1))
     torch.use_deterministic_algorithms(False)
+    only = os.environ.get("SPFF_GOLDEN_ONLY")  # e.g. "fxu3d_" regenerates that family only
+    if only and only.startswith("fxu3d"):
+        _write(unet3d_cases(C, M, Hh, torch), only)
+        return
     cases = {}
 
     # --- Fx1: registry layout via the VARIANTS factory (config.py:423-428) ---
@@ -275,7 +388,14 @@ def main():
                       **fl),
             data=_run_case(torch, Hh, ns_core(5, 9, 8, **fl), x, y, 9, 6 + i, 0.0, True, False))
 
+    cases.update(unet3d_cases(C, M, Hh, torch))
+    _write(cases, only)
+
+
+def _write(cases, only=None):
     for cname, c in cases.items():
+        if only and not cname.startswith(only):
+            continue
         path = HERE / f"{cname}.npz"
         d = dict(c["data"])
         d["meta"] = np.array(json.dumps(c["meta"]))

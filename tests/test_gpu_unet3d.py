@@ -1,0 +1,189 @@
+"""3DUNet baseline variant (BASELINE config 3) on the HIP engine against the
+fixtures the reference itself produced (tests/golden/fxu3d_*).  Marked gpu.
+
+Checks, per fixture and conv arithmetic (f32, bf16x6): train-mode logits within
+1e-3 of the reference PyTorch-CPU forward with identical argmax (near-ties
+within 2 x max|dlogit| reported, not failed), the wrapper's weighted CE within
+1e-5 relative, per_class_metrics_3d exactly, BatchNorm running statistics after
+the step (1e-5 relative) and num_batches_tracked, eval-mode logits on the
+updated statistics within 1e-3, and every parameter gradient against a
+kink-consistent fp64 oracle within max(1e-3, 8 x the fp32 oracle's own error)
+of max|g| (ReLU signs and max-pool argmaxes routed as the engine saw them:
+an activation within fp32 rounding of 0 may legitimately take either side)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from _golden import load, unet3d_fixture_names, unet3d_state_of
+from oracle import unet3d_oracle as U
+import innovative3D.models as M
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def cfg_of(meta):
+    return U.UNet3DCfg(num_classes=meta["K"], base=meta["base"], in_ch=meta["in_ch"],
+                       target_depth=meta["target_depth"])
+
+
+def build(d):
+    meta = d["meta"]
+    if meta.get("lit"):
+        kw = {"class_weights": d["class_weights"].tolist()} if "class_weights" in d else {}
+        m = M.LitCicek3DUNet_DepthAdapter_Published(num_classes=meta["K"], **kw)
+    else:
+        m = M.Cicek3DUNet(num_classes=meta["K"], base=meta["base"])
+    st = unet3d_state_of(d)
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in st.items()}, strict=True)
+    return m.to(DEV)
+
+
+def near_tie_mask(ref_logits, tol):
+    top2 = np.sort(ref_logits, axis=1)[:, -2:]
+    return (top2[:, 1] - top2[:, 0]) < tol
+
+
+def _ncdhw(t_cl, B, D, H, W):
+    """engine channel-last [V, C] -> [B, C, D, H, W]"""
+    return t_cl.view(B, D, H, W, -1).permute(0, 4, 1, 2, 3)
+
+
+def engine_hooks(net, B, Dt, H, W):
+    """ReLU sign patterns and pool argmaxes as the engine saw them (its saved
+    block outputs), for the kink-consistent oracle."""
+    plan = net._last_plan
+    vols = {n: (Dt >> l, H >> l, W >> l) for n, l in
+            zip(U.BLOCKS, (0, 1, 2, 3, 4, 3, 2, 1, 0))}
+    masks, pidx = {}, {}
+    for n in U.BLOCKS:
+        D_, H_, W_ = vols[n]
+        for s in ("a1", "out"):
+            a = _ncdhw(plan.saved(f"{n}.{s}").cpu(), B, D_, H_, W_)
+            masks[f"{n}.{s}"] = (a > 0).double()
+    for l, n in enumerate(("enc1", "enc2", "enc3", "enc4")):
+        D_, H_, W_ = vols[n]
+        e = _ncdhw(plan.saved(f"{n}.out").cpu(), B, D_, H_, W_)
+        pidx[f"pool{l + 1}"] = F.max_pool3d(e, 2, return_indices=True)[1]
+
+    def relu(name, r):
+        return r * masks[name].to(r.dtype)
+
+    def pool(name, t):
+        idx = pidx[name]
+        return t.flatten(2).gather(2, idx.flatten(2)).view(idx.shape)
+    return {"relu": relu, "pool": pool}
+
+
+def oracle_grads(d, hooks, dtype):
+    meta = d["meta"]
+    pre = "backbone." if meta.get("lit") else ""
+    P, Bf = U.params_from_state(unet3d_state_of(d), dtype=dtype, prefix=pre)
+    x = torch.from_numpy(d["x"]).to(dtype)
+    y = torch.from_numpy(d["labels"])
+    cw = torch.from_numpy(d["class_weights"]).to(dtype) if "class_weights" in d else None
+    lg = U.forward(P, Bf, x, cfg_of(meta), True, hooks)
+    loss = U.weighted_ce(lg, y, 255, cw)
+    loss.backward()
+    return {k: v.grad.detach().double().numpy() for k, v in P.items()}
+
+
+@pytest.mark.parametrize("mth", ["f32", "bf16x6"])
+@pytest.mark.parametrize("name", unet3d_fixture_names())
+def test_unet3d_matches_reference(name, mth):
+    d = load(name)
+    meta = d["meta"]
+    K = meta["K"]
+    m = build(d)
+    net = m.backbone if meta.get("lit") else m
+    net.math = mth
+    # remember the plan used (for the saved tensors of the kink-consistent oracle)
+    orig_plan = net._plan
+
+    def _plan(x, td, _o=orig_plan):
+        p = _o(x, td)
+        net._last_plan = p
+        return p
+    net._plan = _plan
+    x = torch.from_numpy(d["x"]).to(DEV)
+    y = torch.from_numpy(d["labels"]).to(DEV)
+    m.train()
+    logits = m(x)
+    if meta.get("lit"):
+        loss = m._weighted_softmax_ce(logits, y, None)
+        conf = m._last_conf
+    else:
+        from innovative3D import _engine as E
+        loss, conf = M._WeightedCE.apply(logits, y, K, 255, None)
+    loss.backward()
+    torch.cuda.synchronize()
+    lg = logits.detach().cpu().numpy()
+    ref = d["logits"]
+    err = float(np.abs(lg - ref).max())
+    print(f"{name}/{mth}: max|dlogit| = {err:.3e}  loss {float(loss):.7f} vs {float(d['loss']):.7f}")
+    assert err <= 1e-3
+    flips = lg.argmax(1) != ref.argmax(1)
+    if flips.any():
+        ties = near_tie_mask(ref, 2 * err)
+        assert not (flips & ~ties).any(), f"{int(flips.sum())} argmax flips outside near-ties"
+    assert math.isclose(float(loss), float(d["loss"]), rel_tol=1e-5)
+    met = M.metrics_from_confusion(conf.cpu().numpy(), K, int(y.numel()))
+    if not flips.any():
+        np.testing.assert_allclose(np.array(met[0]), d["met_dice"], rtol=1e-12, equal_nan=True)
+        np.testing.assert_allclose(np.array(met[3:]), d["met_scalars"], rtol=1e-12, equal_nan=True)
+    # BatchNorm running statistics and num_batches_tracked after the step
+    sd = m.state_dict()
+    for k in d:
+        if k.startswith("bufafter/"):
+            key = k[len("bufafter/"):]
+            np.testing.assert_allclose(sd[key].cpu().numpy(), d[k], rtol=1e-5, atol=1e-6,
+                                       err_msg=key)
+        if k.startswith("nbt/"):
+            assert int(sd[k[len("nbt/"):]]) == int(d[k])
+    # gradients vs the kink-consistent fp64 oracle
+    Bn, Dt = d["x"].shape[0], meta["target_depth"] or d["x"].shape[2]
+    hooks = engine_hooks(net, Bn, Dt, d["x"].shape[3], d["x"].shape[4])
+    g64 = oracle_grads(d, hooks, torch.float64)
+    g32 = oracle_grads(d, hooks, torch.float32)
+    pre = "backbone." if meta.get("lit") else ""
+    named = dict(m.named_parameters())
+    rows, bad = [], []
+    for k, r64 in g64.items():
+        g = named[pre + k].grad.detach().double().cpu().numpy()
+        scale = max(float(np.abs(r64).max()), 1e-12)
+        e_gpu = float(np.abs(g - r64).max()) / scale
+        e_32 = float(np.abs(g32[k] - r64).max()) / scale
+        tol = max(1e-3, 8 * e_32)
+        rows.append((e_gpu, e_32, k))
+        if e_gpu > tol:
+            bad.append(f"{k}: gpu {e_gpu:.2e} vs fp32-oracle {e_32:.2e}")
+    rows.sort(reverse=True)
+    print("\n".join(f"  {k:24s} gpu {a:.2e}  fp32-oracle {b:.2e}" for a, b, k in rows[:5]))
+    assert not bad, "; ".join(bad)
+    # eval mode: normalisation with the updated running statistics
+    m.eval()
+    with torch.no_grad():
+        le = m(x).cpu().numpy()
+    e_eval = float(np.abs(le - d["logits_eval"]).max())
+    print(f"  eval-mode max|dlogit| = {e_eval:.3e}")
+    assert e_eval <= 1e-3
+
+
+def test_unet3d_config3_shape_step():
+    """BASELINE config 3 shape: (4, 1, 5, 96, 96) -> depth adapter 16 -> back; one
+    train step runs, logits finite, loss near ln(K) at init, every grad finite."""
+    torch.manual_seed(0)
+    m = M.LitCicek3DUNet_DepthAdapter_Published(num_classes=13).to(DEV)
+    x = torch.randn(4, 1, 5, 96, 96, device=DEV)
+    y = torch.randint(0, 13, (4, 5, 96, 96), device=DEV)
+    logits = m(x)
+    assert logits.shape == (4, 13, 5, 96, 96)
+    loss = m._weighted_softmax_ce(logits, y, None)
+    loss.backward()
+    assert torch.isfinite(logits).all()
+    assert abs(float(loss) - math.log(13)) < 1.0
+    for n, p in m.named_parameters():
+        assert p.grad is not None and torch.isfinite(p.grad).all(), n
