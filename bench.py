@@ -88,6 +88,146 @@ def cpu_baseline(st, K, base, in_ch, H, W, depth, steps, threads):
                       f"steps after 1 warm-up ({med:.2f} s/step)"}
 
 
+def unet3d_flops(B, D, H, W, K, f=32, cin=1):
+    """Algorithmic fwd+bwd FLOPs of one 3DUNet step at backbone shape B x D x H x W:
+    3x3x3 convs (fwd, input grad except the first conv, weight grad), the 2x2x2
+    ConvTransposes (x3) and the 1x1x1 head (x3, input grad included)."""
+    fl = 0.0
+    chans = [(cin, f), (f, 2 * f), (2 * f, 4 * f), (4 * f, 8 * f), (8 * f, 16 * f),
+             (16 * f, 8 * f), (8 * f, 4 * f), (4 * f, 2 * f), (2 * f, f)]
+    lvls = [0, 1, 2, 3, 4, 3, 2, 1, 0]
+    for i, ((ci, co), l) in enumerate(zip(chans, lvls)):
+        V = B * (D >> l) * (H >> l) * (W >> l)
+        for a, b_ in ((ci, co), (co, co)):
+            mm = 2.0 * V * a * b_ * 27
+            fl += mm * (3 if not (i == 0 and a == ci) else 2)
+    for u in range(4):
+        Vlow = B * (D >> (4 - u)) * (H >> (4 - u)) * (W >> (4 - u))
+        fl += 3 * 2.0 * Vlow * (16 * f >> u) * 8 * (8 * f >> u)
+    fl += 3 * 2.0 * B * D * H * W * f * K
+    return fl
+
+
+def bench_unet3d(args, world, rank, device):
+    """BASELINE configs[2]: the 3DUNet variant (Cicek3DUNet + depth adapter,
+    registry "3DUNet") on batch 4 x 1 x 5 x 96 x 96 per GPU: train-mode forward,
+    the wrapper's weighted CE, backward (optimizer excluded, as in the headline
+    metric).  N > 1: batch data parallelism (per-replica BatchNorm statistics,
+    as DDP without SyncBN), global valid count, gradient all-reduce."""
+    import innovative3D.models as M
+    from innovative3D.weightgen import synth_state
+    from innovative3D.synthetic import synthetic_batch
+    from innovative3D.distributed import allreduce_gradients, global_valid_count
+    K, Bt, D0, HW = args.classes, 4, 5, 96
+    m = M.LitCicek3DUNet_DepthAdapter_Published(num_classes=K)
+    sd = m.state_dict()
+    st = synth_state([(k, tuple(v.shape)) for k, v in sd.items()], seed=0)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in st.items()})
+    m = m.to(device).train()
+    m.backbone.math = args.math
+    x, y = synthetic_batch(Bt, 1, D0, HW, HW, K, ignore_frac=0.01, seed=1000 + rank, device=device)
+    params = list(m.parameters())
+
+    def step():
+        for q in params:
+            q.grad = None
+        logits = m(x)
+        cnt = global_valid_count(y, 255) if world > 1 else None
+        from innovative3D.models import _WeightedCE
+        loss, _conf = _WeightedCE.apply(logits, y, K, 255, None) if cnt is None else \
+            _weighted_ce_global(logits, y, K, cnt)
+        loss.backward()
+        allreduce_gradients(params)
+        return loss
+
+    def _weighted_ce_global(logits, y_, K_, cnt):
+        from innovative3D import _engine as E
+
+        class _F(torch.autograd.Function):
+            @staticmethod
+            def forward(ctx, lg):
+                lcl = lg.permute(0, 2, 3, 4, 1).contiguous()
+                out4, dl, conf = E.weighted_ce_forward(lcl, y_, K_, 255, None, count_override=cnt)
+                ctx.dl = dl
+                return out4[0]
+
+            @staticmethod
+            def backward(ctx, g):
+                E.scale_(ctx.dl, g.reshape(1))
+                return ctx.dl.permute(0, 4, 1, 2, 3)
+        return _F.apply(logits), None
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    vox = Bt * D0 * HW * HW
+    value = world * vox * args.steps / elapsed
+    fl = unet3d_flops(Bt, 16, HW, HW, K)
+    out = {
+        "metric": "voxels/sec fwd+bwd, 3DUNet variant (Cicek3DUNet + depth adapter 5->16->5), "
+                  "1-ch 5x96x96 patches",
+        "value": value, "unit": "voxels/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "conv_math": args.math,
+        "data": "synthetic (x~N(0,1), labels U[0,K) with 1% ignore=255; weights from weightgen seed 0)",
+        "config": {"workload": f"3DUNet fwd+weighted CE+bwd, batch {Bt} x 1ch x {D0} x {HW} x {HW} "
+                               f"per GPU (backbone at 16 x {HW} x {HW}), K={K}, base 32, "
+                               "BatchNorm train mode (BASELINE configs[2])",
+                   "global_batch": Bt * world, "shape": [Bt, 1, D0, HW, HW],
+                   "parallelism": f"dp{world}"},
+        "loss": float(loss.item()),
+        "backbone_voxels_per_s": value * 16 / D0,
+        "step_tflops": fl * world * args.steps / elapsed / 1e12 / world,
+        "algorithmic_flops_per_step": fl,
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and args.cpu_baseline == "auto":
+        out["cpu_baseline"] = cpu_baseline_unet3d(st, K, args.cpu_steps)
+        out["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline_unet3d(st, K, steps):
+    """unet3d_oracle (PyTorch-CPU restatement of the reference) fwd + weighted CE + bwd."""
+    from oracle import unet3d_oracle as U
+    from innovative3D.synthetic import synthetic_batch
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    threads = min(threads, os.cpu_count() or threads)
+    torch.set_num_threads(threads)
+    P, B = U.params_from_state(st)
+    cfg = U.UNet3DCfg(num_classes=K, base=32, in_ch=1, target_depth=16)
+    x, y = synthetic_batch(4, 1, 5, 96, 96, K, ignore_frac=0.01, seed=123)
+    times = []
+    for i in range(steps + 1):
+        t0 = time.perf_counter()
+        U.fwd_bwd(P, B, x, y, cfg)
+        if i > 0:
+            times.append(time.perf_counter() - t0)
+    med = statistics.median(times)
+    return {"value": 4 * 5 * 96 * 96 / med, "unit": "voxels/s", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": f"unet3d_oracle fwd+weighted CE+bwd on the full 4x1x5x96x96 batch; "
+                      f"median of {steps} steps after 1 warm-up ({med:.2f} s/step)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -102,10 +242,11 @@ def main():
     ap.add_argument("--math", choices=("f32", "bf16x6", "bf16x3"), default="bf16x6",
                     help="conv arithmetic: bf16x6 = fp32 operands split exactly into 3 bf16 "
                          "planes, 6 products, fp32 accumulate (fp32 accuracy class; default)")
-    ap.add_argument("--workload", choices=("patch128", "volume512"), default="patch128",
+    ap.add_argument("--workload", choices=("patch128", "volume512", "unet3d"), default="patch128",
                     help="patch128 = the headline (BASELINE configs[1]): batch data parallelism; "
                          "volume512 = BASELINE configs[3]: one 5 x (64 N) x 512 x 512 volume "
-                         "depth-sharded over the N ranks (64-slice slab per rank, RCCL halos)")
+                         "depth-sharded over the N ranks (64-slice slab per rank, RCCL halos); "
+                         "unet3d = BASELINE configs[2]: the 3DUNet variant, batch 4 x 1 x 5 x 96^2")
     ap.add_argument("--slab-depth", type=int, default=64)
     ap.add_argument("--hw", type=int, default=512)
     ap.add_argument("--cpu-depth", type=int, default=32)
@@ -121,6 +262,9 @@ def main():
     torch.cuda.set_device(device)
     if world > 1:
         dist.init_process_group("nccl", device_id=device)
+
+    if args.workload == "unet3d":
+        return bench_unet3d(args, world, rank, device)
 
     from innovative3D.distributed import DataParallelSPFF
     from innovative3D.synthetic import synthetic_batch

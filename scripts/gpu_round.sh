@@ -12,6 +12,7 @@ for step in "$@"; do
     tests) timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -s --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1; rc=$? ;;
     smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$? ;;
     bench) timeout -k 10 600 python bench.py --steps 3 --warmup 1 --cpu-steps 1 > gpurun_out/bench_quick.log 2>&1; rc=$? ;;
+    benchu3d) timeout -k 10 600 python bench.py --workload unet3d --steps 10 --warmup 3 > gpurun_out/bench_unet3d.log 2>&1; rc=$? ;;
     bench512) timeout -k 10 900 python bench.py --workload volume512 --steps 3 --warmup 1 > gpurun_out/bench512.log 2>&1; rc=$? ;;
     benchfull) timeout -k 10 900 python bench.py > gpurun_out/bench.log 2>&1; rc=$? ;;
     prof) (cd "$GRAFT_REPO_ROOT" && timeout -k 10 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --cpu-baseline skip > gpurun_out/prof.log 2>&1); rc=$? ;;
