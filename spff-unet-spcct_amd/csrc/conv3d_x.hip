@@ -125,7 +125,7 @@ constexpr size_t xt_lds_bytes() {
 template <int BN, int KD, int NS, int MB, int NW>
 __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
     Src2 x, const uint4* __restrict__ wp, Dst2 y, Vol vol, int Cin, int nkc, int Cout, int npad,
-    int tilesD, int tilesH, int tilesW) {
+    int tilesD, int tilesH, int tilesW, float* __restrict__ part, int kps) {
   constexpr int XT_THREADS = NW * 64;
   constexpr int TD = XT_D, TH = NW * MB, TW = XT_W;
   constexpr int HH = TH + 2, HWD = TW + 2;
@@ -240,17 +240,21 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
     }
   };
 
-  fetch(0);
+  // split-K (small volumes): this workgroup reduces chunks [kc0, kc1) only and
+  // writes fp32 partial sums that k_splitk_reduce adds in a fixed order
+  const int kc0 = part ? blockIdx.z * kps : 0;
+  const int kc1 = part ? min(nkc, kc0 + kps) : nkc;
+  fetch(kc0);
 #pragma unroll
   for (int k = 0; k < RH; ++k) split_one(k);
   // the second-dispatched half of the workgroup loses every issue arbitration
   // on its SIMD: one static priority bump (MI355X_MICROARCH "two waves per SIMD")
   if (SPFF_XPRIO && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
-  for (int kc = 0; kc < nkc; ++kc) {
-    if (kc) __syncthreads();
+  for (int kc = kc0; kc < kc1; ++kc) {
+    if (kc != kc0) __syncthreads();
     stash(kc);
     __syncthreads();  // (vmcnt(0): the weight DMA has landed)
-    if (kc + 1 < nkc) fetch(kc + 1);
+    if (kc + 1 < kc1) fetch(kc + 1);
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       // split one prefetched halo float4 per tap pair from the middle of the
@@ -315,6 +319,11 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
       for (int nb = 0; nb < NB; ++nb) {
         const int n = n0 + nb * 32 + l32;
         if (n >= Cout) continue;
+        if (part) {
+          part[((int64_t)blockIdx.z * ((int64_t)vol.B * D * H * W) + vox) * npad + n] =
+              acc[mb][nb][r];
+          continue;
+        }
         float* p = n < y.split ? y.p0 + vox * y.ld0 + n : y.p1 + vox * y.ld1 + (n - y.split);
         *p = acc[mb][nb][r];
       }
@@ -322,9 +331,25 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
   }
 }
 
+// y[v][n] = sum over the nsplit partial slabs part[z][v][n], z in order
+__global__ void k_splitk_reduce(const float* __restrict__ part, int nsplit, int64_t V, int npad,
+                                int N, Dst2 y) {
+  const int64_t total = V * N;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int n = (int)(i % N);
+    const int64_t v = i / N;
+    float acc = 0.f;
+    for (int z = 0; z < nsplit; ++z) acc += part[((int64_t)z * V + v) * npad + n];
+    float* p = n < y.split ? y.p0 + v * y.ld0 + n : y.p1 + v * y.ld1 + (n - y.split);
+    *p = acc;
+  }
+}
+
 template <int BN, int KD, int NS, int MB, int NW = 8>
 static hipError_t launch_fwd_x(const Src2& x, const uint4* wx, const Dst2& y, Vol vol, int K,
-                               int nkc, int N, int npad, hipStream_t s) {
+                               int nkc, int N, int npad, hipStream_t s, float* part = nullptr,
+                               int nsplit = 1, int kps = 0) {
   constexpr size_t shm = xt_lds_bytes<BN, KD, NS, NW * MB>();
   static_assert(shm <= (NW == 8 ? 160 : 80) * 1024, "LDS budget");
   auto kern = k_conv3d_fwd_x<BN, KD, NS, MB, NW>;
@@ -336,9 +361,14 @@ static hipError_t launch_fwd_x(const Src2& x, const uint4* wx, const Dst2& y, Vo
     attr = true;
   }
   const int tilesD = cdiv(vol.D, XT_D), tilesH = cdiv(vol.H, NW * MB), tilesW = cdiv(vol.W, XT_W);
-  dim3 grid(vol.B * tilesD * tilesH * tilesW, npad / BN);
+  dim3 grid(vol.B * tilesD * tilesH * tilesW, npad / BN, part ? nsplit : 1);
   hipLaunchKernelGGL(kern, grid, dim3(NW * 64), shm, s, x, wx, y, vol, K, nkc, N, npad, tilesD,
-                     tilesH, tilesW);
+                     tilesH, tilesW, part, part ? kps : nkc);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || !part) return e;
+  const int64_t total = nvox(vol) * N;
+  hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)std::min<int64_t>((total + 255) / 256, 8192)),
+                     dim3(256), 0, s, part, nsplit, nvox(vol), npad, N, y);
   return hipGetLastError();
 }
 
@@ -369,7 +399,25 @@ int debug_split_dir() {
 bool use_split(Vol vol, int math, bool dgrad) {
   const int dbg = debug_split_dir();
   if (dbg && dbg != (dgrad ? 2 : 1)) return false;
-  return math != SPFF_MATH_F32 && vol.H >= XT_H && vol.W >= XT_W;
+  return math != SPFF_MATH_F32;
+}
+// split-K for launches that would not fill the chip (the deep levels of the
+// 3DUNet: 2 x 12 x 12 and 1 x 6 x 6 voxels with 256-512 channels): the input
+// channel chunks are divided over grid.z so that >= ~512 workgroups run
+struct SplitK {
+  int nsplit = 1, kps = 0;
+};
+SplitK splitk_plan(Vol vol, const XDims& d) {
+  SplitK k;
+  k.kps = d.nkc;
+  const int64_t wgs = (int64_t)vol.B * cdiv(vol.D, XT_D) * cdiv(vol.H, XT_H) * cdiv(vol.W, XT_W) *
+                      (d.npad / d.BN);
+  if (wgs >= 256 || d.nkc < 4) return k;
+  int ns = (int)std::min<int64_t>(d.nkc / 2, (512 + wgs - 1) / wgs);
+  ns = std::max(1, ns);
+  k.kps = cdiv(d.nkc, ns);
+  k.nsplit = cdiv(d.nkc, k.kps);
+  return k;
 }
 }  // namespace
 
@@ -405,23 +453,40 @@ hipError_t conv3d_pack(const float* w, void* wpack, Vol vol, int KD, int Cin_w, 
 
 template <int NS>
 static hipError_t run_x(const Src2& x, const uint4* wu, const Dst2& y, Vol vol, int KD,
-                        const XDims& d, hipStream_t s) {
+                        const XDims& d, hipStream_t s, float* ws) {
   // (MB = 4, 1024-voxel tiles for Cout <= 32, fits LDS but spills 91 VGPRs at NS = 3)
   // (NW = 4 waves, 2 x 8 x 16 tiles, BN 32, two workgroups per CU: measured 6 % slower)
+  SplitK k = ws ? splitk_plan(vol, d) : SplitK{1, d.nkc};
+  float* part = k.nsplit > 1 ? ws : nullptr;
   if (d.BN == 64)
-    return KD == 3 ? launch_fwd_x<64, 3, NS, 2>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s)
-                   : launch_fwd_x<64, 1, NS, 2>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s);
-  return KD == 3 ? launch_fwd_x<32, 3, NS, 2>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s)
-                 : launch_fwd_x<32, 1, NS, 2>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s);
+    return KD == 3
+               ? launch_fwd_x<64, 3, NS, 2>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s, part,
+                                            k.nsplit, k.kps)
+               : launch_fwd_x<64, 1, NS, 2>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s, part,
+                                            k.nsplit, k.kps);
+  return KD == 3 ? launch_fwd_x<32, 3, NS, 2>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s, part,
+                                              k.nsplit, k.kps)
+                 : launch_fwd_x<32, 1, NS, 2>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s, part,
+                                              k.nsplit, k.kps);
+}
+
+size_t conv3d_splitk_bytes(Vol vol, int KD, int Cin, int Cout) {
+  size_t b = 0;
+  for (int dg = 0; dg < 2; ++dg) {
+    const XDims d = xdims(KD, Cin, Cout, dg != 0);
+    const SplitK k = splitk_plan(vol, d);
+    if (k.nsplit > 1) b = std::max(b, (size_t)k.nsplit * nvox(vol) * d.npad * sizeof(float));
+  }
+  return b;
 }
 
 hipError_t conv3d_run(const Src2& x, const void* wpack, const Dst2& y, Vol vol, int KD,
-                      int Cin_w, int Cout_w, bool dgrad, int math, hipStream_t s) {
+                      int Cin_w, int Cout_w, bool dgrad, int math, hipStream_t s, float* ws) {
   const XDims d = xdims(KD, Cin_w, Cout_w, dgrad);
   if (use_split(vol, math, dgrad)) {
     const uint4* wu = static_cast<const uint4*>(wpack);
-    return math == SPFF_MATH_BF16X3 ? run_x<2>(x, wu, y, vol, KD, d, s)
-                                    : run_x<3>(x, wu, y, vol, KD, d, s);
+    return math == SPFF_MATH_BF16X3 ? run_x<2>(x, wu, y, vol, KD, d, s, ws)
+                                    : run_x<3>(x, wu, y, vol, KD, d, s, ws);
   }
   return conv3d_fwd(x, static_cast<const float*>(wpack), y, vol, KD, d.K, rup(d.K, 8), d.N,
                     rup(d.N, conv3d_bn(d.N)), s);

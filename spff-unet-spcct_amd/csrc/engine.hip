@@ -340,6 +340,8 @@ int build_plan(spff_plan* p) {
     bcd = std::max(bcd, bcdz);
     wg = std::max(wg, conv3d_wgrad_ws_bytes(v, p->KD, b.Cin, b.C));
     wg = std::max(wg, conv3d_wgrad_ws_bytes(v, p->KD, b.C, b.C));
+    wg = std::max(wg, conv3d_splitk_bytes(v, p->KD, b.Cin, b.C));
+    wg = std::max(wg, conv3d_splitk_bytes(v, p->KD, b.C, b.C));
     wt = std::max(wt, conv_pack_bytes(b.c1, p->KD));
     wt = std::max(wt, conv_pack_bytes(b.c2, p->KD));
   }
@@ -486,7 +488,7 @@ int fwd_block(spff_plan* p, Blk& b, const Src2& in) {
   CK(halo_src(p, in, v));
   const double V = (double)nvox(v), T = 9.0 * KD;
   PROFB(p, 0, 2.0 * V * b.Cin * C * T, cbytes(V, b.Cin, C, T),
-       conv3d_run(in, p->F(p->wt), dst1(p->F(b.y1), C), v, KD, b.Cin, C, false, math, p->st));
+       conv3d_run(in, p->F(p->wt), dst1(p->F(b.y1), C), v, KD, b.Cin, C, false, math, p->st, p->F(p->wg_ws)));
   CK(in_stats(p, v, C, b.y1, b.mean1, b.rstd1, b.al1, b.de1, b.g1, b.b1));
   HIPCK(act_apply(p->F(b.y1), p->F(b.a1), p->F(b.al1), p->F(b.de1), nullptr, nullptr, v, C,
                   p->st));
@@ -494,7 +496,7 @@ int fwd_block(spff_plan* p, Blk& b, const Src2& in) {
   CK(halo(p, p->F(b.a1), v, C));
   PROFB(p, 0, 2.0 * V * C * C * T, cbytes(V, C, C, T),
        conv3d_run(src1(p->F(b.a1), C), p->F(p->wt), dst1(p->F(b.y2), C), v, KD, C, C, false,
-                  math, p->st));
+                  math, p->st, p->F(p->wg_ws)));
   CK(in_stats(p, v, C, b.y2, b.mean2, b.rstd2, b.al2, b.de2, b.g2, b.b2));
   if (b.tail()) {
     RedArgs a{};
@@ -570,7 +572,7 @@ int bwd_block(spff_plan* p, Blk& b, const float* dout, const Dst2* dx, const Src
   HIPCK(conv3d_pack(p->P(b.c2.w), p->F(p->wt), v, KD, C, C, true, math, p->st));
   CK(halo(p, dy2, v, C));
   PROFB(p, 1, 2.0 * V * C * C * T, cbytes(V, C, C, T),
-       conv3d_run(src1(dy2, C), p->F(p->wt), dst1(da1, C), v, KD, C, C, true, math, p->st));
+       conv3d_run(src1(dy2, C), p->F(p->wt), dst1(da1, C), v, KD, C, C, true, math, p->st, p->F(p->wg_ws)));
   {
     RedArgs a{};
     a.y = p->F(b.y1); a.g = da1; a.mean = p->F(b.mean1); a.rstd = p->F(b.rstd1);
@@ -588,7 +590,7 @@ int bwd_block(spff_plan* p, Blk& b, const float* dout, const Dst2* dx, const Src
     HIPCK(conv3d_pack(p->P(b.c1.w), p->F(p->wt), v, KD, b.Cin, C, true, math, p->st));
     CK(halo(p, da1, v, C));
     PROFB(p, 1, 2.0 * V * b.Cin * C * T, cbytes(V, b.Cin, C, T),
-          conv3d_run(src1(da1, C), p->F(p->wt), *dx, v, KD, b.Cin, C, true, math, p->st));
+          conv3d_run(src1(da1, C), p->F(p->wt), *dx, v, KD, b.Cin, C, true, math, p->st, p->F(p->wg_ws)));
   }
   return SPFF_OK;
 }

@@ -52,8 +52,12 @@ int conv3d_bn(int Cout);        // output-channel tile the fwd kernel uses
 size_t conv3d_pack_bytes(int KD, int Cin_w, int Cout_w);
 hipError_t conv3d_pack(const float* w, void* wpack, Vol vol, int KD, int Cin_w, int Cout_w,
                        bool dgrad, int math, hipStream_t s);
+// ws (optional, >= conv3d_splitk_bytes): scratch for split-K partial sums on
+// launches that would not fill the chip; null = no split
 hipError_t conv3d_run(const Src2& x, const void* wpack, const Dst2& y, Vol vol, int KD,
-                      int Cin_w, int Cout_w, bool dgrad, int math, hipStream_t s);
+                      int Cin_w, int Cout_w, bool dgrad, int math, hipStream_t s,
+                      float* ws = nullptr);
+size_t conv3d_splitk_bytes(Vol vol, int KD, int Cin_w, int Cout_w);
 // dW partials + reduction into reference layout dw[Cout][Cin][KD][3][3].
 // math = SPFF_MATH_F32: fp32 MFMA kernel (conv3d.hip); otherwise the split-bf16
 // kernel of conv3d_wgx.hip.  ws >= conv3d_wgrad_ws_bytes (covers both).

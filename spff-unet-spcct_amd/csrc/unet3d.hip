@@ -198,6 +198,8 @@ int build(spff_unet3d* p) {
     red_out = std::max(red_out, (size_t)B * b.C * v.D * 2 * sizeof(float));
     wg = std::max(wg, conv3d_wgrad_ws_bytes(v, 3, b.Cin, b.C));
     wg = std::max(wg, conv3d_wgrad_ws_bytes(v, 3, b.C, b.C));
+    wg = std::max(wg, conv3d_splitk_bytes(v, 3, b.Cin, b.C));
+    wg = std::max(wg, conv3d_splitk_bytes(v, 3, b.C, b.C));
     wt = std::max(wt, conv3d_pack_bytes(3, b.Cin, b.C));
     wt = std::max(wt, conv3d_pack_bytes(3, b.C, b.C));
   }
@@ -262,13 +264,13 @@ int fwd_block(spff_unet3d* p, UBlk& b, const Src2& in, bool training) {
   const Vol& v = p->vol[b.lvl];
   const int C = b.C, math = p->cfg.math;
   UHIPCK(conv3d_pack(p->P(b.w1), p->F(p->wt), v, 3, b.Cin, C, false, math, p->st));
-  UHIPCK(conv3d_run(in, p->F(p->wt), dst1(p->F(b.y1), C), v, 3, b.Cin, C, false, math, p->st));
+  UHIPCK(conv3d_run(in, p->F(p->wt), dst1(p->F(b.y1), C), v, 3, b.Cin, C, false, math, p->st, p->F(p->wg_ws)));
   UCK(bn_fwd(p, v, C, b.y1, b.mean1, b.rstd1, b.al1, b.de1, b.g1, b.b1, b.rm1, b.rv1, training));
   UHIPCK(act_apply(p->F(b.y1), p->F(b.a1), p->F(b.al1), p->F(b.de1), nullptr, nullptr, v, C,
                    p->st, 0.f));
   UHIPCK(conv3d_pack(p->P(b.w2), p->F(p->wt), v, 3, C, C, false, math, p->st));
   UHIPCK(conv3d_run(src1(p->F(b.a1), C), p->F(p->wt), dst1(p->F(b.y2), C), v, 3, C, C, false,
-                    math, p->st));
+                    math, p->st, p->F(p->wg_ws)));
   UCK(bn_fwd(p, v, C, b.y2, b.mean2, b.rstd2, b.al2, b.de2, b.g2, b.b2, b.rm2, b.rv2, training));
   UHIPCK(act_apply(p->F(b.y2), p->F(b.out), p->F(b.al2), p->F(b.de2), nullptr, nullptr, v, C,
                    p->st, 0.f));
@@ -298,12 +300,12 @@ int bwd_block(spff_unet3d* p, UBlk& b, const float* dout, const Dst2* dx, const 
   UHIPCK(conv3d_wgrad(src1(p->F(b.a1), C), dy2, C, p->DP(b.w2), v, 3, C, C, math,
                       p->F(p->wg_ws), p->st));
   UHIPCK(conv3d_pack(p->P(b.w2), p->F(p->wt), v, 3, C, C, true, math, p->st));
-  UHIPCK(conv3d_run(src1(dy2, C), p->F(p->wt), dst1(da1, C), v, 3, C, C, true, math, p->st));
+  UHIPCK(conv3d_run(src1(dy2, C), p->F(p->wt), dst1(da1, C), v, 3, C, C, true, math, p->st, p->F(p->wg_ws)));
   UCK(bn_bwd(p, v, C, b.y1, da1, da1, b.mean1, b.rstd1, b.al1, b.de1, b.g1, b.b1));
   UHIPCK(conv3d_wgrad(in, da1, C, p->DP(b.w1), v, 3, b.Cin, C, math, p->F(p->wg_ws), p->st));
   if (dx) {
     UHIPCK(conv3d_pack(p->P(b.w1), p->F(p->wt), v, 3, b.Cin, C, true, math, p->st));
-    UHIPCK(conv3d_run(src1(da1, C), p->F(p->wt), *dx, v, 3, b.Cin, C, true, math, p->st));
+    UHIPCK(conv3d_run(src1(da1, C), p->F(p->wt), *dx, v, 3, b.Cin, C, true, math, p->st, p->F(p->wg_ws)));
   }
   return SPFF_OK;
 }
