@@ -33,6 +33,12 @@
 #include <cstdlib>
 #include <cstring>
 
+#ifndef SPFF_XDIAG
+#define SPFF_XDIAG 0  // timing diagnostics only: 1 = no restaging, 2 = no MFMA loop
+#endif
+#ifndef SPFF_XIGLP
+#define SPFF_XIGLP -1
+#endif
 #ifndef SPFF_XPRIO
 #define SPFF_XPRIO 1
 #endif
@@ -252,11 +258,12 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
   if (SPFF_XPRIO && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
   for (int kc = kc0; kc < kc1; ++kc) {
     if (kc != kc0) __syncthreads();
-    stash(kc);
+    if (SPFF_XDIAG != 1 || kc == kc0) stash(kc);
     __syncthreads();  // (vmcnt(0): the weight DMA has landed)
     if (kc + 1 < kc1) fetch(kc + 1);
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
+    for (int j = 0; j < (SPFF_XDIAG == 2 ? 0 : NJ); ++j) {
+      if constexpr (SPFF_XIGLP >= 0) __builtin_amdgcn_iglp_opt(SPFF_XIGLP);
       // split one prefetched halo float4 per tap pair from the middle of the
       // chunk on; the fences keep this VALU (and its vmcnt wait) in place
       // while MFMAs and LDS reads may still move across
