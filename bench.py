@@ -347,8 +347,29 @@ def main():
                              "profiles/r01_pmc_conv.json, same bench config)"),
             "per_class_ms_per_step": {k: v[0] / args.steps for k, v in prof.items()},
             "per_class_tflops": {k: (v[1] / (v[0] * 1e-3) / 1e12 if v[0] > 0 else None)
-                                 for k, v in prof.items()},
+                                 for k, v in prof.items() if k not in plan.MEM_CLASSES},
             "step_tflops": value / world * 2462016 / 1e12}
+    # the HBM-bound passes (each judged on its own algorithmic bytes =
+    # operands read once + result written once), timed live like the conv kernels
+    mem = {}
+    tb = tm = 0.0
+    for k in plan.MEM_CLASSES:
+        ms_k, _f, n_k, by = prof[k]
+        if ms_k > 0:
+            gbs = by / (ms_k * 1e-3) / 1e9
+            mem[k] = {"achieved_GBps": gbs, "frac": gbs / HBM_PEAK_GBS, "launches": int(n_k),
+                      "algorithmic_bytes_per_launch": by / max(1, n_k),
+                      "ms_per_step": ms_k / args.steps}
+            tb += by
+            tm += ms_k
+    roof["memory_bound"] = {
+        "peak_GBps": HBM_PEAK_GBS, "kernels": mem,
+        "aggregate": {"achieved_GBps": tb / (tm * 1e-3) / 1e9 if tm else None,
+                      "frac": (tb / (tm * 1e-3) / 1e9 / HBM_PEAK_GBS) if tm else None},
+        "note": ("slab_reduce = per-(b,c,d) hw-reductions (IN statistics, gate sums; C*4 B per "
+                 "input tensor per voxel, incl. the split combine); act_apply = IN/gate apply "
+                 "(8*C B/voxel); in_bwd_apply = IN backward apply (12*C B/voxel); HIP events "
+                 "on the engine stream")}
     if sharded:
         cfg = {"workload": f"SPFF-UNet fwd+ce_plus_macro_dice+bwd, one 1 x {args.in_ch}ch x "
                            f"{Dl * world} x {HW} x {HW} volume depth-sharded into {world} x "

@@ -110,11 +110,14 @@ int spff_saved_tensor(const spff_plan* plan, void* workspace, const char* name,
 /* debug knobs (tests): key 0 = stop the backward after N decoder blocks (-1 off) */
 int spff_debug_set(spff_plan* plan, int key, int value);
 
-/* optional HIP-event timing of the MFMA kernels on the plan's stream (bench.py):
+/* optional HIP-event timing of the engine's kernels on the plan's stream (bench.py):
  * classes 0 = conv3d fwd, 1 = conv3d dgrad (same kernel), 2 = conv3d wgrad,
- * 3 = ConvTranspose / 1x1 head GEMMs.  collect() syncs on the recorded events
- * and writes out[4*c + {0,1,2,3}] = {total ms, algorithmic FLOPs, launches,
- * compulsory HBM bytes (operands read once, result written once; conv classes)}. */
+ * 3 = ConvTranspose / 1x1 head GEMMs, and the HBM-bound passes 4 = per-(b,c,d)
+ * slab reductions (IN statistics, gate sums; incl. the split combine),
+ * 5 = IN/gate apply (act_apply), 6 = IN backward apply (in_bwd_apply).
+ * collect() syncs on the recorded events and writes out[4*c + {0,1,2,3}] =
+ * {total ms, algorithmic FLOPs, launches, algorithmic HBM bytes (operands read
+ * once, result written once)}. */
 int spff_prof_enable(spff_plan* plan, int on);
 int spff_prof_collect(spff_plan* plan, double* out, int nclass);
 

@@ -442,7 +442,8 @@ int in_stats(spff_plan* p, const Vol& v, int C, size_t y, size_t mean, size_t rs
   const bool sh = p->co.on();
   double* pd = sh ? p->D64(p->part_d) : nullptr;
   const double N = (double)p->co.D_glob * v.H * v.W;
-  HIPCK(slab_reduce(RED_SUM, a, v, C, p->F(p->red_out), p->F(p->red_ws), p->st));
+  PROFB(p, 4, 0.0, 4.0 * (double)nvox(v) * C,
+        slab_reduce(RED_SUM, a, v, C, p->F(p->red_out), p->F(p->red_ws), p->st));
   if (sh) {  // per-(b,c) sums over the slab -> group sum -> global mean
     HIPCK(in_partial(p->F(p->red_out), pd, v, C, 1, p->st));
     HIPCK(p->co.sum_f64(pd, (int64_t)v.B * C, p->st));
@@ -451,7 +452,8 @@ int in_stats(spff_plan* p, const Vol& v, int C, size_t y, size_t mean, size_t rs
     HIPCK(in_mean(p->F(p->red_out), p->F(mean), v, C, p->st));
   }
   a.mean = p->F(mean);
-  HIPCK(slab_reduce(RED_SQDEV, a, v, C, p->F(p->red_out), p->F(p->red_ws), p->st));
+  PROFB(p, 4, 0.0, 4.0 * (double)nvox(v) * C,
+        slab_reduce(RED_SQDEV, a, v, C, p->F(p->red_out), p->F(p->red_ws), p->st));
   if (sh) {
     HIPCK(in_partial(p->F(p->red_out), pd, v, C, 1, p->st));
     HIPCK(p->co.sum_f64(pd, (int64_t)v.B * C, p->st));
@@ -490,7 +492,8 @@ int fwd_block(spff_plan* p, Blk& b, const Src2& in) {
   PROFB(p, 0, 2.0 * V * b.Cin * C * T, cbytes(V, b.Cin, C, T),
        conv3d_run(in, p->F(p->wt), dst1(p->F(b.y1), C), v, KD, b.Cin, C, false, math, p->st, p->F(p->wg_ws)));
   CK(in_stats(p, v, C, b.y1, b.mean1, b.rstd1, b.al1, b.de1, b.g1, b.b1));
-  HIPCK(act_apply(p->F(b.y1), p->F(b.a1), p->F(b.al1), p->F(b.de1), nullptr, nullptr, v, C,
+  PROFB(p, 5, 0.0, 8.0 * (double)nvox(v) * C,
+        act_apply(p->F(b.y1), p->F(b.a1), p->F(b.al1), p->F(b.de1), nullptr, nullptr, v, C,
                   p->st));
   HIPCK(conv3d_pack(p->P(b.c2.w), p->F(p->wt), v, KD, C, C, false, math, p->st));
   CK(halo(p, p->F(b.a1), v, C));
@@ -503,17 +506,20 @@ int fwd_block(spff_plan* p, Blk& b, const Src2& in) {
     a.y = p->F(b.y2);
     a.al = p->F(b.al2);
     a.de = p->F(b.de2);
-    HIPCK(slab_reduce(RED_ACT, a, v, C, p->F(b.Sa), p->F(p->red_ws), p->st));
+    PROFB(p, 4, 0.0, 4.0 * (double)nvox(v) * C,
+        slab_reduce(RED_ACT, a, v, C, p->F(b.Sa), p->F(p->red_ws), p->st));
     GateParams gp = gate_params(p, b);
     GateSaved sv = gate_saved(p, b);
     if (p->co.on())
       HIPCK(gates_fwd_sh(gp, p->F(b.Sa), sv, v, C, p->F(p->gscr), p->co, p->st));
     else
       HIPCK(gates_fwd(gp, p->F(b.Sa), sv, v, C, p->F(p->gscr), p->st));
-    HIPCK(act_apply(p->F(b.y2), p->F(b.out), p->F(b.al2), p->F(b.de2), p->F(b.P), p->F(b.Q), v,
+    PROFB(p, 5, 0.0, 8.0 * (double)nvox(v) * C,
+        act_apply(p->F(b.y2), p->F(b.out), p->F(b.al2), p->F(b.de2), p->F(b.P), p->F(b.Q), v,
                     C, p->st));
   } else {
-    HIPCK(act_apply(p->F(b.y2), p->F(b.out), p->F(b.al2), p->F(b.de2), nullptr, nullptr, v, C,
+    PROFB(p, 5, 0.0, 8.0 * (double)nvox(v) * C,
+        act_apply(p->F(b.y2), p->F(b.out), p->F(b.al2), p->F(b.de2), nullptr, nullptr, v, C,
                     p->st));
   }
   return SPFF_OK;
@@ -530,7 +536,8 @@ int bwd_block(spff_plan* p, Blk& b, const float* dout, const Dst2* dx, const Src
     a.g = dout;
     a.al = p->F(b.al2);
     a.de = p->F(b.de2);
-    HIPCK(slab_reduce(RED_BWD_TAIL, a, v, C, p->F(p->red_out), p->F(p->red_ws), p->st));
+    PROFB(p, 4, 0.0, 8.0 * (double)nvox(v) * C,
+        slab_reduce(RED_BWD_TAIL, a, v, C, p->F(p->red_out), p->F(p->red_ws), p->st));
     GateParams gp = gate_params(p, b);
     GateSaved sv = gate_saved(p, b);
     GateGrads gg;
@@ -559,9 +566,11 @@ int bwd_block(spff_plan* p, Blk& b, const float* dout, const Dst2* dx, const Src
     RedArgs a{};
     a.y = p->F(b.y2); a.g = dout; a.mean = p->F(b.mean2); a.rstd = p->F(b.rstd2);
     a.al = p->F(b.al2); a.de = p->F(b.de2); a.A = A; a.Bc = Bc;
-    HIPCK(slab_reduce(RED_BWD_IN, a, v, C, p->F(p->red_out), p->F(p->red_ws), p->st));
+    PROFB(p, 4, 0.0, 8.0 * (double)nvox(v) * C,
+        slab_reduce(RED_BWD_IN, a, v, C, p->F(p->red_out), p->F(p->red_ws), p->st));
     CK(in_bwd(p, v, C, b.g2, b.b2));
-    HIPCK(in_bwd_apply(p->F(b.y2), dout, dy2, p->F(b.mean2), p->F(b.rstd2), p->F(b.al2),
+    PROFB(p, 6, 0.0, 12.0 * (double)nvox(v) * C,
+          in_bwd_apply(p->F(b.y2), dout, dy2, p->F(b.mean2), p->F(b.rstd2), p->F(b.al2),
                        p->F(b.de2), p->P(b.g2), A, Bc, p->F(p->kk1), p->F(p->kk2), v, C, p->st));
   }
   const double V = (double)nvox(v), T = 9.0 * KD;
@@ -577,9 +586,11 @@ int bwd_block(spff_plan* p, Blk& b, const float* dout, const Dst2* dx, const Src
     RedArgs a{};
     a.y = p->F(b.y1); a.g = da1; a.mean = p->F(b.mean1); a.rstd = p->F(b.rstd1);
     a.al = p->F(b.al1); a.de = p->F(b.de1);
-    HIPCK(slab_reduce(RED_BWD_IN, a, v, C, p->F(p->red_out), p->F(p->red_ws), p->st));
+    PROFB(p, 4, 0.0, 8.0 * (double)nvox(v) * C,
+        slab_reduce(RED_BWD_IN, a, v, C, p->F(p->red_out), p->F(p->red_ws), p->st));
     CK(in_bwd(p, v, C, b.g1, b.b1));
-    HIPCK(in_bwd_apply(p->F(b.y1), da1, da1, p->F(b.mean1), p->F(b.rstd1), p->F(b.al1),
+    PROFB(p, 6, 0.0, 12.0 * (double)nvox(v) * C,
+          in_bwd_apply(p->F(b.y1), da1, da1, p->F(b.mean1), p->F(b.rstd1), p->F(b.al1),
                        p->F(b.de1), p->P(b.g1), nullptr, nullptr, p->F(p->kk1), p->F(p->kk2), v,
                        C, p->st));
   }

@@ -291,7 +291,9 @@ class Plan:
                                   _stream(dlogits_cl.device)), "spff_backward")
         return dflat
 
-    PROF_CLASSES = ("conv_fwd", "conv_dgrad", "conv_wgrad", "gemm")
+    PROF_CLASSES = ("conv_fwd", "conv_dgrad", "conv_wgrad", "gemm", "slab_reduce", "act_apply",
+                    "in_bwd_apply")
+    MEM_CLASSES = ("slab_reduce", "act_apply", "in_bwd_apply")
 
     def prof_enable(self, on: bool = True):
         check(lib().spff_prof_enable(self._h, int(bool(on))), "spff_prof_enable")
