@@ -131,7 +131,8 @@ constexpr size_t xt_lds_bytes() {
 template <int BN, int KD, int NS, int MB, int NW>
 __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
     Src2 x, const uint4* __restrict__ wp, Dst2 y, Vol vol, int Cin, int nkc, int Cout, int npad,
-    int tilesD, int tilesH, int tilesW, float* __restrict__ part, int kps) {
+    int tilesD, int tilesH, int tilesW, float* __restrict__ part, int kps,
+    float* __restrict__ stats) {
   constexpr int XT_THREADS = NW * 64;
   constexpr int TD = XT_D, TH = NW * MB, TW = XT_W;
   constexpr int HH = TH + 2, HWD = TW + 2;
@@ -336,6 +337,132 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
       }
     }
   }
+
+  // ---- fused InstanceNorm statistics of this output (replaces two HBM passes):
+  // per (tile, channel) the sum over the tile's valid voxels and the sum of
+  // squared deviations about the tile mean; merged per (b, c) in a fixed order
+  // by k_in_stats_fin (Chan).  stats[(tile*npad + n)*2 + {0,1}], count[tile].
+  if (stats) {
+    __syncthreads();  // every wave is past its last LDS operand read
+    float* sred = reinterpret_cast<float*>(lds4);  // [NW][NB][32]
+    const int nd = min(D - d0, TD), nh = min(H - h0, TH), nwv = min(W - w0, TW);
+    const float cnt = (float)(nd * nh * nwv);
+    bool ok[MB][16];
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        int td, th, tw;
+        vrow(wave * MB + mb, (r & 3) + 8 * (r >> 2) + 4 * khalf, td, th, tw);
+        ok[mb][r] = d0 + td < D && h0 + th < H && w0 + tw < W;
+      }
+    float tsum[NB], mu[NB];
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      float sacc = 0.f;
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sacc += ok[mb][r] ? acc[mb][nb][r] : 0.f;
+      sacc += __shfl_xor(sacc, 32);
+      if (!khalf) sred[(wave * NB + nb) * 32 + l32] = sacc;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      float t = 0.f;
+      for (int w = 0; w < NW; ++w) t += sred[(w * NB + nb) * 32 + l32];
+      tsum[nb] = t;
+      mu[nb] = t / cnt;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      float qacc = 0.f;
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float dl = acc[mb][nb][r] - mu[nb];
+          qacc += ok[mb][r] ? dl * dl : 0.f;
+        }
+      qacc += __shfl_xor(qacc, 32);
+      if (!khalf) sred[(wave * NB + nb) * 32 + l32] = qacc;
+    }
+    __syncthreads();
+    if (wave == 0 && !khalf) {
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) {
+        float q = 0.f;
+        for (int w = 0; w < NW; ++w) q += sred[(w * NB + nb) * 32 + l32];
+        const int n = n0 + nb * 32 + l32;
+        if (n < Cout) {
+          stats[((int64_t)blockIdx.x * npad + n) * 2 + 0] = tsum[nb];
+          stats[((int64_t)blockIdx.x * npad + n) * 2 + 1] = q;
+        }
+      }
+    }
+    if (tid == 0 && blockIdx.y == 0)
+      stats[(int64_t)gridDim.x * npad * 2 + blockIdx.x] = cnt;
+  }
+}
+
+// InstanceNorm3d statistics from the conv's per-tile partials (see the fused
+// epilogue above).  One workgroup per (b, c): in fp64, the sample mean from the
+// tile sums, then M2 = sum_t [M2_t + n_t (mean_t - mean)^2] (the exact
+// decomposition of the squared deviations), each a strided per-thread sum plus
+// a fixed-order LDS tree -> mean, rstd = 1/sqrt(var + eps), al = gamma*rstd,
+// de = beta - mean*al (the outputs of slab_reduce + in_mean + in_rstd).
+__global__ __launch_bounds__(256) void k_in_stats_fin(const float* __restrict__ stats, int ntiles,
+                                                      int tpb, int npad, int C,
+                                                      const float* __restrict__ gamma,
+                                                      const float* __restrict__ beta,
+                                                      float* __restrict__ mean,
+                                                      float* __restrict__ rstd,
+                                                      float* __restrict__ al,
+                                                      float* __restrict__ de) {
+  __shared__ double r0[256], r1[256];
+  const int bc = blockIdx.x, b = bc / C, c = bc % C, tid = threadIdx.x;
+  const float* cnt = stats + (int64_t)ntiles * npad * 2;
+  double s = 0.0, n = 0.0;
+  for (int t = b * tpb + tid; t < (b + 1) * tpb; t += 256) {
+    s += stats[((int64_t)t * npad + c) * 2];
+    n += cnt[t];
+  }
+  r0[tid] = s;
+  r1[tid] = n;
+  __syncthreads();
+  for (int st = 128; st > 0; st >>= 1) {
+    if (tid < st) {
+      r0[tid] += r0[tid + st];
+      r1[tid] += r1[tid + st];
+    }
+    __syncthreads();
+  }
+  const double N = r1[0], mu = r0[0] / N;
+  __syncthreads();
+  double q = 0.0;
+  for (int t = b * tpb + tid; t < (b + 1) * tpb; t += 256) {
+    const double nt = cnt[t];
+    if (nt <= 0.0) continue;
+    const double dl = stats[((int64_t)t * npad + c) * 2] / nt - mu;
+    q += stats[((int64_t)t * npad + c) * 2 + 1] + nt * dl * dl;
+  }
+  r0[tid] = q;
+  __syncthreads();
+  for (int st = 128; st > 0; st >>= 1) {
+    if (tid < st) r0[tid] += r0[tid + st];
+    __syncthreads();
+  }
+  if (tid == 0) {
+    const float rs = (float)(1.0 / sqrt(r0[0] / N + 1e-5));
+    const float m = (float)mu;
+    mean[bc] = m;
+    rstd[bc] = rs;
+    const float a = gamma[c] * rs;
+    al[bc] = a;
+    de[bc] = beta[c] - m * a;
+  }
 }
 
 // y[v][n] = sum over the nsplit partial slabs part[z][v][n], z in order
@@ -356,7 +483,7 @@ __global__ void k_splitk_reduce(const float* __restrict__ part, int nsplit, int6
 template <int BN, int KD, int NS, int MB, int NW = 8>
 static hipError_t launch_fwd_x(const Src2& x, const uint4* wx, const Dst2& y, Vol vol, int K,
                                int nkc, int N, int npad, hipStream_t s, float* part = nullptr,
-                               int nsplit = 1, int kps = 0) {
+                               int nsplit = 1, int kps = 0, float* stats = nullptr) {
   constexpr size_t shm = xt_lds_bytes<BN, KD, NS, NW * MB>();
   static_assert(shm <= (NW == 8 ? 160 : 80) * 1024, "LDS budget");
   auto kern = k_conv3d_fwd_x<BN, KD, NS, MB, NW>;
@@ -370,7 +497,7 @@ static hipError_t launch_fwd_x(const Src2& x, const uint4* wx, const Dst2& y, Vo
   const int tilesD = cdiv(vol.D, XT_D), tilesH = cdiv(vol.H, NW * MB), tilesW = cdiv(vol.W, XT_W);
   dim3 grid(vol.B * tilesD * tilesH * tilesW, npad / BN, part ? nsplit : 1);
   hipLaunchKernelGGL(kern, grid, dim3(NW * 64), shm, s, x, wx, y, vol, K, nkc, N, npad, tilesD,
-                     tilesH, tilesW, part, part ? kps : nkc);
+                     tilesH, tilesW, part, part ? kps : nkc, part ? nullptr : stats);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || !part) return e;
   const int64_t total = nvox(vol) * N;
@@ -460,7 +587,7 @@ hipError_t conv3d_pack(const float* w, void* wpack, Vol vol, int KD, int Cin_w, 
 
 template <int NS>
 static hipError_t run_x(const Src2& x, const uint4* wu, const Dst2& y, Vol vol, int KD,
-                        const XDims& d, hipStream_t s, float* ws) {
+                        const XDims& d, hipStream_t s, float* ws, float* stats) {
   // (MB = 4, 1024-voxel tiles for Cout <= 32, fits LDS but spills 91 VGPRs at NS = 3)
   // (NW = 4 waves, 2 x 8 x 16 tiles, BN 32, two workgroups per CU: measured 6 % slower)
   SplitK k = ws ? splitk_plan(vol, d) : SplitK{1, d.nkc};
@@ -468,13 +595,13 @@ static hipError_t run_x(const Src2& x, const uint4* wu, const Dst2& y, Vol vol, 
   if (d.BN == 64)
     return KD == 3
                ? launch_fwd_x<64, 3, NS, 2>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s, part,
-                                            k.nsplit, k.kps)
+                                            k.nsplit, k.kps, stats)
                : launch_fwd_x<64, 1, NS, 2>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s, part,
-                                            k.nsplit, k.kps);
+                                            k.nsplit, k.kps, stats);
   return KD == 3 ? launch_fwd_x<32, 3, NS, 2>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s, part,
-                                              k.nsplit, k.kps)
+                                              k.nsplit, k.kps, stats)
                  : launch_fwd_x<32, 1, NS, 2>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s, part,
-                                              k.nsplit, k.kps);
+                                              k.nsplit, k.kps, stats);
 }
 
 size_t conv3d_splitk_bytes(Vol vol, int KD, int Cin, int Cout) {
@@ -487,13 +614,38 @@ size_t conv3d_splitk_bytes(Vol vol, int KD, int Cin, int Cout) {
   return b;
 }
 
+// fused IN statistics: per (tile, out channel) {sum, M2} + a count per tile
+static int64_t xt_ntiles(Vol vol) {
+  return (int64_t)vol.B * cdiv(vol.D, XT_D) * cdiv(vol.H, XT_H) * cdiv(vol.W, XT_W);
+}
+size_t conv3d_stats_bytes(Vol vol, int KD, int Cin, int Cout) {
+  const XDims d = xdims(KD, Cin, Cout, false);
+  return (size_t)xt_ntiles(vol) * (2 * d.npad + 1) * sizeof(float);
+}
+bool conv3d_fuses_stats(Vol vol, int KD, int Cin, int Cout, int math) {
+  const XDims d = xdims(KD, Cin, Cout, false);
+  return use_split(vol, math, false) && vol.dh == 0 && splitk_plan(vol, d).nsplit == 1;
+}
+hipError_t conv3d_in_stats_fin(const float* stats, Vol vol, int KD, int Cin, int Cout,
+                               const float* gamma, const float* beta, float* mean, float* rstd,
+                               float* al, float* de, hipStream_t s) {
+  const XDims d = xdims(KD, Cin, Cout, false);
+  const int64_t nt = xt_ntiles(vol);
+  hipLaunchKernelGGL(k_in_stats_fin, dim3(vol.B * Cout), dim3(256), 0, s, stats, (int)nt,
+                     (int)(nt / vol.B), d.npad, Cout, gamma, beta, mean, rstd, al, de);
+  return hipGetLastError();
+}
+
 hipError_t conv3d_run(const Src2& x, const void* wpack, const Dst2& y, Vol vol, int KD,
-                      int Cin_w, int Cout_w, bool dgrad, int math, hipStream_t s, float* ws) {
+                      int Cin_w, int Cout_w, bool dgrad, int math, hipStream_t s, float* ws,
+                      float* stats) {
   const XDims d = xdims(KD, Cin_w, Cout_w, dgrad);
+  if (stats && (dgrad || !conv3d_fuses_stats(vol, KD, Cin_w, Cout_w, math)))
+    return hipErrorInvalidValue;
   if (use_split(vol, math, dgrad)) {
     const uint4* wu = static_cast<const uint4*>(wpack);
-    return math == SPFF_MATH_BF16X3 ? run_x<2>(x, wu, y, vol, KD, d, s, ws)
-                                    : run_x<3>(x, wu, y, vol, KD, d, s, ws);
+    return math == SPFF_MATH_BF16X3 ? run_x<2>(x, wu, y, vol, KD, d, s, ws, stats)
+                                    : run_x<3>(x, wu, y, vol, KD, d, s, ws, stats);
   }
   return conv3d_fwd(x, static_cast<const float*>(wpack), y, vol, KD, d.K, rup(d.K, 8), d.N,
                     rup(d.N, conv3d_bn(d.N)), s);

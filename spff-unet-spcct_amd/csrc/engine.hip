@@ -107,7 +107,7 @@ struct spff_plan {
   size_t head_pk = 0;
   size_t x_cl = 0, pool[3] = {0, 0, 0}, pidx[3] = {0, 0, 0};
   size_t red_ws = 0, red_out = 0, gscr = 0, Abuf = 0, Bbuf = 0, kk1 = 0, kk2 = 0, wg_ws = 0,
-         wt = 0;
+         wt = 0, cst = 0;
   size_t G_out = 0, G_dy2 = 0, G_da1 = 0, G_dx = 0, dskip[3] = {0, 0, 0};
   size_t part_d = 0;  // sharded plans: fp64 IN partials [B][C][2]
   size_t total = 0;
@@ -305,7 +305,7 @@ int build_plan(spff_plan* p) {
   const Vol& v0 = p->vol[0];
   const auto slice = [&](const Vol& v, int C) { return (size_t)v.H * v.W * C * sizeof(float); };
   p->x_cl = p->alloc_halo(nvox(v0) * p->ldx * sizeof(float), slice(v0, p->ldx));
-  size_t red_ws = 0, red_out = 0, gs = 0, bcd = 0, wg = 0, wt = 0;
+  size_t red_ws = 0, red_out = 0, gs = 0, bcd = 0, wg = 0, wt = 0, cst = 0;
   for (int i = 0; i < 7; ++i) {
     Blk& b = p->blk[i];
     const Vol& v = p->vol[b.lvl];
@@ -344,6 +344,8 @@ int build_plan(spff_plan* p) {
     wg = std::max(wg, conv3d_splitk_bytes(v, p->KD, b.C, b.C));
     wt = std::max(wt, conv_pack_bytes(b.c1, p->KD));
     wt = std::max(wt, conv_pack_bytes(b.c2, p->KD));
+    cst = std::max(cst, conv3d_stats_bytes(v, p->KD, b.Cin, b.C));
+    cst = std::max(cst, conv3d_stats_bytes(v, p->KD, b.C, b.C));
   }
   for (int l = 0; l < 3; ++l) {
     const Vol& vl = p->vol[l + 1];
@@ -369,6 +371,7 @@ int build_plan(spff_plan* p) {
   p->kk2 = p->alloc((size_t)B * 8 * f * sizeof(float));
   p->wg_ws = p->alloc(wg);
   p->wt = p->alloc(wt);
+  p->cst = p->alloc(cst);
   const size_t gbytes = nvox(v0) * f * sizeof(float);  // max over levels of V_l * C_l
   p->G_out = p->alloc(gbytes);
   p->G_dy2 = p->alloc_halo(gbytes, slice(v0, f));  // level-0 slice = the largest
@@ -489,18 +492,31 @@ int fwd_block(spff_plan* p, Blk& b, const Src2& in) {
   HIPCK(conv3d_pack(p->P(b.c1.w), p->F(p->wt), v, KD, b.Cin, C, false, math, p->st));
   CK(halo_src(p, in, v));
   const double V = (double)nvox(v), T = 9.0 * KD;
+  // InstanceNorm statistics fused into the conv epilogue where the split kernel
+  // runs unsharded without split-K; otherwise the two slab_reduce passes
+  const bool fuse1 = !p->co.on() && conv3d_fuses_stats(v, KD, b.Cin, C, math);
   PROFB(p, 0, 2.0 * V * b.Cin * C * T, cbytes(V, b.Cin, C, T),
-       conv3d_run(in, p->F(p->wt), dst1(p->F(b.y1), C), v, KD, b.Cin, C, false, math, p->st, p->F(p->wg_ws)));
-  CK(in_stats(p, v, C, b.y1, b.mean1, b.rstd1, b.al1, b.de1, b.g1, b.b1));
+       conv3d_run(in, p->F(p->wt), dst1(p->F(b.y1), C), v, KD, b.Cin, C, false, math, p->st,
+                  p->F(p->wg_ws), fuse1 ? p->F(p->cst) : nullptr));
+  if (fuse1)
+    HIPCK(conv3d_in_stats_fin(p->F(p->cst), v, KD, b.Cin, C, p->P(b.g1), p->P(b.b1),
+                              p->F(b.mean1), p->F(b.rstd1), p->F(b.al1), p->F(b.de1), p->st));
+  else
+    CK(in_stats(p, v, C, b.y1, b.mean1, b.rstd1, b.al1, b.de1, b.g1, b.b1));
   PROFB(p, 5, 0.0, 8.0 * (double)nvox(v) * C,
         act_apply(p->F(b.y1), p->F(b.a1), p->F(b.al1), p->F(b.de1), nullptr, nullptr, v, C,
                   p->st));
   HIPCK(conv3d_pack(p->P(b.c2.w), p->F(p->wt), v, KD, C, C, false, math, p->st));
   CK(halo(p, p->F(b.a1), v, C));
+  const bool fuse2 = !p->co.on() && conv3d_fuses_stats(v, KD, C, C, math);
   PROFB(p, 0, 2.0 * V * C * C * T, cbytes(V, C, C, T),
        conv3d_run(src1(p->F(b.a1), C), p->F(p->wt), dst1(p->F(b.y2), C), v, KD, C, C, false,
-                  math, p->st, p->F(p->wg_ws)));
-  CK(in_stats(p, v, C, b.y2, b.mean2, b.rstd2, b.al2, b.de2, b.g2, b.b2));
+                  math, p->st, p->F(p->wg_ws), fuse2 ? p->F(p->cst) : nullptr));
+  if (fuse2)
+    HIPCK(conv3d_in_stats_fin(p->F(p->cst), v, KD, C, C, p->P(b.g2), p->P(b.b2), p->F(b.mean2),
+                              p->F(b.rstd2), p->F(b.al2), p->F(b.de2), p->st));
+  else
+    CK(in_stats(p, v, C, b.y2, b.mean2, b.rstd2, b.al2, b.de2, b.g2, b.b2));
   if (b.tail()) {
     RedArgs a{};
     a.y = p->F(b.y2);
@@ -804,6 +820,12 @@ int spff_saved_tensor(const spff_plan* p, void* ws, const char* name, const floa
     if (n == b.name + ".a1") return ret(b.a1, v, b.C);
     if (n == b.name + ".y2") return ret(b.y2, v, b.C);
     if (n == b.name + ".out") return ret(b.out, v, b.C);
+    // per-(b,c) normalisation of the IN that follows conv 1 / 2: r = y*al + de
+    const Vol bv{v.B, 1, 1, 1};
+    if (n == b.name + ".al1") return ret(b.al1, bv, b.C);
+    if (n == b.name + ".de1") return ret(b.de1, bv, b.C);
+    if (n == b.name + ".al2") return ret(b.al2, bv, b.C);
+    if (n == b.name + ".de2") return ret(b.de2, bv, b.C);
   }
   for (int l = 0; l < 3; ++l)
     if (n == "pool" + std::to_string(l + 1)) return ret(p->pool[l], p->vol[l + 1], p->f << l);

@@ -54,9 +54,18 @@ hipError_t conv3d_pack(const float* w, void* wpack, Vol vol, int KD, int Cin_w, 
                        bool dgrad, int math, hipStream_t s);
 // ws (optional, >= conv3d_splitk_bytes): scratch for split-K partial sums on
 // launches that would not fill the chip; null = no split
+// stats (optional, forward only, when conv3d_fuses_stats): the conv's epilogue also
+// writes per-tile InstanceNorm partials (>= conv3d_stats_bytes) that
+// conv3d_in_stats_fin turns into mean / rstd / al / de, replacing the two
+// slab_reduce passes of the unfused path.
 hipError_t conv3d_run(const Src2& x, const void* wpack, const Dst2& y, Vol vol, int KD,
                       int Cin_w, int Cout_w, bool dgrad, int math, hipStream_t s,
-                      float* ws = nullptr);
+                      float* ws = nullptr, float* stats = nullptr);
+bool conv3d_fuses_stats(Vol vol, int KD, int Cin, int Cout, int math);
+size_t conv3d_stats_bytes(Vol vol, int KD, int Cin, int Cout);
+hipError_t conv3d_in_stats_fin(const float* stats, Vol vol, int KD, int Cin, int Cout,
+                               const float* gamma, const float* beta, float* mean, float* rstd,
+                               float* al, float* de, hipStream_t s);
 size_t conv3d_splitk_bytes(Vol vol, int KD, int Cin_w, int Cout_w);
 // dW partials + reduction into reference layout dw[Cout][Cin][KD][3][3].
 // math = SPFF_MATH_F32: fp32 MFMA kernel (conv3d.hip); otherwise the split-bf16

@@ -130,7 +130,7 @@ def engine_lrelu_masks(core, d):
     """Sign pattern of every LeakyReLU input, and the argmax of every max-pool
     window, as the ENGINE saw them (the pools: from its saved pool inputs; ties
     resolved first-max like the engine and torch).  The LeakyReLUs: the engine's
-    saved conv outputs y1/y2, normalised in fp64.  A fp32 conv differs from the
+    saved conv outputs y1/y2 under its own per-(b,c) affine (al, de).  A fp32 conv differs from the
     reference's by ~1e-6 relative, so an input sitting within that of the kink
     (|r| ~ 0) can take the other slope (1 vs 0.01) -- a legitimate fp32 outcome
     the reference could equally produce.  Feeding the engine's pattern to the
@@ -150,7 +150,19 @@ def engine_lrelu_masks(core, d):
             y = y.view(B, Dd, Hh_, Ww, C).permute(0, 4, 1, 2, 3)
             g = torch.from_numpy(st[f"{blk}.{tag}.1.weight"]).double()
             bb = torch.from_numpy(st[f"{blk}.{tag}.1.bias"]).double()
-            masks[f"{blk}.{tag}"] = F.instance_norm(y, weight=g, bias=bb, eps=1e-5) > 0
+            m64 = F.instance_norm(y, weight=g, bias=bb, eps=1e-5) > 0
+            # the engine's own fp32 normalisation r = fma(y, al, de): its sign is the
+            # sign of the exact y*al + de, which fp64 reproduces
+            j = "1" if key == "y1" else "2"
+            al = plan.saved(f"{blk}.al{j}").double().cpu().reshape(B, C, 1, 1, 1)
+            de = plan.saved(f"{blk}.de{j}").double().cpu().reshape(B, C, 1, 1, 1)
+            # contiguous: this torch build's CPU instance_norm backward is wrong for a
+            # channels-last-strided grad_output, which torch.where would propagate
+            m = ((y * al + de) > 0).contiguous()
+            nd = int((m != m64).sum())
+            if nd:
+                print(f"  {blk}.{tag}: {nd} knife-edge signs (engine affine vs fp64 IN)")
+            masks[f"{blk}.{tag}"] = m
     # max-pool windows: the engine's own first-max argmax over its pool inputs
     Dd = d["x"].shape[2]
     for k, blk in enumerate(("enc1", "enc2", "enc3")):
@@ -159,7 +171,7 @@ def engine_lrelu_masks(core, d):
         C = y.shape[1]
         y = y.view(B, Dd, Hh_, Ww, C).permute(0, 4, 1, 2, 3)
         v = y.reshape(B, C, Dd, Hh_ // 2, 2, Ww // 2, 2).permute(0, 1, 2, 3, 5, 4, 6)
-        masks[f"pool{k + 1}"] = v.reshape(B, C, Dd, Hh_ // 2, Ww // 2, 4).argmax(-1)
+        masks[f"pool{k + 1}"] = v.reshape(B, C, Dd, Hh_ // 2, Ww // 2, 4).argmax(-1).contiguous()
     return masks
 
 
