@@ -223,6 +223,53 @@ int spff_loss_ex(const float* logits, const int64_t* labels, int64_t nvox, int n
                  const float* class_weights, int clamp_denominator, float* out4,
                  float* dlogits, int64_t* conf, void* ws, void* stream);
 
+/* ------------------------------------------------------------------------
+ * SwinUNETR variant (BASELINE config 5; registry "SwinUNETR", config.py:366-386
+ * -> LitSwinUNETR_Published / SwinUNETR_Published, models.py:858-982, i.e.
+ * MONAI 1.5.2 SwinUNETR).  Replaces SwinUNETR_Published.forward
+ * (models.py:877) and its autograd backward, and LitSwinUNETR_Published._loss
+ * (models.py:910-928).  Parameters: a flat fp32 buffer in MONAI's state-dict
+ * order / names without the "model.model." prefix (spff_swin_param_info);
+ * the relative_position_index buffers are not needed.  D, H, W must be
+ * multiples of 32.  Parity is unpinned (MONAI is not available offline);
+ * semantics in oracle/swin_oracle.py.
+ * ------------------------------------------------------------------------ */
+typedef struct spff_swin_cfg {
+  int batch, in_ch, depth, height, width;  /* input [B][Cin][D][H][W], Cin <= 8 */
+  int num_classes;   /* K (<= 32) */
+  int feature_size;  /* 12 on the registry path */
+  int window;        /* MONAI window_size (7: the registry's (2,2,2) never reaches MONAI) */
+  int heads[4];      /* (1, 2, 4, 8) */
+  float mlp_ratio;   /* 2.0 */
+  int math;          /* SPFF_MATH_* for the 3x3x3 convolutions */
+  int reserved[6];   /* zero */
+} spff_swin_cfg;
+
+typedef struct spff_swin spff_swin;
+
+int spff_swin_create(const spff_swin_cfg* cfg, spff_swin** out);
+void spff_swin_destroy(spff_swin* net);
+int spff_swin_num_params(const spff_swin* net);
+int spff_swin_param_info(const spff_swin* net, int i, const char** name, int* ndim,
+                         int64_t shape[5], int64_t* offset, int64_t* numel);
+int64_t spff_swin_param_floats(const spff_swin* net);
+size_t spff_swin_workspace_bytes(const spff_swin* net);
+/* forward: x [B][Cin][D][H][W] -> logits [B][D][H][W][K] (channel-last) */
+int spff_swin_forward(spff_swin* net, const float* x, const float* params, float* logits,
+                      void* workspace, void* stream);
+/* backward of the last forward: dlogits [B][D][H][W][K] -> dparams (every entry written) */
+int spff_swin_backward(spff_swin* net, const float* dlogits, const float* params,
+                       float* dparams, void* workspace, void* stream);
+int spff_swin_saved_tensor(const spff_swin* net, void* workspace, const char* name,
+                           const float** ptr, int64_t* rows, int* channels);
+/* (1 - ce_weight) * soft-Dice loss (classes >= 1 unless include_bg) + ce_weight * CE
+ * (ignore_index), LitSwinUNETR_Published._loss: out4 = [ce, loss, dice_loss, N_valid],
+ * dlogits [V][K] = dloss/dlogits.  ws >= spff_swin_loss_ws_bytes device bytes. */
+size_t spff_swin_loss_ws_bytes(int batch, int num_classes);
+int spff_swin_loss(const float* logits, const int64_t* labels, int batch, int64_t vox_per_sample,
+                   int num_classes, int ignore_index, int include_bg, double ce_weight,
+                   float* out4, float* dlogits, void* ws, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

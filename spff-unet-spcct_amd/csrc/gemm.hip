@@ -89,6 +89,94 @@ struct StoreUp {  // C[m][n], n = ij*Cout + co -> y[high(m,ij)*Cout + co] + bias
   __device__ void put(int64_t idx, float v) const { p[idx] = v; }
 };
 
+// --- Linear-layer functors (SwinUNETR path, swin.hip) ---
+struct LoadRows2 {  // A[m][k] from a two-source channel view (torch.cat([p0, p1], C))
+  Src2 x; int kmax; int64_t M;
+  __device__ int64_t prep(int64_t m) const { return m < M ? m : -1; }
+  __device__ float4 load4(int64_t m, int k) const {
+    if (m < 0 || k >= kmax) return make_float4(0.f, 0.f, 0.f, 0.f);
+    const float* q = k < x.split ? x.p0 + m * x.ld0 + k : x.p1 + m * x.ld1 + (k - x.split);
+    return *reinterpret_cast<const float4*>(q);
+  }
+};
+// Patch-embedding gather (Conv3d(Cin, f, k = s = 2)): row m = output voxel of the
+// half-resolution grid, k = (ci*2 + kd)*4 + kh*2 + kw (PyTorch's weight flattening)
+// of the channel-last input x[b][D][H][W][ld]
+struct LoadPatch {
+  const float* x; int ld, Cin, D, H, W; int64_t M;  // D, H, W: full resolution
+  __device__ int64_t prep(int64_t m) const {
+    if (m >= M) return -1;
+    const int Wl = W >> 1, Hl = H >> 1, Dl = D >> 1;
+    int64_t t = m;
+    const int w = (int)(t % Wl); t /= Wl;
+    const int h = (int)(t % Hl); t /= Hl;
+    const int d = (int)(t % Dl);
+    const int64_t b = t / Dl;
+    return ((b * D + 2 * d) * H + 2 * h) * (int64_t)W + 2 * w;  // full-res voxel of tap 0
+  }
+  __device__ float4 load4(int64_t v, int k) const {
+    float r[4] = {0.f, 0.f, 0.f, 0.f};
+    if (v >= 0) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int kk = k + j, ci = kk >> 3, t = kk & 7;
+        if (ci < Cin) {
+          const int64_t off = (((int64_t)(t >> 2) * H + ((t >> 1) & 1)) * W + (t & 1));
+          r[j] = x[(v + off) * ld + ci];
+        }
+      }
+    }
+    return make_float4(r[0], r[1], r[2], r[3]);
+  }
+};
+struct StoreRowsRes {  // y[m][n] = res[m][n] + v + bias[n]   (residual add)
+  float* p; const float* res; int ld, ldr, nmax; const float* bias; int64_t M;
+  __device__ int64_t prep(int64_t m) const { return m < M ? (m << 16) : -1; }
+  __device__ int64_t col(int n) const { return n < nmax ? n : -1; }
+  __device__ float bias_of(int n) const { return (bias && n < nmax) ? bias[n] : 0.f; }
+  __device__ void put(int64_t idx, float v) const {
+    const int64_t m = idx >> 16;
+    const int n = (int)(idx & 0xffff);
+    p[m * ld + n] = (res ? res[m * ldr + n] : 0.f) + v;
+  }
+};
+__device__ __forceinline__ float gelu_erf(float x) {
+  return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
+}
+__device__ __forceinline__ float gelu_erf_grad(float x) {
+  const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
+  return cdf + x * 0.39894228040143268f * expf(-0.5f * x * x);
+}
+struct StoreGelu {  // pre[m][n] = v + bias[n]; act[m][n] = gelu(pre)  (nn.GELU, erf form)
+  float* pre; float* act; int ld, nmax; const float* bias; int64_t M;
+  __device__ int64_t prep(int64_t m) const { return m < M ? m * ld : -1; }
+  __device__ int64_t col(int n) const { return n < nmax ? n : -1; }
+  __device__ float bias_of(int n) const { return (bias && n < nmax) ? bias[n] : 0.f; }
+  __device__ void put(int64_t idx, float v) const {
+    pre[idx] = v;
+    act[idx] = gelu_erf(v);
+  }
+};
+struct StoreGeluBwd {  // dpre[m][n] = v * gelu'(pre[m][n])
+  float* p; const float* pre; int ld, nmax; int64_t M;
+  __device__ int64_t prep(int64_t m) const { return m < M ? m * ld : -1; }
+  __device__ int64_t col(int n) const { return n < nmax ? n : -1; }
+  __device__ float bias_of(int) const { return 0.f; }
+  __device__ void put(int64_t idx, float v) const { p[idx] = v * gelu_erf_grad(pre[idx]); }
+};
+struct StoreDst2 {  // C[m][n] -> dst (two-source channel view), optionally accumulated
+  Dst2 y; int nmax; int acc; int64_t M;
+  __device__ int64_t prep(int64_t m) const { return m < M ? (m << 16) : -1; }
+  __device__ int64_t col(int n) const { return n < nmax ? n : -1; }
+  __device__ float bias_of(int) const { return 0.f; }
+  __device__ void put(int64_t idx, float v) const {
+    const int64_t m = idx >> 16;
+    const int n = (int)(idx & 0xffff);
+    float* q = n < y.split ? y.p0 + m * y.ld0 + n : y.p1 + m * y.ld1 + (n - y.split);
+    *q = acc ? *q + v : v;
+  }
+};
+
 // ---------------------------------------------------------------- C = A.B --
 // Tile 128 rows x BN cols (BN <= 128: every column of a ConvT / head GEMM up to
 // 128 wide in one workgroup, so A is read once), 4 waves each 32 rows x BN,
@@ -624,6 +712,85 @@ size_t head_wgrad_ws_bytes(int64_t V, int Cin, int K) { return xty_ws_bytes(V, C
 hipError_t head_wgrad(const float* x, const float* dy, float* dw, float* db, int64_t V, int Cin,
                       int K, float* ws, hipStream_t s) {
   return launch_xty(x, Cin, Cin, dy, K, K, nullptr, V, K, 1, dw, db, ws, s);
+}
+
+// ------------------------------------------------------- linear layers --
+// nn.Linear / 1x1x1 Conv3d on channel-last rows: y = x W^T + b with W [N][K]
+// (PyTorch layout), packed by head_pack(w, wf, wd, K, N) (wf = W^T, wd = W).
+hipError_t linear_fwd(const float* x, int ldx, int K, const float* wf, const float* b, float* y,
+                      int ldy, int N, int64_t M, const float* res, int ldres, hipStream_t s) {
+  if (K > 65535 || N > 65535) return hipErrorInvalidValue;
+  LoadRowsVec A{x, ldx, K, M};
+  StoreRowsRes C{y, res, ldy, ldres, N, b, M};
+  return launch_gemm(A, wf, C, M, head_fk(K), head_fn(N), s);
+}
+hipError_t linear_fwd2(const Src2& x, int K, const float* wf, const float* b, float* y, int ldy,
+                       int N, int64_t M, hipStream_t s) {
+  LoadRows2 A{x, K, M};
+  StoreRowsRes C{y, nullptr, ldy, 0, N, b, M};
+  return launch_gemm(A, wf, C, M, head_fk(K), head_fn(N), s);
+}
+hipError_t linear_fwd_gelu(const float* x, int ldx, int K, const float* wf, const float* b,
+                           float* pre, float* act, int N, int64_t M, hipStream_t s) {
+  LoadRowsVec A{x, ldx, K, M};
+  StoreGelu C{pre, act, N, N, b, M};
+  return launch_gemm(A, wf, C, M, head_fk(K), head_fn(N), s);
+}
+hipError_t patch_embed_fwd(const float* x, int ldx, int Cin, int D, int H, int W, int B,
+                           const float* wf, const float* b, float* y, int N, hipStream_t s) {
+  const int64_t M = (int64_t)B * (D / 2) * (H / 2) * (W / 2);
+  LoadPatch A{x, ldx, Cin, D, H, W, M};
+  StoreRowsRes C{y, nullptr, N, 0, N, b, M};
+  return launch_gemm(A, wf, C, M, head_fk(8 * Cin), head_fn(N), s);
+}
+// dx = dy W  (x [M][K] gradient; dy [M][N]); gelu_pre: dx *= gelu'(pre)
+hipError_t linear_dgrad(const float* dy, int lddy, int N, const float* wd, float* dx, int lddx,
+                        int K, int64_t M, const float* gelu_pre, hipStream_t s) {
+  if (lddy % 4 == 0 && N % 4 == 0) {
+    LoadRowsVec A{dy, lddy, N, M};
+    if (gelu_pre) {
+      StoreGeluBwd C{dx, gelu_pre, lddx, K, M};
+      return launch_gemm(A, wd, C, M, head_dk(N), head_dn(K), s);
+    }
+    StoreRows C{dx, lddx, K, nullptr, M};
+    return launch_gemm(A, wd, C, M, head_dk(N), head_dn(K), s);
+  }
+  LoadRowsScalar A{dy, lddy, N, M};
+  if (gelu_pre) {
+    StoreGeluBwd C{dx, gelu_pre, lddx, K, M};
+    return launch_gemm(A, wd, C, M, head_dk(N), head_dn(K), s);
+  }
+  StoreRows C{dx, lddx, K, nullptr, M};
+  return launch_gemm(A, wd, C, M, head_dk(N), head_dn(K), s);
+}
+// the same into a two-source gradient view, overwriting (acc = 0) or adding (acc = 1)
+hipError_t linear_dgrad2(const float* dy, int lddy, int N, const float* wd, const Dst2& dx, int K,
+                         int64_t M, int acc, hipStream_t s) {
+  LoadRowsScalar A{dy, lddy, N, M};
+  StoreDst2 C{dx, K, acc, M};
+  return launch_gemm(A, wd, C, M, head_dk(N), head_dn(K), s);
+}
+size_t linear_wgrad_ws_bytes(int64_t M, int K, int N) {
+  return std::max(xty_ws_bytes(M, K, N), atb_ws_bytes(M, K, N));
+}
+// dW [N][K] = dy^T x, db [N] = sum dy (db may be null: a scratch column is used)
+hipError_t linear_wgrad(const float* x, int ldx, int K, const float* dy, int lddy, int N,
+                        float* dw, float* db, int64_t M, float* ws, hipStream_t s) {
+  return launch_xty(x, ldx, K, dy, lddy, N, nullptr, M, N, 1, dw, db, ws, s);
+}
+hipError_t linear_wgrad2(const Src2& x, int K, const float* dy, int lddy, int N, float* dw,
+                         float* db, int64_t M, float* ws, hipStream_t s) {
+  LoadRows2 X{x, K, M};
+  LoadRowsScalar Y{dy, lddy, N, M};
+  return launch_atb(X, Y, M, K, N, N, 1, dw, db, ws, s);
+}
+hipError_t patch_embed_wgrad(const float* x, int ldx, int Cin, int D, int H, int W, int B,
+                             const float* dy, int N, float* dw, float* db, float* ws,
+                             hipStream_t s) {
+  const int64_t M = (int64_t)B * (D / 2) * (H / 2) * (W / 2);
+  LoadPatch X{x, ldx, Cin, D, H, W, M};
+  LoadRowsScalar Y{dy, N, N, M};
+  return launch_atb(X, Y, M, 8 * Cin, N, N, 1, dw, db, ws, s);
 }
 
 }  // namespace spff

@@ -19,6 +19,17 @@
 namespace spff {
 
 static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+// voxel lanes per 256-thread block for C/4 channel quads: the largest power of two
+// <= 256 / (C/4), so the fixed-order LDS tree halves evenly (C = 12, 24, 48, ...
+// of the SwinUNETR path leave a few threads idle; powers of two use all 256)
+__host__ __device__ inline int red_vpp(int tpv) {
+  int v = 256 / tpv, p = 1;
+  while (2 * p <= v) p *= 2;
+  return p;
+}
+// elementwise block size: a multiple of C/4, so a thread's channel quad is fixed
+// over its grid-stride loop (256 for power-of-two C)
+static inline int ew_bs(int C) { return (C / 4) * (256 / (C / 4)); }
 // neg = negative slope: 0.01 for LeakyReLU (SPFF), 0 for ReLU (3DUNet)
 __device__ __forceinline__ float lrelu(float r, float neg) { return r > 0.f ? r : neg * r; }
 __device__ __forceinline__ float slope(float r, float neg) { return r > 0.f ? 1.f : neg; }
@@ -31,7 +42,7 @@ RedPlan red_plan(Vol vol, int C) {
   RedPlan p;
   p.HW = vol.H * vol.W;
   p.tpv = C / 4;
-  p.vpp = 256 / p.tpv;
+  p.vpp = red_vpp(p.tpv);
   p.chunk = p.vpp * SPFF_RED_CH;
   p.nsplit = cdiv(p.HW, p.chunk);
   return p;
@@ -45,7 +56,7 @@ __global__ __launch_bounds__(256) void k_slab_reduce(RedArgs a, Vol vol, int C, 
   const int split = blockIdx.x;
   const int b = bd / vol.D, d = bd % vol.D;
   const int HW = vol.H * vol.W;
-  const int tpv = C >> 2, vpp = 256 / tpv;
+  const int tpv = C >> 2, vpp = red_vpp(tpv);
   const int cq = threadIdx.x % tpv, vo = threadIdx.x / tpv;
   const int c = 4 * cq;
   float acc[NQ][4];
@@ -431,7 +442,7 @@ hipError_t bn_bwd_stats(const float* sums, float* dgamma, float* dbeta, float* k
 
 // ------------------------------------------------------------ elementwise --
 // grid.y = b*D + d ; grid.x strides over the (h,w,c/4) float4s of that slab.
-// The stride (gridDim.x * 256) is a multiple of C/4 (C/4 <= 64, power of two),
+// The stride (gridDim.x * ew_bs(C)) is a multiple of C/4 (C/4 <= 64),
 // so a thread's channel quad is fixed: its per-(b,c[,d]) parameters are loaded
 // once into registers, and the loop is pure float4 streaming.
 __global__ __launch_bounds__(256) void k_act_apply(const float* __restrict__ y, float* __restrict__ out,
@@ -463,13 +474,13 @@ __global__ __launch_bounds__(256) void k_act_apply(const float* __restrict__ y, 
 
 static dim3 ew_grid(Vol vol, int C) {
   const int n4 = vol.H * vol.W * (C / 4);
-  int gx = std::min(cdiv(n4, 256), SPFF_EW_GX);
+  int gx = std::min(cdiv(n4, ew_bs(C)), SPFF_EW_GX);
   return dim3(gx, vol.B * vol.D);
 }
 
 hipError_t act_apply(const float* y, float* out, const float* al, const float* de, const float* P,
                      const float* Q, Vol vol, int C, hipStream_t s, float neg) {
-  hipLaunchKernelGGL(k_act_apply, ew_grid(vol, C), dim3(256), 0, s, y, out, al, de, P, Q, vol, C,
+  hipLaunchKernelGGL(k_act_apply, ew_grid(vol, C), dim3(ew_bs(C)), 0, s, y, out, al, de, P, Q, vol, C,
                      neg);
   return hipGetLastError();
 }
@@ -514,7 +525,7 @@ hipError_t in_bwd_apply(const float* y, const float* g, float* dy, const float* 
                         const float* rstd, const float* al, const float* de, const float* gamma,
                         const float* A, const float* Bc, const float* k1, const float* k2, Vol vol,
                         int C, hipStream_t s, float neg) {
-  hipLaunchKernelGGL(k_in_bwd_apply, ew_grid(vol, C), dim3(256), 0, s, y, g, dy, mean, rstd, al,
+  hipLaunchKernelGGL(k_in_bwd_apply, ew_grid(vol, C), dim3(ew_bs(C)), 0, s, y, g, dy, mean, rstd, al,
                      de, gamma, A, Bc, k1, k2, vol, C, neg);
   return hipGetLastError();
 }

@@ -107,6 +107,34 @@ size_t head_wgrad_ws_bytes(int64_t V, int Cin, int K);
 hipError_t head_wgrad(const float* x, const float* dy, float* dw, float* db, int64_t V,
                       int Cin, int K, float* ws, hipStream_t s);
 
+// nn.Linear / 1x1x1 Conv3d on channel-last rows (SwinUNETR path): W [N][K] packed by
+// head_pack(w, wf, wd, K, N) (wf = W^T for the forward, wd = W for dgrad).
+// y = res + x W^T + b (res, b optional); ld* = row pitches in floats.
+hipError_t linear_fwd(const float* x, int ldx, int K, const float* wf, const float* b, float* y,
+                      int ldy, int N, int64_t M, const float* res, int ldres, hipStream_t s);
+hipError_t linear_fwd2(const Src2& x, int K, const float* wf, const float* b, float* y, int ldy,
+                       int N, int64_t M, hipStream_t s);
+// pre = x W^T + b, act = gelu(pre) (erf form, nn.GELU default)
+hipError_t linear_fwd_gelu(const float* x, int ldx, int K, const float* wf, const float* b,
+                           float* pre, float* act, int N, int64_t M, hipStream_t s);
+// Conv3d(Cin, N, kernel = stride = 2) + bias of a channel-last [B][D][H][W][ldx] input
+hipError_t patch_embed_fwd(const float* x, int ldx, int Cin, int D, int H, int W, int B,
+                           const float* wf, const float* b, float* y, int N, hipStream_t s);
+// dx = dy W (gelu_pre: times gelu'(pre))
+hipError_t linear_dgrad(const float* dy, int lddy, int N, const float* wd, float* dx, int lddx,
+                        int K, int64_t M, const float* gelu_pre, hipStream_t s);
+hipError_t linear_dgrad2(const float* dy, int lddy, int N, const float* wd, const Dst2& dx, int K,
+                         int64_t M, int acc, hipStream_t s);
+size_t linear_wgrad_ws_bytes(int64_t M, int K, int N);
+// dW [N][K] = dy^T x, db [N] = column sums of dy (db must be valid memory)
+hipError_t linear_wgrad(const float* x, int ldx, int K, const float* dy, int lddy, int N,
+                        float* dw, float* db, int64_t M, float* ws, hipStream_t s);
+hipError_t linear_wgrad2(const Src2& x, int K, const float* dy, int lddy, int N, float* dw,
+                         float* db, int64_t M, float* ws, hipStream_t s);
+hipError_t patch_embed_wgrad(const float* x, int ldx, int Cin, int D, int H, int W, int B,
+                             const float* dy, int N, float* dw, float* db, float* ws,
+                             hipStream_t s);
+
 // ------------------------------------------------------------- norm/gates --
 // Per-(b,d,c) reductions over (h,w) with per-(b,c) affine/recompute ops.
 enum RedOp {

@@ -42,6 +42,15 @@ class spff_unet3d_cfg(ctypes.Structure):
     ]
 
 
+class spff_swin_cfg(ctypes.Structure):
+    _fields_ = [
+        ("batch", ctypes.c_int), ("in_ch", ctypes.c_int), ("depth", ctypes.c_int),
+        ("height", ctypes.c_int), ("width", ctypes.c_int), ("num_classes", ctypes.c_int),
+        ("feature_size", ctypes.c_int), ("window", ctypes.c_int), ("heads", ctypes.c_int * 4),
+        ("mlp_ratio", ctypes.c_float), ("math", ctypes.c_int), ("reserved", ctypes.c_int * 6),
+    ]
+
+
 # spff_coll (include/spff.h): the shard group's collectives, called back by the engine
 ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                                 ctypes.c_int, ctypes.c_void_p)
@@ -118,6 +127,20 @@ _SIGS = {
     "spff_unet3d_backward": (_I, [_P, _P, _P, _P, _P, _P]),
     "spff_unet3d_saved_tensor": (_I, [_P, _P, ctypes.c_char_p, ctypes.POINTER(_P),
                                       ctypes.POINTER(_L), ctypes.POINTER(_I)]),
+    # SwinUNETR variant (BASELINE config 5)
+    "spff_swin_create": (_I, [ctypes.POINTER(spff_swin_cfg), ctypes.POINTER(_P)]),
+    "spff_swin_destroy": (None, [_P]),
+    "spff_swin_num_params": (_I, [_P]),
+    "spff_swin_param_info": (_I, [_P, _I, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(_I),
+                                  ctypes.POINTER(_L), ctypes.POINTER(_L), ctypes.POINTER(_L)]),
+    "spff_swin_param_floats": (_L, [_P]),
+    "spff_swin_workspace_bytes": (_S, [_P]),
+    "spff_swin_forward": (_I, [_P, _P, _P, _P, _P, _P]),
+    "spff_swin_backward": (_I, [_P, _P, _P, _P, _P, _P]),
+    "spff_swin_saved_tensor": (_I, [_P, _P, ctypes.c_char_p, ctypes.POINTER(_P),
+                                    ctypes.POINTER(_L), ctypes.POINTER(_I)]),
+    "spff_swin_loss_ws_bytes": (_S, [_I, _I]),
+    "spff_swin_loss": (_I, [_P, _P, _I, _L, _I, _I, _I, ctypes.c_double, _P, _P, _P, _P]),
     "spff_loss_ex": (_I, [_P, _P, _L, _I, _I, ctypes.c_double, _P, _P, _I, _P, _P, _P, _P, _P]),
 }
 EXPORTED = tuple(_SIGS)
@@ -449,6 +472,128 @@ def get_unet3d_plan(**kw) -> UNet3DPlan:
         kk.pop("tag", None)
         _UPLANS[key] = UNet3DPlan(**kk)
     return _UPLANS[key]
+
+
+class SwinPlan:
+    """One spff_swin plan (SwinUNETR variant) + its workspace."""
+
+    def __init__(self, batch, in_ch, depth, height, width, num_classes, feature_size=12,
+                 window=7, heads=(1, 2, 4, 8), mlp_ratio=2.0, device=None, math=None):
+        math = math or default_math()
+        if math not in MATH_NAMES:
+            raise SpffError(f"math={math!r}: expected one of {sorted(MATH_NAMES)}")
+        cfg = spff_swin_cfg()
+        cfg.batch, cfg.in_ch, cfg.depth, cfg.height, cfg.width = batch, in_ch, depth, height, width
+        cfg.num_classes, cfg.feature_size, cfg.window = num_classes, feature_size, window
+        for i, h in enumerate(heads):
+            cfg.heads[i] = int(h)
+        cfg.mlp_ratio = float(mlp_ratio)
+        cfg.math = MATH_NAMES[math]
+        self.cfg, self.math, self.device = cfg, math, device
+        L = lib()
+        h = ctypes.c_void_p()
+        check(L.spff_swin_create(ctypes.byref(cfg), ctypes.byref(h)), "spff_swin_create")
+        self._h = h
+        self.params: List[Tuple[str, Tuple[int, ...], int, int]] = []
+        for i in range(L.spff_swin_num_params(h)):
+            name, nd = ctypes.c_char_p(), ctypes.c_int()
+            shape, off, n = (ctypes.c_int64 * 5)(), ctypes.c_int64(), ctypes.c_int64()
+            check(L.spff_swin_param_info(h, i, ctypes.byref(name), ctypes.byref(nd), shape,
+                                         ctypes.byref(off), ctypes.byref(n)),
+                  "spff_swin_param_info")
+            self.params.append((name.value.decode(), tuple(shape[k] for k in range(nd.value)),
+                                off.value, n.value))
+        self.nfloats = int(L.spff_swin_param_floats(h))
+        self.ws_bytes = int(L.spff_swin_workspace_bytes(h))
+        self._ws: Optional[torch.Tensor] = None
+        self.generation = 0
+
+    def __del__(self):
+        try:
+            if getattr(self, "_h", None) is not None and _lib is not None:
+                _lib.spff_swin_destroy(self._h)
+        except Exception:
+            pass
+
+    def workspace(self, device) -> torch.Tensor:
+        if self._ws is None or self._ws.device != device:
+            self._ws = torch.empty(self.ws_bytes, dtype=torch.uint8, device=device)
+        return self._ws
+
+    def forward(self, x: torch.Tensor, flat: torch.Tensor,
+                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """x [B,Cin,D,H,W] fp32 -> logits channel-last [B,D,H,W,K]."""
+        c = self.cfg
+        require_device(x, "SwinUNETR forward")
+        if tuple(x.shape) != (c.batch, c.in_ch, c.depth, c.height, c.width):
+            raise SpffError(f"input shape {tuple(x.shape)} does not match plan")
+        if x.dtype != torch.float32:
+            raise SpffError("the engine computes in fp32; got " + str(x.dtype))
+        x = x.contiguous()
+        if out is None:
+            out = torch.empty((c.batch, c.depth, c.height, c.width, c.num_classes),
+                              dtype=torch.float32, device=x.device)
+        ws = self.workspace(x.device)
+        self.generation += 1
+        check(lib().spff_swin_forward(self._h, _ptr(x), _ptr(flat), _ptr(out), _ptr(ws),
+                                      _stream(x.device)), "spff_swin_forward")
+        return out
+
+    def backward(self, dlogits_cl: torch.Tensor, flat: torch.Tensor,
+                 dflat: Optional[torch.Tensor] = None) -> torch.Tensor:
+        dlogits_cl = dlogits_cl.contiguous()
+        if dflat is None:
+            dflat = torch.empty(self.nfloats, dtype=torch.float32, device=dlogits_cl.device)
+        ws = self.workspace(dlogits_cl.device)
+        check(lib().spff_swin_backward(self._h, _ptr(dlogits_cl), _ptr(flat), _ptr(dflat), _ptr(ws),
+                                       _stream(dlogits_cl.device)), "spff_swin_backward")
+        return dflat
+
+    def saved(self, name: str) -> torch.Tensor:
+        ws = self._ws
+        if ws is None:
+            raise SpffError("no forward has run")
+        ptr, nv, ch = ctypes.c_void_p(), ctypes.c_int64(), ctypes.c_int()
+        check(lib().spff_swin_saved_tensor(self._h, _ptr(ws), name.encode(), ctypes.byref(ptr),
+                                           ctypes.byref(nv), ctypes.byref(ch)),
+              "spff_swin_saved_tensor")
+        off = ptr.value - ws.data_ptr()
+        n = nv.value * ch.value
+        return ws[off:off + 4 * n].view(torch.float32).view(nv.value, ch.value).clone()
+
+
+_SPLANS: Dict[tuple, SwinPlan] = {}
+
+
+def get_swin_plan(**kw) -> SwinPlan:
+    key = (kw["batch"], kw["in_ch"], kw["depth"], kw["height"], kw["width"], kw["num_classes"],
+           kw.get("feature_size", 12), kw.get("window", 7), tuple(kw.get("heads", (1, 2, 4, 8))),
+           float(kw.get("mlp_ratio", 2.0)), kw.get("math") or default_math(), kw.get("tag", ""))
+    if key not in _SPLANS:
+        kk = dict(kw)
+        kk.pop("tag", None)
+        _SPLANS[key] = SwinPlan(**kk)
+    return _SPLANS[key]
+
+
+def swin_loss_forward(logits_cl: torch.Tensor, labels: torch.Tensor, K: int, ignore_index: int,
+                      include_bg: bool, ce_weight: float):
+    """LitSwinUNETR_Published._loss on the HIP kernels: returns (out4, dlogits_cl)."""
+    require_device(logits_cl, "SwinUNETR loss")
+    logits_cl = logits_cl.contiguous()
+    B = logits_cl.shape[0]
+    labels = labels.to(device=logits_cl.device, dtype=torch.int64).contiguous()
+    V = labels.numel()
+    if logits_cl.numel() != V * K or V % B:
+        raise SpffError(f"logits ({tuple(logits_cl.shape)}) / labels ({tuple(labels.shape)}) mismatch")
+    dev = logits_cl.device
+    out4 = torch.empty(4, dtype=torch.float32, device=dev)
+    dl = torch.empty_like(logits_cl)
+    ws = torch.empty(int(lib().spff_swin_loss_ws_bytes(B, K)), dtype=torch.uint8, device=dev)
+    check(lib().spff_swin_loss(_ptr(logits_cl), _ptr(labels), B, V // B, K, int(ignore_index),
+                               int(bool(include_bg)), float(ce_weight), _ptr(out4), _ptr(dl),
+                               _ptr(ws), _stream(dev)), "spff_swin_loss")
+    return out4, dl
 
 
 # ------------------------------------------------------------------ loss ops --

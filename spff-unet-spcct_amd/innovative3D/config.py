@@ -9,9 +9,10 @@ engine implements.  Differences, all deliberate:
   and CHECKPOINT_DIR/LOG_DIR at import (config.py:19, 258-259); here
   directories are created by whoever writes to them (train.py);
 * ``INNOVATIVE3D_VARIANT`` actually selects (SURVEY F11): ``selected_variants()``;
-* of the non-SPCT baselines only "3DUNet" is registered (BASELINE config 3,
-  SURVEY §8(f) rank 2: Cicek3DUNet + depth adapter on the engine); UNETR,
-  R2UNet3D, SwinUNETR and ResUNet++ are outside the SPFF hot path (SURVEY §8);
+* of the non-SPCT baselines "3DUNet" (BASELINE config 3, SURVEY §8(f) rank 2:
+  Cicek3DUNet + depth adapter) and "SwinUNETR" (BASELINE config 5, §8(f) rank 3)
+  are registered, both on the engine; UNETR, R2UNet3D and ResUNet++ are outside
+  the SPFF hot path (SURVEY §8);
 * the DICOM data modules are outside the hot path: ``MultiDicomDataModule3D``
   raises with a pointer to the synthetic data path used by bench.py.
 """
@@ -131,6 +132,18 @@ def make_cicek_depth_adapter_sgd_wce():
 
 _add_variant("3DUNet", make_cicek_depth_adapter_sgd_wce, MultiDicomDataModule3D,
              CHECKPOINT_DIR / "3DUNet")
+
+# SwinUNETR (config.py:366-386; BASELINE config 5).  build_class drops the kwargs
+# LitSwinUNETR_Published does not take (window_size), exactly like the reference.
+_add_variant("SwinUNETR",
+             build_class("LitSwinUNETR_Published", num_classes=NUM_CLASSES, img_size=(64, 64, 64),
+                         in_channels=1, feature_size=12, depths=(1, 1, 1, 1),
+                         num_heads=(1, 2, 4, 8), window_size=(2, 2, 2), mlp_ratio=2.0,
+                         drop_rate=0.0, attn_drop_rate=0.0, dropout_path_rate=0.0,
+                         norm_name="instance", use_checkpoint=True, lr=8e-4, weight_decay=1e-2,
+                         warmup_epochs=5, use_ce_alongside_dice=True, ce_weight=0.5,
+                         ignore_index=IGNORE_INDEX, include_bg_in_dice=False),
+             MultiDicomDataModule3D, CHECKPOINT_DIR / "SwinUNETR")
 
 VARIANT_NAMES = [v[0] for v in VARIANTS]
 SELECTED_VARIANT = os.getenv("INNOVATIVE3D_VARIANT")

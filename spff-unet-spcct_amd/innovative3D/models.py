@@ -754,3 +754,313 @@ class LitCicek3DUNet_DepthAdapter_Published(pl.LightningModule):
                                momentum=self.hparams.momentum,
                                nesterov=bool(self.hparams.nesterov),
                                weight_decay=self.hparams.weight_decay)
+
+
+# ============================================================================
+# SwinUNETR variant (BASELINE config 5; registry "SwinUNETR", config.py:366-386):
+# LitSwinUNETR_Published (models.py:880-982) around SwinUNETR_Published
+# (models.py:858-878), i.e. MONAI 1.5.2 SwinUNETR, on the engine's spff_swin
+# plan.  The module tree below only holds parameters under MONAI's state-dict
+# names; forward runs on the HIP engine.  Parity unpinned (no MONAI offline):
+# semantics in oracle/swin_oracle.py.
+# ============================================================================
+class _SwinFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, plan, flat, *params):
+        logits_cl = plan.forward(x, flat)
+        ctx.plan, ctx.gen, ctx.flat = plan, plan.generation, flat
+        ctx.slices = [(off, n, shape) for (_name, shape, off, n) in plan.params]
+        return logits_cl.permute(0, 4, 1, 2, 3)
+
+    @staticmethod
+    def backward(ctx, g):
+        plan = ctx.plan
+        if plan.generation != ctx.gen:
+            raise E.SpffError("SwinUNETR engine: another forward ran on this model before the "
+                              "backward of this one; the engine keeps one forward's activations")
+        g_cl = g.permute(0, 2, 3, 4, 1).contiguous()
+        dflat = plan.backward(g_cl, ctx.flat)
+        grads = [dflat[o:o + n].view(s) for (o, n, s) in ctx.slices]
+        return (None, None, None, *grads)
+
+
+class _Holder(nn.Module):
+    """Parameter container (MONAI module names; no forward)."""
+
+
+def _conv_holder(conv: nn.Module) -> nn.Module:
+    h = _Holder()
+    h.conv = conv
+    return h
+
+
+def _res_block(ci: int, co: int) -> nn.Module:
+    """MONAI UnetResBlock (conv1.conv, conv2.conv[, conv3.conv]; InstanceNorm3d
+    without affine has no parameters)."""
+    r = _Holder()
+    r.conv1 = _conv_holder(nn.Conv3d(ci, co, 3, padding=1, bias=False))
+    r.conv2 = _conv_holder(nn.Conv3d(co, co, 3, padding=1, bias=False))
+    if ci != co:
+        r.conv3 = _conv_holder(nn.Conv3d(ci, co, 1, bias=False))
+    return r
+
+
+class _WindowAttentionP(nn.Module):
+    def __init__(self, dim: int, heads: int, window: int):
+        super().__init__()
+        self.relative_position_bias_table = nn.Parameter(
+            torch.zeros((2 * window - 1) ** 3, heads))
+        nn.init.trunc_normal_(self.relative_position_bias_table, std=0.02)
+        c = torch.stack(torch.meshgrid(torch.arange(window), torch.arange(window),
+                                       torch.arange(window), indexing="ij")).flatten(1)
+        r = (c[:, :, None] - c[:, None, :]).permute(1, 2, 0) + (window - 1)
+        idx = r[..., 0] * (2 * window - 1) ** 2 + r[..., 1] * (2 * window - 1) + r[..., 2]
+        self.register_buffer("relative_position_index", idx)
+        self.qkv = nn.Linear(dim, 3 * dim, bias=True)
+        self.proj = nn.Linear(dim, dim)
+
+
+class _SwinBlockP(nn.Module):
+    def __init__(self, dim: int, heads: int, window: int, mlp_ratio: float):
+        super().__init__()
+        self.norm1 = nn.LayerNorm(dim)
+        self.attn = _WindowAttentionP(dim, heads, window)
+        self.norm2 = nn.LayerNorm(dim)
+        self.mlp = _Holder()
+        self.mlp.linear1 = nn.Linear(dim, int(dim * mlp_ratio))
+        self.mlp.linear2 = nn.Linear(int(dim * mlp_ratio), dim)
+
+
+class _BasicLayerP(nn.Module):
+    def __init__(self, dim: int, heads: int, window: int, mlp_ratio: float):
+        super().__init__()
+        self.blocks = nn.ModuleList([_SwinBlockP(dim, heads, window, mlp_ratio)])
+        self.downsample = _Holder()
+        self.downsample.reduction = nn.Linear(8 * dim, 2 * dim, bias=False)
+        self.downsample.norm = nn.LayerNorm(8 * dim)
+
+
+class SwinUNETR(nn.Module):
+    """MONAI 1.5.2 SwinUNETR (patch_size 2, depths (1,1,1,1) -- the registry's --,
+    normalize=True, res_block, InstanceNorm, downsample "merging", use_v2 False)
+    with MONAI's parameter names; forward on the HIP engine (D, H, W multiples
+    of 32, as MONAI's _check_input_size requires)."""
+
+    def __init__(self, in_channels: int = 1, out_channels: int = 2, feature_size: int = 24,
+                 depths=(2, 2, 2, 2), num_heads=(3, 6, 12, 24), window_size=7,
+                 mlp_ratio: float = 4.0, qkv_bias: bool = True, norm_name="instance",
+                 drop_rate: float = 0.0, attn_drop_rate: float = 0.0,
+                 dropout_path_rate: float = 0.0, normalize: bool = True, use_checkpoint=False,
+                 spatial_dims: int = 3, downsample="merging", use_v2: bool = False, **_):
+        super().__init__()
+        ws = window_size if isinstance(window_size, int) else int(window_size[0])
+        if not isinstance(window_size, int) and len(set(window_size)) != 1:
+            raise NotImplementedError("cubic windows only")
+        if tuple(depths) != (1, 1, 1, 1):
+            raise NotImplementedError("depths (1,1,1,1) only (the registry's, config.py:374)")
+        if (not qkv_bias or not normalize or use_v2 or downsample != "merging" or spatial_dims != 3
+                or str(norm_name).lower() != "instance"):
+            raise NotImplementedError("the registry's SwinUNETR settings only (qkv_bias, normalize, "
+                                      "merging, instance norm, 3D, use_v2=False)")
+        if drop_rate or attn_drop_rate or dropout_path_rate:
+            raise NotImplementedError("dropout / drop-path are 0 on the registry path")
+        f = int(feature_size)
+        self.in_channels, self.num_classes, self.feature_size = int(in_channels), int(out_channels), f
+        self.window, self.num_heads, self.mlp_ratio = ws, tuple(int(h) for h in num_heads), float(mlp_ratio)
+        self.swinViT = _Holder()
+        self.swinViT.patch_embed = _Holder()
+        self.swinViT.patch_embed.proj = nn.Conv3d(in_channels, f, 2, stride=2)
+        for s in range(4):
+            setattr(self.swinViT, f"layers{s + 1}",
+                    nn.ModuleList([_BasicLayerP(f << s, self.num_heads[s], ws, mlp_ratio)]))
+        self.encoder1 = _Holder(); self.encoder1.layer = _res_block(in_channels, f)  # noqa: E702
+        self.encoder2 = _Holder(); self.encoder2.layer = _res_block(f, f)  # noqa: E702
+        self.encoder3 = _Holder(); self.encoder3.layer = _res_block(2 * f, 2 * f)  # noqa: E702
+        self.encoder4 = _Holder(); self.encoder4.layer = _res_block(4 * f, 4 * f)  # noqa: E702
+        self.encoder10 = _Holder(); self.encoder10.layer = _res_block(16 * f, 16 * f)  # noqa: E702
+        for name, ci, co in (("decoder5", 16 * f, 8 * f), ("decoder4", 8 * f, 4 * f),
+                             ("decoder3", 4 * f, 2 * f), ("decoder2", 2 * f, f), ("decoder1", f, f)):
+            d = _Holder()
+            d.transp_conv = _conv_holder(nn.ConvTranspose3d(ci, co, 2, stride=2, bias=False))
+            d.conv_block = _res_block(2 * co, co)
+            setattr(self, name, d)
+        self.out = _Holder()
+        self.out.conv = _conv_holder(nn.Conv3d(f, out_channels, 1, bias=True))
+        self._flat = None
+
+    def _plan(self, x):
+        B, C, D, H, W = x.shape
+        if C != self.in_channels:
+            raise ValueError(f"expected {self.in_channels} input channels, got {C}")
+        if D % 32 or H % 32 or W % 32:
+            raise ValueError(f"spatial dims {(D, H, W)} must be divisible by 2**5 = 32")
+        return E.get_swin_plan(batch=B, in_ch=C, depth=D, height=H, width=W,
+                               num_classes=self.num_classes, feature_size=self.feature_size,
+                               window=self.window, heads=self.num_heads, mlp_ratio=self.mlp_ratio,
+                               device=x.device, math=getattr(self, "math", None),
+                               tag=str(id(self)))
+
+    def _engine_params(self, plan):
+        named = dict(self.named_parameters())
+        out = []
+        for name, shape, _off, _n in plan.params:
+            p = named.get(name)
+            if p is None or tuple(p.shape) != tuple(shape):
+                raise E.SpffError(f"parameter {name} {shape} missing or mis-shaped in the module")
+            out.append(p)
+        return out
+
+    def _ensure_flat(self, plan, params, device):
+        flat = self._flat
+        ok = flat is not None and flat.device == device and flat.numel() == plan.nfloats
+        if ok:
+            base = flat.data_ptr()
+            ok = all(p.data_ptr() == base + 4 * off and p.dtype == torch.float32
+                     for p, (_n, _s, off, _k) in zip(params, plan.params))
+        if not ok:
+            flat = torch.empty(plan.nfloats, dtype=torch.float32, device=device)
+            with torch.no_grad():
+                for p, (_name, shape, off, n) in zip(params, plan.params):
+                    flat[off:off + n].copy_(p.detach().reshape(-1).to(device=device,
+                                                                     dtype=torch.float32))
+                    p.data = flat[off:off + n].view(shape)
+            self._flat = flat
+        return flat
+
+    def forward(self, x_in):
+        E.require_device(x_in, "SwinUNETR.forward")
+        plan = self._plan(x_in)
+        params = self._engine_params(plan)
+        flat = self._ensure_flat(plan, params, x_in.device)
+        if torch.is_grad_enabled() and any(p.requires_grad for p in params):
+            return _SwinFunction.apply(x_in.float(), plan, flat, *params)
+        return plan.forward(x_in.float(), flat).permute(0, 4, 1, 2, 3)
+
+
+class SwinUNETR_Published(nn.Module):
+    """models.py:858-878: builds SwinUNETR with the kwargs MONAI 1.5.2 accepts
+    (img_size dropped, drop_path_rate -> dropout_path_rate, spatial_dims=3)."""
+
+    def __init__(self, num_classes, img_size=(96, 96, 96), in_channels=1, feature_size=48,
+                 depths=(2, 2, 2, 2), num_heads=(3, 6, 12, 24), mlp_ratio=4.0, drop_rate=0.0,
+                 attn_drop_rate=0.0, dropout_path_rate=0.0, use_checkpoint=False,
+                 norm_name="instance", **kwargs):
+        super().__init__()
+        self.model = SwinUNETR(in_channels=in_channels, out_channels=num_classes,
+                               feature_size=feature_size, depths=depths, num_heads=num_heads,
+                               mlp_ratio=mlp_ratio, drop_rate=drop_rate,
+                               attn_drop_rate=attn_drop_rate, dropout_path_rate=dropout_path_rate,
+                               use_checkpoint=use_checkpoint, norm_name=norm_name, spatial_dims=3)
+
+    def forward(self, x):
+        return self.model(x)
+
+
+class _SwinLoss(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, labels, K, ignore_index, include_bg, ce_weight):
+        lcl = logits.permute(0, 2, 3, 4, 1).contiguous()
+        out4, dl = E.swin_loss_forward(lcl, labels, K, ignore_index, include_bg, ce_weight)
+        ctx.dl = dl
+        return out4[1]
+
+    @staticmethod
+    def backward(ctx, g):
+        dl = ctx.dl
+        E.scale_(dl, g.reshape(1))
+        return dl.permute(0, 4, 1, 2, 3), None, None, None, None, None
+
+
+class LitSwinUNETR_Published(pl.LightningModule):
+    """models.py:880-982 (registry "SwinUNETR"): pad to a multiple of 32 (replicate,
+    centred) -> SwinUNETR -> crop; loss (1 - w) soft-Dice + w CE(ignore) on the
+    fused HIP loss kernels; AdamW with linear warm-up + cosine decay."""
+
+    def __init__(self, num_classes: int, img_size=(96, 96, 96), in_channels: int = 1,
+                 feature_size: int = 48, depths=(2, 2, 2, 2), num_heads=(3, 6, 12, 24),
+                 mlp_ratio: float = 4.0, drop_rate: float = 0.0, attn_drop_rate: float = 0.0,
+                 dropout_path_rate: float = 0.0, use_checkpoint: bool = False,
+                 norm_name: str = "instance", lr: float = 1e-4, weight_decay: float = 1e-2,
+                 warmup_epochs: int = 5, use_ce_alongside_dice: bool = True,
+                 ce_weight: float = 0.5, ignore_index: Optional[int] = IGNORE_INDEX,
+                 include_bg_in_dice: bool = True):
+        super().__init__()
+        self.save_hyperparameters({
+            "num_classes": num_classes, "img_size": img_size, "in_channels": in_channels,
+            "feature_size": feature_size, "depths": depths, "num_heads": num_heads,
+            "mlp_ratio": mlp_ratio, "drop_rate": drop_rate, "attn_drop_rate": attn_drop_rate,
+            "dropout_path_rate": dropout_path_rate, "use_checkpoint": use_checkpoint,
+            "norm_name": norm_name, "lr": lr, "weight_decay": weight_decay,
+            "warmup_epochs": warmup_epochs, "use_ce_alongside_dice": use_ce_alongside_dice,
+            "ce_weight": ce_weight, "ignore_index": ignore_index,
+            "include_bg_in_dice": include_bg_in_dice})
+        self.model = SwinUNETR_Published(
+            num_classes, img_size=img_size, in_channels=in_channels, feature_size=feature_size,
+            depths=depths, num_heads=num_heads, mlp_ratio=mlp_ratio, drop_rate=drop_rate,
+            attn_drop_rate=attn_drop_rate, dropout_path_rate=dropout_path_rate,
+            use_checkpoint=use_checkpoint, norm_name=norm_name)
+        self._total_train_iters = None
+        self._iters_done = 0
+
+    def forward(self, x):
+        x = _pick_first_if_seq(x)
+        if x.ndim == 4:
+            x = x.unsqueeze(1)
+        x_pad, orig = _pad_to_mult16_3d(x, multiple=32)
+        y_pad = self.model(x_pad)
+        return _center_crop_3d(y_pad, orig)
+
+    def _loss(self, logits, labels):
+        if labels.ndim == 5 and labels.shape[1] == 1:
+            labels = labels[:, 0]
+        if not self.hparams.use_ce_alongside_dice:
+            raise NotImplementedError("dice-only loss is off on the registry path (config.py:383)")
+        ign = self.hparams.ignore_index
+        return _SwinLoss.apply(logits, labels, int(logits.shape[1]),
+                               int(ign) if ign is not None else -1000,
+                               bool(self.hparams.include_bg_in_dice), float(self.hparams.ce_weight))
+
+    def on_train_batch_start(self, batch, batch_idx):
+        """linear warm-up then cosine decay of the learning rate (models.py:941-951)."""
+        tr = getattr(self, "trainer", None)
+        nb = int(getattr(tr, "num_training_batches", 0) or 1) if tr is not None else 1
+        warmup_iters = int(self.hparams.warmup_epochs * nb)
+        t, T = self._iters_done, max(1, self._total_train_iters or 1)
+        if t < warmup_iters:
+            lr = self.hparams.lr * float(t + 1) / max(1, warmup_iters)
+        else:
+            prog = (t - warmup_iters) / max(1, T - warmup_iters)
+            lr = 0.5 * self.hparams.lr * (1.0 + math.cos(math.pi * prog))
+        opt = self.optimizers() if hasattr(self, "optimizers") and tr is not None else None
+        if opt:
+            for pg in opt.param_groups:
+                pg["lr"] = lr
+        return lr
+
+    def on_train_batch_end(self, outputs, batch, batch_idx):
+        self._iters_done += 1
+
+    def _step(self, batch, stage):
+        imgs, lbls = batch if isinstance(batch, (list, tuple)) else (batch["image"], batch["label"])
+        logits = self(imgs)
+        tgt = _canonicalize_targets_3d(lbls).to(logits.device)
+        loss = self._loss(logits, tgt)
+        met = per_class_metrics_3d(logits, tgt, self.hparams.num_classes,
+                                   ignore_index=self.hparams.ignore_index)
+        self.log(f"{stage}_loss", loss, on_epoch=True, prog_bar=True, sync_dist=True)
+        self.log(f"{stage}_macro_dice", met[3], on_epoch=True, prog_bar=True, sync_dist=True)
+        self.log(f"{stage}_micro_dice", met[6], on_epoch=True, prog_bar=False, sync_dist=True)
+        return loss
+
+    def training_step(self, batch, _):
+        return self._step(batch, "train")
+
+    def validation_step(self, batch, _):
+        return self._step(batch, "val")
+
+    def test_step(self, batch, _):
+        return self._step(batch, "test")
+
+    def configure_optimizers(self):
+        return torch.optim.AdamW(self.parameters(), lr=self.hparams.lr,
+                                 weight_decay=self.hparams.weight_decay, betas=(0.9, 0.999))
