@@ -228,6 +228,142 @@ def cpu_baseline_unet3d(st, K, steps):
                       f"median of {steps} steps after 1 warm-up ({med:.2f} s/step)"}
 
 
+def swin_flops(B, D, H, W, K, f=12, cin=1, heads=(1, 2, 4, 8), w=7, mlp=2.0):
+    """Algorithmic fwd+bwd FLOPs of one SwinUNETR step (registry config) at input
+    B x D x H x W: 3x3x3 / 1x1 convs of the residual blocks (fwd, input grad except
+    on the network input, weight grad), the Swin stages' linear layers (x3), window
+    attention over the padded windows (QK^T and PV: 4 n^2 C per window forward,
+    8 n^2 C backward), transposed convs (x3), patch embedding (x2) and the head (x3)."""
+    vol = lambda l: B * (D >> l) * (H >> l) * (W >> l)  # noqa: E731
+    fl = 0.0
+    rbs = [(0, cin, f, True), (1, f, f, False), (2, 2 * f, 2 * f, False), (3, 4 * f, 4 * f, False),
+           (5, 16 * f, 16 * f, False), (4, 16 * f, 8 * f, False), (3, 8 * f, 4 * f, False),
+           (2, 4 * f, 2 * f, False), (1, 2 * f, f, False), (0, 2 * f, f, False)]
+    for L, ci, co, first in rbs:
+        V = vol(L)
+        fl += 2.0 * V * ci * co * 27 * (2 if first else 3) + 2.0 * V * co * co * 27 * 3
+        if ci != co:
+            fl += 2.0 * V * ci * co * (2 if first else 3)
+    for s in range(4):
+        T, C = vol(s + 1), f << s
+        hid = int(C * mlp)
+        fl += 3 * 2.0 * T * (3 * C * C + C * C + 2 * C * hid) + 3 * 2.0 * (T // 8) * 8 * C * 2 * C
+        dims = [(D >> (s + 1)), (H >> (s + 1)), (W >> (s + 1))]
+        ws = [min(w, d) for d in dims]
+        nwin = B
+        for d, k in zip(dims, ws):
+            nwin *= -(-d // k)
+        n = ws[0] * ws[1] * ws[2]
+        fl += 12.0 * n * n * C * nwin
+    for u, (ci, co) in enumerate(((16 * f, 8 * f), (8 * f, 4 * f), (4 * f, 2 * f), (2 * f, f),
+                                  (f, f))):
+        fl += 3 * 2.0 * vol(5 - u) * ci * 8 * co
+    fl += 2 * 2.0 * vol(1) * 8 * cin * f + 3 * 2.0 * vol(0) * f * K
+    return fl
+
+
+def bench_swin(args, world, rank, device):
+    """BASELINE configs[4]: the SwinUNETR variant (registry "SwinUNETR": MONAI 1.5.2
+    SwinUNETR, feature 12, depths 1, heads 1/2/4/8, window 7) on batch 2 x 1 x 128^3
+    per GPU: forward, the Lit loss (0.5 soft-Dice + 0.5 CE), backward (optimizer
+    excluded).  N > 1: batch data parallelism with the gradient all-reduced."""
+    import innovative3D.models as M
+    from innovative3D.config import variant
+    from innovative3D.weightgen import synth_state
+    from innovative3D.synthetic import synthetic_batch
+    from innovative3D.distributed import allreduce_gradients
+    K, Bt, S_ = args.classes, 2, 128
+    lit = variant("SwinUNETR")[1](num_classes=K)
+    sd = lit.state_dict()
+    st = synth_state([(k, tuple(v.shape)) for k, v in sd.items()
+                      if not k.endswith("relative_position_index")], seed=0)
+    sd.update({k: torch.from_numpy(v) for k, v in st.items()})
+    lit.load_state_dict(sd)
+    lit = lit.to(device)
+    lit.model.model.math = args.math
+    x, y = synthetic_batch(Bt, 1, S_, S_, S_, K, ignore_frac=0.01, seed=1000 + rank, device=device)
+    params = list(lit.parameters())
+
+    def step():
+        for q in params:
+            q.grad = None
+        logits = lit(x)
+        loss = M._SwinLoss.apply(logits, y, K, 255, False, 0.5)
+        loss.backward()
+        allreduce_gradients(params)
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    vox = Bt * S_ ** 3
+    value = world * vox * args.steps / elapsed
+    fl = swin_flops(Bt, S_, S_, S_, K)
+    out = {
+        "metric": "voxels/sec fwd+bwd, SwinUNETR variant (MONAI 1.5.2 SwinUNETR, registry "
+                  "settings), 1-ch 128^3 patches",
+        "value": value, "unit": "voxels/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "conv_math": args.math,
+        "data": "synthetic (x~N(0,1), labels U[0,K) with 1% ignore=255; weights from weightgen seed 0)",
+        "config": {"workload": f"SwinUNETR fwd+0.5 softDice+0.5 CE+bwd, batch {Bt} x 1ch x {S_}^3 "
+                               f"per GPU, K={K}, feature 12, depths (1,1,1,1), heads (1,2,4,8), "
+                               "window 7 (BASELINE configs[4])",
+                   "global_batch": Bt * world, "shape": [Bt, 1, S_, S_, S_],
+                   "parallelism": f"dp{world}"},
+        "loss": float(loss.item()),
+        "step_tflops": fl * args.steps / elapsed / 1e12,
+        "algorithmic_flops_per_step": fl,
+        "parity": "unpinned (MONAI absent offline); engine vs the restated oracle: tests/test_gpu_swin.py",
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and args.cpu_baseline == "auto":
+        out["cpu_baseline"] = cpu_baseline_swin(st, K, args.cpu_steps)
+        out["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline_swin(st, K, steps):
+    """swin_oracle (PyTorch-CPU restatement) fwd + Lit loss + bwd on 1 x 1 x 128^3."""
+    from oracle import swin_oracle as S
+    from innovative3D.synthetic import synthetic_batch
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    threads = min(threads, os.cpu_count() or threads)
+    torch.set_num_threads(threads)
+    P = S.params_from_state(st, prefix="model.model.")
+    cfg = S.SwinCfg(num_classes=K)
+    x, y = synthetic_batch(1, 1, 128, 128, 128, K, ignore_frac=0.01, seed=123)
+    times = []
+    for i in range(steps + 1):
+        t0 = time.perf_counter()
+        S.fwd_bwd(P, x, y, cfg)
+        if i > 0:
+            times.append(time.perf_counter() - t0)
+    med = statistics.median(times)
+    return {"value": 128 ** 3 / med, "unit": "voxels/s", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": f"swin_oracle fwd+loss+bwd on 1x1x128^3 (half the batch); median of "
+                      f"{steps} steps after 1 warm-up ({med:.2f} s/step)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -242,11 +378,13 @@ def main():
     ap.add_argument("--math", choices=("f32", "bf16x6", "bf16x3"), default="bf16x6",
                     help="conv arithmetic: bf16x6 = fp32 operands split exactly into 3 bf16 "
                          "planes, 6 products, fp32 accumulate (fp32 accuracy class; default)")
-    ap.add_argument("--workload", choices=("patch128", "volume512", "unet3d"), default="patch128",
+    ap.add_argument("--workload", choices=("patch128", "volume512", "unet3d", "swin"),
+                    default="patch128",
                     help="patch128 = the headline (BASELINE configs[1]): batch data parallelism; "
                          "volume512 = BASELINE configs[3]: one 5 x (64 N) x 512 x 512 volume "
                          "depth-sharded over the N ranks (64-slice slab per rank, RCCL halos); "
-                         "unet3d = BASELINE configs[2]: the 3DUNet variant, batch 4 x 1 x 5 x 96^2")
+                         "unet3d = BASELINE configs[2]: the 3DUNet variant, batch 4 x 1 x 5 x 96^2; "
+                         "swin = BASELINE configs[4]: the SwinUNETR variant, batch 2 x 1 x 128^3")
     ap.add_argument("--slab-depth", type=int, default=64)
     ap.add_argument("--hw", type=int, default=512)
     ap.add_argument("--cpu-depth", type=int, default=32)
@@ -265,6 +403,8 @@ def main():
 
     if args.workload == "unet3d":
         return bench_unet3d(args, world, rank, device)
+    if args.workload == "swin":
+        return bench_swin(args, world, rank, device)
 
     from innovative3D.distributed import DataParallelSPFF
     from innovative3D.synthetic import synthetic_batch

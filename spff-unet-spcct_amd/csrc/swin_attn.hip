@@ -253,50 +253,32 @@ __global__ __launch_bounds__(AT_THREADS) void k_attn_bwd(
     for (int wv = 0; wv < (int)(blockDim.x >> 6); ++wv) t += wred[wv * 2 * HD + tid];
     ppart[(win * g.nh + h) * 2 * HD + tid] = t;
   }
-  // ---- bias table: thread per entry, its (i, j) pairs in query order
+  // ---- bias table: thread per entry, its (i, j) pairs in query order; the
+  // pairs of offset o = c_i - c_j are the box c_i in [max(0,o), min(w,w+o))^3
   const int W2 = 2 * w - 1;
   for (int r = tid; r < R; r += blockDim.x) {
     const int od = r / (W2 * W2) - (w - 1), oh = (r / W2) % W2 - (w - 1), ow = r % W2 - (w - 1);
+    const int jo = (od * w + oh) * w + ow;  // i - j
     float acc = 0.f;
-    for (int i = 0; i < n; ++i) {
-      const int cd = i / (w * w) - od, ch = (i / w) % w - oh, cw = i % w - ow;
-      if ((unsigned)cd >= (unsigned)w || (unsigned)ch >= (unsigned)w || (unsigned)cw >= (unsigned)w)
-        continue;
-      const int j = (cd * w + ch) * w + cw;
-      if (j >= n) continue;
-      float sc = 0.f, dp = 0.f;
+    for (int cd = max(0, od); cd < min(w, w + od); ++cd) {
+      for (int ch = max(0, oh); ch < min(w, w + oh); ++ch) {
+        const int i0 = (cd * w + ch) * w;
+        for (int cw = max(0, ow); cw < min(w, w + ow); ++cw) {
+          const int i = i0 + cw, j = i - jo;
+          if (i >= n || j >= n) continue;
+          float sc = 0.f, dp = 0.f;
 #pragma unroll
-      for (int e = 0; e < HD; ++e) {
-        sc += Qs[i * HD + e] * Ks[j * HD + e];
-        dp += Gs[i * HD + e] * Vs[j * HD + e];
+          for (int e = 0; e < HD; ++e) {
+            sc += Qs[i * HD + e] * Ks[j * HD + e];
+            dp += Gs[i * HD + e] * Vs[j * HD + e];
+          }
+          const float p = expf(sc + tab[r] - Ls[i]);
+          acc += p * (dp - Dd[i]);
+        }
       }
-      const float p = expf(sc + tab[r] - Ls[i]);
-      acc += p * (dp - Dd[i]);
     }
     tpart[(win * g.nh + h) * R + r] = acc;
   }
-}
-
-// dtable[r][h] = sum over windows of tpart[win][h][r]
-__global__ void k_tab_reduce(const float* __restrict__ tpart, int64_t nwin, int nh, int R,
-                             float* __restrict__ dtable) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nh * R) return;
-  const int r = i / nh, h = i % nh;
-  float s = 0.f;
-  for (int64_t w = 0; w < nwin; ++w) s += tpart[(w * nh + h) * R + r];
-  dtable[i] = s;
-}
-// dbqkv[C + h*hd + e] += sum_win ppart[win][h][e]; dbqkv[2C + ...] += ...[hd + e]
-__global__ void k_pad_reduce(const float* __restrict__ ppart, int64_t nwin, int nh, int hd, int C,
-                             float* __restrict__ dbqkv) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nh * 2 * hd) return;
-  const int h = i / (2 * hd), e2 = i % (2 * hd);
-  float s = 0.f;
-  for (int64_t w = 0; w < nwin; ++w) s += ppart[(w * nh + h) * 2 * hd + e2];
-  const int col = e2 < hd ? C + h * hd + e2 : 2 * C + h * hd + (e2 - hd);
-  dbqkv[col] += s;
 }
 
 static size_t fwd_lds(const AttnGeo& g) {
@@ -360,18 +342,18 @@ hipError_t swin_attn_bwd(const float* qkv, const float* bqkv, const float* table
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  const int nt = g.nh * g.R();
-  hipLaunchKernelGGL(k_tab_reduce, dim3((nt + 255) / 256), dim3(256), 0, s, tpart, g.nwin(), g.nh,
-                     g.R(), dtable);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
+  // dtable[r][h] = sum over windows of tpart[win][h][r]
+  if ((e = col_reduce_map(tpart, (int)g.nwin(), (int64_t)g.nh * g.R(), g.nh * g.R(), dtable, 0, 1,
+                          g.R(), g.nh, g.hd, g.C, s)) != hipSuccess)
+    return e;
   return dbqkv ? swin_attn_pad_grad(g, ws, dbqkv, s) : hipSuccess;
 }
 
 hipError_t swin_attn_pad_grad(const AttnGeo& g, const float* ws, float* dbqkv, hipStream_t s) {
+  // dbqkv[C + h*hd + e] += sum_win ppart[win][h][e]; dbqkv[2C + ...] += ...[hd + e]
   const float* ppart = ws + (size_t)g.nwin() * g.nh * g.R();
-  hipLaunchKernelGGL(k_pad_reduce, dim3((g.nh * 2 * g.hd + 255) / 256), dim3(256), 0, s, ppart,
-                     g.nwin(), g.nh, g.hd, g.C, dbqkv);
-  return hipGetLastError();
+  return col_reduce_map(ppart, (int)g.nwin(), (int64_t)g.nh * 2 * g.hd, g.nh * 2 * g.hd, dbqkv, 1,
+                        2, g.R(), g.nh, g.hd, g.C, s);
 }
 
 }  // namespace spff

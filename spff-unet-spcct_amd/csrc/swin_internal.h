@@ -38,6 +38,10 @@ hipError_t add_inplace(float* y, const float* x, int64_t n, hipStream_t s);
 // out[i] (+)= sum_k part[k*stride + i] (k < n, in order), i < count
 hipError_t col_reduce(const float* part, int n, int64_t stride, int count, float* out, int acc,
                       hipStream_t s);
+// the same with an output index map (see swin_ops.hip): mode 1 = bias-table transpose,
+// mode 2 = padded-token k / v bias columns
+hipError_t col_reduce_map(const float* part, int n, int64_t stride, int count, float* out,
+                          int acc, int mode, int R, int nh, int hd, int C, hipStream_t s);
 
 // ------------------------------------------------------------- loss --
 size_t dice_ce_ws_bytes(int B, int K);

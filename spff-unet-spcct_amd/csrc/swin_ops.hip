@@ -157,21 +157,48 @@ __global__ __launch_bounds__(256) void k_ln_bwd(LnSrc src, int C, const float* _
   }
 }
 
-// out[i] (+)= sum over k < n of part[k*stride + i], in order (i < count)
-__global__ void k_col_reduce(const float* __restrict__ part, int n, int64_t stride, int count,
-                             float* __restrict__ out, int acc) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= count) return;
+// out[i] (+)= sum over k < n of part[k*stride + i] (i < count): one workgroup per
+// column, each thread a strided partial sum over k, then a fixed LDS tree --
+// deterministic, and parallel over k (n runs to thousands of blocks / windows).
+// map = 1: out index of column i = (i % R) * nh + i / R (bias-table transpose);
+// map = 2: i = h*2hd + e2 -> C + h*hd + e2 (k part) or 2C + h*hd + e2 - hd (v part).
+struct ColMap {
+  int mode, R, nh, hd, C;
+};
+__global__ __launch_bounds__(256) void k_col_reduce(const float* __restrict__ part, int n,
+                                                    int64_t stride, float* __restrict__ out,
+                                                    int acc, ColMap mp) {
+  const int i = blockIdx.x;
   float s = 0.f;
-  for (int k = 0; k < n; ++k) s += part[(int64_t)k * stride + i];
-  out[i] = acc ? out[i] + s : s;
+  for (int k = threadIdx.x; k < n; k += 256) s += part[(int64_t)k * stride + i];
+  __shared__ float red[256];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int st = 128; st > 0; st >>= 1) {
+    if (threadIdx.x < st) red[threadIdx.x] += red[threadIdx.x + st];
+    __syncthreads();
+  }
+  if (threadIdx.x) return;
+  int o = i;
+  if (mp.mode == 1) {
+    o = (i % mp.R) * mp.nh + i / mp.R;
+  } else if (mp.mode == 2) {
+    const int h = i / (2 * mp.hd), e2 = i % (2 * mp.hd);
+    o = e2 < mp.hd ? mp.C + h * mp.hd + e2 : 2 * mp.C + h * mp.hd + (e2 - mp.hd);
+  }
+  out[o] = acc ? out[o] + red[0] : red[0];
+}
+
+hipError_t col_reduce_map(const float* part, int n, int64_t stride, int count, float* out,
+                          int acc, int mode, int R, int nh, int hd, int C, hipStream_t s) {
+  hipLaunchKernelGGL(k_col_reduce, dim3(count), dim3(256), 0, s, part, n, stride, out, acc,
+                     ColMap{mode, R, nh, hd, C});
+  return hipGetLastError();
 }
 
 hipError_t col_reduce(const float* part, int n, int64_t stride, int count, float* out, int acc,
                       hipStream_t s) {
-  hipLaunchKernelGGL(k_col_reduce, dim3(cdiv(count, 256)), dim3(256), 0, s, part, n, stride,
-                     count, out, acc);
-  return hipGetLastError();
+  return col_reduce_map(part, n, stride, count, out, acc, 0, 1, 1, 1, 0, s);
 }
 
 hipError_t ln_fwd(const float* x, int ldx, int C, const float* g, const float* b, float* y,
@@ -397,22 +424,35 @@ __global__ __launch_bounds__(DL_T) void k_dice_stats(const float* __restrict__ x
   }
 }
 
+// per (b, q) column sums of the k_dice_stats partials, one workgroup each, fixed tree
+__global__ __launch_bounds__(256) void k_dice_sum(const double* __restrict__ part, int nblk,
+                                                  int nq, double* __restrict__ tot) {
+  const int b = blockIdx.y, q = blockIdx.x;
+  double s = 0.0;
+  for (int j = threadIdx.x; j < nblk; j += 256) s += part[((int64_t)b * nblk + j) * nq + q];
+  __shared__ double red[256];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int st = 128; st > 0; st >>= 1) {
+    if (threadIdx.x < st) red[threadIdx.x] += red[threadIdx.x + st];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) tot[(int64_t)b * nq + q] = red[0];
+}
+
 // coef[b][k][2] = (alpha, beta): dL/dp_k = m * (alpha g_k + beta) for k >= sc;
-// out4 = [ce, loss, dice_loss, N_valid]; nvalid64 = N_valid (int64, for the CE grad)
-__global__ void k_dice_final(const double* __restrict__ part, int nblk, int B, int K, int sc,
-                             double w, float* __restrict__ coef, float* __restrict__ out4,
+// out4 = [ce, loss, dice_loss, N_valid]; scal[0] = w / N_valid (the CE gradient scale)
+__global__ void k_dice_final(const double* __restrict__ tot, int B, int K, int sc, double w,
+                             float* __restrict__ coef, float* __restrict__ out4,
                              double* __restrict__ scal) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   const int nq = 3 * K + 2;
   double ce = 0.0, N = 0.0, dsum = 0.0;
   const int nc = K - sc;
   for (int b = 0; b < B; ++b) {
+    const double* q = tot + (int64_t)b * nq;
     for (int k = 0; k < K; ++k) {
-      double I = 0.0, P = 0.0, G = 0.0;
-      for (int j = 0; j < nblk; ++j) {
-        const double* q = part + ((int64_t)b * nblk + j) * nq;
-        I += q[k]; P += q[K + k]; G += q[2 * K + k];
-      }
+      const double I = q[k], P = q[K + k], G = q[2 * K + k];
       float a = 0.f, be = 0.f;
       if (k >= sc && nc > 0) {
         const double den = P + G + 1e-6;
@@ -423,11 +463,8 @@ __global__ void k_dice_final(const double* __restrict__ part, int nblk, int B, i
       coef[((int64_t)b * K + k) * 2 + 0] = a;
       coef[((int64_t)b * K + k) * 2 + 1] = be;
     }
-    for (int j = 0; j < nblk; ++j) {
-      const double* q = part + ((int64_t)b * nblk + j) * nq;
-      ce += q[3 * K];
-      N += q[3 * K + 1];
-    }
+    ce += q[3 * K];
+    N += q[3 * K + 1];
   }
   const double dice_loss = nc > 0 ? 1.0 - dsum / ((double)B * nc) : 0.0;
   const double cem = N > 0 ? ce / N : NAN;  // F.cross_entropy: 0/0 -> nan
@@ -483,7 +520,7 @@ __global__ __launch_bounds__(DL_T) void k_dice_grad(const float* __restrict__ x,
 }
 
 size_t dice_ce_ws_bytes(int B, int K) {
-  return ((size_t)B * DL_GRID * (3 * K + 2) + 8) * sizeof(double) +
+  return ((size_t)B * (DL_GRID + 1) * (3 * K + 2) + 8) * sizeof(double) +
          (size_t)B * K * 2 * sizeof(float) + 64;
 }
 
@@ -492,14 +529,18 @@ hipError_t dice_ce_loss(const float* logits, const int64_t* labels, int B, int64
                         void* ws, hipStream_t s) {
   if (K < 1 || K > DL_KMAX) return hipErrorInvalidValue;
   double* part = static_cast<double*>(ws);
-  double* scal = part + (size_t)B * DL_GRID * (3 * K + 2);
+  double* tot = part + (size_t)B * DL_GRID * (3 * K + 2);
+  double* scal = tot + (size_t)B * (3 * K + 2);
   float* coef = reinterpret_cast<float*>(scal + 8);
   hipLaunchKernelGGL(k_dice_stats, dim3(DL_GRID, B), dim3(DL_T), 0, s, logits, labels, vps, K,
                      ignore, part);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_dice_final, dim3(1), dim3(64), 0, s, part, DL_GRID, B, K,
-                     include_bg ? 0 : 1, ce_weight, coef, out4, scal);
+  hipLaunchKernelGGL(k_dice_sum, dim3(3 * K + 2, B), dim3(256), 0, s, part, DL_GRID, 3 * K + 2,
+                     tot);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(k_dice_final, dim3(1), dim3(64), 0, s, tot, B, K, include_bg ? 0 : 1,
+                     ce_weight, coef, out4, scal);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   const int64_t V = (int64_t)B * vps;
   hipLaunchKernelGGL(k_dice_grad, dim3((unsigned)std::min<int64_t>(cdiv64(V, DL_T), 8192)),
