@@ -8,8 +8,9 @@
 // LDS; each thread owns one query and streams the keys with an online
 // softmax (fp32, exp / max rescaling), so the n x n score matrix never exists.
 // The backward recomputes scores from the saved log-sum-exp: dq per query
-// thread, dk / dv per key thread, and the bias-table gradient per table entry
-// (each entry sums its (query, key) pairs in query order) -- every reduction
+// thread; dk / dv per key thread, which also accumulates the bias-table
+// gradient into its wave's private LDS table (the lanes of a wave always hit
+// distinct entries), the 6 wave tables then summed in order -- every reduction
 // has a fixed order, so the results are deterministic; per-window partials of
 // the table and the padded tokens' k / v gradients are summed over windows in
 // window order by small reduce kernels.
@@ -24,6 +25,13 @@
 #include "swin_internal.h"
 
 #include <math.h>
+
+#ifndef SPFF_ATTN_DIAG
+#define SPFF_ATTN_DIAG 0  // timing diagnostics only: skip phase 1 (dq) or 2 (dk/dv/table)
+#endif
+#ifndef SPFF_ATTN_UNROLL
+#define SPFF_ATTN_UNROLL 2  // key / query loop unroll of the backward (ILP at 1 WG per CU)
+#endif
 
 namespace spff {
 
@@ -145,7 +153,8 @@ __global__ __launch_bounds__(AT_THREADS) void k_attn_bwd(
   float* Dd = Ls + n;             // rowsum(dO * O) [n]
   float* tab = Dd + n;            // [R]
   float* wred = tab + R;          // [6][2 HD]
-  int* k7 = reinterpret_cast<int*>(wred + 6 * 2 * HD);  // [n]
+  float* wtab = wred + 6 * 2 * HD;  // [6 waves][R] private bias-table accumulators
+  int* k7 = reinterpret_cast<int*>(wtab + 6 * R);  // [n]
   const int tid = threadIdx.x;
   for (int t = tid; t < n; t += blockDim.x) {
     const int64_t row = tok_row(g, win, t);
@@ -165,10 +174,11 @@ __global__ __launch_bounds__(AT_THREADS) void k_attn_bwd(
     k7[t] = key7(t, w);
   }
   for (int r = tid; r < R; r += blockDim.x) tab[r] = table[(int64_t)r * g.nh + h];
+  for (int r = tid; r < 6 * R; r += blockDim.x) wtab[r] = 0.f;
   __syncthreads();
   const int off0 = (w - 1) * ((2 * w - 1) * (2 * w - 1) + (2 * w - 1) + 1);
   // ---- dq: thread per query
-  if (tid < n) {
+  if (SPFF_ATTN_DIAG != 1 && tid < n) {
     const int i = tid;
     const int64_t row = tok_row(g, win, i);
     if (row >= 0) {
@@ -181,6 +191,7 @@ __global__ __launch_bounds__(AT_THREADS) void k_attn_bwd(
       }
       const float li = Ls[i], di = Dd[i];
       const int base = k7[i] + off0;
+#pragma unroll SPFF_ATTN_UNROLL
       for (int j = 0; j < n; ++j) {
         float sc = 0.f, dp = 0.f;
 #pragma unroll
@@ -198,7 +209,7 @@ __global__ __launch_bounds__(AT_THREADS) void k_attn_bwd(
     }
   }
   // ---- dk, dv: thread per key
-  {
+  if (SPFF_ATTN_DIAG != 2) {
     const int j = tid;
     float dk[HD], dv[HD];
 #pragma unroll
@@ -213,6 +224,11 @@ __global__ __launch_bounds__(AT_THREADS) void k_attn_bwd(
         v[e] = Vs[j * HD + e];
       }
       const int kj = k7[j] - off0;
+      // bias-table gradient: at each query i the wave's lanes (keys j) hit distinct
+      // entries k7[i] - kj of the wave's private table -> plain read-add-write, in
+      // query order; the 6 tables are summed in wave order below (deterministic)
+      float* mt = wtab + (tid >> 6) * R;
+#pragma unroll SPFF_ATTN_UNROLL
       for (int i = 0; i < n; ++i) {
         float sc = 0.f, dp = 0.f;
 #pragma unroll
@@ -220,8 +236,10 @@ __global__ __launch_bounds__(AT_THREADS) void k_attn_bwd(
           sc += Qs[i * HD + e] * k[e];
           dp += Gs[i * HD + e] * v[e];
         }
-        const float p = expf(sc + tab[k7[i] - kj] - Ls[i]);
+        const int ri = k7[i] - kj;
+        const float p = expf(sc + tab[ri] - Ls[i]);
         const float ds = p * (dp - Dd[i]);
+        mt[ri] += ds;
 #pragma unroll
         for (int e = 0; e < HD; ++e) {
           dk[e] += ds * Qs[i * HD + e];
@@ -253,30 +271,10 @@ __global__ __launch_bounds__(AT_THREADS) void k_attn_bwd(
     for (int wv = 0; wv < (int)(blockDim.x >> 6); ++wv) t += wred[wv * 2 * HD + tid];
     ppart[(win * g.nh + h) * 2 * HD + tid] = t;
   }
-  // ---- bias table: thread per entry, its (i, j) pairs in query order; the
-  // pairs of offset o = c_i - c_j are the box c_i in [max(0,o), min(w,w+o))^3
-  const int W2 = 2 * w - 1;
+  // ---- bias table: the waves' private tables, summed in wave order
   for (int r = tid; r < R; r += blockDim.x) {
-    const int od = r / (W2 * W2) - (w - 1), oh = (r / W2) % W2 - (w - 1), ow = r % W2 - (w - 1);
-    const int jo = (od * w + oh) * w + ow;  // i - j
     float acc = 0.f;
-    for (int cd = max(0, od); cd < min(w, w + od); ++cd) {
-      for (int ch = max(0, oh); ch < min(w, w + oh); ++ch) {
-        const int i0 = (cd * w + ch) * w;
-        for (int cw = max(0, ow); cw < min(w, w + ow); ++cw) {
-          const int i = i0 + cw, j = i - jo;
-          if (i >= n || j >= n) continue;
-          float sc = 0.f, dp = 0.f;
-#pragma unroll
-          for (int e = 0; e < HD; ++e) {
-            sc += Qs[i * HD + e] * Ks[j * HD + e];
-            dp += Gs[i * HD + e] * Vs[j * HD + e];
-          }
-          const float p = expf(sc + tab[r] - Ls[i]);
-          acc += p * (dp - Dd[i]);
-        }
-      }
-    }
+    for (int wv = 0; wv < (int)(blockDim.x >> 6); ++wv) acc += wtab[wv * R + r];
     tpart[(win * g.nh + h) * R + r] = acc;
   }
 }
@@ -285,7 +283,7 @@ static size_t fwd_lds(const AttnGeo& g) {
   return (size_t)(2 * g.n * g.hd + g.R()) * sizeof(float) + (size_t)g.n * sizeof(int);
 }
 static size_t bwd_lds(const AttnGeo& g) {
-  return (size_t)(4 * g.n * g.hd + 2 * g.n + g.R() + 6 * 2 * g.hd) * sizeof(float) +
+  return (size_t)(4 * g.n * g.hd + 2 * g.n + 7 * g.R() + 6 * 2 * g.hd) * sizeof(float) +
          (size_t)g.n * sizeof(int);
 }
 
