@@ -270,6 +270,28 @@ int spff_swin_loss(const float* logits, const int64_t* labels, int batch, int64_
                    int num_classes, int ignore_index, int include_bg, double ce_weight,
                    float* out4, float* dlogits, void* ws, void* stream);
 
+/* ------------------------------------------------------------------------
+ * Training data path on the device (oracle/data_oracle.py).
+ * ------------------------------------------------------------------------ */
+/* label map of the ellipse ROIs (x0, y0, w0, h0, label) [nroi][5] (device int32), later
+ * ROIs overwriting earlier ones, replicated over `frames`: labels [frames][H][W] int64.
+ * Replaces the ROI loop of create_image_and_labels_for_dataset (helpers.py:125-129, 199-204). */
+int spff_rasterize_ellipses(const int* rois, int nroi, int frames, int height, int width,
+                            int64_t* labels, void* stream);
+/* [n][hin][win] -> [n][hout][wout] antialiased bilinear (align_corners=False), PyTorch's
+ * weights: TF.resize(t, (H, W)) of helpers.py:196.  tmp >= n*hin*wout floats. */
+int spff_resize_bilinear_aa(const float* in, int n, int hin, int win, float* out, int hout,
+                            int wout, float* tmp, void* stream);
+/* TrainGridAug.__call__ (datasets.py:158-209) on a batch x [B][F][H][W] (+ labels y, may be
+ * NULL): per sample, prm[8] = {flip_w, flip_h, rot_k, jitter_on, scale, shift, noise_cap
+ * (0: no noise), stamp} and maps[H + W] = source row / column of the stripe shuffle in the
+ * rotated frame (device arrays; the random draws are the caller's).  xo / yo [B][F][Ho][Wo].
+ * ws >= spff_grid_aug_ws_bytes(B). */
+size_t spff_grid_aug_ws_bytes(int batch);
+int spff_grid_aug(const float* x, const int64_t* y, int batch, int frames, int height, int width,
+                  const int* maps, const float* prm, uint64_t seed, float* xo, int64_t* yo,
+                  void* ws, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -140,6 +140,11 @@ _SIGS = {
     "spff_swin_saved_tensor": (_I, [_P, _P, ctypes.c_char_p, ctypes.POINTER(_P),
                                     ctypes.POINTER(_L), ctypes.POINTER(_I)]),
     "spff_swin_loss_ws_bytes": (_S, [_I, _I]),
+    # data path
+    "spff_rasterize_ellipses": (_I, [_P, _I, _I, _I, _I, _P, _P]),
+    "spff_resize_bilinear_aa": (_I, [_P, _I, _I, _I, _P, _I, _I, _P, _P]),
+    "spff_grid_aug_ws_bytes": (_S, [_I]),
+    "spff_grid_aug": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, ctypes.c_uint64, _P, _P, _P, _P]),
     "spff_swin_loss": (_I, [_P, _P, _I, _L, _I, _I, _I, ctypes.c_double, _P, _P, _P, _P]),
     "spff_loss_ex": (_I, [_P, _P, _L, _I, _I, ctypes.c_double, _P, _P, _I, _P, _P, _P, _P, _P]),
 }
@@ -594,6 +599,49 @@ def swin_loss_forward(logits_cl: torch.Tensor, labels: torch.Tensor, K: int, ign
                                int(bool(include_bg)), float(ce_weight), _ptr(out4), _ptr(dl),
                                _ptr(ws), _stream(dev)), "spff_swin_loss")
     return out4, dl
+
+
+# ------------------------------------------------------------- data path ops --
+def rasterize_ellipses(rois: torch.Tensor, frames: int, height: int, width: int) -> torch.Tensor:
+    """rois [n, 5] int32 (x0, y0, w0, h0, label) on the device -> labels [F, H, W] int64."""
+    require_device(rois, "rasterize_ellipses")
+    rois = rois.to(torch.int32).contiguous()
+    lab = torch.empty((frames, height, width), dtype=torch.int64, device=rois.device)
+    check(lib().spff_rasterize_ellipses(_ptr(rois), rois.shape[0], frames, height, width,
+                                        _ptr(lab), _stream(rois.device)), "spff_rasterize_ellipses")
+    return lab
+
+
+def resize_bilinear_aa(frames: torch.Tensor, height: int, width: int) -> torch.Tensor:
+    """[N, h, w] fp32 -> [N, height, width] (F.interpolate bilinear, antialias)."""
+    require_device(frames, "resize_bilinear_aa")
+    x = frames.to(torch.float32).contiguous()
+    n, hin, win = x.shape
+    out = torch.empty((n, height, width), dtype=torch.float32, device=x.device)
+    tmp = torch.empty((n, hin, width), dtype=torch.float32, device=x.device)
+    check(lib().spff_resize_bilinear_aa(_ptr(x), n, hin, win, _ptr(out), height, width, _ptr(tmp),
+                                        _stream(x.device)), "spff_resize_bilinear_aa")
+    return out
+
+
+def grid_aug(x: torch.Tensor, y: Optional[torch.Tensor], maps: torch.Tensor, prm: torch.Tensor,
+             seed: int, out_hw) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+    """x [B,F,H,W] fp32 (+ y int64) -> augmented [B,F,Ho,Wo]; maps [B,H+W] int32 and
+    prm [B,8] fp32 on the device (see include/spff.h spff_grid_aug)."""
+    require_device(x, "grid_aug")
+    x = x.contiguous()
+    B, F_, H, W = x.shape
+    Ho, Wo = out_hw
+    xo = torch.empty((B, F_, Ho, Wo), dtype=torch.float32, device=x.device)
+    yo = None
+    if y is not None:
+        y = y.to(device=x.device, dtype=torch.int64).contiguous()
+        yo = torch.empty((B, F_, Ho, Wo), dtype=torch.int64, device=x.device)
+    ws = torch.empty(int(lib().spff_grid_aug_ws_bytes(B)), dtype=torch.uint8, device=x.device)
+    check(lib().spff_grid_aug(_ptr(x), _ptr(y), B, F_, H, W, _ptr(maps.contiguous()),
+                              _ptr(prm.contiguous()), ctypes.c_uint64(int(seed) & (2**64 - 1)),
+                              _ptr(xo), _ptr(yo), _ptr(ws), _stream(x.device)), "spff_grid_aug")
+    return xo, yo
 
 
 # ------------------------------------------------------------------ loss ops --

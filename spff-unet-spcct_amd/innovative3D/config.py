@@ -13,8 +13,9 @@ engine implements.  Differences, all deliberate:
   Cicek3DUNet + depth adapter) and "SwinUNETR" (BASELINE config 5, §8(f) rank 3)
   are registered, both on the engine; UNETR, R2UNet3D and ResUNet++ are outside
   the SPFF hot path (SURVEY §8);
-* the DICOM data modules are outside the hot path: ``MultiDicomDataModule3D``
-  raises with a pointer to the synthetic data path used by bench.py.
+* the DICOM data module (``MultiDicomDataModule3D``) is the device-resident
+  one of innovative3D/datasets.py (resize, ROI rasterisation and TrainGridAug as
+  HIP kernels); decoding DICOM itself needs pydicom, absent offline.
 """
 from __future__ import annotations
 
@@ -51,10 +52,9 @@ CKPT_DIR = CHECKPOINT_DIR
 
 
 def MultiDicomDataModule3D(*args, **kwargs):
-    raise NotImplementedError(
-        "The DICOM data path (datasets.py / helpers.create_image_and_labels_for_dataset) is outside "
-        "the SPFF hot path (SURVEY §8(f) rank 4); feed tensors directly, e.g. "
-        "innovative3D.synthetic.SyntheticSPCCT")
+    """datasets.py:280-338 on the device (innovative3D/datasets.py)."""
+    from .datasets import MultiDicomDataModule3D as _DM
+    return _DM(*args, **kwargs)
 
 
 MultiDicomDataModule2D = MultiDicomDataModule3D

@@ -156,3 +156,76 @@ LOSS_REGISTRY = {
     "focal_plus_gradient": _out_of_scope("focal_plus_gradient"),
     "dice_ce_nnunet": _out_of_scope("dice_ce_nnunet"),
 }
+
+
+# ------------------------------------------------------------- data path ---
+# helpers.py:125-211 / 280-289, device-side: see
+# innovative3D/datasets.py and csrc/data.hip.
+def is_pixel_in_ellipse(x, y, roi):
+    """helpers.py:125-129."""
+    cx, cy = roi[0] + roi[2] / 2, roi[1] + roi[3] / 2
+    a, b = roi[2] / 2, roi[3] / 2
+    return ((x - cx) ** 2) / (a * a) + ((y - cy) ** 2) / (b * b) <= 1
+
+
+def generate_cumulative_grid_sizes(num_images, num_grid_sizes=10, cumulative_percentage=0.2):
+    """helpers.py:280-289 (module-level random, same draws)."""
+    import random
+    per = int(num_images * cumulative_percentage)
+    out = []
+    for gs in range(1, num_grid_sizes + 1):
+        out.extend([gs] * per)
+    rem = num_images - len(out)
+    if rem > 0:
+        out.extend(random.choices(range(1, num_grid_sizes + 1), k=rem))
+    random.shuffle(out)
+    return out
+
+
+def read_dicom_frames(path):
+    """Decoded frames [n, h, w] of one DICOM file (pydicom, as helpers.py:190-191)."""
+    try:
+        import pydicom  # noqa: F401
+    except ImportError as e:  # pragma: no cover - pydicom is absent offline
+        raise ImportError("reading DICOM needs pydicom; pass frames_reader=callable(path) -> "
+                          "array [n, h, w] to create_image_and_labels_for_dataset instead") from e
+    return pydicom.dcmread(path).pixel_array
+
+
+def create_image_and_labels_for_dataset(cfg, num_frames, frames_reader=None, device=None):
+    """helpers.py:132-211 on the device: every DICOM under cfg["dir"] -> frames resized to
+    IMAGE_HEIGHT x IMAGE_WIDTH (antialiased bilinear, TF.resize) and the ellipse-ROI label
+    map (later ROIs overwrite).  Returns (images [N,F,H,W] fp32, labels [N,F,H,W] int64) on
+    the device.  A list of configs is concatenated, as in the reference."""
+    import os
+    from pathlib import Path
+    from .config import IMAGE_HEIGHT, IMAGE_WIDTH, global_label_names
+    if isinstance(cfg, (list, tuple)):
+        parts = [create_image_and_labels_for_dataset(c, num_frames, frames_reader, device)
+                 for c in cfg]
+        return torch.cat([p[0] for p in parts]), torch.cat([p[1] for p in parts])
+    dev = device or torch.device("cuda")
+    folder = os.path.expanduser(os.path.expandvars(str(Path(cfg["dir"]).resolve())))
+    if not os.path.isdir(folder):
+        raise FileNotFoundError(f"Images folder not found or not a directory: {folder}")
+    paths = []
+    for root, _, files in os.walk(folder):
+        paths += [os.path.join(root, f) for f in files if f.lower().endswith((".dcm", ".dicom"))]
+    if not paths:
+        raise FileNotFoundError(f"No DICOM files (.dcm/.dicom) found under: {folder}")
+    sx, sy = IMAGE_WIDTH / 1300.0, IMAGE_HEIGHT / 1300.0
+    ox, oy = cfg["offset"]
+    rois = []
+    for (x, y, w, h, lab_str) in cfg["original_rois"]:
+        lab = next((i for i, n in global_label_names.items() if n == lab_str), 0)
+        rois.append((int((x + ox) * sx), int((y + oy) * sy), int(w * sx), int(h * sy), lab))
+    rois_t = torch.tensor(rois, dtype=torch.int32).reshape(-1, 5).to(dev)
+    reader = frames_reader or read_dicom_frames
+    imgs, lbls = [], []
+    for fn in paths:
+        frames = np.asarray(reader(fn))
+        n = min(frames.shape[0], num_frames)
+        fr = torch.from_numpy(frames[:n].astype(np.float32)).to(dev)
+        imgs.append(E.resize_bilinear_aa(fr, IMAGE_HEIGHT, IMAGE_WIDTH))
+        lbls.append(E.rasterize_ellipses(rois_t, n, IMAGE_HEIGHT, IMAGE_WIDTH))
+    return torch.stack(imgs), torch.stack(lbls)
