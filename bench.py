@@ -290,7 +290,10 @@ def bench_swin(args, world, rank, device):
         logits = lit(x)
         loss = M._SwinLoss.apply(logits, y, K, 255, False, 0.5)
         loss.backward()
-        allreduce_gradients(params)
+        if world > 1:  # DDP semantics (the reference trains it under Lightning DDP): mean
+            allreduce_gradients(params)
+            for q in params:
+                q.grad.div_(world)
         return loss
 
     for _ in range(args.warmup):
