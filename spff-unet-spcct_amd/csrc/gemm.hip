@@ -352,7 +352,8 @@ template <int TM, int TN, bool UP>
 __global__ __launch_bounds__(256) void k_xty(const float* __restrict__ X, int ldx, int K1,
                                              const float* __restrict__ Y, int ldy, int N, UpGeo g,
                                              float* __restrict__ part, float* __restrict__ csum,
-                                             int64_t M, int64_t rps, int k1pad, int npad) {
+                                             int64_t M, int64_t rps, int k1pad, int npad,
+                                             const float* __restrict__ X2, int ldx2, int xsplit) {
   constexpr int NE = TM * TN * 16;
   __shared__ float red[4][NE][64];
   __shared__ float cred[4][2][TN][32];
@@ -392,11 +393,16 @@ __global__ __launch_bounds__(256) void k_xty(const float* __restrict__ X, int ld
     for (int u = 0; u < U; ++u) {
       const int64_t v = vb + 2 * (p0 + 4 * u) + khalf;
       const bool vok = (p0 + 4 * u < npairs) && v < ve;
-      const int64_t xr = vok ? v * ldx + k10 + l32 : 0;
       int64_t yr = 0;
       if (vok) yr = UP ? up_high_base((uint32_t)v, g.D, g.Hl, g.Wl, g.nsub) * ldy : v * ldy;
 #pragma unroll
-      for (int t = 0; t < TM; ++t) xa[u][t] = (vok && kok[t]) ? X[xr + 32 * t] : 0.f;
+      for (int t = 0; t < TM; ++t) {
+        // X columns >= xsplit come from the second source (torch.cat([X, X2], 1) rows)
+        const int col = k10 + 32 * t + l32;
+        xa[u][t] = (vok && kok[t])
+                       ? (col < xsplit ? X[v * ldx + col] : X2[v * ldx2 + (col - xsplit)])
+                       : 0.f;
+      }
 #pragma unroll
       for (int t = 0; t < TN; ++t) yb[u][t] = (vok && nok[t]) ? Y[yr + noff[t]] : 0.f;
     }
@@ -465,7 +471,8 @@ static size_t xty_ws_bytes(int64_t M, int K1, int N) {
 // X rows [M][ldx] (K1 used), Y rows [M][ldy] (N used) or the up-conv gather
 static hipError_t launch_xty(const float* X, int ldx, int K1, const float* Y, int ldy, int N,
                              const UpGeo* up, int64_t M, int Cout, int mode, float* dw, float* db,
-                             float* ws, hipStream_t s);
+                             float* ws, hipStream_t s, const float* X2 = nullptr, int ldx2 = 0,
+                             int xsplit = 1 << 30);
 
 // dW layouts: mode 0 = upconv W[Cin][Cout][1][2][2] from C[ci][ij*Cout+co]
 //             mode 2 = upconv W[Cin][Cout][2][2][2] from C[ci][ij*Cout+co]
@@ -520,7 +527,8 @@ __global__ __launch_bounds__(256) void k_atb_reduce(const float* __restrict__ pa
 
 static hipError_t launch_xty(const float* X, int ldx, int K1, const float* Y, int ldy, int N,
                              const UpGeo* up, int64_t M, int Cout, int mode, float* dw, float* db,
-                             float* ws, hipStream_t s) {
+                             float* ws, hipStream_t s, const float* X2, int ldx2, int xsplit) {
+  if (!X2) X2 = X;
   if (M >= (int64_t(1) << 31)) return hipErrorInvalidValue;
   const XtyPlan p = xty_plan(M, K1, N);
   float* part = ws;
@@ -529,7 +537,7 @@ static hipError_t launch_xty(const float* X, int ldx, int K1, const float* Y, in
   const UpGeo g = up ? *up : UpGeo{1, 1, 1, 4, 1};
 #define SPFF_XTY(TM_, TN_, UP_)                                                                   \
   hipLaunchKernelGGL((k_xty<TM_, TN_, UP_>), grid, dim3(256), 0, s, X, ldx, K1, Y, ldy, N, g,     \
-                     part, csum, M, p.rps, p.k1pad, p.npad)
+                     part, csum, M, p.rps, p.k1pad, p.npad, X2, ldx2, xsplit)
   if (up) {
     if (p.tm == 2 && p.tn == 2) SPFF_XTY(2, 2, true);
     else if (p.tm == 2) SPFF_XTY(2, 1, true);
@@ -780,9 +788,10 @@ hipError_t linear_wgrad(const float* x, int ldx, int K, const float* dy, int ldd
 }
 hipError_t linear_wgrad2(const Src2& x, int K, const float* dy, int lddy, int N, float* dw,
                          float* db, int64_t M, float* ws, hipStream_t s) {
-  LoadRows2 X{x, K, M};
-  LoadRowsScalar Y{dy, lddy, N, M};
-  return launch_atb(X, Y, M, K, N, N, 1, dw, db, ws, s);
+  // streaming X^T Y with the two-source column split (the 64 x 64 LDS tiles of
+  // k_atb measured 3-4x slower at K = 24, N = 12)
+  return launch_xty(x.p0, x.ld0, K, dy, lddy, N, nullptr, M, N, 1, dw, db, ws, s, x.p1, x.ld1,
+                    x.split);
 }
 hipError_t patch_embed_wgrad(const float* x, int ldx, int Cin, int D, int H, int W, int B,
                              const float* dy, int N, float* dw, float* db, float* ws,

@@ -157,6 +157,108 @@ __global__ __launch_bounds__(256) void k_ln_bwd(LnSrc src, int C, const float* _
   }
 }
 
+// Narrow rows (C = 12, 24: the first Swin stages): one THREAD per row, the row in
+// registers (float4 loads), no cross-lane reductions; 64 lanes cover 64 rows.
+template <int C>
+__global__ __launch_bounds__(256) void k_ln_fwd_t(const float* __restrict__ x, int ldx,
+                                                  const float* __restrict__ g,
+                                                  const float* __restrict__ bta,
+                                                  float* __restrict__ y, int ldy,
+                                                  float* __restrict__ mu, float* __restrict__ rs,
+                                                  int64_t M) {
+  const int64_t m = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (m >= M) return;
+  float v[C];
+#pragma unroll
+  for (int c = 0; c < C; c += 4) {
+    const float4 t = *reinterpret_cast<const float4*>(x + m * ldx + c);
+    v[c] = t.x; v[c + 1] = t.y; v[c + 2] = t.z; v[c + 3] = t.w;
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < C; ++c) s += v[c];
+  const float mean = s / (float)C;
+  float q = 0.f;
+#pragma unroll
+  for (int c = 0; c < C; ++c) q += (v[c] - mean) * (v[c] - mean);
+  const float rstd = 1.f / sqrtf(q / (float)C + 1e-5f);
+#pragma unroll
+  for (int c = 0; c < C; c += 4) {
+    float o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      o[k] = (v[c + k] - mean) * rstd;
+      if (g) o[k] = o[k] * g[c + k] + bta[c + k];
+    }
+    *reinterpret_cast<float4*>(y + m * ldy + c) = make_float4(o[0], o[1], o[2], o[3]);
+  }
+  mu[m] = mean;
+  rs[m] = rstd;
+}
+
+constexpr int LNT_R = 8;  // rows per thread (strided by 256): 2048 rows per block
+template <int C>
+__global__ __launch_bounds__(256) void k_ln_bwd_t(const float* __restrict__ x, int ldx,
+                                                  const float* __restrict__ g,
+                                                  const float* __restrict__ mu,
+                                                  const float* __restrict__ rs,
+                                                  const float* __restrict__ dy, int lddy,
+                                                  float* __restrict__ dx, int lddx,
+                                                  const float* __restrict__ res, int ldres,
+                                                  float* __restrict__ part, int64_t M) {
+  float pg[C], pb[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) pg[c] = pb[c] = 0.f;
+  for (int r = 0; r < LNT_R; ++r) {
+    const int64_t m = (int64_t)blockIdx.x * 256 * LNT_R + r * 256 + threadIdx.x;
+    if (m >= M) break;
+    const float mean = mu[m], rstd = rs[m];
+    float xh[C], gd[C];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int c = 0; c < C; c += 4) {
+      const float4 tx = *reinterpret_cast<const float4*>(x + m * ldx + c);
+      const float4 td = *reinterpret_cast<const float4*>(dy + m * lddy + c);
+      const float xv[4] = {tx.x, tx.y, tx.z, tx.w}, dv[4] = {td.x, td.y, td.z, td.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        xh[c + k] = (xv[k] - mean) * rstd;
+        gd[c + k] = g ? dv[k] * g[c + k] : dv[k];
+        pg[c + k] += dv[k] * xh[c + k];
+        pb[c + k] += dv[k];
+        s1 += gd[c + k];
+        s2 += gd[c + k] * xh[c + k];
+      }
+    }
+    const float c1 = s1 / (float)C, c2 = s2 / (float)C;
+#pragma unroll
+    for (int c = 0; c < C; c += 4) {
+      float o[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) o[k] = rstd * (gd[c + k] - c1 - xh[c + k] * c2);
+      if (res) {
+        const float4 t = *reinterpret_cast<const float4*>(res + m * ldres + c);
+        o[0] += t.x; o[1] += t.y; o[2] += t.z; o[3] += t.w;
+      }
+      *reinterpret_cast<float4*>(dx + m * lddx + c) = make_float4(o[0], o[1], o[2], o[3]);
+    }
+  }
+  if (!part) return;
+  __shared__ float red[2 * C][257];
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    red[c][threadIdx.x] = pg[c];
+    red[C + c][threadIdx.x] = pb[c];
+  }
+  __syncthreads();
+  for (int st = 128; st > 0; st >>= 1) {
+    if (threadIdx.x < st)
+      for (int i = 0; i < 2 * C; ++i) red[i][threadIdx.x] += red[i][threadIdx.x + st];
+    __syncthreads();
+  }
+  if (threadIdx.x < 2 * C) part[(int64_t)blockIdx.x * 2 * C + threadIdx.x] = red[threadIdx.x][0];
+}
+
 // out[i] (+)= sum over k < n of part[k*stride + i] (i < count): one workgroup per
 // column, each thread a strided partial sum over k, then a fixed LDS tree --
 // deterministic, and parallel over k (n runs to thousands of blocks / windows).
@@ -204,6 +306,15 @@ hipError_t col_reduce(const float* part, int n, int64_t stride, int count, float
 hipError_t ln_fwd(const float* x, int ldx, int C, const float* g, const float* b, float* y,
                   int ldy, float* mu, float* rs, int64_t M, hipStream_t s) {
   if (C > 64 * LN_NJ) return hipErrorInvalidValue;
+  const bool vec = ldx % 4 == 0 && ldy % 4 == 0;
+  if (vec && (C == 12 || C == 24)) {
+    const dim3 gr((unsigned)cdiv64(M, 256));
+    if (C == 12)
+      hipLaunchKernelGGL(k_ln_fwd_t<12>, gr, dim3(256), 0, s, x, ldx, g, b, y, ldy, mu, rs, M);
+    else
+      hipLaunchKernelGGL(k_ln_fwd_t<24>, gr, dim3(256), 0, s, x, ldx, g, b, y, ldy, mu, rs, M);
+    return hipGetLastError();
+  }
   LnSrc src{x, ldx, C, 0, 0, 0};
   hipLaunchKernelGGL(k_ln_fwd<0>, dim3((unsigned)cdiv64(M, 4)), dim3(256), 0, s, src, C, g, b, y,
                      ldy, mu, rs, M);
@@ -222,7 +333,7 @@ hipError_t ln_merge_fwd(const float* xf, int Cf, int B, int D, int H, int W, con
 }
 
 size_t ln_bwd_ws_bytes(int64_t M, int C) {
-  return (size_t)cdiv64(M, LN_RPB) * 2 * C * sizeof(float);
+  return (size_t)std::max(cdiv64(M, LN_RPB), cdiv64(M, 256 * LNT_R)) * 2 * C * sizeof(float);
 }
 
 // dgb (may be null): [2][C] = dgamma, dbeta (written)
@@ -230,6 +341,20 @@ hipError_t ln_bwd(const float* x, int ldx, int C, const float* g, const float* m
                   const float* rs, const float* dy, int lddy, float* dx, int lddx,
                   const float* res, int ldres, float* dgb, float* ws, int64_t M, hipStream_t s) {
   if (C > 64 * LN_NJ) return hipErrorInvalidValue;
+  const bool vec = ldx % 4 == 0 && lddy % 4 == 0 && lddx % 4 == 0 && (!res || ldres % 4 == 0);
+  if (vec && (C == 12 || C == 24)) {
+    const int64_t nbt = cdiv64(M, 256 * LNT_R);
+    float* pt = dgb ? ws : nullptr;
+    if (C == 12)
+      hipLaunchKernelGGL(k_ln_bwd_t<12>, dim3((unsigned)nbt), dim3(256), 0, s, x, ldx, g, mu, rs,
+                         dy, lddy, dx, lddx, res, ldres, pt, M);
+    else
+      hipLaunchKernelGGL(k_ln_bwd_t<24>, dim3((unsigned)nbt), dim3(256), 0, s, x, ldx, g, mu, rs,
+                         dy, lddy, dx, lddx, res, ldres, pt, M);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || !dgb) return e;
+    return col_reduce(ws, (int)nbt, 2 * C, 2 * C, dgb, 0, s);
+  }
   LnSrc src{x, ldx, C, 0, 0, 0};
   const int64_t nb = cdiv64(M, LN_RPB);
   hipLaunchKernelGGL(k_ln_bwd<0>, dim3((unsigned)nb), dim3(256), 0, s, src, C, g, mu, rs, dy, lddy,
