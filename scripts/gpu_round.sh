@@ -27,6 +27,9 @@ for step in "$@"; do
     unet3d) timeout -k 10 600 python -u -m pytest tests/test_gpu_unet3d.py -m gpu -x -v -s --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_unet3d.log 2>&1; rc=$? ;;
     split) timeout -k 10 600 python -m pytest tests/test_gpu_ops.py -m gpu -q -p no:cacheprovider -k split > gpurun_out/pytest_split.log 2>&1; rc=$? ;;
     kpmc) (cd "$GRAFT_REPO_ROOT" && timeout -k 10 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT --kernel-trace --output-format csv -d gpurun_out/kpmc -o run -- python3 scripts/kbench.py --iters 1 --layers ${KPMC_LAYERS:-dec1} --math ${KPMC_MATH:-bf16x6} > gpurun_out/kpmc.log 2>&1 && timeout -k 10 600 rocprofv3 --pmc GRBM_GUI_ACTIVE GRBM_COUNT SQ_WAIT_INST_LDS SQ_LDS_IDX_ACTIVE --kernel-trace --output-format csv -d gpurun_out/kpmc2 -o run -- python3 scripts/kbench.py --iters 1 --layers ${KPMC_LAYERS:-dec1} --math ${KPMC_MATH:-bf16x6} >> gpurun_out/kpmc.log 2>&1); rc=$? ;;
+    swin) timeout -k 10 600 python -u -m pytest tests/test_gpu_swin.py -m gpu -x -v -s --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_swin.log 2>&1; rc=$? ;;
+    benchswin) timeout -k 10 600 python bench.py --workload swin --steps 10 --warmup 3 > gpurun_out/bench_swin.log 2>&1; rc=$? ;;
+    profswin) (cd "$GRAFT_REPO_ROOT" && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profswin -o run --output-format csv -- python3 bench.py --workload swin --steps 3 --warmup 1 --cpu-baseline skip > gpurun_out/profswin.log 2>&1); rc=$? ;;
     *) echo "unknown step $step"; rc=2 ;;
   esac
   echo "[gpu_round] $step rc=$rc" | tee -a gpurun_out/steps.log

@@ -36,20 +36,26 @@ __device__ __forceinline__ void merge_off(int q, int& od, int& oh, int& ow) {
 struct LnSrc {
   const float* x; int ldx, Cf, D, H, W;
 };
+// split into a per-row base and a per-channel offset so the (64-bit) row
+// decomposition runs once per row, not once per element
 template <int MODE>
-__device__ __forceinline__ float ln_load(const LnSrc& s, int64_t m, int c) {
-  if (MODE == 0) return s.x[m * s.ldx + c];
-  const int q = c / s.Cf, cf = c - q * s.Cf;
+__device__ __forceinline__ int64_t ln_base(const LnSrc& s, int64_t m) {
+  if (MODE == 0) return m * s.ldx;
   const int Wl = s.W >> 1, Hl = s.H >> 1, Dl = s.D >> 1;
   int64_t t = m;
   const int w = (int)(t % Wl); t /= Wl;
   const int h = (int)(t % Hl); t /= Hl;
   const int d = (int)(t % Dl);
   const int64_t b = t / Dl;
+  return (((b * s.D + 2 * d) * s.H + 2 * h) * (int64_t)s.W + 2 * w) * s.Cf;
+}
+template <int MODE>
+__device__ __forceinline__ int64_t ln_off(const LnSrc& s, int c) {
+  if (MODE == 0) return c;
+  const int q = c / s.Cf, cf = c - q * s.Cf;
   int od, oh, ow;
   merge_off(q, od, oh, ow);
-  const int64_t v = ((b * s.D + 2 * d + od) * s.H + 2 * h + oh) * (int64_t)s.W + 2 * w + ow;
-  return s.x[v * s.Cf + cf];
+  return ((int64_t)(od * s.H + oh) * s.W + ow) * s.Cf + cf;
 }
 constexpr int LN_NJ = 12;  // channels per lane: C <= 768
 }  // namespace
@@ -65,10 +71,11 @@ __global__ __launch_bounds__(256) void k_ln_fwd(LnSrc src, int C, const float* _
   if (m >= M) return;
   float v[LN_NJ];
   float s = 0.f;
+  const float* xr = src.x + ln_base<MODE>(src, m);
 #pragma unroll
   for (int j = 0; j < LN_NJ; ++j) {
     const int c = lane + 64 * j;
-    v[j] = c < C ? ln_load<MODE>(src, m, c) : 0.f;
+    v[j] = c < C ? xr[ln_off<MODE>(src, c)] : 0.f;
     s += v[j];
   }
   const float mean = wave_sum(s) / (float)C;
@@ -97,7 +104,13 @@ __global__ __launch_bounds__(256) void k_ln_fwd(LnSrc src, int C, const float* _
 
 // dx = rstd * (dy*g - mean(dy*g) - xhat * mean(dy*g*xhat)) [+ res]; per-block
 // partial sums of dy*xhat and dy (dgamma, dbeta) over the block's rows
-constexpr int LN_RPB = 128;  // rows per block (4 waves x 32)
+// rows per block: a multiple of the 4 waves, shrunk (as a function of M only,
+// so the partial-sum order stays fixed) until the grid has >= 4096 blocks
+inline int ln_rpb(int64_t M) {
+  int r = 128;
+  while (r > 8 && cdiv64(M, r) < 4096) r >>= 1;
+  return r;
+}
 template <int MODE>
 __global__ __launch_bounds__(256) void k_ln_bwd(LnSrc src, int C, const float* __restrict__ g,
                                                 const float* __restrict__ mu,
@@ -105,16 +118,24 @@ __global__ __launch_bounds__(256) void k_ln_bwd(LnSrc src, int C, const float* _
                                                 const float* __restrict__ dy, int lddy,
                                                 float* __restrict__ dx, int lddx,
                                                 const float* __restrict__ res, int ldres,
-                                                float* __restrict__ part, int64_t M) {
+                                                float* __restrict__ part, int64_t M,
+                                                int rpb) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float pg[LN_NJ], pb[LN_NJ];
 #pragma unroll
   for (int j = 0; j < LN_NJ; ++j) pg[j] = pb[j] = 0.f;
-  const int64_t r0 = (int64_t)blockIdx.x * LN_RPB;
-  for (int rr = wave; rr < LN_RPB; rr += 4) {
+  const int64_t r0 = (int64_t)blockIdx.x * rpb;
+  int64_t off[LN_NJ];
+#pragma unroll
+  for (int j = 0; j < LN_NJ; ++j) {
+    const int c = lane + 64 * j;
+    off[j] = c < C ? ln_off<MODE>(src, c) : 0;
+  }
+  for (int rr = wave; rr < rpb; rr += 4) {
     const int64_t m = r0 + rr;
     if (m >= M) break;
     const float mean = mu[m], rstd = rs[m];
+    const float* xr = src.x + ln_base<MODE>(src, m);
     float xh[LN_NJ], gd[LN_NJ];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -123,7 +144,7 @@ __global__ __launch_bounds__(256) void k_ln_bwd(LnSrc src, int C, const float* _
       xh[j] = 0.f; gd[j] = 0.f;
       if (c < C) {
         const float d = dy[m * lddy + c];
-        xh[j] = (ln_load<MODE>(src, m, c) - mean) * rstd;
+        xh[j] = (xr[off[j]] - mean) * rstd;
         gd[j] = g ? d * g[c] : d;
         pg[j] += d * xh[j];
         pb[j] += d;
@@ -333,7 +354,7 @@ hipError_t ln_merge_fwd(const float* xf, int Cf, int B, int D, int H, int W, con
 }
 
 size_t ln_bwd_ws_bytes(int64_t M, int C) {
-  return (size_t)std::max(cdiv64(M, LN_RPB), cdiv64(M, 256 * LNT_R)) * 2 * C * sizeof(float);
+  return (size_t)std::max(cdiv64(M, ln_rpb(M)), cdiv64(M, 256 * LNT_R)) * 2 * C * sizeof(float);
 }
 
 // dgb (may be null): [2][C] = dgamma, dbeta (written)
@@ -356,9 +377,10 @@ hipError_t ln_bwd(const float* x, int ldx, int C, const float* g, const float* m
     return col_reduce(ws, (int)nbt, 2 * C, 2 * C, dgb, 0, s);
   }
   LnSrc src{x, ldx, C, 0, 0, 0};
-  const int64_t nb = cdiv64(M, LN_RPB);
+  const int rpb = ln_rpb(M);
+  const int64_t nb = cdiv64(M, rpb);
   hipLaunchKernelGGL(k_ln_bwd<0>, dim3((unsigned)nb), dim3(256), 0, s, src, C, g, mu, rs, dy, lddy,
-                     dx, lddx, res, ldres, dgb ? ws : nullptr, M);
+                     dx, lddx, res, ldres, dgb ? ws : nullptr, M, rpb);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || !dgb) return e;
   return col_reduce(ws, (int)nb, 2 * C, 2 * C, dgb, 0, s);
@@ -370,9 +392,10 @@ hipError_t ln_merge_bwd(const float* xf, int Cf, int B, int D, int H, int W, con
   const int C = 8 * Cf;
   const int64_t M = (int64_t)B * (D / 2) * (H / 2) * (W / 2);
   LnSrc src{xf, Cf, Cf, D, H, W};
-  const int64_t nb = cdiv64(M, LN_RPB);
+  const int rpb = ln_rpb(M);
+  const int64_t nb = cdiv64(M, rpb);
   hipLaunchKernelGGL(k_ln_bwd<1>, dim3((unsigned)nb), dim3(256), 0, s, src, C, g, mu, rs, dy, C,
-                     dcat, C, nullptr, 0, ws, M);
+                     dcat, C, nullptr, 0, ws, M, rpb);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   return col_reduce(ws, (int)nb, 2 * C, 2 * C, dgb, 0, s);
