@@ -13,7 +13,7 @@
 
 namespace spff {
 
-constexpr int LOSS_GRID = 1024, LOSS_T = 256, KMAX = 32;
+constexpr int LOSS_GRID = 2048, LOSS_T = 256, KMAX = 32;
 
 __global__ void k_count_valid(const int64_t* __restrict__ lab, int64_t V, int ignore,
                               unsigned long long* __restrict__ cnt) {
@@ -31,6 +31,12 @@ __global__ void k_count_valid(const int64_t* __restrict__ lab, int64_t V, int ig
   if (threadIdx.x == 0) atomicAdd(cnt, red[0]);
 }
 
+// Each wave owns 64 consecutive voxels at a time: their 64 x K logits (one
+// contiguous run) are staged into the wave's LDS slice with coalesced loads, a
+// thread per voxel reads its row from LDS (odd K: conflict-free stride) and
+// writes its dlogits row back in place, and the wave stores the run coalesced.
+// No per-thread K-arrays (a runtime-K register array would live in scratch).
+constexpr int LOSS_WAVES = LOSS_T / 64;
 template <bool WITH_CE>
 __global__ __launch_bounds__(LOSS_T) void k_loss(const float* __restrict__ x,
                                                  const int64_t* __restrict__ lab, int64_t V, int K,
@@ -42,7 +48,10 @@ __global__ __launch_bounds__(LOSS_T) void k_loss(const float* __restrict__ x,
                                                  const float* __restrict__ cw, int clamp1) {
   __shared__ unsigned int hist[KMAX * (KMAX + 1)];
   __shared__ double red[LOSS_T];
+  extern __shared__ __attribute__((aligned(16))) float stage[];  // [LOSS_WAVES][64 K]
   const int K1 = K + 1;  // column K = label outside [0,K) (not ignored)
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  float* sx = stage + wv * 64 * K;
   for (int i = threadIdx.x; i < K * K1; i += LOSS_T) hist[i] = 0;
   __syncthreads();
   // clamp1: the 3DUNet's weighted CE divides by max(N_valid, 1) (models.py:796)
@@ -50,46 +59,59 @@ __global__ __launch_bounds__(LOSS_T) void k_loss(const float* __restrict__ x,
       WITH_CE ? 1.f / (float)(clamp1 && *count < 1 ? (int64_t)1 : *count) : 0.f;
   double ce = 0.0;
   unsigned int bad = 0;
-  for (int64_t v = blockIdx.x * (int64_t)LOSS_T + threadIdx.x; v < V;
-       v += (int64_t)gridDim.x * LOSS_T) {
-    const float* xv = x + v * K;
-    float xs[KMAX];
-    float m = xv[0];
-    int am = 0;
-    xs[0] = m;
-    for (int k = 1; k < K; ++k) {
-      const float t = xv[k];
-      xs[k] = t;
-      if (t > m || (isnan(t) && !isnan(m))) { m = t; am = k; }
-    }
-    const int64_t y = lab[v];
-    const bool valid = (y != ignore);
-    if (valid && (y < 0 || y >= K)) {
-      ++bad;
-      atomicAdd(&hist[am * K1 + K], 1u);
-      if (WITH_CE) for (int k = 0; k < K; ++k) dx[v * K + k] = 0.f;
-      continue;
-    }
-    if (valid) atomicAdd(&hist[am * K1 + (int)y], 1u);
-    if (WITH_CE) {
-      float* dv = dx + v * K;
-      if (valid) {
-        float ssum = 0.f;
-        for (int k = 0; k < K; ++k) ssum += expf(xs[k] - m);
-        const float lse = m + logf(ssum);
-        // class weights (F.cross_entropy(weight=w), reduction='none'): w[y] * nll
-        const float wy = cw ? cw[(int)y] : 1.f;
-        ce += cw ? (double)(wy * (lse - xs[(int)y])) : (double)(lse - xs[(int)y]);
-        const float inv = 1.f / ssum;
-        for (int k = 0; k < K; ++k) {
-          const float p = expf(xs[k] - m) * inv;
-          dv[k] = cw ? wy * (p - (k == (int)y ? 1.f : 0.f)) * invN
-                     : (p - (k == (int)y ? 1.f : 0.f)) * invN;
-        }
+  const int64_t ngroups = (V + 63) / 64;
+  for (int64_t grp = (int64_t)blockIdx.x * LOSS_WAVES + wv; grp < ngroups;
+       grp += (int64_t)gridDim.x * LOSS_WAVES) {
+    const int64_t v0 = grp * 64;
+    const int nv = (int)(V - v0 < 64 ? V - v0 : 64);
+    const int nf = nv * K;
+    wave_copy_rows(sx, x + v0 * K, nf, lane);
+    wave_lds_sync();
+    if (lane < nv) {
+      const int64_t v = v0 + lane;
+      float* xr = sx + lane * K;
+      float m = xr[0];
+      int am = 0;
+      for (int k = 1; k < K; ++k) {
+        const float t = xr[k];
+        if (t > m || (isnan(t) && !isnan(m))) { m = t; am = k; }
+      }
+      const int64_t y = lab[v];
+      const bool valid = (y != ignore);
+      if (valid && (y < 0 || y >= K)) {
+        ++bad;
+        atomicAdd(&hist[am * K1 + K], 1u);
+        if (WITH_CE) for (int k = 0; k < K; ++k) xr[k] = 0.f;
       } else {
-        for (int k = 0; k < K; ++k) dv[k] = 0.f;
+        if (valid) atomicAdd(&hist[am * K1 + (int)y], 1u);
+        if (WITH_CE) {
+          if (valid) {
+            const float xy = xr[(int)y];
+            float ssum = 0.f;
+            for (int k = 0; k < K; ++k) {  // exp once, kept in the row
+              const float e = expf(xr[k] - m);
+              xr[k] = e;
+              ssum += e;
+            }
+            const float lse = m + logf(ssum);
+            // class weights (F.cross_entropy(weight=w), reduction='none'): w[y] * nll
+            const float wy = cw ? cw[(int)y] : 1.f;
+            ce += cw ? (double)(wy * (lse - xy)) : (double)(lse - xy);
+            const float inv = 1.f / ssum;
+            for (int k = 0; k < K; ++k) {
+              const float p = xr[k] * inv;
+              xr[k] = cw ? wy * (p - (k == (int)y ? 1.f : 0.f)) * invN
+                         : (p - (k == (int)y ? 1.f : 0.f)) * invN;
+            }
+          } else {
+            for (int k = 0; k < K; ++k) xr[k] = 0.f;
+          }
+        }
       }
     }
+    wave_lds_sync();
+    if (WITH_CE) wave_copy_rows(dx + v0 * K, sx, nf, lane);
+    wave_lds_sync();  // the next group overwrites the slice
   }
   if (WITH_CE) {
     red[threadIdx.x] = ce;
@@ -112,20 +134,34 @@ __global__ void k_loss_final(const double* __restrict__ part, int nparts,
                              const int64_t* __restrict__ count,
                              const unsigned long long* __restrict__ conf, int K, double smooth,
                              float* __restrict__ out4, int clamp1) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  double s = 0.0;
-  for (int i = 0; i < nparts; ++i) s += part[i];
-  const double N = (clamp1 && *count < 1) ? 1.0 : (double)(*count);
-  const float ce = (float)(s / N);
-  double dsum = 0.0;
+  // the partials: per-thread strided sums, then a fixed tree (deterministic)
+  __shared__ double red[LOSS_T];
+  double t = 0.0;
+  for (int i = threadIdx.x; i < nparts; i += LOSS_T) t += part[i];
+  red[threadIdx.x] = t;
+  __syncthreads();
+  for (int o = LOSS_T / 2; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  // per-class hard-Dice terms, one thread per class, summed in class order
+  __shared__ double term[KMAX];
   const int K1 = K + 1;
-  for (int c = 1; c < K; ++c) {
+  const int c = threadIdx.x;
+  if (c >= 1 && c < K) {
     double tp = (double)conf[c * K1 + c], rowp = 0.0, coll = 0.0;
     for (int j = 0; j < K1; ++j) rowp += (double)conf[c * K1 + j];
     for (int j = 0; j < K; ++j) coll += (double)conf[j * K1 + c];
     const double fp = rowp - tp, fn = coll - tp;
-    dsum += (2.0 * tp + smooth) / (2.0 * tp + fp + fn + smooth);
+    term[c] = (2.0 * tp + smooth) / (2.0 * tp + fp + fn + smooth);
   }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  const double s = red[0];
+  const double N = (clamp1 && *count < 1) ? 1.0 : (double)(*count);
+  const float ce = (float)(s / N);
+  double dsum = 0.0;
+  for (int cc = 1; cc < K; ++cc) dsum += term[cc];
   const double macro = K > 1 ? dsum / (double)(K - 1) : 1.0;
   const double dice_loss = 1.0 - macro;
   out4[0] = ce;
@@ -133,6 +169,8 @@ __global__ void k_loss_final(const double* __restrict__ part, int nparts,
   out4[2] = (float)dice_loss;
   out4[3] = (float)N;
 }
+
+static size_t loss_lds(int K) { return (size_t)LOSS_WAVES * 64 * K * sizeof(float); }
 
 size_t loss_ws_bytes(int64_t V, int K) {
   (void)V; (void)K;
@@ -165,11 +203,11 @@ hipError_t loss_fwd(const float* logits, const int64_t* labels, int64_t V, int K
   }
   if ((e = hipMemsetAsync(conf, 0, sizeof(int64_t) * K * (K + 1), s)) != hipSuccess) return e;
   if ((e = hipMemsetAsync(nbad, 0, sizeof(unsigned long long), s)) != hipSuccess) return e;
-  hipLaunchKernelGGL(k_loss<true>, dim3(LOSS_GRID), dim3(LOSS_T), 0, s, logits, labels, V, K,
-                     ignore, cptr, dlogits, reinterpret_cast<unsigned long long*>(conf), part,
-                     nbad, class_w, clamp1);
+  hipLaunchKernelGGL(k_loss<true>, dim3(LOSS_GRID), dim3(LOSS_T), loss_lds(K), s, logits, labels,
+                     V, K, ignore, cptr, dlogits, reinterpret_cast<unsigned long long*>(conf),
+                     part, nbad, class_w, clamp1);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  hipLaunchKernelGGL(k_loss_final, dim3(1), dim3(64), 0, s, part, LOSS_GRID, cptr,
+  hipLaunchKernelGGL(k_loss_final, dim3(1), dim3(LOSS_T), 0, s, part, LOSS_GRID, cptr,
                      reinterpret_cast<unsigned long long*>(conf), K, smooth, out4, clamp1);
   return hipGetLastError();
 }
@@ -179,8 +217,8 @@ hipError_t confusion_only(const float* logits, const int64_t* labels, int64_t V,
   if (K > KMAX || K < 1) return hipErrorInvalidValue;
   hipError_t e = hipMemsetAsync(conf, 0, sizeof(int64_t) * K * (K + 1), s);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_loss<false>, dim3(LOSS_GRID), dim3(LOSS_T), 0, s, logits, labels, V, K,
-                     ignore, nullptr, nullptr, reinterpret_cast<unsigned long long*>(conf),
+  hipLaunchKernelGGL(k_loss<false>, dim3(LOSS_GRID), dim3(LOSS_T), loss_lds(K), s, logits, labels,
+                     V, K, ignore, nullptr, nullptr, reinterpret_cast<unsigned long long*>(conf),
                      nullptr, nullptr, nullptr, 0);
   return hipGetLastError();
 }

@@ -288,4 +288,25 @@ hipError_t count_valid(const int64_t* labels, int64_t V, int ignore, int64_t* co
 hipError_t confusion_only(const float* logits, const int64_t* labels, int64_t V, int K,
                           int ignore, int64_t* conf, hipStream_t s);
 
+// ------------------------------------------------ wave-staged voxel rows --
+// The loss kernels read [V][K] channel-last rows (K = 13: 52 B per voxel).  A
+// wave copies the contiguous run of its 64 voxels between HBM and its LDS slice
+// with coalesced (float4 when aligned) accesses; threads then work on their own
+// row in LDS.  wave_lds_sync orders one wave's LDS writes before its reads by
+// other lanes (LDS executes a wave's instructions in order; the fence and
+// wave_barrier keep the compiler from moving accesses across it).
+__device__ __forceinline__ void wave_copy_rows(float* __restrict__ dst,
+                                               const float* __restrict__ src, int n, int lane) {
+  if ((((uintptr_t)src | (uintptr_t)dst) & 15) == 0 && (n & 3) == 0) {
+    for (int i = lane; i < (n >> 2); i += 64)
+      reinterpret_cast<float4*>(dst)[i] = reinterpret_cast<const float4*>(src)[i];
+  } else {
+    for (int i = lane; i < n; i += 64) dst[i] = src[i];
+  }
+}
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
 }  // namespace spff

@@ -506,69 +506,91 @@ hipError_t add_inplace(float* y, const float* x, int64_t n, hipStream_t s) {
 //   I = sum_v m p g, P = sum_v m p, G = sum_v g,  m = [y != ignore],
 //   g = onehot(y with ignored -> 0),  p = softmax(logits).
 constexpr int DL_T = 256, DL_GRID = 256, DL_KMAX = 32;
+// Per (block, sample) partial sums of I_k = sum p_k g_k, P_k = sum p_k, G_k =
+// sum g_k (g = one-hot of the label, ignored voxels counted at class 0 with p =
+// 0, as the oracle's one_hot of the zero-filled labels), the CE sum and the
+// valid count.  A wave stages 64 voxels' logit rows in its LDS slice
+// (coalesced), each lane turns its row into p in place, then lane l sums
+// column k = l % K over the rows r = l / K (mod 64 / K) -- three scalar
+// accumulators per lane instead of 3 K-arrays per thread.
 __global__ __launch_bounds__(DL_T) void k_dice_stats(const float* __restrict__ x,
                                                      const int64_t* __restrict__ lab, int64_t vps,
                                                      int K, int ignore,
                                                      double* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) float dsm[];
   const int b = blockIdx.y;
-  float I[DL_KMAX], P[DL_KMAX], G[DL_KMAX];
-#pragma unroll
-  for (int k = 0; k < DL_KMAX; ++k) I[k] = P[k] = G[k] = 0.f;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  float* sx = dsm + wv * 64 * K;
+  int* ys = reinterpret_cast<int*>(dsm + (DL_T / 64) * 64 * K) + wv * 64;
+  const int nset = 64 / K, kcol = lane % K, rset = lane / K;
+  const bool colane = rset < nset;
+  float I = 0.f, P = 0.f, G = 0.f;
   double ce = 0.0;
   unsigned cnt = 0;
-  for (int64_t v = blockIdx.x * (int64_t)DL_T + threadIdx.x; v < vps;
-       v += (int64_t)gridDim.x * DL_T) {
-    const int64_t gv = (int64_t)b * vps + v;
-    const float* xv = x + gv * K;
-    float xs[DL_KMAX];
-    float m = -INFINITY;
-#pragma unroll
-    for (int k = 0; k < DL_KMAX; ++k)
-      if (k < K) { xs[k] = xv[k]; m = fmaxf(m, xs[k]); }
-    float ssum = 0.f;
-#pragma unroll
-    for (int k = 0; k < DL_KMAX; ++k)
-      if (k < K) ssum += expf(xs[k] - m);
-    const int64_t y = lab[gv];
-    const bool valid = y != ignore;
-    const int yl = valid ? (int)y : 0;
-    const float inv = 1.f / ssum;
-#pragma unroll
-    for (int k = 0; k < DL_KMAX; ++k)
-      if (k < K) {
-        const float p = valid ? expf(xs[k] - m) * inv : 0.f;
-        const float gk = k == yl ? 1.f : 0.f;
-        I[k] += p * gk;
-        P[k] += p;
-        G[k] += gk;
+  const int64_t ngroups = (vps + 63) / 64;
+  for (int64_t grp = (int64_t)blockIdx.x * (DL_T / 64) + wv; grp < ngroups;
+       grp += (int64_t)gridDim.x * (DL_T / 64)) {
+    const int64_t v0 = grp * 64;
+    const int nv = (int)(vps - v0 < 64 ? vps - v0 : 64);
+    wave_copy_rows(sx, x + ((int64_t)b * vps + v0) * K, nv * K, lane);
+    wave_lds_sync();
+    if (lane < nv) {
+      const int64_t y = lab[(int64_t)b * vps + v0 + lane];
+      const bool valid = y != ignore;
+      float* xv = sx + lane * K;
+      float m = -INFINITY;
+      for (int k = 0; k < K; ++k) m = fmaxf(m, xv[k]);
+      const int yl = valid ? (int)y : 0;
+      const float xy = xv[yl];
+      float ssum = 0.f;
+      for (int k = 0; k < K; ++k) {  // exp once, kept in the row
+        const float e = expf(xv[k] - m);
+        xv[k] = e;
+        ssum += e;
       }
-    if (valid) {
-      ce += (double)(m + logf(ssum) - xs[yl]);
-      ++cnt;
+      if (valid) {
+        ce += (double)(m + logf(ssum) - xy);
+        ++cnt;
+      }
+      const float inv = 1.f / ssum;
+      for (int k = 0; k < K; ++k) xv[k] = valid ? xv[k] * inv : 0.f;
+      ys[lane] = yl;
     }
+    wave_lds_sync();
+    if (colane) {
+      for (int r = rset; r < nv; r += nset) {
+        const float p = sx[r * K + kcol];
+        const bool hit = ys[r] == kcol;
+        I += hit ? p : 0.f;
+        P += p;
+        G += hit ? 1.f : 0.f;
+      }
+    }
+    wave_lds_sync();  // the next group overwrites the slice
   }
+  __shared__ float rq[3][DL_T];
   __shared__ double red[DL_T];
+  rq[0][threadIdx.x] = colane ? I : 0.f;
+  rq[1][threadIdx.x] = colane ? P : 0.f;
+  rq[2][threadIdx.x] = colane ? G : 0.f;
   const int nq = 3 * K + 2;
-  for (int q = 0; q < nq; ++q) {
-    double val;
-    if (q < 3 * K) {
-      const int k = q % K, w = q / K;
-      float t = 0.f;
-#pragma unroll
-      for (int kk = 0; kk < DL_KMAX; ++kk)
-        if (kk == k) t = w == 0 ? I[kk] : (w == 1 ? P[kk] : G[kk]);
-      val = t;
-    } else {
-      val = q == 3 * K ? ce : (double)cnt;
-    }
-    red[threadIdx.x] = val;
+  double* out = part + ((int64_t)b * gridDim.x + blockIdx.x) * nq;
+  for (int q = 0; q < 2; ++q) {
+    red[threadIdx.x] = q == 0 ? ce : (double)cnt;
     __syncthreads();
     for (int st = DL_T / 2; st > 0; st >>= 1) {
       if (threadIdx.x < st) red[threadIdx.x] += red[threadIdx.x + st];
       __syncthreads();
     }
-    if (threadIdx.x == 0) part[((int64_t)b * gridDim.x + blockIdx.x) * nq + q] = red[0];
+    if (threadIdx.x == 0) out[3 * K + q] = red[0];
     __syncthreads();
+  }
+  if (threadIdx.x < 3 * K) {  // (quantity, class): waves, then row sets, in order
+    const int w = threadIdx.x / K, k = threadIdx.x % K;
+    double t = 0.0;
+    for (int ww = 0; ww < DL_T / 64; ++ww)
+      for (int j = 0; j < nset; ++j) t += (double)rq[w][ww * 64 + j * K + k];
+    out[threadIdx.x] = t;
   }
 }
 
@@ -623,47 +645,59 @@ __global__ void k_dice_final(const double* __restrict__ tot, int B, int K, int s
   scal[0] = N > 0 ? w / N : 0.0;
 }
 
+// dlogits = p (G - <p, G>) + (w / N)(p - g), G_k = alpha_k g_k + beta_k; rows
+// staged per wave as in k_dice_stats, overwritten in place, stored coalesced
 __global__ __launch_bounds__(DL_T) void k_dice_grad(const float* __restrict__ x,
                                                     const int64_t* __restrict__ lab, int64_t vps,
                                                     int64_t V, int K, int ignore,
                                                     const float* __restrict__ coef,
                                                     const double* __restrict__ scal,
                                                     float* __restrict__ dx) {
+  extern __shared__ __attribute__((aligned(16))) float dsm[];
   const float wN = (float)scal[0];
-  for (int64_t v = blockIdx.x * (int64_t)DL_T + threadIdx.x; v < V;
-       v += (int64_t)gridDim.x * DL_T) {
-    const int b = (int)(v / vps);
-    const float* xv = x + v * K;
-    float xs[DL_KMAX];
-    float m = -INFINITY;
-#pragma unroll
-    for (int k = 0; k < DL_KMAX; ++k)
-      if (k < K) { xs[k] = xv[k]; m = fmaxf(m, xs[k]); }
-    float ssum = 0.f;
-#pragma unroll
-    for (int k = 0; k < DL_KMAX; ++k)
-      if (k < K) { xs[k] = expf(xs[k] - m); ssum += xs[k]; }
-    const int64_t y = lab[v];
-    const bool valid = y != ignore;
-    float* dv = dx + v * K;
-    if (!valid) {
-      for (int k = 0; k < K; ++k) dv[k] = 0.f;
-      continue;
-    }
-    const float inv = 1.f / ssum;
-    float Gs[DL_KMAX];
-    float pg = 0.f;
-#pragma unroll
-    for (int k = 0; k < DL_KMAX; ++k)
-      if (k < K) {
-        xs[k] *= inv;  // p_k
-        const float2 cf = *reinterpret_cast<const float2*>(coef + ((int64_t)b * K + k) * 2);
-        Gs[k] = cf.x * (k == (int)y ? 1.f : 0.f) + cf.y;
-        pg += xs[k] * Gs[k];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  float* sx = dsm + wv * 64 * K;
+  const int64_t ngroups = (V + 63) / 64;
+  for (int64_t grp = (int64_t)blockIdx.x * (DL_T / 64) + wv; grp < ngroups;
+       grp += (int64_t)gridDim.x * (DL_T / 64)) {
+    const int64_t v0 = grp * 64;
+    const int nv = (int)(V - v0 < 64 ? V - v0 : 64);
+    wave_copy_rows(sx, x + v0 * K, nv * K, lane);
+    wave_lds_sync();
+    if (lane < nv) {
+      const int64_t v = v0 + lane;
+      const int64_t y = lab[v];
+      float* xv = sx + lane * K;  // logits in, dlogits out (in place)
+      if (y == ignore) {
+        for (int k = 0; k < K; ++k) xv[k] = 0.f;
+      } else {
+        const float2* cf = reinterpret_cast<const float2*>(coef) + (int64_t)(v / vps) * K;
+        const int yi = (int)y;
+        float m = -INFINITY;
+        for (int k = 0; k < K; ++k) m = fmaxf(m, xv[k]);
+        float ssum = 0.f;
+        for (int k = 0; k < K; ++k) {  // exp once, kept in the row
+          const float e = expf(xv[k] - m);
+          xv[k] = e;
+          ssum += e;
+        }
+        const float inv = 1.f / ssum;
+        float pg = 0.f;
+        for (int k = 0; k < K; ++k) {
+          const float2 c = cf[k];
+          pg += xv[k] * inv * (c.x * (k == yi ? 1.f : 0.f) + c.y);
+        }
+        for (int k = 0; k < K; ++k) {
+          const float2 c = cf[k];
+          const float pk = xv[k] * inv;
+          const float Gk = c.x * (k == yi ? 1.f : 0.f) + c.y;
+          xv[k] = pk * (Gk - pg) + wN * (pk - (k == yi ? 1.f : 0.f));
+        }
       }
-#pragma unroll
-    for (int k = 0; k < DL_KMAX; ++k)
-      if (k < K) dv[k] = xs[k] * (Gs[k] - pg) + wN * (xs[k] - (k == (int)y ? 1.f : 0.f));
+    }
+    wave_lds_sync();
+    wave_copy_rows(dx + v0 * K, sx, nv * K, lane);
+    wave_lds_sync();  // the next group overwrites the slice
   }
 }
 
@@ -680,7 +714,8 @@ hipError_t dice_ce_loss(const float* logits, const int64_t* labels, int B, int64
   double* tot = part + (size_t)B * DL_GRID * (3 * K + 2);
   double* scal = tot + (size_t)B * (3 * K + 2);
   float* coef = reinterpret_cast<float*>(scal + 8);
-  hipLaunchKernelGGL(k_dice_stats, dim3(DL_GRID, B), dim3(DL_T), 0, s, logits, labels, vps, K,
+  const size_t lds = (size_t)(DL_T / 64) * 64 * (K + 1) * sizeof(float);
+  hipLaunchKernelGGL(k_dice_stats, dim3(DL_GRID, B), dim3(DL_T), lds, s, logits, labels, vps, K,
                      ignore, part);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
@@ -691,8 +726,8 @@ hipError_t dice_ce_loss(const float* logits, const int64_t* labels, int B, int64
                      ce_weight, coef, out4, scal);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   const int64_t V = (int64_t)B * vps;
-  hipLaunchKernelGGL(k_dice_grad, dim3((unsigned)std::min<int64_t>(cdiv64(V, DL_T), 8192)),
-                     dim3(DL_T), 0, s, logits, labels, vps, V, K, ignore, coef, scal, dlogits);
+  hipLaunchKernelGGL(k_dice_grad, dim3((unsigned)std::min<int64_t>(cdiv64(V, DL_T), 2048)),
+                     dim3(DL_T), lds, s, logits, labels, vps, V, K, ignore, coef, scal, dlogits);
   return hipGetLastError();
 }
 
