@@ -430,12 +430,12 @@ __global__ __launch_bounds__(256, 1) void k_conv3d_wgrad(Src2 x, const float* __
   }
 }
 
-// 256 threads = 32 consecutive outputs (co fastest -> coalesced slab reads) x 8
-// split groups; group g sums splits g, g+8, ... in order, then a fixed-order LDS
+// Small layers (fewer than 1024 (ci, 32-co) tiles): one workgroup per 32
+// consecutive outputs (co fastest -> coalesced slab reads) x 8 split groups; group g sums splits g, g+8, ... in order, then a fixed-order LDS
 // combine: deterministic, and 8x more loads in flight than one thread per output.
-__global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ part,
-                                                      float* __restrict__ dw, int nsplit, int T,
-                                                      int kpad, int npad, int Cin, int Cout) {
+__global__ __launch_bounds__(256) void k_wgrad_reduce_co(const float* __restrict__ part,
+                                                         float* __restrict__ dw, int nsplit, int T,
+                                                         int kpad, int npad, int Cin, int Cout) {
   __shared__ float red[8][33];
   const int64_t total = (int64_t)T * Cin * Cout;
   const int o = threadIdx.x & 31, g = threadIdx.x >> 5;
@@ -460,6 +460,38 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ 
   }
 }
 
+// One workgroup per (input channel ci, 32 output channels): 256 threads = 32
+// co lanes (co fastest -> coalesced slab reads) x 8 split groups.  For every tap
+// group g sums splits g, g+8, ... in order into LDS; the groups are then
+// combined in fixed order while the tile is written transposed, tap fastest, so
+// each co's T taps land contiguously in dw [Cout][Cin][T] (deterministic; 8x
+// more loads in flight than one thread per output).
+__global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ part,
+                                                      float* __restrict__ dw, int nsplit, int T,
+                                                      int kpad, int npad, int Cin, int Cout) {
+  extern __shared__ float red[];  // [8][T][33]
+  const int ci = blockIdx.x, co0 = blockIdx.y * 32;
+  const int o = threadIdx.x & 31, g = threadIdx.x >> 5;
+  const int64_t stride = (int64_t)T * kpad * npad;
+  for (int tap = 0; tap < T; ++tap) {
+    float s = 0.f;
+    if (co0 + o < Cout) {
+      const float* p = part + ((int64_t)tap * kpad + ci) * npad + co0 + o;
+      for (int k = g; k < nsplit; k += 8) s += p[k * stride];
+    }
+    red[(g * T + tap) * 33 + o] = s;
+  }
+  __syncthreads();
+  const int nco = Cout - co0 < 32 ? Cout - co0 : 32;
+  for (int w = threadIdx.x; w < nco * T; w += 256) {
+    const int c = w / T, tap = w - c * T;
+    float t = red[tap * 33 + c];
+#pragma unroll
+    for (int q = 1; q < 8; ++q) t += red[(q * T + tap) * 33 + c];
+    dw[((int64_t)(co0 + c) * Cin + ci) * T + tap] = t;
+  }
+}
+
 size_t conv3d_wgrad_ws_bytes(Vol vol, int KD, int Cin, int Cout) {
   WgradPlan p = wgrad_plan(vol, Cin, Cout);
   return std::max((size_t)p.nsplit * KD * 9 * p.kpad * p.npad * sizeof(float),
@@ -468,9 +500,16 @@ size_t conv3d_wgrad_ws_bytes(Vol vol, int KD, int Cin, int Cout) {
 
 hipError_t conv3d_wgrad_reduce(const float* part, float* dw, int nsplit, int T, int kpad,
                                int npad, int Cin, int Cout, hipStream_t s) {
-  const int64_t total = (int64_t)T * Cin * Cout;
-  hipLaunchKernelGGL(k_wgrad_reduce, dim3((unsigned)((total + 31) / 32)), dim3(256), 0, s, part,
-                     dw, nsplit, T, kpad, npad, Cin, Cout);
+  // same per-output summation order either way: results are bitwise identical
+  if ((int64_t)Cin * ((Cout + 31) / 32) < 1024) {
+    const int64_t total = (int64_t)T * Cin * Cout;
+    hipLaunchKernelGGL(k_wgrad_reduce_co, dim3((unsigned)((total + 31) / 32)), dim3(256), 0, s,
+                       part, dw, nsplit, T, kpad, npad, Cin, Cout);
+  } else {
+    const size_t lds = (size_t)8 * T * 33 * sizeof(float);
+    hipLaunchKernelGGL(k_wgrad_reduce, dim3((unsigned)Cin, (unsigned)((Cout + 31) / 32)),
+                       dim3(256), lds, s, part, dw, nsplit, T, kpad, npad, Cin, Cout);
+  }
   return hipGetLastError();
 }
 
