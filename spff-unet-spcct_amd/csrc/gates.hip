@@ -28,6 +28,7 @@ __device__ __forceinline__ double ck_coef(int k, int D) {
 int se_hidden(int C) { return C / 16 > 4 ? C / 16 : 4; }
 
 constexpr int GT = 1024;  // threads per gate workgroup
+constexpr size_t GATE_LDS_MAX = 160 * 1024;
 
 // twiddles: twc[m] = cos(2 pi m / D), tws[m] = sin(2 pi m / D)
 __device__ void make_twiddles(double* twc, double* tws, int D) {
@@ -77,11 +78,16 @@ __global__ void k_efilm_fwd(const float* __restrict__ pe, const float* __restric
                             const float* __restrict__ fb2, float* __restrict__ t,
                             float* __restrict__ bt, float* __restrict__ hid, int C, int D,
                             int pitch) {
-  extern __shared__ float hs[];  // [32][D]
+  extern __shared__ float hs[];  // [32][D] hidden, then pe [16][D] and fw0 [32][16] staged
+  float* pes = hs + 32 * D;
+  float* w0s = pes + 16 * D;
+  for (int i = threadIdx.x; i < 16 * D; i += blockDim.x) pes[i] = pe[(i / D) * pitch + i % D];
+  for (int i = threadIdx.x; i < 32 * 16; i += blockDim.x) w0s[i] = fw0[i];
+  __syncthreads();
   for (int i = threadIdx.x; i < 32 * D; i += blockDim.x) {
     const int j = i / D, d = i % D;
     float s = 0.f;
-    for (int q = 0; q < 16; ++q) s += fw0[j * 16 + q] * pe[q * pitch + d];
+    for (int q = 0; q < 16; ++q) s += w0s[j * 16 + q] * pes[q * D + d];
     s += fb0[j];
     hs[i] = s;
     if (blockIdx.x == 0) hid[i] = s;
@@ -99,10 +105,24 @@ __global__ void k_efilm_fwd(const float* __restrict__ pe, const float* __restric
   }
 }
 
+static hipError_t efilm_fwd(const GateParams& gp, const GateSaved& sv, int C, int D,
+                            hipStream_t s) {
+  const size_t shm = (48 * (size_t)D + 512) * sizeof(float);
+  if (shm > 64 * 1024) {
+    if (shm > GATE_LDS_MAX) return hipErrorInvalidValue;
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_efilm_fwd),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(k_efilm_fwd, dim3(cdiv(2 * C, 32)), dim3(256), shm, s, gp.pe + gp.d_off,
+                     gp.fw0, gp.fb0, gp.fw2, gp.fb2, sv.t, sv.bt, sv.hid, C, D, gp.pe_pitch);
+  return hipGetLastError();
+}
+
 // ------------------------------------------------------------- gates fwd --
 struct GFShm {
   double *twc, *tws, *Sre, *Sim, *part, *tmp;
-  float *s1, *g1, *sg2, *p, *h, *e;
+  float *s1, *g1, *sg2, *p, *h, *e, *zc;
 };
 __device__ GFShm gf_carve(void* base, int C, int D, int Hse) {
   const int L = D / 2 + 1;
@@ -120,15 +140,20 @@ __device__ GFShm gf_carve(void* base, int C, int D, int Hse) {
   m.sg2 = fp; fp += D;
   m.p = fp; fp += C;
   m.h = fp; fp += Hse;
-  m.e = fp;
+  m.e = fp; fp += C;
+  m.zc = fp;  // [C][D] (cached kernels only)
   return m;
 }
-static size_t gates_fwd_shmem(int C, int D, int Hse) {
+// cached: Z[c][d] staged in LDS once (one parallel pass over the inputs) so the
+// serial chain of row sums reads LDS, not HBM/L2 -- these one-workgroup-per-
+// sample kernels are latency-bound
+static size_t gates_fwd_shmem(int C, int D, int Hse, bool cached) {
   const int L = D / 2 + 1;
   return (2 * (size_t)D + 2 * L + GT + (C > D ? C : D) + 1) * sizeof(double) +
-         (3 * (size_t)D + 2 * C + Hse) * sizeof(float);
+         (3 * (size_t)D + 2 * C + Hse + (cached ? (size_t)C * D : 0)) * sizeof(float);
 }
 
+template <bool CACHED>
 __global__ __launch_bounds__(GT) void k_gates_fwd(GateParams gp, const float* __restrict__ Sa,
                                                   GateSaved sv, Vol vol, int C, int Hse,
                                                   int efilm) {
@@ -137,10 +162,15 @@ __global__ __launch_bounds__(GT) void k_gates_fwd(GateParams gp, const float* __
   extern __shared__ double shd[];
   GFShm m = gf_carve(shd, C, D, Hse);
   const float* Sab = Sa + (int64_t)b * C * D;
-  auto Z = [&](int c, int d) -> float {
+  auto Zg = [&](int c, int d) -> float {
     const float sa = Sab[c * D + d];
     return efilm ? (1.f + sv.t[c * D + d]) * sa + sv.bt[c * D + d] * (float)HW : sa;
   };
+  auto Z = [&](int c, int d) -> float { return CACHED ? m.zc[c * D + d] : Zg(c, d); };
+  if (CACHED) {
+    for (int i = threadIdx.x; i < C * D; i += blockDim.x) m.zc[i] = Zg(i / D, i % D);
+    __syncthreads();
+  }
   make_twiddles(m.twc, m.tws, D);
   // s1[d] = mean_{c,hw} z
   rowsum(D, C, [&](int d, int c) { return (double)Z(c, d); }, m.part, 1.0 / ((double)C * HW),
@@ -210,14 +240,20 @@ hipError_t gates_fwd(const GateParams& gp, const float* Sa, GateSaved& sv, Vol v
   const int D = vol.D, Hse = se_hidden(C);
   const int efilm = gp.fw0 != nullptr;
   if (efilm) {
-    hipLaunchKernelGGL(k_efilm_fwd, dim3(cdiv(2 * C, 32)), dim3(256), 32 * D * sizeof(float), s,
-                       gp.pe + gp.d_off, gp.fw0, gp.fb0, gp.fw2, gp.fb2, sv.t, sv.bt, sv.hid, C,
-                       D, gp.pe_pitch);
-    hipError_t e = hipGetLastError();
+    hipError_t e = efilm_fwd(gp, sv, C, D, s);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(k_gates_fwd, dim3(vol.B), dim3(GT), gates_fwd_shmem(C, D, Hse), s, gp, Sa,
-                     sv, vol, C, Hse, efilm);
+  const size_t shc = gates_fwd_shmem(C, D, Hse, true);
+  if (shc <= GATE_LDS_MAX) {
+    hipError_t e0 = hipFuncSetAttribute(reinterpret_cast<const void*>(k_gates_fwd<true>),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)shc);
+    if (e0 != hipSuccess) return e0;
+    hipLaunchKernelGGL(k_gates_fwd<true>, dim3(vol.B), dim3(GT), shc, s, gp, Sa, sv, vol, C, Hse,
+                       efilm);
+  } else {
+    hipLaunchKernelGGL(k_gates_fwd<false>, dim3(vol.B), dim3(GT),
+                       gates_fwd_shmem(C, D, Hse, false), s, gp, Sa, sv, vol, C, Hse, efilm);
+  }
   return hipGetLastError();
 }
 
@@ -250,7 +286,7 @@ size_t gates_scratch_bytes(Vol vol, int C) {
 
 struct GBShm {
   double *twc, *tws, *Sre, *Sim, *Tre, *Tim, *part, *tmp;
-  float *e, *c0, *dq, *dh, *g1, *sg2, *ds2, *dw, *ds1;
+  float *e, *c0, *dq, *dh, *g1, *sg2, *ds2, *dw, *ds1, *zc, *rc;
 };
 __device__ GBShm gb_carve(void* base, int C, int D, int Hse) {
   const int L = D / 2 + 1;
@@ -273,15 +309,19 @@ __device__ GBShm gb_carve(void* base, int C, int D, int Hse) {
   m.sg2 = fp; fp += D;
   m.ds2 = fp; fp += D;
   m.dw = fp; fp += D;
-  m.ds1 = fp;
+  m.ds1 = fp; fp += D;
+  m.rc = fp; fp += (size_t)C * D;  // [C][D] R1, then Z (cached kernels only)
+  m.zc = fp;
   return m;
 }
-static size_t gates_bwd_shmem(int C, int D, int Hse) {
+// ncache: how many of the [C][D] inputs R1, Z are staged in LDS (2, 1 = R1 only, 0)
+static size_t gates_bwd_shmem(int C, int D, int Hse, int ncache) {
   const int L = D / 2 + 1;
   return (2 * (size_t)D + 4 * L + GT + (C > D ? C : D) + 1) * sizeof(double) +
-         (3 * (size_t)C + Hse + 5 * (size_t)D) * sizeof(float);
+         (3 * (size_t)C + Hse + 5 * (size_t)D + (size_t)ncache * C * D) * sizeof(float);
 }
 
+template <int NCACHE>
 __global__ __launch_bounds__(GT) void k_gates_bwd(GateParams gp, GateSaved sv,
                                                   const float* __restrict__ Sa,
                                                   const float* __restrict__ Sg, GScr gs,
@@ -293,14 +333,20 @@ __global__ __launch_bounds__(GT) void k_gates_bwd(GateParams gp, GateSaved sv,
   extern __shared__ double shd[];
   GBShm m = gb_carve(shd, C, D, Hse);
   const int64_t bo = (int64_t)b * C * D;
-  auto Zf = [&](int c, int d) -> float {
+  auto Zg = [&](int c, int d) -> float {
     const float sa = Sa[bo + c * D + d];
     return efilm ? (1.f + sv.t[c * D + d]) * sa + sv.bt[c * D + d] * (float)HW : sa;
   };
-  auto R1 = [&](int c, int d) -> float {  // sum_hw dout * z
+  auto R1g = [&](int c, int d) -> float {  // sum_hw dout * z
     const float sgd = Sg[(bo + c * D + d) * 2 + 0], sda = Sg[(bo + c * D + d) * 2 + 1];
     return efilm ? (1.f + sv.t[c * D + d]) * sda + sv.bt[c * D + d] * sgd : sda;
   };
+  auto Zf = [&](int c, int d) -> float { return NCACHE >= 2 ? m.zc[c * D + d] : Zg(c, d); };
+  auto R1 = [&](int c, int d) -> float { return NCACHE >= 1 ? m.rc[c * D + d] : R1g(c, d); };
+  for (int i = threadIdx.x; NCACHE >= 1 && i < C * D; i += blockDim.x) {
+    m.rc[i] = R1g(i / D, i % D);
+    if (NCACHE >= 2) m.zc[i] = Zg(i / D, i % D);
+  }
   make_twiddles(m.twc, m.tws, D);
   for (int d = threadIdx.x; d < D; d += blockDim.x) {
     m.g1[d] = sv.g1[b * D + d];
@@ -456,40 +502,55 @@ __global__ void k_efilm_bwd1(GScr gs, const float* __restrict__ t, int B, int C,
     gs.dgb[i] = s;
   }
 }
-__global__ void k_efilm_bwd2(GateParams gp, GateGrads gg, GScr gs, const float* __restrict__ hid,
-                             int C, int D) {
-  const int n = 2 * C * 33 + 32 * D;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    if (i < 2 * C * 33) {
-      const int o = i / 33, j = i % 33;
-      float s = 0.f;
-      if (j < 32) {
-        for (int d = 0; d < D; ++d) s += gs.dgb[o * D + d] * fmaxf(hid[j * D + d], 0.f);
-        gg.fw2[o * 32 + j] = s;
-      } else {
-        for (int d = 0; d < D; ++d) s += gs.dgb[o * D + d];
-        gg.fb2[o] = s;
-      }
+// one wave per output: lanes take strided slices of the reduction, then a fixed
+// shuffle tree (deterministic; 64x shorter dependent chains than a thread per
+// output -- these tiny kernels are latency-bound)
+__device__ __forceinline__ float gate_wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+__global__ __launch_bounds__(256) void k_efilm_bwd2(GateParams gp, GateGrads gg, GScr gs,
+                                                    const float* __restrict__ hid, int C, int D) {
+  const int lane = threadIdx.x & 63;
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= 2 * C * 33 + 32 * D) return;
+  float s = 0.f;
+  if (i < 2 * C * 33) {
+    const int o = i / 33, j = i % 33;
+    if (j < 32) {
+      for (int d = lane; d < D; d += 64) s += gs.dgb[o * D + d] * fmaxf(hid[j * D + d], 0.f);
+      s = gate_wave_sum(s);
+      if (lane == 0) gg.fw2[o * 32 + j] = s;
     } else {
-      const int k = i - 2 * C * 33;
-      const int j = k / D, d = k % D;
-      float s = 0.f;
-      for (int o = 0; o < 2 * C; ++o) s += gp.fw2[o * 32 + j] * gs.dgb[o * D + d];
-      gs.dh[k] = hid[k] > 0.f ? s : 0.f;
+      for (int d = lane; d < D; d += 64) s += gs.dgb[o * D + d];
+      s = gate_wave_sum(s);
+      if (lane == 0) gg.fb2[o] = s;
     }
+  } else {
+    const int k = i - 2 * C * 33;
+    const int j = k / D, d = k % D;
+    for (int o = lane; o < 2 * C; o += 64) s += gp.fw2[o * 32 + j] * gs.dgb[o * D + d];
+    s = gate_wave_sum(s);
+    if (lane == 0) gs.dh[k] = hid[k] > 0.f ? s : 0.f;
   }
 }
-__global__ void k_efilm_bwd3(GateParams gp, GateGrads gg, GScr gs, int D) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(256) void k_efilm_bwd3(GateParams gp, GateGrads gg, GScr gs,
+                                                    int D) {
+  const int lane = threadIdx.x & 63;
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i >= 32 * 17) return;
   const int j = i / 17, q = i % 17;
   float s = 0.f;
   if (q < 16) {
-    for (int d = 0; d < D; ++d) s += gs.dh[j * D + d] * gp.pe[q * gp.pe_pitch + gp.d_off + d];
-    gg.fw0[j * 16 + q] = s;
+    const float* pe = gp.pe + q * gp.pe_pitch + gp.d_off;
+    for (int d = lane; d < D; d += 64) s += gs.dh[j * D + d] * pe[d];
+    s = gate_wave_sum(s);
+    if (lane == 0) gg.fw0[j * 16 + q] = s;
   } else {
-    for (int d = 0; d < D; ++d) s += gs.dh[j * D + d];
-    gg.fb0[j] = s;
+    for (int d = lane; d < D; d += 64) s += gs.dh[j * D + d];
+    s = gate_wave_sum(s);
+    if (lane == 0) gg.fb0[j] = s;
   }
 }
 
@@ -507,10 +568,10 @@ static hipError_t gates_bwd_tail(const GateParams& gp, const GateSaved& sv, Gate
     hipLaunchKernelGGL(k_efilm_bwd1, dim3(std::min(cdiv(2 * C * D, 256), 1024)), dim3(256), 0, s,
                        g, sv.t, B, C, D);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_efilm_bwd2, dim3(cdiv(2 * C * 33 + 32 * D, 64)), dim3(64), 0, s, gp, gg,
-                       g, sv.hid, C, D);
+    hipLaunchKernelGGL(k_efilm_bwd2, dim3(cdiv(2 * C * 33 + 32 * D, 4)), dim3(256), 0, s, gp,
+                       gg, g, sv.hid, C, D);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_efilm_bwd3, dim3(cdiv(32 * 17, 64)), dim3(64), 0, s, gp, gg, g, D);
+    hipLaunchKernelGGL(k_efilm_bwd3, dim3(cdiv(32 * 17, 4)), dim3(256), 0, s, gp, gg, g, D);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   return hipSuccess;
@@ -522,8 +583,17 @@ hipError_t gates_bwd(const GateParams& gp, const GateSaved& sv, const float* Sa,
   const int D = vol.D, B = vol.B, Hse = se_hidden(C);
   const int efilm = gp.fw0 != nullptr;
   GScr g = gscr(scratch, B, C, D, Hse);
-  hipLaunchKernelGGL(k_gates_bwd, dim3(B), dim3(GT), gates_bwd_shmem(C, D, Hse), s, gp, sv, Sa,
-                     Sg, g, A, Bc, vol, C, Hse, efilm);
+  int nc = 2;
+  while (nc > 0 && gates_bwd_shmem(C, D, Hse, nc) > GATE_LDS_MAX) --nc;
+  const size_t shm = gates_bwd_shmem(C, D, Hse, nc);
+  auto kern = nc == 2 ? k_gates_bwd<2> : nc == 1 ? k_gates_bwd<1> : k_gates_bwd<0>;
+  if (shm > 64 * 1024) {
+    hipError_t e0 = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+    if (e0 != hipSuccess) return e0;
+  }
+  hipLaunchKernelGGL(kern, dim3(B), dim3(GT), shm, s, gp, sv, Sa, Sg, g, A, Bc, vol, C, Hse,
+                     efilm);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   return gates_bwd_tail(gp, sv, gg, g, B, C, D, D, Hse, s);
@@ -718,9 +788,7 @@ hipError_t gates_fwd_sh(const GateParams& gp, const float* Sa, GateSaved& sv, Vo
   if (C > 1024 || Hse > 64) return hipErrorInvalidValue;
   hipError_t e;
   if (efilm) {
-    hipLaunchKernelGGL(k_efilm_fwd, dim3(cdiv(2 * C, 32)), dim3(256), 32 * D * sizeof(float), s,
-                       gp.pe + gp.d_off, gp.fw0, gp.fb0, gp.fw2, gp.fb2, sv.t, sv.bt, sv.hid, C,
-                       D, gp.pe_pitch);
+    if ((e = efilm_fwd(gp, sv, C, D, s)) != hipSuccess) return e;
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   ShScr sc = shscr(scratch, vol, C, Dg);

@@ -216,33 +216,49 @@ hipError_t in_rstd(const float* sq, const float* gamma, const float* beta, const
   return hipGetLastError();
 }
 
-__global__ void k_in_bwd_stats(const float* __restrict__ sums, float* __restrict__ dgamma,
-                               float* __restrict__ dbeta, float* __restrict__ k1,
-                               float* __restrict__ k2, Vol vol, int C) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+// one wave per channel c: lanes take strided depths, fp64 shuffle tree per
+// sample, samples summed in order (deterministic; short dependent chains --
+// the per-(b, c, d) sums are tiny and this kernel is latency-bound)
+__global__ __launch_bounds__(256) void k_in_bwd_stats(const float* __restrict__ sums,
+                                                      float* __restrict__ dgamma,
+                                                      float* __restrict__ dbeta,
+                                                      float* __restrict__ k1,
+                                                      float* __restrict__ k2, Vol vol, int C) {
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (c >= C) return;
   const double N = (double)vol.D * vol.H * vol.W;
   double tg = 0.0, tb = 0.0;
   for (int b = 0; b < vol.B; ++b) {
     const int64_t bc = (int64_t)b * C + c;
     double s0 = 0.0, s1 = 0.0;
-    for (int d = 0; d < vol.D; ++d) {
-      s0 += sums[(bc * vol.D + d) * 2 + 0];
-      s1 += sums[(bc * vol.D + d) * 2 + 1];
+    for (int d = lane; d < vol.D; d += 64) {
+      const float2 v = *reinterpret_cast<const float2*>(sums + (bc * vol.D + d) * 2);
+      s0 += v.x;
+      s1 += v.y;
     }
-    k1[bc] = (float)(s0 / N);
-    k2[bc] = (float)(s1 / N);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      s0 += __shfl_xor(s0, o);
+      s1 += __shfl_xor(s1, o);
+    }
+    if (lane == 0) {
+      k1[bc] = (float)(s0 / N);
+      k2[bc] = (float)(s1 / N);
+    }
     tb += s0;
     tg += s1;
   }
-  if (dgamma) dgamma[c] = (float)tg;
-  if (dbeta) dbeta[c] = (float)tb;
+  if (lane == 0) {
+    if (dgamma) dgamma[c] = (float)tg;
+    if (dbeta) dbeta[c] = (float)tb;
+  }
 }
 
 hipError_t in_bwd_stats(const float* sums, const float* gamma, float* dgamma, float* dbeta,
                         float* k1, float* k2, Vol vol, int C, hipStream_t s) {
   (void)gamma;
-  hipLaunchKernelGGL(k_in_bwd_stats, dim3(cdiv(C, 64)), dim3(64), 0, s, sums, dgamma, dbeta, k1,
+  hipLaunchKernelGGL(k_in_bwd_stats, dim3(cdiv(C, 4)), dim3(256), 0, s, sums, dgamma, dbeta, k1,
                      k2, vol, C);
   return hipGetLastError();
 }
