@@ -448,6 +448,7 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce_co(const float* __restrict
     tap = (int)(i / ((int64_t)Cout * Cin));
     const int64_t stride = (int64_t)T * kpad * npad;
     const float* p = part + ((int64_t)tap * kpad + ci) * npad + co;
+#pragma unroll 4
     for (int k = g; k < nsplit; k += 8) s += p[k * stride];
   }
   red[g][o] = s;

@@ -497,6 +497,7 @@ __global__ __launch_bounds__(256) void k_atb_reduce(const float* __restrict__ pa
     valid = k1 < K1 && n < N;
     if (valid) {
       const int64_t stride = (int64_t)k1pad * npad;
+#pragma unroll 4
       for (int k = g; k < nsplit; k += 8) s += part[k * stride + j];
     }
   } else {

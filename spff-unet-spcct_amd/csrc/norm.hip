@@ -147,6 +147,7 @@ __global__ void k_slab_combine(const float* __restrict__ ws, float* __restrict__
     const int bd = i / (nq * C);
     const int b = bd / vol.D, d = bd % vol.D;
     float s = 0.f;
+#pragma unroll 4
     for (int k = 0; k < nsplit; ++k) s += ws[(((int64_t)bd * nsplit + k) * C + c) * nq + q];
     out[(((int64_t)b * C + c) * vol.D + d) * nq + q] = s;
   }
