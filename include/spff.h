@@ -87,6 +87,16 @@ void spff_plan_destroy(spff_plan* plan);
 /* attach the shard group's collectives (required before the first forward of a
  * plan with shard_world > 1; the table is copied) */
 int spff_plan_set_coll(spff_plan* plan, const spff_coll* coll);
+/* gradient-ready hook (data parallelism; replaces the bucketed gradient
+ * all-reduce torch DDP hangs on autograd for the reference's module, SURVEY
+ * §8(e) DP row): during spff_backward the engine calls fn(ctx, off, n, stream)
+ * in stream order as soon as dparams[off, off + n) is final (one call per
+ * block's parameters, per SE / up-conv / head group; together they cover every
+ * float once), so the caller can issue that range's all-reduce on a
+ * collective stream that waits on `stream` while the backward continues.
+ * fn == NULL removes the hook.  Return 0 from fn, else the backward fails. */
+typedef int (*spff_grad_ready_fn)(void* ctx, int64_t off, int64_t n, void* stream);
+int spff_plan_set_grad_hook(spff_plan* plan, spff_grad_ready_fn fn, void* ctx);
 const char* spff_last_error(void);
 
 /* flat parameter layout (reference state-dict order, models.py:655-681) */

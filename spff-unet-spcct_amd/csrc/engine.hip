@@ -80,6 +80,7 @@ struct Blk {
   int64_t fw0 = -1, fb0 = -1, fw2 = -1, fb2 = -1;
   int64_t mag = -1, mask = -1;
   int64_t sw0 = -1, sb0 = -1, sw2 = -1, sb2 = -1;
+  int64_t pr0 = 0, pr1 = 0, se0 = 0, se1 = 0;  // flat ranges of the block's / SE parameters
   size_t y1, a1, y2, out;
   size_t mean1, rstd1, al1, de1, mean2, rstd2, al2, de2;
   size_t Sa, t, bt, hid, s1, g1s, sg2, p, h, e, P, Q;
@@ -113,6 +114,8 @@ struct spff_plan {
   size_t total = 0;
   Coll co;             // depth-sharding group (world 1: unsharded)
   bool coll_set = false;
+  spff_grad_ready_fn grad_fn = nullptr;  // data-parallel gradient-ready hook
+  void* grad_ctx = nullptr;
   float* pe_dev = nullptr;
   std::vector<float> pe_host;
   // optional HIP-event timing of the MFMA kernels (bench.py roofline)
@@ -175,6 +178,7 @@ namespace {
 void reg_block(spff_plan* p, Blk& b) {
   const std::string a = b.novel ? "pre" : "b1", bb = b.novel ? "body" : "b2";
   const int KD = p->KD, C = b.C;
+  b.pr0 = p->nparam;
   b.c1.w = p->reg(b.name + "." + a + ".0.weight", {C, b.Cin, KD, 3, 3});
   b.g1 = p->reg(b.name + "." + a + ".1.weight", {C});
   b.b1 = p->reg(b.name + "." + a + ".1.bias", {C});
@@ -191,6 +195,7 @@ void reg_block(spff_plan* p, Blk& b) {
     b.mag = p->reg(b.name + ".fgate.mag_scale", {1});
     b.mask = p->reg(b.name + ".fgate.freq_mask", {1, 1, p->co.D_glob / 2 + 1, 1, 1});
   }
+  b.pr1 = p->nparam;
 }
 
 void conv_dims(ConvL& c, int Cin, int Cout) {
@@ -293,10 +298,12 @@ int build_plan(spff_plan* p) {
       const int C = chs[i], h = se_hidden(C);
       const std::string pre = "se." + std::to_string(i) + ".fc.";
       Blk& b = p->blk[i];
+      b.se0 = p->nparam;
       b.sw0 = p->reg(pre + "0.weight", {h, C, 1, 1, 1});
       b.sb0 = p->reg(pre + "0.bias", {h});
       b.sw2 = p->reg(pre + "2.weight", {C, h, 1, 1, 1});
       b.sb2 = p->reg(pre + "2.bias", {C});
+      b.se1 = p->nparam;
     }
   }
 
@@ -624,6 +631,17 @@ int bwd_block(spff_plan* p, Blk& b, const float* dout, const Dst2* dx, const Src
 
 Src2 src2(const float* a, const float* b, int C) { return Src2{a, b, C, C, C}; }
 
+// report dparams[a, b) final to the gradient-ready hook (no-op without one)
+int grad_ready(spff_plan* p, int64_t a, int64_t b) {
+  if (!p->grad_fn || b <= a) return SPFF_OK;
+  if (p->grad_fn(p->grad_ctx, a, b - a, p->st) != 0) return fail(SPFF_EHIP, "gradient hook failed");
+  return SPFF_OK;
+}
+int block_grads_ready(spff_plan* p, const Blk& b) {
+  CK(grad_ready(p, b.pr0, b.pr1));
+  return grad_ready(p, b.se0, b.se1);
+}
+
 int forward(spff_plan* p, const float* x, float* logits) {
   const int f = p->f;
   const spff_cfg& c = p->cfg;
@@ -667,6 +685,7 @@ int backward(spff_plan* p, const float* dl) {
   PROF(p, 3, 2.0 * V0 * f * p->K,
        head_wgrad(p->F(B[6].out), dl, p->DP(p->out_w), p->DP(p->out_b), V0, f, p->K,
                   p->F(p->wg_ws), p->st));
+  CK(grad_ready(p, p->out_w, p->out_b + p->K));
   PROF(p, 3, 2.0 * V0 * f * p->K,
        head_dgrad(dl, hp + head_pack_dgrad_offset(f, p->K), p->F(p->G_out), V0, f, p->K,
                   p->st));
@@ -680,12 +699,14 @@ int backward(spff_plan* p, const float* dl) {
     const int lvl = d.lvl;
     Dst2 dx{p->F(p->G_dx), p->F(p->dskip[lvl]), C, C, C};
     CK(bwd_block(p, d, p->F(p->G_out), &dx, src2(p->F(U.out), p->F(B[lvl].out), C)));
+    CK(block_grads_ready(p, d));
     if (p->dbg_stop == k + 1) return SPFF_OK;
     const float* upin = (ui == 0) ? p->F(B[3].out) : p->F(B[bi - 1].out);
     const Vol& low = p->vol[U.lvl_low];
     PROF(p, 3, 2.0 * nvox(low) * U.Cin * 4.0 * U.Cout,
          upconv_wgrad(upin, p->F(p->G_dx), C, p->DP(U.w), p->DP(U.b), low, U.Cin, U.Cout,
                       p->F(p->wg_ws), p->st));
+    CK(grad_ready(p, U.w, U.b + U.Cout));
     float* pk = p->F(U.pk);
     PROF(p, 3, 2.0 * nvox(low) * U.Cin * 4.0 * U.Cout,
          upconv_dgrad(p->F(p->G_dx), C, pk + upconv_pack_dgrad_offset(U.Cin, U.Cout),
@@ -695,6 +716,7 @@ int backward(spff_plan* p, const float* dl) {
   {
     Dst2 dx = dst1(p->F(p->G_dx), 4 * f);
     CK(bwd_block(p, B[3], p->F(p->G_out), &dx, src1(p->F(p->pool[2]), 4 * f)));
+    CK(block_grads_ready(p, B[3]));
   }
   for (int l = 2; l >= 0; --l) {
     const int C = f << l;
@@ -706,6 +728,7 @@ int backward(spff_plan* p, const float* dl) {
     } else {
       CK(bwd_block(p, B[0], p->F(p->dskip[0]), nullptr, src1(p->F(p->x_cl), p->ldx)));
     }
+    CK(block_grads_ready(p, B[l]));
   }
   return SPFF_OK;
 }
@@ -738,6 +761,13 @@ int spff_plan_set_coll(spff_plan* p, const spff_coll* coll) {
   p->co.allreduce = coll->allreduce;
   p->co.halo = coll->halo;
   p->coll_set = true;
+  return SPFF_OK;
+}
+
+int spff_plan_set_grad_hook(spff_plan* p, spff_grad_ready_fn fn, void* ctx) {
+  if (!p) return fail(SPFF_EINVAL, "null plan");
+  p->grad_fn = fn;
+  p->grad_ctx = ctx;
   return SPFF_OK;
 }
 

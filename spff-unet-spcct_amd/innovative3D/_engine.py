@@ -9,6 +9,7 @@ import ctypes
 import os
 import pathlib
 import threading
+import weakref
 from typing import Dict, List, Optional, Tuple
 
 import torch
@@ -62,6 +63,11 @@ class spff_coll(ctypes.Structure):
     _fields_ = [("ctx", ctypes.c_void_p), ("allreduce", ALLREDUCE_FN), ("halo", HALO_FN)]
 
 
+# spff_grad_ready_fn (include/spff.h): dparams[off, off + n) final during spff_backward
+GRAD_READY_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
+                                 ctypes.c_void_p)
+
+
 # conv arithmetic (include/spff.h SPFF_MATH_*)
 MATH_F32, MATH_BF16X6, MATH_BF16X3 = 0, 1, 2
 MATH_NAMES = {"f32": MATH_F32, "bf16x6": MATH_BF16X6, "bf16x3": MATH_BF16X3}
@@ -84,6 +90,7 @@ _SIGS = {
     "spff_plan_create": (_I, [ctypes.POINTER(spff_cfg), ctypes.POINTER(_P)]),
     "spff_plan_set_coll": (_I, [_P, ctypes.POINTER(spff_coll)]),
     "spff_plan_destroy": (None, [_P]),
+    "spff_plan_set_grad_hook": (_I, [_P, GRAD_READY_FN, _P]),
     "spff_last_error": (ctypes.c_char_p, []),
     "spff_num_params": (_I, [_P]),
     "spff_param_info": (_I, [_P, _I, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(_I),
@@ -310,13 +317,45 @@ class Plan:
         return out
 
     def backward(self, dlogits_cl: torch.Tensor, flat: torch.Tensor,
-                 dflat: Optional[torch.Tensor] = None) -> torch.Tensor:
+                 dflat: Optional[torch.Tensor] = None, grad_hook=None) -> torch.Tensor:
+        """``grad_hook``: an object with begin(dflat), ready(off, n) and finish()
+        (innovative3D.distributed.GradBucketer); ready() is called while the
+        backward is being enqueued, as each parameter group's gradient becomes
+        final, and finish() after it."""
         dlogits_cl = dlogits_cl.contiguous()
         if dflat is None:
             dflat = torch.empty(self.nfloats, dtype=torch.float32, device=dlogits_cl.device)
         ws = self.workspace(dlogits_cl.device)
-        check(lib().spff_backward(self._h, _ptr(dlogits_cl), _ptr(flat), _ptr(dflat), _ptr(ws),
+        L = lib()
+        if grad_hook is None:
+            check(L.spff_backward(self._h, _ptr(dlogits_cl), _ptr(flat), _ptr(dflat), _ptr(ws),
                                   _stream(dlogits_cl.device)), "spff_backward")
+            return dflat
+        covered = [0]
+        err = []
+
+        def _ready(_ctx, off, n, _stream_):
+            try:
+                covered[0] += int(n)
+                grad_hook.ready(int(off), int(n))
+                return 0
+            except Exception as e:  # noqa: BLE001 -- reported through the engine status
+                err.append(e)
+                return 1
+        fn = GRAD_READY_FN(_ready)
+        grad_hook.begin(dflat)
+        check(L.spff_plan_set_grad_hook(self._h, fn, None), "spff_plan_set_grad_hook")
+        try:
+            rc = L.spff_backward(self._h, _ptr(dlogits_cl), _ptr(flat), _ptr(dflat), _ptr(ws),
+                                 _stream(dlogits_cl.device))
+        finally:
+            L.spff_plan_set_grad_hook(self._h, GRAD_READY_FN(), None)
+        if err:
+            raise SpffError(f"gradient hook failed: {err[0]!r}")
+        check(rc, "spff_backward")
+        if covered[0] != self.nfloats:
+            raise SpffError(f"gradient hook covered {covered[0]} of {self.nfloats} floats")
+        grad_hook.finish()
         return dflat
 
     PROF_CLASSES = ("conv_fwd", "conv_dgrad", "conv_wgrad", "gemm", "slab_reduce", "act_apply",
@@ -350,22 +389,53 @@ class Plan:
         return ws[off:off + 4 * n].view(torch.float32).view(nv.value, ch.value).clone()
 
 
-_PLANS: Dict[tuple, Plan] = {}
+# Plans (and the workspace each pins: ~2.9 KB per voxel) belong to the module
+# that created them: one plan per (module, tag) -- a new shape replaces the old
+# plan -- dropped with the module (weak keys), or explicitly by release_plans().
+_OWNER_PLANS: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
+_ANON_PLANS: Dict[tuple, object] = {}
 
 
-def get_plan(**kw) -> Plan:
-    """Plans are cached per (shape, flags, tag); the tag keeps one workspace per model."""
+def _owned_plan(owner, tag: str, key: tuple, make):
+    if owner is None:
+        if key not in _ANON_PLANS:
+            _ANON_PLANS[key] = make()
+        return _ANON_PLANS[key]
+    slots = _OWNER_PLANS.get(owner)
+    if slots is None:
+        slots = {}
+        _OWNER_PLANS[owner] = slots
+    cur = slots.get(tag)
+    if cur is None or cur[0] != key:
+        slots.pop(tag, None)  # free the old plan's workspace before allocating a new one
+        cur = (key, make())
+        slots[tag] = cur
+    return cur[1]
+
+
+def release_plans(owner=None) -> None:
+    """Drop the engine plans (and workspaces) of ``owner`` -- every module-owned
+    and anonymous plan when owner is None."""
+    if owner is None:
+        _OWNER_PLANS.clear()
+        _ANON_PLANS.clear()
+    else:
+        _OWNER_PLANS.pop(owner, None)
+
+
+def get_plan(owner=None, tag: str = "", **kw) -> Plan:
+    """The plan of ``owner`` (an nn.Module) for tag ``tag`` and this shape/flag set."""
     key = (kw["batch"], kw["in_ch"], kw["depth"], kw["height"], kw["width"], kw["num_classes"],
            kw.get("base", 32), kw.get("ksd", 3), bool(kw.get("efilm", True)),
            bool(kw.get("fgate", True)), bool(kw.get("se", True)), bool(kw.get("specse", True)),
-           kw.get("math") or default_math(), tuple(kw.get("shard", (1, 0))), kw.get("tag", ""))
-    if key not in _PLANS:
+           kw.get("math") or default_math(), tuple(kw.get("shard", (1, 0))))
+
+    def make():
         kk = dict(kw)
-        kk.pop("tag", None)
         sh = kk.pop("shard", (1, 0))
         kk["shard_world"], kk["shard_rank"] = sh
-        _PLANS[key] = Plan(**kk)
-    return _PLANS[key]
+        return Plan(**kk)
+    return _owned_plan(owner, tag, key, make)
 
 
 class UNet3DPlan:
@@ -464,19 +534,12 @@ class UNet3DPlan:
         return ws[off:off + 4 * n].view(torch.float32).view(nv.value, ch.value).clone()
 
 
-_UPLANS: Dict[tuple, UNet3DPlan] = {}
-
-
-def get_unet3d_plan(**kw) -> UNet3DPlan:
-    """UNet3D plans cached per (shape, math, tag) like get_plan."""
-    key = (kw["batch"], kw["in_ch"], kw["depth"], kw["height"], kw["width"], kw["num_classes"],
-           kw.get("base", 32), kw.get("target_depth", 0), kw.get("math") or default_math(),
-           kw.get("tag", ""))
-    if key not in _UPLANS:
-        kk = dict(kw)
-        kk.pop("tag", None)
-        _UPLANS[key] = UNet3DPlan(**kk)
-    return _UPLANS[key]
+def get_unet3d_plan(owner=None, tag: str = "", **kw) -> UNet3DPlan:
+    """UNet3D plans, owned like get_plan."""
+    key = ("unet3d", kw["batch"], kw["in_ch"], kw["depth"], kw["height"], kw["width"],
+           kw["num_classes"], kw.get("base", 32), kw.get("target_depth", 0),
+           kw.get("math") or default_math())
+    return _owned_plan(owner, "unet3d:" + tag, key, lambda: UNet3DPlan(**kw))
 
 
 class SwinPlan:
@@ -567,18 +630,13 @@ class SwinPlan:
         return ws[off:off + 4 * n].view(torch.float32).view(nv.value, ch.value).clone()
 
 
-_SPLANS: Dict[tuple, SwinPlan] = {}
-
-
-def get_swin_plan(**kw) -> SwinPlan:
-    key = (kw["batch"], kw["in_ch"], kw["depth"], kw["height"], kw["width"], kw["num_classes"],
-           kw.get("feature_size", 12), kw.get("window", 7), tuple(kw.get("heads", (1, 2, 4, 8))),
-           float(kw.get("mlp_ratio", 2.0)), kw.get("math") or default_math(), kw.get("tag", ""))
-    if key not in _SPLANS:
-        kk = dict(kw)
-        kk.pop("tag", None)
-        _SPLANS[key] = SwinPlan(**kk)
-    return _SPLANS[key]
+def get_swin_plan(owner=None, tag: str = "", **kw) -> SwinPlan:
+    """SwinUNETR plans, owned like get_plan."""
+    key = ("swin", kw["batch"], kw["in_ch"], kw["depth"], kw["height"], kw["width"],
+           kw["num_classes"], kw.get("feature_size", 12), kw.get("window", 7),
+           tuple(kw.get("heads", (1, 2, 4, 8))), float(kw.get("mlp_ratio", 2.0)),
+           kw.get("math") or default_math())
+    return _owned_plan(owner, "swin:" + tag, key, lambda: SwinPlan(**kw))
 
 
 def swin_loss_forward(logits_cl: torch.Tensor, labels: torch.Tensor, K: int, ignore_index: int,

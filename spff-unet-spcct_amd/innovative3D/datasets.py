@@ -11,7 +11,11 @@ Here the volumes live in HBM (a 512 x 512 x 5 volume is 5 MB; hundreds fit in
 processes.  The random decisions keep the reference's exact draw order on
 Python's module-level ``random`` (so ``random.seed`` reproduces the reference's
 decisions); only the gaussian-noise values come from a counter-based device RNG
-instead of ``torch.randn_like``.
+instead of ``torch.randn_like``.  The shuffled sample order is RandomSampler's
+(torch default generator), as the reference DataLoader draws it.  One stated
+difference: the reference augments in 16 worker processes, each re-seeding
+``random`` per worker, so its per-sample decisions are reproducible only with
+num_workers=0; that single-process order is the one kept here.
 
 DICOM decoding needs ``pydicom`` (absent offline): ``read_dicom_frames`` raises
 with a pointer to passing pre-decoded frames instead.
@@ -168,9 +172,18 @@ class DeviceBatchLoader:
         return n // self.bs if self.drop_last else (n + self.bs - 1) // self.bs
 
     def __iter__(self):
+        # torch's default-generator draws in DataLoader order: the iterator's base
+        # seed (dataloader.py _BaseDataLoaderIter.__init__), then RandomSampler's
+        # shuffle seed and its randperm (sampler.py RandomSampler.__iter__) -- so a
+        # seeded run visits the samples in the reference DataLoader's order and
+        # Python's `random` stream is left to TrainGridAug's draws
+        torch.empty((), dtype=torch.int64).random_()
         idx = list(range(len(self.ds)))
         if self.shuffle:
-            random.shuffle(idx)
+            seed = int(torch.empty((), dtype=torch.int64).random_().item())
+            g = torch.Generator()
+            g.manual_seed(seed)
+            idx = torch.randperm(len(idx), generator=g).tolist()
         for k in range(len(self)):
             sel = idx[k * self.bs:(k + 1) * self.bs]
             t = torch.as_tensor(sel, device=self.ds.images.device)

@@ -4,14 +4,23 @@ torch.distributed over RCCL ("nccl" backend on ROCm), xGMI between GPUs.
 The reference trains on one device only (train.py:1486-1503); this
 module is new.  Exactness argument: InstanceNorm, the FourierGate/SpectralSE
 means and the channel-SE pool are all per sample, so a rank's forward on its
-own samples is exactly the single-device forward restricted to them.  The only
-cross-sample couplings are the CE mean (normalised by the GLOBAL number of
-non-ignored voxels -> one int64 all-reduce before the loss) and the hard-Dice
-term (computed from the all-reduced confusion counts; it carries no
-gradient).  The weight gradient is then a plain SUM over ranks: one
-all-reduce of the flat fp32 gradient (22 MB for SPFF-UNet), issued after the
-backward.  At ~22 MB against ~100 ms of compute per step the collective is
-<1% of a step on xGMI, so no bucketing/overlap is needed yet.
+own samples is exactly the single-device forward restricted to them.  The
+cross-sample couplings are the loss terms (DP row):
+
+* the CE mean is normalised by the GLOBAL number of non-ignored voxels (one
+  int64 all-reduce before the loss), so each rank's CE term is its share of
+  the global mean and its dlogits are exactly the global-batch dlogits;
+* the reported loss and hard-Dice (helpers.py:782-803, logged per step at
+  models.py:486-507) come from ONE fp64 all-reduce of [CE share, K x (K+1)
+  confusion counts] -- the global CE and the confusion of the whole batch, so
+  the values equal the single-device ones (the Dice term carries no gradient);
+* the weight gradient is a plain SUM over ranks.  It is all-reduced in
+  buckets while the backward is still running: the engine reports each block's
+  finished parameter-gradient range (spff_plan_set_grad_hook) in the order the
+  backward completes them, and ``GradBucketer`` issues an async all-reduce of
+  every contiguous run that has reached the bucket size.  RCCL's stream waits
+  on the compute stream at issue time, so each all-reduce overlaps the
+  remaining backward kernels.
 """
 from __future__ import annotations
 
@@ -23,8 +32,10 @@ import torch.distributed as dist
 from . import _engine as E
 
 
-def world() -> int:
-    return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+def world(group=None) -> int:
+    if not (dist.is_available() and dist.is_initialized()):
+        return 1
+    return dist.get_world_size(group)
 
 
 def global_valid_count(labels: torch.Tensor, ignore_index: int = 255, group=None,
@@ -32,14 +43,14 @@ def global_valid_count(labels: torch.Tensor, ignore_index: int = 255, group=None
     """All-reduced number of labels != ignore_index (int64 tensor on labels' device).
     ``count_fn`` defaults to the HIP counting kernel."""
     cnt = (count_fn or E.count_valid)(labels, ignore_index)
-    if world() > 1:
+    if world(group) > 1:
         dist.all_reduce(cnt, group=group)
     return cnt
 
 
 def allreduce_gradients(params: Iterable[torch.nn.Parameter], group=None) -> None:
     """SUM-all-reduce every .grad with ONE collective over a flat buffer."""
-    if world() <= 1:
+    if world(group) <= 1:
         return
     gs: List[torch.Tensor] = [p.grad for p in params if p.grad is not None]
     if not gs:
@@ -54,27 +65,110 @@ def allreduce_gradients(params: Iterable[torch.nn.Parameter], group=None) -> Non
 
 
 def allreduce_confusion(conf: torch.Tensor, group=None) -> torch.Tensor:
-    if world() > 1:
+    if world(group) > 1:
         dist.all_reduce(conf, group=group)
     return conf
 
 
+def global_loss(ce_share: torch.Tensor, conf: torch.Tensor, num_classes: int,
+                smooth: float = 1e-6, group=None):
+    """(loss, ce, conf) of the whole global batch from this rank's CE share (CE
+    normalised by the global valid count) and its confusion counts, with one
+    fp64 all-reduce and no host sync.  loss = fp32(ce) + fp32(0.5 * dice_loss),
+    as the reference adds the python-float Dice term to the fp32 CE tensor
+    (helpers.py:797-803)."""
+    from .helpers import dice_loss_from_confusion_t
+    K = int(num_classes)
+    buf = torch.cat([ce_share.detach().reshape(1).to(torch.float64),
+                     conf.detach().reshape(-1).to(torch.float64)])
+    if world(group) > 1:
+        dist.all_reduce(buf, group=group)
+    ce = buf[0].to(torch.float32)
+    conf_g = buf[1:].round().to(torch.int64).view(conf.shape)
+    dice = dice_loss_from_confusion_t(conf_g, K, smooth)
+    loss = ce + (0.5 * dice).to(torch.float32)
+    return loss, ce, conf_g
+
+
+class GradBucketer:
+    """Overlaps the gradient all-reduce with the engine's backward.
+
+    ``ready(off, n)`` is called (through the engine's grad hook, in stream
+    order) when floats [off, off + n) of the flat gradient are final.  Adjacent
+    ranges are merged; a merged run of >= ``bucket_bytes`` is all-reduced
+    asynchronously at once.  ``finish()`` all-reduces what is left and makes the
+    current stream wait for every collective."""
+
+    def __init__(self, group=None, bucket_bytes: int = 4 << 20):
+        self.group, self.bucket_floats = group, max(1, bucket_bytes // 4)
+        self.flat: Optional[torch.Tensor] = None
+        self.runs: List[List[int]] = []   # pending [start, end) runs, disjoint
+        self.works = []
+        self.launched: List[tuple] = []   # (start, end) of every issued all-reduce
+
+    def begin(self, flat: torch.Tensor) -> None:
+        self.flat, self.runs, self.works, self.launched = flat, [], [], []
+
+    def _launch(self, a: int, b: int) -> None:
+        self.launched.append((a, b))
+        self.works.append(dist.all_reduce(self.flat[a:b], group=self.group, async_op=True))
+
+    def ready(self, off: int, n: int) -> None:
+        a, b = int(off), int(off) + int(n)
+        keep = []
+        for r in self.runs:
+            if r[1] == a:
+                a = r[0]
+            elif r[0] == b:
+                b = r[1]
+            else:
+                keep.append(r)
+        if b - a >= self.bucket_floats:
+            self.runs = keep
+            self._launch(a, b)
+        else:
+            self.runs = keep + [[a, b]]
+
+    def finish(self) -> None:
+        for a, b in sorted(self.runs):
+            self._launch(a, b)
+        self.runs = []
+        for w in self.works:
+            w.wait()
+        self.works = []
+
+
 class DataParallelSPFF:
     """Minimal DDP for an SPFF module (Lit or core): ``step(x, y)`` runs
-    forward, the global-count loss, backward and the gradient all-reduce."""
+    forward, the global-count loss, backward with the bucketed, overlapped
+    gradient all-reduce, and returns (loss, conf) of the GLOBAL batch -- the
+    values a single device would report for the concatenated batch."""
 
     def __init__(self, module: torch.nn.Module, num_classes: int, ignore_index: int = 255,
-                 group=None):
+                 group=None, bucket_bytes: int = 4 << 20, overlap: bool = True):
         self.module, self.K, self.ignore, self.group = module, int(num_classes), ignore_index, group
         self.params = [p for p in module.parameters()]
+        self.core = getattr(module, "model", module)
+        self.bucketer = GradBucketer(group, bucket_bytes) if overlap else None
 
     def step(self, x: torch.Tensor, y: torch.Tensor):
-        from .helpers import ce_dice_with_confusion
+        from .helpers import ce_dice_parts
         for p in self.params:
             p.grad = None
-        logits = self.module(x)
-        cnt = global_valid_count(y, self.ignore, self.group) if world() > 1 else None
-        loss, conf = ce_dice_with_confusion(logits, y, self.K, self.ignore, count_override=cnt)
-        loss.backward()
-        allreduce_gradients(self.params, self.group)
-        return loss, conf
+        n = world(self.group)
+        hook = self.bucketer if (n > 1 and self.bucketer is not None) else None
+        self.core.grad_hook = hook
+        try:
+            logits = self.module(x)
+            cnt = global_valid_count(y, self.ignore, self.group) if n > 1 else None
+            loss_loc, conf, ce = ce_dice_parts(logits, y, self.K, self.ignore,
+                                               count_override=cnt)
+            loss_loc.backward()
+        finally:
+            self.core.grad_hook = None
+        if n > 1 and hook is None:
+            allreduce_gradients(self.params, self.group)
+        if n == 1:
+            return loss_loc.detach(), conf
+        loss, _ce, conf_g = global_loss(ce, conf, self.K, group=self.group)
+        return loss, conf_g

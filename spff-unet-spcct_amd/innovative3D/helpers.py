@@ -24,6 +24,7 @@ from . import _engine as E
 
 __all__ = ["ce_plus_macro_dice_loss", "macro_dice_loss", "per_class_metrics_3d",
            "per_class_metrics_2d", "metrics_from_confusion", "ce_dice_with_confusion",
+           "ce_dice_parts", "dice_loss_from_confusion_t",
            "LOSS_REGISTRY"]
 
 
@@ -38,34 +39,47 @@ def _logits_cl(logits: torch.Tensor) -> torch.Tensor:
 
 
 class _CEDice(torch.autograd.Function):
+    """Outputs (loss, conf, ce): loss = ce + 0.5 * hard-Dice term (out4[1]); conf
+    [K, K+1] and the CE share ce (out4[0]) carry no gradient."""
+
     @staticmethod
     def forward(ctx, logits, labels, K, ignore_index, smooth, count_override):
         lcl = _logits_cl(logits)
         out4, dl, conf = E.ce_dice_forward(lcl, labels, K, ignore_index, smooth, count_override)
         ctx.dl = dl
         ctx.ndim = logits.ndim
-        ctx.conf = conf
-        ctx.mark_non_differentiable(conf)
-        return out4[1], conf
+        ce = out4[0]
+        ctx.mark_non_differentiable(conf, ce)
+        return out4[1], conf, ce
 
     @staticmethod
-    def backward(ctx, g, _gconf=None):
-        dl = ctx.dl
-        E.scale_(dl, g.reshape(1))
-        d = dl.permute(0, 4, 1, 2, 3)
+    def backward(ctx, g, _gconf=None, _gce=None):
+        # out of place: ctx.dl stays d(ce)/dlogits for a retained-graph second backward
+        d = torch.mul(ctx.dl, g.reshape(1).to(ctx.dl.dtype)).permute(0, 4, 1, 2, 3)
         if ctx.ndim == 4:
             d = d.squeeze(2)
         return d, None, None, None, None, None
 
 
-def ce_dice_with_confusion(logits, labels, num_classes, ignore_index=255, smooth=1e-6,
-                           count_override: Optional[torch.Tensor] = None):
-    """(loss, conf[K, K+1]) -- loss as ce_plus_macro_dice_loss; conf[pred, label]."""
+def ce_dice_parts(logits, labels, num_classes, ignore_index=255, smooth=1e-6,
+                  count_override: Optional[torch.Tensor] = None):
+    """(loss, conf[K, K+1], ce) on the device with no host sync: loss as
+    ce_plus_macro_dice_loss (differentiable through the CE only, as in the
+    reference), conf[pred, label] of the argmax, ce = the CE term (with
+    ``count_override`` = the global valid count, this rank's share of it)."""
     E.require_device(logits, "ce_plus_macro_dice_loss")
     if labels.ndim == logits.ndim and labels.shape[1] == 1:
         labels = labels[:, 0]
     return _CEDice.apply(logits, labels, int(num_classes), int(ignore_index), float(smooth),
                          count_override)
+
+
+def ce_dice_with_confusion(logits, labels, num_classes, ignore_index=255, smooth=1e-6,
+                           count_override: Optional[torch.Tensor] = None):
+    """(loss, conf[K, K+1]) -- loss as ce_plus_macro_dice_loss; conf[pred, label]."""
+    loss, conf, _ce = ce_dice_parts(logits, labels, num_classes, ignore_index, smooth,
+                                    count_override)
+    return loss, conf
 
 
 def ce_plus_macro_dice_loss(logits, labels, num_classes, ignore_index=255, smooth=1e-6):
@@ -96,6 +110,20 @@ def dice_loss_from_confusion(conf, num_classes, smooth=1e-6):
         fn = int(conf[:K, c].sum()) - tp
         vals.append((2 * tp + smooth) / (2 * tp + fp + fn + smooth))
     return 1.0 - (float(np.mean(vals)) if vals else 1.0)
+
+
+def dice_loss_from_confusion_t(conf: torch.Tensor, num_classes: int,
+                               smooth: float = 1e-6) -> torch.Tensor:
+    """dice_loss_from_confusion with torch ops on conf's device (fp64, no host sync).
+    conf: [K, K+1] or [K, K] counts (int64 or exactly-integer fp64)."""
+    K = int(num_classes)
+    c = conf.to(torch.float64)
+    if K < 2:
+        return torch.zeros((), dtype=torch.float64, device=conf.device)
+    tp = torch.diagonal(c[:, :K])[1:]
+    fp = c[1:K, :].sum(1) - tp
+    fn = c[:K, 1:K].sum(0) - tp
+    return 1.0 - ((2 * tp + smooth) / (2 * tp + fp + fn + smooth)).mean()
 
 
 def metrics_from_confusion(conf: np.ndarray, K: int, n_voxels: int, smooth: float = 1e-6):

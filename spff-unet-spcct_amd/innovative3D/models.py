@@ -187,6 +187,7 @@ class _SPFFFunction(torch.autograd.Function):
         ctx.plan = plan
         ctx.gen = plan.generation
         ctx.flat = flat
+        ctx.grad_hook = getattr(core, "grad_hook", None)
         ctx.slices = [(off, n, shape) for (_name, shape, off, n) in plan.params]
         return logits_cl.permute(0, 4, 1, 2, 3)
 
@@ -199,7 +200,7 @@ class _SPFFFunction(torch.autograd.Function):
         g_cl = g.permute(0, 2, 3, 4, 1)
         if not g_cl.is_contiguous():
             g_cl = g_cl.contiguous()
-        dflat = plan.backward(g_cl, ctx.flat)
+        dflat = plan.backward(g_cl, ctx.flat, grad_hook=ctx.grad_hook)
         grads = [dflat[o:o + n].view(s) for (o, n, s) in ctx.slices]
         return (None, None, None, *grads)
 
@@ -273,7 +274,7 @@ class UNet3D_SpectralCore(nn.Module):
                           num_classes=self.num_classes, base=self.base, ksd=self.ksd,
                           efilm=efilm, fgate=fgate, se=self.use_se, specse=self.use_specse,
                           device=x.device, math=getattr(self, "math", None), shard=shard,
-                          tag=f"{id(self)}:{tag}")
+                          owner=self, tag=tag)
         if shard[0] > 1:
             coll = getattr(self, "shard_coll", None)
             if coll is None:
@@ -504,7 +505,7 @@ class _UNet3DFunction(torch.autograd.Function):
             raise E.SpffError("3DUNet engine: another forward ran on this model before the "
                               "backward of this one; the engine keeps one forward's activations")
         g_cl = g.permute(0, 2, 3, 4, 1).contiguous()
-        dflat = plan.backward(g_cl, ctx.flat)
+        dflat = plan.backward(g_cl, ctx.flat, grad_hook=ctx.grad_hook)
         grads = [dflat[o:o + n].view(s) for (o, n, s) in ctx.slices]
         return (None, None, None, None, None, *grads)
 
@@ -562,7 +563,7 @@ class Cicek3DUNet(nn.Module):
                                  num_classes=self.num_classes, base=self.base,
                                  target_depth=int(target_depth) if target_depth != D else 0,
                                  device=x.device, math=getattr(self, "math", None),
-                                 tag=str(id(self)))
+                                 owner=self)
 
     def _engine_params(self, plan):
         named = dict(self.named_parameters())
@@ -779,7 +780,7 @@ class _SwinFunction(torch.autograd.Function):
             raise E.SpffError("SwinUNETR engine: another forward ran on this model before the "
                               "backward of this one; the engine keeps one forward's activations")
         g_cl = g.permute(0, 2, 3, 4, 1).contiguous()
-        dflat = plan.backward(g_cl, ctx.flat)
+        dflat = plan.backward(g_cl, ctx.flat, grad_hook=ctx.grad_hook)
         grads = [dflat[o:o + n].view(s) for (o, n, s) in ctx.slices]
         return (None, None, None, *grads)
 
@@ -898,7 +899,7 @@ class SwinUNETR(nn.Module):
                                num_classes=self.num_classes, feature_size=self.feature_size,
                                window=self.window, heads=self.num_heads, mlp_ratio=self.mlp_ratio,
                                device=x.device, math=getattr(self, "math", None),
-                               tag=str(id(self)))
+                               owner=self)
 
     def _engine_params(self, plan):
         named = dict(self.named_parameters())

@@ -105,23 +105,15 @@ class DepthShardedSPFF:
         self.params = [p for p in core.parameters()]
 
     def step(self, x: torch.Tensor, y: torch.Tensor):
-        from .helpers import ce_dice_with_confusion, dice_loss_from_confusion
+        from .helpers import ce_dice_parts
         for p in self.params:
             p.grad = None
         logits = self.core(x)
         self.last_logits = logits.detach()
         cnt = Dd.global_valid_count(y, self.ignore, self.group)
-        loss_loc, conf = ce_dice_with_confusion(logits, y, self.K, self.ignore,
-                                                count_override=cnt)
+        loss_loc, conf, ce = ce_dice_parts(logits, y, self.K, self.ignore, count_override=cnt)
         loss_loc.backward()
         Dd.allreduce_gradients(self.params, self.group)
-        # local value = local CE share + 0.5 * Dice of the LOCAL confusion; rebuild
-        # the global one from the summed CE shares and the summed confusion
-        conf_loc = conf.detach().cpu().numpy()
-        ce = (loss_loc.detach().double() -
-              0.5 * dice_loss_from_confusion(conf_loc, self.K)).reshape(1)
-        if Dd.world() > 1:
-            dist.all_reduce(ce, group=self.group)
-        Dd.allreduce_confusion(conf, self.group)
-        loss = ce[0] + 0.5 * dice_loss_from_confusion(conf.cpu().numpy(), self.K)
-        return loss, conf
+        # the global value: summed CE shares + 0.5 * Dice of the summed confusion
+        loss, _ce, conf_g = Dd.global_loss(ce, conf, self.K, group=self.group)
+        return loss, conf_g

@@ -39,6 +39,7 @@ if str(HERE) not in sys.path:
 
 import torch  # noqa: E402
 
+from innovative3D import _engine as E  # noqa: E402
 from innovative3D import config as C  # noqa: E402
 from innovative3D.lightning_compat import pl  # noqa: E402
 from innovative3D.synthetic import SyntheticSPCCT  # noqa: E402
@@ -196,6 +197,9 @@ def train_and_log(model_name, builder, seed, S: Settings, datasets=None):
         w.writerow(["metric", "value"])
         for k in sorted(tem):
             w.writerow([k, tem[k]])
+    # free this run's engine plans / workspaces before the next (variant, seed)
+    for m in model.modules():
+        E.release_plans(m)
     return tem.get("test_macro_dice", float("nan"))
 
 

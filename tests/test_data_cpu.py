@@ -71,3 +71,32 @@ def test_resize_is_interpolate_antialias():
     ref = F.interpolate(t.unsqueeze(1), size=(5, 7), mode="bilinear", align_corners=False,
                         antialias=True).squeeze(1)
     assert torch.equal(DO.resize_frames(t, 5, 7), ref)
+
+
+def test_device_batch_loader_order_matches_torch_dataloader():
+    """DeviceBatchLoader(shuffle=True) visits samples in the order the reference's
+    DataLoader(shuffle=True) draws (datasets.py:318-323: RandomSampler on torch's
+    default generator) for the same torch seed."""
+    import torch
+    from innovative3D.datasets import DeviceBatchLoader
+    n = 11
+
+    class _DS:
+        images = torch.arange(n, dtype=torch.float32).view(n, 1, 1, 1)
+        labels = torch.zeros(n, 1, 1, 1, dtype=torch.int64)
+        transform = None
+
+        def __len__(self):
+            return n
+
+        def __getitem__(self, i):
+            return i
+    for seed in (0, 7):
+        torch.manual_seed(seed)
+        ref = [int(i) for b in torch.utils.data.DataLoader(_DS(), batch_size=3, shuffle=True)
+               for i in b]
+        after_ref = torch.rand(1)
+        torch.manual_seed(seed)
+        got = [int(v) for x, _y in DeviceBatchLoader(_DS(), 3, True) for v in x.reshape(-1)]
+        assert got == ref
+        assert torch.equal(torch.rand(1), after_ref)  # same number of default-generator draws

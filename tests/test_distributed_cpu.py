@@ -79,3 +79,82 @@ def test_single_process_helpers_are_noops():
     c = Dd.global_valid_count(torch.tensor([1, 255, 3]), 255,
                               count_fn=lambda t, ig: (t != ig).sum().reshape(1))
     assert int(c) == 2
+
+
+def _worker_loss(rank, world, port, out_path):
+    """Per rank: the CE share (CE normalised by the global count) and confusion
+    of its own sample -> distributed.global_loss; and a GradBucketer run over a
+    flat vector with ranges reported in the engine's backward order."""
+    import sys
+    import pathlib
+    root = pathlib.Path(__file__).resolve().parents[1]
+    sys.path[:0] = [str(root / "tests"), str(root), str(root / "spff-unet-spcct_amd")]
+    from _golden import cfg_of, load, state_of
+    from oracle import spff_oracle as O
+    from innovative3D import distributed as Dd
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(1)
+    d = load("fx3_fgate_even_b2")
+    cfg = cfg_of(d["meta"])
+    K = cfg.num_classes
+    P = O.params_from_state(state_of(d), requires_grad=False)
+    x = torch.from_numpy(d["x"][rank:rank + 1])
+    y = torch.from_numpy(d["labels"][rank:rank + 1])
+    cnt = Dd.global_valid_count(y, 255, count_fn=lambda t, ig: (t != ig).sum().reshape(1))
+    logits = O.forward(P, x, cfg)
+    ce = F.cross_entropy(logits, y, ignore_index=255, reduction="sum") / cnt.double()
+    conf = torch.zeros(K, K + 1, dtype=torch.int64)
+    conf[:, :K] = torch.from_numpy(O.confusion(logits, y, K, 255))
+    loss, ce_g, conf_g = Dd.global_loss(ce.float(), conf, K)
+    # bucketed gradient all-reduce: rank-dependent values, engine-like range order
+    n = 1000
+    flat = torch.arange(n, dtype=torch.float32) * (rank + 1)
+    b = Dd.GradBucketer(bucket_bytes=4 * 150)
+    b.begin(flat)
+    for a, m in ((900, 100), (700, 200), (650, 50), (990 - 990, 100), (300, 350), (100, 200)):
+        b.ready(a, m)
+    b.finish()
+    if rank == 0:
+        np.savez(out_path, loss=loss.numpy(), ce=ce_g.numpy(), conf=conf_g.numpy(),
+                 flat=flat.numpy(), launched=np.array(b.launched))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_dp_global_loss_and_bucketed_allreduce(tmp_path):
+    """DataParallelSPFF semantics (SURVEY §8(e) DP row; helpers.py:782-803): the
+    loss / confusion of a world-2 step equal the single-process full-batch
+    values, and the bucketed all-reduce sums every float exactly once."""
+    from oracle import spff_oracle as O
+    d = load("fx3_fgate_even_b2")
+    out = str(tmp_path / "l.npz")
+    mp.spawn(_worker_loss, args=(2, _free_port(), out), nprocs=2, join=True)
+    got = np.load(out)
+    cfg = cfg_of(d["meta"])
+    K = cfg.num_classes
+    P = O.params_from_state(state_of(d), requires_grad=False)
+    logits = O.forward(P, torch.from_numpy(d["x"]), cfg)
+    y = torch.from_numpy(d["labels"])
+    loss, ce, dice = O.ce_plus_macro_dice(logits, y, K)
+    conf = O.confusion(logits, y, K, 255)
+    assert np.array_equal(got["conf"][:, :K], conf) and not got["conf"][:, K].any()
+    assert abs(float(got["ce"]) - float(ce)) <= 2e-7 * abs(float(ce))
+    assert abs(float(got["loss"]) - float(loss)) <= 2e-7 * abs(float(loss))
+    assert np.array_equal(got["flat"], np.arange(1000, dtype=np.float32) * 3)
+    spans = sorted(map(tuple, got["launched"]))
+    assert spans[0][0] == 0 and spans[-1][1] == 1000
+    assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+    assert len(spans) < 6  # adjacent ranges were merged into buckets
+
+
+def test_dice_loss_from_confusion_t_matches_host():
+    import innovative3D.helpers as Hh
+    rng = np.random.default_rng(0)
+    for K in (2, 9, 13):
+        conf = rng.integers(0, 50, size=(K, K + 1))
+        conf[rng.integers(0, K), :] = 0
+        a = Hh.dice_loss_from_confusion(conf, K)
+        b = float(Hh.dice_loss_from_confusion_t(torch.from_numpy(conf), K))
+        assert abs(a - b) <= 1e-15
