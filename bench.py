@@ -58,11 +58,51 @@ def build_model(K, base, in_ch, D, device, seed=0):
     return core.to(device), st
 
 
-def cpu_baseline(st, K, base, in_ch, H, W, depth, steps, threads):
-    """Oracle (PyTorch-CPU restatement of the reference) fwd+loss+bwd on host cores."""
+def host_cpu_info():
+    """Host CPU topology (lscpu-style): physical cores = distinct (package, core) pairs
+    in /proc/cpuinfo; logical CPUs; the CPUs this process may run on; OMP_NUM_THREADS."""
+    phys, logical = set(), 0
+    try:
+        pkg = core = None
+        for line in open("/proc/cpuinfo"):
+            k, _, v = line.partition(":")
+            k = k.strip()
+            if k == "processor":
+                logical += 1
+            elif k == "physical id":
+                pkg = v.strip()
+            elif k == "core id":
+                core = v.strip()
+                phys.add((pkg, core))
+    except OSError:
+        pass
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return {"physical_cores": len(phys) or None, "logical_cpus": logical or os.cpu_count(),
+            "affinity_cpus": aff, "omp_num_threads": omp or None}
+
+
+def baseline_threads():
+    """All physical cores, bounded by this process's CPU share (affinity /
+    OMP_NUM_THREADS: the GPU box grants 16 CPUs per GPU)."""
+    h = host_cpu_info()
+    n = h["physical_cores"] or h["affinity_cpus"]
+    n = min(n, h["affinity_cpus"])
+    if h["omp_num_threads"]:
+        n = min(n, h["omp_num_threads"])
+    return max(1, n), h
+
+
+def cpu_baseline(st, K, base, x_cpu, y_cpu, depth, steps):
+    """Oracle (PyTorch-CPU restatement of the reference) fwd+loss+bwd on host cores, on a
+    bounded sample of the SAME inputs the GPU run uses: sample 0, depths [0, depth) of
+    config 2's batch (BASELINE.md 'CPU baseline timing': x ~ N(0,1) seed 0, labels with
+    1 % ignore).  voxels/s of the sample; the CPU cost is linear in the voxel count (a
+    fixed-work-per-voxel conv net), so this is the full batch's rate."""
     from oracle import spff_oracle as O
-    from innovative3D.synthetic import synthetic_batch
+    threads, host = baseline_threads()
     torch.set_num_threads(threads)
+    in_ch = x_cpu.shape[1]
     cfg = O.SpffCfg(in_ch=in_ch, num_classes=K, base=base)
     st_d = {k: v for k, v in st.items() if not k.endswith("._mask")}
     # masks for the sample depth (all ones, as in the reference, SURVEY F10)
@@ -71,7 +111,9 @@ def cpu_baseline(st, K, base, in_ch, H, W, depth, steps, threads):
         if k.endswith("freq_mask"):
             st_d[k] = np.ones((1, 1, depth // 2 + 1, 1, 1), np.float32)
     P = O.params_from_state(st_d)
-    x, y = synthetic_batch(1, in_ch, depth, H, W, K, ignore_frac=0.01, seed=123)
+    x = x_cpu[0:1, :, :depth].contiguous()
+    y = y_cpu[0:1, :depth].contiguous()
+    H, W = x.shape[3], x.shape[4]
     times = []
     for i in range(steps + 1):
         t0 = time.perf_counter()
@@ -81,11 +123,14 @@ def cpu_baseline(st, K, base, in_ch, H, W, depth, steps, threads):
             times.append(dt)
     med = statistics.median(times)
     vox = depth * H * W
+    full = x_cpu.shape[0] * x_cpu.shape[2] * H * W
     return {"value": vox / med, "unit": "voxels/s", "cores": torch.get_num_threads(),
-            "kind": "port",
-            "sample": f"oracle fwd+ce_plus_macro_dice+bwd on 1x{in_ch}x{depth}x{H}x{W} (K={K}, base "
-                      f"{base}) = 1/{(2 * 128) // depth} of the headline voxels; median of {steps} "
-                      f"steps after 1 warm-up ({med:.2f} s/step)"}
+            "kind": "port", "host": host,
+            "sample": f"oracle fwd+ce_plus_macro_dice+bwd on sample 0, depths 0..{depth - 1} of the "
+                      f"GPU run's own batch (synthetic_batch seed 0: 1x{in_ch}x{depth}x{H}x{W}, K={K}, "
+                      f"base {base}) = 1/{full // vox} of the headline voxels; median of {steps} "
+                      f"steps after 1 warm-up ({med:.2f} s/step; full batch extrapolated "
+                      f"{med * full / vox:.1f} s/step)"}
 
 
 def unet3d_flops(B, D, H, W, K, f=32, cin=1):
@@ -209,8 +254,7 @@ def cpu_baseline_unet3d(st, K, steps):
     """unet3d_oracle (PyTorch-CPU restatement of the reference) fwd + weighted CE + bwd."""
     from oracle import unet3d_oracle as U
     from innovative3D.synthetic import synthetic_batch
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
-    threads = min(threads, os.cpu_count() or threads)
+    threads, _host = baseline_threads()
     torch.set_num_threads(threads)
     P, B = U.params_from_state(st)
     cfg = U.UNet3DCfg(num_classes=K, base=32, in_ch=1, target_depth=16)
@@ -348,8 +392,7 @@ def cpu_baseline_swin(st, K, steps):
     """swin_oracle (PyTorch-CPU restatement) fwd + Lit loss + bwd on 1 x 1 x 128^3."""
     from oracle import swin_oracle as S
     from innovative3D.synthetic import synthetic_batch
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
-    threads = min(threads, os.cpu_count() or threads)
+    threads, _host = baseline_threads()
     torch.set_num_threads(threads)
     P = S.params_from_state(st, prefix="model.model.")
     cfg = S.SwinCfg(num_classes=K)
@@ -365,6 +408,15 @@ def cpu_baseline_swin(st, K, steps):
             "kind": "port",
             "sample": f"swin_oracle fwd+loss+bwd on 1x1x128^3 (half the batch); median of "
                       f"{steps} steps after 1 warm-up ({med:.2f} s/step)"}
+
+
+def rank_report(elapsed_local, steps, device):
+    """World size, backend and every rank's own ms/step (all ranks must call)."""
+    t = torch.tensor([elapsed_local], dtype=torch.float64, device=device)
+    ts = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(ts, t)
+    return {"world_size": dist.get_world_size(), "backend": str(dist.get_backend()),
+            "ms_per_step_by_rank": [float(v.item()) / steps * 1e3 for v in ts]}
 
 
 def main():
@@ -427,8 +479,10 @@ def main():
         B, S = args.batch, args.size
         core, st = build_model(K, args.base, args.in_ch, S, device)
         core.math = args.math
-        x, y = synthetic_batch(B, args.in_ch, S, S, S, K, ignore_frac=0.01, seed=1000 + rank,
-                               device=device)
+        # rank r's batch = synthetic_batch(seed r): rank 0 holds BASELINE.md's config-2
+        # inputs (seed 0), the ones tests/test_gpu_baseline_sizes.py checks against the oracle
+        x_cpu, y_cpu = synthetic_batch(B, args.in_ch, S, S, S, K, ignore_frac=0.01, seed=rank)
+        x, y = x_cpu.to(device), y_cpu.to(device)
         runner = DataParallelSPFF(core, K, 255)
         vox_step = B * S * S * S
 
@@ -452,6 +506,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    elapsed_local = elapsed
     prof = plan.prof_collect()
     plan.prof_enable(False)
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
@@ -538,11 +593,11 @@ def main():
         "roofline": roof,
         "cpu_baseline": None,
     }
+    if world > 1:
+        out["ranks"] = rank_report(elapsed_local, args.steps, device)
     if rank == 0 and world == 1 and args.cpu_baseline == "auto" and not sharded:
-        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
-        threads = min(threads, os.cpu_count() or threads)
-        out["cpu_baseline"] = cpu_baseline(st, K, args.base, args.in_ch, S, S, args.cpu_depth,
-                                           args.cpu_steps, threads)
+        out["cpu_baseline"] = cpu_baseline(st, K, args.base, x_cpu, y_cpu, args.cpu_depth,
+                                           args.cpu_steps)
         out["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
     if rank == 0:
         print(json.dumps(out), flush=True)
