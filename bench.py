@@ -441,6 +441,13 @@ def main():
                          "unet3d = BASELINE configs[2]: the 3DUNet variant, batch 4 x 1 x 5 x 96^2; "
                          "swin = BASELINE configs[4]: the SwinUNETR variant, batch 2 x 1 x 128^3")
     ap.add_argument("--slab-depth", type=int, default=64)
+    ap.add_argument("--strong", action="store_true",
+                    help="volume512: strong scaling -- ONE 5 x D x 512 x 512 volume (D = "
+                         "--volume-depth, 512 = the north star's volume) split into N slabs of "
+                         "D / N; N = 1 runs it whole on one GPU (lean memory layout)")
+    ap.add_argument("--volume-depth", type=int, default=512)
+    ap.add_argument("--memory", choices=("auto", "full", "lean"), default="auto",
+                    help="saved-activation layout (include/spff.h SPFF_MEM_*)")
     ap.add_argument("--hw", type=int, default=512)
     ap.add_argument("--cpu-depth", type=int, default=32)
     ap.add_argument("--cpu-steps", type=int, default=3)
@@ -466,11 +473,19 @@ def main():
 
     K = args.classes
     sharded = args.workload == "volume512"
-    if sharded:  # weak scaling: a fixed slab per rank, global depth = slab * world
+    if sharded:  # weak scaling: a fixed slab per rank, global depth = slab * world;
+        # --strong: one volume of --volume-depth slices, D / world per rank
         from innovative3D.sharded import DepthShardedSPFF
-        B, Dl, HW = 1, args.slab_depth, args.hw
+        B, HW = 1, args.hw
+        if args.strong:
+            if args.volume_depth % world:
+                raise SystemExit(f"--volume-depth {args.volume_depth} not divisible by {world}")
+            Dl = args.volume_depth // world
+        else:
+            Dl = args.slab_depth
         core, st = build_model(K, args.base, args.in_ch, Dl * world, device)
         core.math = args.math
+        core.memory = args.memory
         x, y = synthetic_batch(1, args.in_ch, Dl, HW, HW, K, ignore_frac=0.01, seed=1000 + rank,
                                device=device)
         runner = DepthShardedSPFF(core, K, 255) if world > 1 else DataParallelSPFF(core, K, 255)
@@ -479,6 +494,7 @@ def main():
         B, S = args.batch, args.size
         core, st = build_model(K, args.base, args.in_ch, S, device)
         core.math = args.math
+        core.memory = args.memory
         # rank r's batch = synthetic_batch(seed r): rank 0 holds BASELINE.md's config-2
         # inputs (seed 0), the ones tests/test_gpu_baseline_sizes.py checks against the oracle
         x_cpu, y_cpu = synthetic_batch(B, args.in_ch, S, S, S, K, ignore_frac=0.01, seed=rank)
@@ -573,8 +589,12 @@ def main():
                            f"{Dl * world} x {HW} x {HW} volume depth-sharded into {world} x "
                            f"{Dl}-slice slabs (BASELINE configs[3] at 8 GPUs), K={K}, base {args.base}",
                "global_batch": 1, "shape": [1, args.in_ch, Dl * world, HW, HW],
-               "parallelism": f"depth{world}"}
-        metric = "voxels/sec fwd+bwd, SPFF-UNet 5-ch volume depth-sharded (512^3 at 8 GPUs)"
+               "parallelism": f"depth{world}", "memory_layout": plan.memory,
+               "workspace_GiB": plan.ws_bytes / 2 ** 30}
+        metric = ("voxels/sec fwd+bwd, SPFF-UNet 5-ch volume depth-sharded (512^3 at 8 GPUs)"
+                  if not args.strong else
+                  f"voxels/sec fwd+bwd, SPFF-UNet one 5x{args.volume_depth}x{HW}x{HW} volume, "
+                  f"depth-sharded over N GPUs (strong scaling)")
     else:
         cfg = {"workload": f"SPFF-UNet fwd+ce_plus_macro_dice+bwd, batch {B} x {args.in_ch}ch x "
                            f"{S}^3 per GPU, K={K}, base {args.base}",
@@ -585,8 +605,8 @@ def main():
         "metric": metric,
         "value": value, "unit": "voxels/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-        "conv_math": args.math,
+        "scaling": "strong" if (sharded and args.strong) else "weak", "vs_baseline": None,
+        "dtype": "f32", "conv_math": args.math,
         "data": "synthetic (x~N(0,1), labels U[0,K) with 1% ignore=255; weights from weightgen seed 0)",
         "config": cfg,
         "loss": float(loss.item()),

@@ -59,8 +59,18 @@ typedef struct spff_cfg {
    * shard_world * depth; requires batch == 1 and a collectives table, see spff_coll below.
    * shard_world <= 1: unsharded. */
   int shard_world, shard_rank;
-  int reserved[5];                          /* zero */
+  /* saved-activation layout: SPFF_MEM_FULL keeps every block's conv outputs, IN /
+   * gate outputs and up-conv outputs (~2.8 KB per input voxel); SPFF_MEM_LEAN keeps
+   * only the conv outputs y1, y2 and per-(b,c[,d]) coefficients and recomputes the
+   * rest in the backward (~1.7 KB per voxel: one 5 x 512^3 volume fits one MI355X;
+   * +~3 % step time); SPFF_MEM_AUTO (0) = lean from 2^26 voxels per plan. */
+  int memory_mode;
+  int reserved[4];                          /* zero */
 } spff_cfg;
+
+#define SPFF_MEM_AUTO 0
+#define SPFF_MEM_FULL 1
+#define SPFF_MEM_LEAN 2
 
 /* The shard group's collectives, implemented by the caller (e.g. RCCL through
  * torch.distributed) and called by the engine in stream order on the stream of

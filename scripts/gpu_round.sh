@@ -12,6 +12,8 @@ for step in "$@"; do
     tests) timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -s --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1; rc=$? ;;
     dp) timeout -k 10 400 python -u -m pytest tests/test_gpu_dp.py -m gpu -x -v -s --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_dp.log 2>&1; rc=$? ;;
     sizes) timeout -k 10 1000 python -u -m pytest tests/test_gpu_baseline_sizes.py -m gpu -x -v -s --timeout 900 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_sizes.log 2>&1; rc=$? ;;
+    memory) timeout -k 10 400 python -u -m pytest tests/test_gpu_memory.py -m gpu -x -v -s --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_memory.log 2>&1; rc=$? ;;
+    strong1) timeout -k 10 600 python bench.py --workload volume512 --strong --steps 2 --warmup 1 > gpurun_out/bench_strong1.log 2>&1; rc=$? ;;
     smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$? ;;
     bench) timeout -k 10 600 python bench.py --steps 3 --warmup 1 --cpu-steps 1 > gpurun_out/bench_quick.log 2>&1; rc=$? ;;
     benchu3d) timeout -k 10 600 python bench.py --workload unet3d --steps 10 --warmup 3 > gpurun_out/bench_unet3d.log 2>&1; rc=$? ;;

@@ -100,6 +100,8 @@ struct spff_plan {
   spff_cfg cfg;
   Vol vol[4];
   int f, KD, ldx, K;
+  bool lean = false;  // SPFF_MEM_LEAN layout: a1 / out / up-conv outputs live in the
+                      // gradient scratch and are recomputed in the backward
   std::vector<PEnt> params;
   int64_t nparam = 0;
   Blk blk[7];
@@ -237,6 +239,11 @@ int build_plan(spff_plan* p) {
   if (c.in_ch > 64) return fail(SPFF_EINVAL, "in_ch > 64 not supported");
   if (c.math < SPFF_MATH_F32 || c.math > SPFF_MATH_BF16X3)
     return fail(SPFF_EINVAL, "math must be one of SPFF_MATH_*");
+  if (c.memory_mode < SPFF_MEM_AUTO || c.memory_mode > SPFF_MEM_LEAN)
+    return fail(SPFF_EINVAL, "memory_mode must be one of SPFF_MEM_*");
+  p->lean = c.memory_mode == SPFF_MEM_LEAN ||
+            (c.memory_mode == SPFF_MEM_AUTO &&
+             (int64_t)c.batch * c.depth * c.height * c.width >= (int64_t(1) << 26));
   const int world = c.shard_world > 1 ? c.shard_world : 1;
   if (world > 1) {
     if (c.batch != 1) return fail(SPFF_EINVAL, "depth-sharded plans take batch == 1");
@@ -318,9 +325,13 @@ int build_plan(spff_plan* p) {
     const Vol& v = p->vol[b.lvl];
     const size_t act = nvox(v) * b.C * sizeof(float);
     b.y1 = p->alloc(act);
-    b.a1 = p->alloc_halo(act, slice(v, b.C));
     b.y2 = p->alloc(act);
-    b.out = p->alloc_halo(act, slice(v, b.C));
+    if (!p->lean) {
+      b.a1 = p->alloc_halo(act, slice(v, b.C));
+      b.out = p->alloc_halo(act, slice(v, b.C));
+    } else if (i == 3) {
+      b.out = p->alloc(act);  // the bottleneck output (up3's input) is kept: 1/64 size
+    }
     const size_t bc = (size_t)B * b.C * sizeof(float);
     b.mean1 = p->alloc(bc); b.rstd1 = p->alloc(bc); b.al1 = p->alloc(bc); b.de1 = p->alloc(bc);
     b.mean2 = p->alloc(bc); b.rstd2 = p->alloc(bc); b.al2 = p->alloc(bc); b.de2 = p->alloc(bc);
@@ -363,7 +374,7 @@ int build_plan(spff_plan* p) {
   for (int u = 0; u < 3; ++u) {
     UpL& U = p->up[u];
     const Vol& vh = p->vol[U.lvl_low - 1];
-    U.out = p->alloc_halo(nvox(vh) * U.Cout * sizeof(float), slice(vh, U.Cout));
+    if (!p->lean) U.out = p->alloc_halo(nvox(vh) * U.Cout * sizeof(float), slice(vh, U.Cout));
     U.pk = p->alloc(upconv_pack_floats(U.Cin, U.Cout) * sizeof(float));
     wg = std::max(wg, upconv_wgrad_ws_bytes(p->vol[U.lvl_low], U.Cin, U.Cout));
   }
@@ -379,12 +390,37 @@ int build_plan(spff_plan* p) {
   p->wg_ws = p->alloc(wg);
   p->wt = p->alloc(wt);
   p->cst = p->alloc(cst);
-  const size_t gbytes = nvox(v0) * f * sizeof(float);  // max over levels of V_l * C_l
-  p->G_out = p->alloc(gbytes);
-  p->G_dy2 = p->alloc_halo(gbytes, slice(v0, f));  // level-0 slice = the largest
+  // gradient scratch, sized for level 0 ([V0][f]); a level-l tensor of the path
+  // (V0 / 4^l voxels x f 2^l channels) fills 1 / 2^l of a buffer.  Halo'd (level-0
+  // slice = the largest) so any of them can hold a conv input.
+  const size_t gbytes = nvox(v0) * f * sizeof(float);
+  p->G_out = p->alloc_halo(gbytes, slice(v0, f));
+  p->G_dy2 = p->alloc_halo(gbytes, slice(v0, f));
   p->G_da1 = p->alloc_halo(gbytes, slice(v0, f));
-  p->G_dx = p->alloc(gbytes);
-  for (int l = 0; l < 3; ++l) p->dskip[l] = p->alloc(nvox(p->vol[l]) * (f << l) * sizeof(float));
+  p->G_dx = p->alloc_halo(gbytes, slice(v0, f));
+  // skip gradients: dskip0 needs a level-0 buffer of its own; dskip1 (alive from
+  // dec2's input gradient to enc2's backward) and dskip2 (dec3 -> enc3) sit in the
+  // upper halves of G_dx / G_out, which only level-0 tensors reach (dec1, before)
+  p->dskip[0] = p->alloc(gbytes);
+  p->dskip[1] = p->G_dx + gbytes / 2;
+  p->dskip[2] = p->G_out + gbytes / 2;
+  if (p->lean) {
+    // forward placement of the unsaved tensors (lifetimes in DESIGN.md §2):
+    //   enc1 a1/out -> G_da1 (out alive until dec1's first conv)
+    //   enc2 a1/out -> G_dy2 [lower half]     enc3 a1/out -> G_out [lower quarter]
+    //   bott a1, dec3 a1, dec2 a1, up3/up2/up1 outputs -> G_dx (each dead before the next)
+    //   dec3 out -> G_dy2 upper half (enc2's output still alive below it)
+    //   dec2 out -> G_dy2 (enc2's output dead)   dec1 a1 -> G_da1   dec1 out -> G_out
+    Blk* B = p->blk;
+    B[0].a1 = B[0].out = p->G_da1;
+    B[1].a1 = B[1].out = p->G_dy2;
+    B[2].a1 = B[2].out = p->G_out;
+    B[3].a1 = p->G_dx;
+    B[4].a1 = p->G_dx; B[4].out = p->G_dy2 + gbytes / 2;
+    B[5].a1 = p->G_dx; B[5].out = p->G_dy2;
+    B[6].a1 = p->G_da1; B[6].out = p->G_out;
+    for (int u = 0; u < 3; ++u) p->up[u].out = p->G_dx;
+  }
   if (world > 1) p->part_d = p->alloc((size_t)B * 8 * f * 2 * sizeof(double));
 
   host_pe(p->co.D_glob, p->pe_host);  // global depths; a slab reads columns d_off + d  // uploaded on the first forward (plan creation needs no GPU)
@@ -548,9 +584,41 @@ int fwd_block(spff_plan* p, Blk& b, const Src2& in) {
   return SPFF_OK;
 }
 
-int bwd_block(spff_plan* p, Blk& b, const float* dout, const Dst2* dx, const Src2& in) {
+Src2 src2(const float* a, const float* b, int C) { return Src2{a, b, C, C, C}; }
+
+// block output out = lrelu(y2 * al2 + de2) [* P + Q] into dst (lean recompute)
+int recompute_out(spff_plan* p, const Blk& b, float* dst) {
+  const Vol& v = p->vol[b.lvl];
+  PROFB(p, 5, 0.0, 8.0 * (double)nvox(v) * b.C,
+        act_apply(p->F(b.y2), dst, p->F(b.al2), p->F(b.de2), b.tail() ? p->F(b.P) : nullptr,
+                  b.tail() ? p->F(b.Q) : nullptr, v, b.C, p->st));
+  return SPFF_OK;
+}
+
+// lean plans: rebuild the first conv's input [up | skip] of decoder block bi for its
+// weight gradient -- called once that block's dout (G_out) and dy2 (G_dy2) are dead:
+// the previous decoder's output (up-conv input) at its forward place, the up-conv
+// output into G_dx, the encoder skip into G_out, plus their halos when sharded
+int lean_dec_input(spff_plan* p, int bi, Src2* in) {
+  Blk* B = p->blk;
+  const Blk& d = B[bi];
+  const Blk& skip = B[6 - bi];
+  const Blk& prev = B[bi - 1];
+  UpL& U = p->up[bi - 4];
+  if (bi - 1 >= 4) CK(recompute_out(p, prev, p->F(prev.out)));
+  PROF(p, 3, 2.0 * nvox(p->vol[U.lvl_low]) * U.Cin * 4.0 * U.Cout,
+       upconv_fwd(p->F(prev.out), p->F(U.pk), p->P(U.b), p->F(U.out), p->vol[U.lvl_low], U.Cin,
+                  U.Cout, p->st));
+  CK(recompute_out(p, skip, p->F(p->G_out)));
+  *in = src2(p->F(U.out), p->F(p->G_out), d.C);
+  return halo_src(p, *in, p->vol[d.lvl]);
+}
+
+int bwd_block(spff_plan* p, Blk& b, const float* dout, const Dst2* dx, const Src2& in_saved,
+              int dec_bi = -1) {
   const Vol& v = p->vol[b.lvl];
   const int C = b.C, KD = p->KD;
+  Src2 in = in_saved;
   const float* A = nullptr;
   const float* Bc = nullptr;
   if (b.tail()) {
@@ -597,8 +665,15 @@ int bwd_block(spff_plan* p, Blk& b, const float* dout, const Dst2* dx, const Src
                        p->F(b.de2), p->P(b.g2), A, Bc, p->F(p->kk1), p->F(p->kk2), v, C, p->st));
   }
   const double V = (double)nvox(v), T = 9.0 * KD;
+  const float* a1 = p->F(b.a1);
+  if (p->lean) {  // a1 = lrelu(IN(y1)) again, into the buffer da1 overwrites next
+    PROFB(p, 5, 0.0, 8.0 * (double)nvox(v) * C,
+          act_apply(p->F(b.y1), da1, p->F(b.al1), p->F(b.de1), nullptr, nullptr, v, C, p->st));
+    CK(halo(p, da1, v, C));
+    a1 = da1;
+  }
   PROFB(p, 2, 2.0 * V * C * C * T, cbytes(V, C, C, T),
-       conv3d_wgrad(src1(p->F(b.a1), C), dy2, C, p->DP(b.c2.w), v, KD, C, C, p->cfg.math,
+       conv3d_wgrad(src1(a1, C), dy2, C, p->DP(b.c2.w), v, KD, C, C, p->cfg.math,
                     p->F(p->wg_ws), p->st));
   const int math = p->cfg.math;
   HIPCK(conv3d_pack(p->P(b.c2.w), p->F(p->wt), v, KD, C, C, true, math, p->st));
@@ -617,6 +692,7 @@ int bwd_block(spff_plan* p, Blk& b, const float* dout, const Dst2* dx, const Src
                        p->F(b.de1), p->P(b.g1), nullptr, nullptr, p->F(p->kk1), p->F(p->kk2), v,
                        C, p->st));
   }
+  if (p->lean && dec_bi >= 0) CK(lean_dec_input(p, dec_bi, &in));
   PROFB(p, 2, 2.0 * V * b.Cin * C * T, cbytes(V, b.Cin, C, T),
        conv3d_wgrad(in, da1, C, p->DP(b.c1.w), v, KD, b.Cin, C, p->cfg.math, p->F(p->wg_ws),
                     p->st));
@@ -628,8 +704,6 @@ int bwd_block(spff_plan* p, Blk& b, const float* dout, const Dst2* dx, const Src
   }
   return SPFF_OK;
 }
-
-Src2 src2(const float* a, const float* b, int C) { return Src2{a, b, C, C, C}; }
 
 // report dparams[a, b) final to the gradient-ready hook (no-op without one)
 int grad_ready(spff_plan* p, int64_t a, int64_t b) {
@@ -698,7 +772,7 @@ int backward(spff_plan* p, const float* dl) {
     const int C = d.C;             // = U.Cout = skip channels
     const int lvl = d.lvl;
     Dst2 dx{p->F(p->G_dx), p->F(p->dskip[lvl]), C, C, C};
-    CK(bwd_block(p, d, p->F(p->G_out), &dx, src2(p->F(U.out), p->F(B[lvl].out), C)));
+    CK(bwd_block(p, d, p->F(p->G_out), &dx, src2(p->F(U.out), p->F(B[lvl].out), C), bi));
     CK(block_grads_ready(p, d));
     if (p->dbg_stop == k + 1) return SPFF_OK;
     const float* upin = (ui == 0) ? p->F(B[3].out) : p->F(B[bi - 1].out);

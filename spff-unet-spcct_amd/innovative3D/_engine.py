@@ -30,7 +30,7 @@ class spff_cfg(ctypes.Structure):
         ("base", ctypes.c_int), ("ksd", ctypes.c_int), ("use_efilm", ctypes.c_int),
         ("use_fgate", ctypes.c_int), ("use_se", ctypes.c_int), ("use_specse", ctypes.c_int),
         ("math", ctypes.c_int), ("shard_world", ctypes.c_int), ("shard_rank", ctypes.c_int),
-        ("reserved", ctypes.c_int * 5),
+        ("memory_mode", ctypes.c_int), ("reserved", ctypes.c_int * 4),
     ]
 
 
@@ -66,6 +66,19 @@ class spff_coll(ctypes.Structure):
 # spff_grad_ready_fn (include/spff.h): dparams[off, off + n) final during spff_backward
 GRAD_READY_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
                                  ctypes.c_void_p)
+
+
+# saved-activation layout (include/spff.h SPFF_MEM_*)
+MEMORY_MODES = {"auto": 0, "full": 1, "lean": 2}
+
+
+def default_memory() -> str:
+    """Saved-activation layout for new plans: $SPFF_MEMORY, else "auto" (lean from 2^26
+    voxels per plan)."""
+    m = os.environ.get("SPFF_MEMORY", "auto")
+    if m not in MEMORY_MODES:
+        raise SpffError(f"SPFF_MEMORY={m!r}: expected one of {sorted(MEMORY_MODES)}")
+    return m
 
 
 # conv arithmetic (include/spff.h SPFF_MATH_*)
@@ -211,12 +224,17 @@ class Plan:
 
     def __init__(self, batch, in_ch, depth, height, width, num_classes, base=32, ksd=3,
                  efilm=True, fgate=True, se=True, specse=True, device=None, math=None,
-                 shard_world=1, shard_rank=0):
+                 shard_world=1, shard_rank=0, memory=None):
         math = default_math() if math is None else math
         if math not in MATH_NAMES:
             raise SpffError(f"math={math!r}: expected one of {sorted(MATH_NAMES)}")
+        memory = default_memory() if memory is None else memory
+        if memory not in MEMORY_MODES:
+            raise SpffError(f"memory={memory!r}: expected one of {sorted(MEMORY_MODES)}")
         cfg = spff_cfg()
         cfg.math = MATH_NAMES[math]
+        cfg.memory_mode = MEMORY_MODES[memory]
+        self.memory = memory
         cfg.shard_world, cfg.shard_rank = int(shard_world), int(shard_rank)
         self.math = math
         self.shard = (int(shard_world), int(shard_rank))
@@ -226,7 +244,7 @@ class Plan:
                                                                     int(bool(se)), int(bool(specse)))
         self.cfg = cfg
         self.key = (batch, in_ch, depth, height, width, num_classes, base, ksd, bool(efilm),
-                    bool(fgate), bool(se), bool(specse), math, self.shard)
+                    bool(fgate), bool(se), bool(specse), math, self.shard, memory)
         L = lib()
         h = ctypes.c_void_p()
         check(L.spff_plan_create(ctypes.byref(cfg), ctypes.byref(h)), "spff_plan_create")
@@ -428,7 +446,8 @@ def get_plan(owner=None, tag: str = "", **kw) -> Plan:
     key = (kw["batch"], kw["in_ch"], kw["depth"], kw["height"], kw["width"], kw["num_classes"],
            kw.get("base", 32), kw.get("ksd", 3), bool(kw.get("efilm", True)),
            bool(kw.get("fgate", True)), bool(kw.get("se", True)), bool(kw.get("specse", True)),
-           kw.get("math") or default_math(), tuple(kw.get("shard", (1, 0))))
+           kw.get("math") or default_math(), tuple(kw.get("shard", (1, 0))),
+           kw.get("memory") or default_memory())
 
     def make():
         kk = dict(kw)

@@ -54,8 +54,15 @@ class _CEDice(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g, _gconf=None, _gce=None):
-        # out of place: ctx.dl stays d(ce)/dlogits for a retained-graph second backward
-        d = torch.mul(ctx.dl, g.reshape(1).to(ctx.dl.dtype)).permute(0, 4, 1, 2, 3)
+        # scaled in place (no second logits-sized buffer: 7 GB at 5 x 512^3) and handed
+        # out exactly once; a retained-graph second backward would see a scaled tensor
+        dl = ctx.dl
+        if dl is None:
+            raise RuntimeError("ce_plus_macro_dice_loss: backward ran twice through the same "
+                               "graph (retain_graph); recompute the loss for a second backward")
+        ctx.dl = None
+        E.scale_(dl, g.reshape(1))
+        d = dl.permute(0, 4, 1, 2, 3)
         if ctx.ndim == 4:
             d = d.squeeze(2)
         return d, None, None, None, None, None

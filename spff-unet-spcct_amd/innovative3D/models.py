@@ -274,6 +274,7 @@ class UNet3D_SpectralCore(nn.Module):
                           num_classes=self.num_classes, base=self.base, ksd=self.ksd,
                           efilm=efilm, fgate=fgate, se=self.use_se, specse=self.use_specse,
                           device=x.device, math=getattr(self, "math", None), shard=shard,
+                          memory=getattr(self, "memory", None),
                           owner=self, tag=tag)
         if shard[0] > 1:
             coll = getattr(self, "shard_coll", None)

@@ -61,3 +61,21 @@ def test_workspace_size_headline_config_fits_hbm():
     assert 5e9 < p.ws_bytes < 40e9
     # 5 491 284 (registry, Cin=1) + 27*32*4 (Cin=5 first conv) + 7 lazy masks of L=65
     assert p.nfloats == 5491284 + 27 * 32 * 4 + 7 * 65
+
+
+def test_full_volume_512_fits_one_mi355x():
+    """BASELINE configs[3]: one 1 x 5 x 512^3 volume on ONE GPU (the north star's
+    8-vs-1 comparison on the same volume).  memory_mode auto picks the lean layout
+    from 2^26 voxels; its workspace must leave room on 288 GB of HBM for the input
+    (2.7 GB), labels (1.1 GB), logits and dlogits (7.0 GB each) and the flat params."""
+    p = E.Plan(1, 5, 512, 512, 512, 13)
+    V = 512 ** 3
+    assert p.memory == "auto"
+    assert p.ws_bytes / V <= 1750, p.ws_bytes / V
+    assert p.ws_bytes + V * (5 * 4 + 8 + 2 * 13 * 4) < 250 * 2 ** 30
+    full = E.Plan(1, 5, 512, 512, 512, 13, memory="full")
+    assert full.ws_bytes > 288e9  # why the lean layout exists
+    head = E.Plan(2, 5, 128, 128, 128, 13)  # the headline keeps the full (fastest) layout
+    assert head.ws_bytes == E.Plan(2, 5, 128, 128, 128, 13, memory="full").ws_bytes
+    with pytest.raises(E.SpffError):
+        E.Plan(1, 5, 8, 32, 32, 5, memory="small")

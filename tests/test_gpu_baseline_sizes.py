@@ -110,7 +110,7 @@ def test_config2_headline_matches_oracle(config2_oracle, mth):
     loss, _conf = Hh.ce_dice_with_confusion(logits, y.to(DEV), K13, 255)
     loss.backward()
     torch.cuda.synchronize()
-    grads = {k: p.grad for k, p in core.named_parameters() if not k.endswith("._mask")}
+    grads = {k: p.grad for k, p in core.named_parameters(remove_duplicate=False)}
     _compare(f"config2 2x5x128^3 {mth}", logits.detach().cpu(), float(loss), grads, ref_logits,
              ref_loss, ref_grads)
 
@@ -154,7 +154,7 @@ def _sh_worker(rank, world, port, out):
                            y[:, off:off + d].contiguous().to(DEV))
     torch.cuda.synchronize()
     np.savez(f"{out}.{rank}.npz", logits=step.last_logits.cpu().numpy(), loss=float(loss),
-             **({"g_" + k: p.grad.cpu().numpy() for k, p in core.named_parameters()
+             **({"g_" + k: p.grad.cpu().numpy() for k, p in core.named_parameters(remove_duplicate=False)
                  if p.grad is not None and not k.endswith("._mask")} if rank == 0 else {}))
     del step, core
     dist.barrier()
