@@ -57,19 +57,25 @@ def test_unet3d_oracle_matches_reference(name):
             key = k[len("bufafter/"):]
             np.testing.assert_allclose(B[key[len(pre):]].numpy(), d[k], rtol=1e-5, atol=1e-6,
                                        err_msg=key)
-    # gradients
+    # gradients.  5e-4 of max|ref| + 2e-5 of the largest gradient entry of the model: the
+    # fixture is one CPU's fp32 result and another CPU's oneDNN sums in another order
+    # (observed on a second host: 1.3e-4 relative on the Cin=5 first-layer weight gradient,
+    # 4.4e-7 absolute on a nearly cancelling BatchNorm bias gradient of max 2.8e-4; bitwise
+    # equal on the host that wrote the fixtures).
+    gmax = max(float(np.abs(d[k]).max()) for k in d
+               if k.startswith("grad/") or k.startswith("gradhead/"))
     for k in d["param_names"]:
         k = str(k)
         g = P[k[len(pre):]].grad.numpy()
         if "grad/" + k in d:
             ref_g = d["grad/" + k]
             scale = max(1e-6, float(np.abs(ref_g).max()))
-            assert float(np.abs(g - ref_g).max()) <= 1e-4 * scale + 1e-7, k
+            assert float(np.abs(g - ref_g).max()) <= 5e-4 * scale + 2e-5 * gmax, k
         else:
             flat = g.reshape(-1)
             scale = max(1e-6, float(np.abs(d["gradhead/" + k]).max()))
-            np.testing.assert_allclose(flat[:64], d["gradhead/" + k], atol=1e-4 * scale + 1e-7)
-            np.testing.assert_allclose(flat[-64:], d["gradtail/" + k], atol=1e-4 * scale + 1e-7)
+            np.testing.assert_allclose(flat[:64], d["gradhead/" + k], atol=5e-4 * scale + 2e-5 * gmax)
+            np.testing.assert_allclose(flat[-64:], d["gradtail/" + k], atol=5e-4 * scale + 2e-5 * gmax)
             s = d["gradsum/" + k]
             assert math.isclose(float(np.sqrt((flat.astype(np.float64) ** 2).sum())), float(s[1]),
                                 rel_tol=1e-4, abs_tol=1e-9), k
