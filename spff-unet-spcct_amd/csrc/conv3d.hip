@@ -516,7 +516,7 @@ hipError_t conv3d_wgrad_reduce(const float* part, float* dw, int nsplit, int T, 
 
 hipError_t conv3d_wgrad(const Src2& x, const float* dy, int lddy, float* dw, Vol vol, int KD,
                         int Cin, int Cout, int math, float* ws, hipStream_t s) {
-  if (math != SPFF_MATH_F32)
+  if (math != SPFF_MATH_F32 && debug_split_wgrad())
     return conv3d_wgrad_x(x, dy, lddy, dw, vol, KD, Cin, Cout, math, ws, s);
   if (lddy % 4) return hipErrorInvalidValue;
   WgradPlan p = wgrad_plan(vol, Cin, Cout);

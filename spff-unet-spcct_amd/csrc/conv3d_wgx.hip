@@ -161,7 +161,7 @@ __global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x(
       yreg[k] = v;
     }
   };
-  auto stash = [&]() {
+  auto stash = [&](bool negate) {
 #pragma unroll
     for (int k = 0; k < NH; ++k) {
       const int i = tid + 256 * k;
@@ -177,7 +177,9 @@ __global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x(
     for (int k = 0; k < NY; ++k) {
       const int i = tid + 256 * k;
       uint2 o[NS];
-      split4<NS>(yreg[k], o);
+      const float4 yv = negate ? make_float4(-yreg[k].x, -yreg[k].y, -yreg[k].z, -yreg[k].w)
+                               : yreg[k];
+      split4<NS>(yv, o);
 #pragma unroll
       for (int p = 0; p < NS; ++p)
         *reinterpret_cast<uint2*>(Ys + p * WX_TV * WX_CO + 4 * i) = o[p];
@@ -222,12 +224,24 @@ __global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x(
   const int tend = min(ntiles, tbeg + tps);
   if (tbeg < tend) fetch(tbeg);
   for (int tile = tbeg; tile < tend; ++tile) {
+    // sign-alternating accumulation (conv3d_x.hip): odd tiles stage -dy and the
+    // accumulators flip sign at every tile boundary, so the bf16 MFMA's one-sided
+    // rounding of the small split products cancels between consecutive tiles
+    if (tile != tbeg) {
+#pragma unroll
+      for (int j = 0; j < NJMAX; ++j) acc[j] = -acc[j];
+    }
     __syncthreads();  // previous compute done reading LDS
-    stash();
+    stash(((tile - tbeg) & 1) != 0);
     __syncthreads();
     if (tile + 1 < tend) fetch(tile + 1);
     if (nj == NJMAX) compute(std::integral_constant<int, NJMAX>{});
     else if constexpr (NJMAX > 1) compute(std::integral_constant<int, NJMAX - 1>{});
+  }
+
+  if (tend > tbeg && ((tend - 1 - tbeg) & 1)) {
+#pragma unroll
+    for (int j = 0; j < NJMAX; ++j) acc[j] = -acc[j];
   }
 
   // partial slab [split][tap][kpad][npad]: row i = chunk (i/4) channel i%4, col = co

@@ -25,6 +25,15 @@
 //    distinct pos mod 16: a 32-row block covers two W-rows of 16 voxels and the
 //    second row is rotated by 2 (tw = (r + 14) mod 16), which cancels the halo
 //    row pitch 18 = 2 mod 16 -- conflict-free without padding.
+//  * sign-alternating accumulation.  The bf16 MFMA adds products much smaller
+//    than its fp32 accumulator (the hm / mh / hl / lh / mm terms) with a bias
+//    toward -infinity of a few thousandths of an ulp per instruction (measured:
+//    scripts/mfma_round4.hip, -0.75 ulp of rms(D) after 54 k-steps of 6 products;
+//    the f32 MFMA's fma chain has none).  Small, but the same sign at every
+//    output, so sums over voxels -- the InstanceNorm / gate reductions the
+//    backward is made of -- keep it coherently.  Odd input-channel chunks carry
+//    negated weights and the accumulator is negated at every chunk boundary, so
+//    consecutive chunks' biases cancel.
 //  * register-prefetch pipeline as in k_conv3d_fwd: chunk c+1's halo (fp32)
 //    and weight slab (both fp32) are in flight during chunk c's MFMAs, and
 //    are split into bf16 planes on their way into LDS.
@@ -72,6 +81,7 @@ __device__ __forceinline__ void split_bf16(float x, unsigned short (&o)[NS]) {
 // global->LDS DMA copy: wp[nb][kc][plane][T2][BN] units of 8 bf16 (16 B), unit
 // element e = gemm k = kc*8 + e, gemm n = nb*BN + co; fwd: k = ci, n = co;
 // dgrad: k = co, n = ci with the tap flipped.  Taps >= T and padded k/n are zero.
+// Odd chunks kc are stored NEGATED (sign-alternating accumulation, see below).
 template <int NS>
 __global__ void k_conv_pack_x(const float* __restrict__ w, uint4* __restrict__ wp, int Cout,
                               int Cin, int T, int T2, int nkc, int npad, int BN, int dgrad) {
@@ -95,7 +105,7 @@ __global__ void k_conv_pack_x(const float* __restrict__ w, uint4* __restrict__ w
           if (k < Cout && n < Cin) v = w[((int64_t)k * Cin + n) * T + (T - 1 - tap)];
         }
       }
-      split_bf16<NS>(v, s[e]);
+      split_bf16<NS>((kc & 1) ? -v : v, s[e]);
     }
     const int64_t base = (((int64_t)nb * nkc + kc) * NS) * T2 * BN + (int64_t)tap * BN + co;
 #pragma unroll
@@ -258,7 +268,15 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
   // on its SIMD: one static priority bump (MI355X_MICROARCH "two waves per SIMD")
   if (SPFF_XPRIO && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
   for (int kc = kc0; kc < kc1; ++kc) {
-    if (kc != kc0) __syncthreads();
+    if (kc != kc0) {
+      // sign-alternating accumulation: odd chunks carry negated weights, so the
+      // accumulator holds (-1)^kc x the partial sum; flip it at every chunk boundary
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) acc[mb][nb] = -acc[mb][nb];
+      __syncthreads();
+    }
     if (SPFF_XDIAG != 1 || kc == kc0) stash(kc);
     __syncthreads();  // (vmcnt(0): the weight DMA has landed)
     if (kc + 1 < kc1) fetch(kc + 1);
@@ -310,6 +328,13 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
           acc[mb][nb] = c;
         }
     }
+  }
+
+  if ((kc1 - 1) & 1) {
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) acc[mb][nb] = -acc[mb][nb];
   }
 
 // ---- epilogue: C[i][j], row i = voxel (vrow mapping), col j = out channel ----
@@ -521,20 +546,28 @@ XDims xdims(int KD, int Cin_w, int Cout_w, bool dgrad) {
   d.T2 = (d.T + 1) & ~1;
   return d;
 }
-// SPFF_DEBUG_SPLIT=fwd|dgrad (diagnostics only) limits the split path to one direction
+// SPFF_DEBUG_SPLIT (diagnostics only): a comma list of the directions that take
+// the split path, e.g. "fwd,wgrad"; the others run the f32 MFMA kernels.  Unset:
+// all three.  Bits: 1 fwd, 2 dgrad, 4 wgrad.
 int debug_split_dir() {
   static int v = [] {
     const char* e = getenv("SPFF_DEBUG_SPLIT");
-    if (!e) return 0;
-    return strcmp(e, "fwd") == 0 ? 1 : strcmp(e, "dgrad") == 0 ? 2 : 0;
+    if (!e) return 7;
+    int m = 0;
+    if (strstr(e, "fwd")) m |= 1;
+    if (strstr(e, "dgrad")) m |= 2;
+    if (strstr(e, "wgrad")) m |= 4;
+    return m;
   }();
   return v;
 }
 bool use_split(Vol vol, int math, bool dgrad) {
-  const int dbg = debug_split_dir();
-  if (dbg && dbg != (dgrad ? 2 : 1)) return false;
+  if (!(debug_split_dir() & (dgrad ? 2 : 1))) return false;
   return math != SPFF_MATH_F32;
 }
+}  // namespace
+bool debug_split_wgrad() { return (debug_split_dir() & 4) != 0; }
+namespace {
 // split-K for launches that would not fill the chip (the deep levels of the
 // 3DUNet: 2 x 12 x 12 and 1 x 6 x 6 voxels with 256-512 channels): the input
 // channel chunks are divided over grid.z so that >= ~512 workgroups run
@@ -595,14 +628,15 @@ static hipError_t run_x(const Src2& x, const uint4* wu, const Dst2& y, Vol vol, 
   if (d.BN == 64)
     return KD == 3
                ? launch_fwd_x<64, 3, NS, 2>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s, part,
-                                            k.nsplit, k.kps, stats)
+                                                k.nsplit, k.kps, stats)
                : launch_fwd_x<64, 1, NS, 2>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s, part,
-                                            k.nsplit, k.kps, stats);
-  return KD == 3 ? launch_fwd_x<32, 3, NS, 2>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s, part,
-                                              k.nsplit, k.kps, stats)
-                 : launch_fwd_x<32, 1, NS, 2>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s, part,
-                                              k.nsplit, k.kps, stats);
+                                                k.nsplit, k.kps, stats);
+  return KD == 3 ? launch_fwd_x<32, 3, NS, 2>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s,
+                                                  part, k.nsplit, k.kps, stats)
+                 : launch_fwd_x<32, 1, NS, 2>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s,
+                                                  part, k.nsplit, k.kps, stats);
 }
+
 
 size_t conv3d_splitk_bytes(Vol vol, int KD, int Cin, int Cout) {
   size_t b = 0;

@@ -74,6 +74,7 @@ size_t conv3d_wgrad_ws_bytes(Vol vol, int KD, int Cin, int Cout);
 hipError_t conv3d_wgrad(const Src2& x, const float* dy, int lddy, float* dw, Vol vol, int KD,
                         int Cin, int Cout, int math, float* ws, hipStream_t s);
 size_t conv3d_wgrad_x_ws_bytes(Vol vol, int KD, int Cin, int Cout);
+bool debug_split_wgrad();  // SPFF_DEBUG_SPLIT (conv3d_x.hip)
 hipError_t conv3d_wgrad_x(const Src2& x, const float* dy, int lddy, float* dw, Vol vol, int KD,
                           int Cin, int Cout, int math, float* ws, hipStream_t s);
 // fixed-order sum of the [nsplit][T][kpad][npad] partial slabs into dw[Cout][Cin][T]

@@ -531,13 +531,16 @@ class UNet3DPlan:
               "spff_unet3d_forward")
         return out
 
-    def backward(self, dlogits_cl: torch.Tensor, flat: torch.Tensor) -> torch.Tensor:
+    def backward(self, dlogits_cl: torch.Tensor, flat: torch.Tensor, grad_hook=None) -> torch.Tensor:
+        """``grad_hook`` (GradBucketer protocol): this plan reports its whole
+        gradient as ready once the backward is enqueued (no per-block hook)."""
         dlogits_cl = dlogits_cl.contiguous()
         dflat = torch.empty(self.nfloats, dtype=torch.float32, device=dlogits_cl.device)
         ws = self.workspace(dlogits_cl.device)
         check(lib().spff_unet3d_backward(self._h, _ptr(dlogits_cl), _ptr(flat), _ptr(dflat),
                                          _ptr(ws), _stream(dlogits_cl.device)),
               "spff_unet3d_backward")
+        _whole_buffer_hook(grad_hook, dflat)
         return dflat
 
     def saved(self, name: str) -> torch.Tensor:
@@ -551,6 +554,14 @@ class UNet3DPlan:
         off = ptr.value - ws.data_ptr()
         n = nv.value * ch.value
         return ws[off:off + 4 * n].view(torch.float32).view(nv.value, ch.value).clone()
+
+
+def _whole_buffer_hook(grad_hook, dflat: torch.Tensor) -> None:
+    if grad_hook is None:
+        return
+    grad_hook.begin(dflat)
+    grad_hook.ready(0, int(dflat.numel()))
+    grad_hook.finish()
 
 
 def get_unet3d_plan(owner=None, tag: str = "", **kw) -> UNet3DPlan:
@@ -627,13 +638,15 @@ class SwinPlan:
         return out
 
     def backward(self, dlogits_cl: torch.Tensor, flat: torch.Tensor,
-                 dflat: Optional[torch.Tensor] = None) -> torch.Tensor:
+                 dflat: Optional[torch.Tensor] = None, grad_hook=None) -> torch.Tensor:
+        """``grad_hook`` as UNet3DPlan.backward: the whole gradient at once."""
         dlogits_cl = dlogits_cl.contiguous()
         if dflat is None:
             dflat = torch.empty(self.nfloats, dtype=torch.float32, device=dlogits_cl.device)
         ws = self.workspace(dlogits_cl.device)
         check(lib().spff_swin_backward(self._h, _ptr(dlogits_cl), _ptr(flat), _ptr(dflat), _ptr(ws),
                                        _stream(dlogits_cl.device)), "spff_swin_backward")
+        _whole_buffer_hook(grad_hook, dflat)
         return dflat
 
     def saved(self, name: str) -> torch.Tensor:

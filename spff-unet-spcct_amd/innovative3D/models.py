@@ -493,9 +493,9 @@ class LitSPCT_ControlUNet(BaseLitModel):
 # ============================================================================
 class _UNet3DFunction(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, plan, flat, bufs, training, *params):
+    def forward(ctx, x, plan, flat, bufs, training, grad_hook, *params):
         logits_cl = plan.forward(x, flat, bufs, training)
-        ctx.plan, ctx.gen, ctx.flat = plan, plan.generation, flat
+        ctx.plan, ctx.gen, ctx.flat, ctx.grad_hook = plan, plan.generation, flat, grad_hook
         ctx.slices = [(off, n, shape) for (_name, shape, off, n) in plan.params]
         return logits_cl.permute(0, 4, 1, 2, 3)
 
@@ -508,7 +508,7 @@ class _UNet3DFunction(torch.autograd.Function):
         g_cl = g.permute(0, 2, 3, 4, 1).contiguous()
         dflat = plan.backward(g_cl, ctx.flat, grad_hook=ctx.grad_hook)
         grads = [dflat[o:o + n].view(s) for (o, n, s) in ctx.slices]
-        return (None, None, None, None, None, *grads)
+        return (None, None, None, None, None, None, *grads)
 
 
 class Cicek3DUNet(nn.Module):
@@ -631,7 +631,8 @@ class Cicek3DUNet(nn.Module):
                     m.num_batches_tracked.add_(1)
         need_grad = torch.is_grad_enabled() and any(p.requires_grad for p in params)
         if need_grad:
-            return _UNet3DFunction.apply(x.float(), plan, flat, bufs, training, *params)
+            return _UNet3DFunction.apply(x.float(), plan, flat, bufs, training,
+                                         getattr(self, "grad_hook", None), *params)
         return plan.forward(x.float(), flat, bufs, training).permute(0, 4, 1, 2, 3)
 
     def forward(self, x):
@@ -768,9 +769,9 @@ class LitCicek3DUNet_DepthAdapter_Published(pl.LightningModule):
 # ============================================================================
 class _SwinFunction(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, plan, flat, *params):
+    def forward(ctx, x, plan, flat, grad_hook, *params):
         logits_cl = plan.forward(x, flat)
-        ctx.plan, ctx.gen, ctx.flat = plan, plan.generation, flat
+        ctx.plan, ctx.gen, ctx.flat, ctx.grad_hook = plan, plan.generation, flat, grad_hook
         ctx.slices = [(off, n, shape) for (_name, shape, off, n) in plan.params]
         return logits_cl.permute(0, 4, 1, 2, 3)
 
@@ -783,7 +784,7 @@ class _SwinFunction(torch.autograd.Function):
         g_cl = g.permute(0, 2, 3, 4, 1).contiguous()
         dflat = plan.backward(g_cl, ctx.flat, grad_hook=ctx.grad_hook)
         grads = [dflat[o:o + n].view(s) for (o, n, s) in ctx.slices]
-        return (None, None, None, *grads)
+        return (None, None, None, None, *grads)
 
 
 class _Holder(nn.Module):
@@ -935,7 +936,8 @@ class SwinUNETR(nn.Module):
         params = self._engine_params(plan)
         flat = self._ensure_flat(plan, params, x_in.device)
         if torch.is_grad_enabled() and any(p.requires_grad for p in params):
-            return _SwinFunction.apply(x_in.float(), plan, flat, *params)
+            return _SwinFunction.apply(x_in.float(), plan, flat, getattr(self, "grad_hook", None),
+                                       *params)
         return plan.forward(x_in.float(), flat).permute(0, 4, 1, 2, 3)
 
 

@@ -149,3 +149,36 @@ def resolve_kinks(st, x, labels, cfg, err, tol, n_cand=16, max_flips=3):
         best_e, best_g = step[0], step[2]
         taken = taken + [step[1]]
     return best_g, taken, best_e
+
+
+class forced_branches:
+    """Context manager: the oracle's LeakyReLUs and MaxPools take the given
+    branch decisions (``masks`` as tests/test_gpu_parity.engine_branch_masks
+    returns them: a bool sign mask per "<block>.<conv>" and an argmax-slot
+    tensor per "pool1..3"), in whatever dtype the oracle runs."""
+
+    def __init__(self, masks):
+        self.masks = masks
+        self.npool = 0
+
+    def _lrelu(self, P, pre, inp, ksd):
+        y = F.conv3d(inp, P[pre + ".0.weight"], None, padding=(ksd // 2, 1, 1))
+        r = F.instance_norm(y, weight=P[pre + ".1.weight"], bias=P[pre + ".1.bias"], eps=1e-5)
+        return torch.where(self.masks[pre], r, 0.01 * r)
+
+    def _pool(self, t):
+        k = self.npool % 3
+        self.npool += 1
+        B_, C_, D_, H_, W_ = t.shape
+        v = t.reshape(B_, C_, D_, H_ // 2, 2, W_ // 2, 2).permute(0, 1, 2, 3, 5, 4, 6)
+        v = v.reshape(B_, C_, D_, H_ // 2, W_ // 2, 4)
+        return v.gather(-1, self.masks[f"pool{k + 1}"].unsqueeze(-1)).squeeze(-1)
+
+    def __enter__(self):
+        self._orig = O.conv_in_lrelu, O.maxpool
+        O.conv_in_lrelu, O.maxpool = self._lrelu, self._pool
+        return self
+
+    def __exit__(self, *exc):
+        O.conv_in_lrelu, O.maxpool = self._orig
+        return False

@@ -8,8 +8,8 @@ Marked gpu; the CPU oracle runs on the host cores of the GPU box.
   tests/test_oracle_golden.py): logits within 1e-3 (north star), argmax
   identical except at near-ties (reference top-2 margin < 2 max|dlogit|;
   counted and printed), loss within 1e-5 relative, every parameter gradient
-  within 1e-3 relative L2 of the oracle's fp32 backward (head/tail elements
-  printed).  Reference: models.py:693-701, helpers.py:797-803.
+  within 1e-3 relative L2 of a kink-consistent fp32 oracle backward (head/tail
+  elements printed).  Reference: models.py:693-701, helpers.py:797-803.
 * configs[3] path: the depth-sharded engine at production H = W = 512 --
   world 2 on one GPU through host-staged gloo, volume 1 x 5 x 16 x 512^2 --
   vs the UNSHARDED oracle: gathered logits, argmax, loss and gradients.
@@ -17,9 +17,17 @@ Marked gpu; the CPU oracle runs on the host cores of the GPU box.
   (parity unpinned: MONAI absent; kink-consistent LeakyReLU masks as in
   tests/test_gpu_swin.py).
 
-The fp32 CPU oracle carries its own rounding (~1e-6 relative on the logits);
-the LeakyReLU kink can make a legitimate per-element gradient difference (see
-test_gpu_parity.py), which a relative-L2 criterion over a 4M-voxel sum absorbs.
+The fp32 CPU oracle carries its own rounding (~1e-6 relative on the logits; its
+gradients, sums over millions of voxels with heavy cancellation at random
+init, land ~1e-3 relative L2 from exact at these sizes).
+At these sizes thousands of LeakyReLU inputs and MaxPool windows sit within
+that rounding of their knife edge, and each one that lands on the other side
+moves whole gradient tensors (observed: 5e-3 relative L2 on every parameter at
+config 2 against the unconstrained oracle).  So the logits, argmax and loss are
+checked against the unconstrained fp32 oracle, and the gradients against the
+fp64 oracle whose LeakyReLU signs and pool argmaxes are the engine's own
+(tests/test_gpu_parity.engine_branch_masks, tests/_kink.forced_branches),
+within max(1e-3, 4 x the fp32 oracle's own distance from it) relative L2.
 """
 import os
 import socket
@@ -50,16 +58,66 @@ def _spff_state(D):
     return core, st
 
 
-def _oracle_fwd_bwd(st, x, y):
+def _oracle_cfg():
+    from oracle import spff_oracle as O
+    return O.SpffCfg(in_ch=5, num_classes=K13, base=32)
+
+
+def _oracle_forward(st, x, y):
+    """Unconstrained fp32 oracle: logits and loss (no backward)."""
     from oracle import spff_oracle as O
     torch.set_num_threads(_threads())
-    P = O.params_from_state({k: v for k, v in st.items() if not k.endswith("._mask")})
-    cfg = O.SpffCfg(in_ch=5, num_classes=K13, base=32)
-    logits, loss, ce, dice = O.fwd_bwd(P, x, y, cfg)
-    return logits, float(loss), {k: v.grad.clone() for k, v in P.items()}
+    P = O.params_from_state({k: v for k, v in st.items() if not k.endswith("._mask")},
+                            requires_grad=False)
+    with torch.no_grad():
+        logits = O.forward(P, x, _oracle_cfg())
+        loss, _ce, _dice = O.ce_plus_macro_dice(logits, y, K13)
+    return logits, float(loss)
 
 
-def _compare(tag, lg, loss, grads, ref_logits, ref_loss, ref_grads, loss_rtol=1e-5):
+def _oracle_grads(st, x, y, masks):
+    """fp64 and fp32 oracle gradients with the engine's LeakyReLU / MaxPool branch
+    decisions.  fp64 is the reference the engine is judged against; the fp32 run
+    measures how far the reference's own arithmetic lands from it at this size."""
+    from oracle import spff_oracle as O
+    from _kink import forced_branches
+    torch.set_num_threads(_threads())
+    out = []
+    for dt in (torch.float64, torch.float32):
+        P = O.params_from_state({k: v for k, v in st.items() if not k.endswith("._mask")},
+                                dtype=dt)
+        with forced_branches(masks):
+            O.fwd_bwd(P, x.to(dt), y, _oracle_cfg())
+        out.append({k: v.grad.clone() for k, v in P.items()})
+        del P
+    return out
+
+
+def _engine_masks(core, xshape, st):
+    from test_gpu_parity import engine_branch_masks
+    return engine_branch_masks(core, xshape, st, _oracle_cfg())
+
+
+def _mag_scales(st, g64s):
+    """FourierGate mag_scale: d/d(mag) = sum_k mask_k dL/dM_k (M = mask * mag) is a sum
+    over the rfft bins that can cancel almost completely (the fp32 oracle lands 1e-3
+    from fp64 on it at 512^2); judge it against the sum of its absolute terms,
+    sum_k |mask_k dL/dmask_k| / |mag|, as tests/test_gpu_parity.py does."""
+    out = {}
+    for k in g64s:
+        if k.endswith("fgate.mag_scale"):
+            pre = k[: -len("mag_scale")]
+            mag = abs(float(np.asarray(st[k]).reshape(-1)[0]))
+            terms = (np.abs(np.asarray(st[pre + "freq_mask"]).reshape(-1) *
+                            g64s[pre + "freq_mask"].double().numpy().reshape(-1))).sum()
+            out[k] = float(terms) / max(mag, 1e-30)
+    return out
+
+
+def _compare(tag, lg, loss, grads, ref_logits, ref_loss, ref_grads, loss_rtol=1e-5, scales=None):
+    """``ref_grads`` = (fp64, fp32) kink-consistent oracle gradients: every engine
+    gradient within max(1e-3, 4 x the fp32 oracle's own distance) relative L2 of fp64
+    (relative to ``scales[k]`` instead of |g64| where given)."""
     err = float((lg - ref_logits).abs().max())
     am, am_ref = lg.argmax(1), ref_logits.argmax(1)
     flips = am != am_ref
@@ -72,19 +130,22 @@ def _compare(tag, lg, loss, grads, ref_logits, ref_loss, ref_grads, loss_rtol=1e
     assert err <= 1e-3
     assert not (flips & ~ties).any(), f"{int((flips & ~ties).sum())} argmax flips outside near-ties"
     assert abs(loss - ref_loss) <= loss_rtol * abs(ref_loss)
+    g64s, g32s = ref_grads
     rows, bad = [], []
-    for k, g_ref in ref_grads.items():
+    for k, g64 in g64s.items():
         g = grads[k].detach().double().cpu().reshape(-1)
-        r = g_ref.double().reshape(-1)
-        nrm = float(r.norm())
-        rel = float((g - r).norm()) / max(nrm, 1e-30)
-        rows.append((rel, k, g[:2].tolist(), r[:2].tolist(), g[-1].item(), r[-1].item()))
-        if rel > 1e-3:
-            bad.append(f"{k}: rel L2 {rel:.2e}")
+        r = g64.double().reshape(-1)
+        nrm = max(float(r.norm()), (scales or {}).get(k, 0.0), 1e-30)
+        rel = float((g - r).norm()) / nrm
+        rel32 = float((g32s[k].double().reshape(-1) - r).norm()) / nrm
+        tol = max(1e-3, 4 * rel32)
+        rows.append((rel, rel32, k, g[0].item(), r[0].item(), g[-1].item(), r[-1].item()))
+        if rel > tol:
+            bad.append(f"{k}: rel L2 {rel:.2e} (fp32 oracle {rel32:.2e})")
     rows.sort(reverse=True)
-    for rel, k, gh, rh, gt, rt in rows[:8]:
-        print(f"  {k:34s} relL2 {rel:.2e} head {gh[0]:+.6e} vs {rh[0]:+.6e} tail {gt:+.6e} vs "
-              f"{rt:+.6e}")
+    for rel, rel32, k, gh, rh, gt, rt in rows[:8]:
+        print(f"  {k:34s} relL2 {rel:.2e} (fp32 oracle {rel32:.2e}) head {gh:+.6e} vs {rh:+.6e} "
+              f"tail {gt:+.6e} vs {rt:+.6e}")
     assert not bad, "; ".join(bad)
 
 
@@ -93,15 +154,15 @@ def config2_oracle():
     from innovative3D.synthetic import synthetic_batch
     _core, st = _spff_state(128)
     x, y = synthetic_batch(2, 5, 128, 128, 128, K13, ignore_frac=0.01, seed=0)
-    logits, loss, grads = _oracle_fwd_bwd(st, x, y)
-    return st, x, y, logits, loss, grads
+    logits, loss = _oracle_forward(st, x, y)
+    return st, x, y, logits, loss
 
 
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize("mth", ["bf16x6", "f32"])
 def test_config2_headline_matches_oracle(config2_oracle, mth):
     import innovative3D.helpers as Hh
-    st, x, y, ref_logits, ref_loss, ref_grads = config2_oracle
+    st, x, y, ref_logits, ref_loss = config2_oracle
     core, _ = _spff_state(128)
     core.load_state_dict({k: torch.from_numpy(v) for k, v in st.items()})
     core = core.to(DEV)
@@ -111,8 +172,9 @@ def test_config2_headline_matches_oracle(config2_oracle, mth):
     loss.backward()
     torch.cuda.synchronize()
     grads = {k: p.grad for k, p in core.named_parameters(remove_duplicate=False)}
+    ref_grads = _oracle_grads(st, x, y, _engine_masks(core, tuple(x.shape), st))
     _compare(f"config2 2x5x128^3 {mth}", logits.detach().cpu(), float(loss), grads, ref_logits,
-             ref_loss, ref_grads)
+             ref_loss, ref_grads, scales=_mag_scales(st, ref_grads[0]))
 
 
 # ------------------------------------------------- configs[3] path (sharded)
@@ -137,7 +199,7 @@ def _sh_worker(rank, world, port, out):
     import sys
     root = pathlib.Path(__file__).resolve().parents[1]
     sys.path[:0] = [str(root), str(root / "tests"), str(root / "spff-unet-spcct_amd")]
-    from test_gpu_baseline_sizes import _sh_data, _spff_state
+    from test_gpu_baseline_sizes import _engine_masks, _sh_data, _spff_state
     from innovative3D.sharded import DepthShardedSPFF, shard_bounds
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -153,7 +215,14 @@ def _sh_worker(rank, world, port, out):
     loss, conf = step.step(x[:, :, off:off + d].contiguous().to(DEV),
                            y[:, off:off + d].contiguous().to(DEV))
     torch.cuda.synchronize()
-    np.savez(f"{out}.{rank}.npz", logits=step.last_logits.cpu().numpy(), loss=float(loss),
+    # this rank's LeakyReLU signs / pool argmaxes over its own depth slab
+    masks = _engine_masks(core, (1, SH_SHAPE[1], d) + SH_SHAPE[3:], st)
+    mk = {}
+    for k, m in masks.items():
+        a = m.numpy()
+        mk["m_" + k] = np.packbits(a) if a.dtype == np.bool_ else a.astype(np.uint8)
+        mk["s_" + k] = np.array(a.shape)
+    np.savez(f"{out}.{rank}.npz", logits=step.last_logits.cpu().numpy(), loss=float(loss), **mk,
              **({"g_" + k: p.grad.cpu().numpy() for k, p in core.named_parameters(remove_duplicate=False)
                  if p.grad is not None and not k.endswith("._mask")} if rank == 0 else {}))
     del step, core
@@ -170,10 +239,23 @@ def test_config4_sharded_512_matches_oracle(tmp_path):
     lg = torch.from_numpy(np.concatenate([p["logits"] for p in parts], axis=2))
     _core, st = _spff_state(SH_SHAPE[2])
     x, y = _sh_data()
-    ref_logits, ref_loss, ref_grads = _oracle_fwd_bwd(st, x, y)
-    grads = {k: torch.from_numpy(parts[0]["g_" + k]) for k in ref_grads}
+    ref_logits, ref_loss = _oracle_forward(st, x, y)
+    # branch decisions: the sharded engine's own, each rank's slab concatenated along D
+    masks = {}
+    for k in (f[2:] for f in parts[0].files if f.startswith("m_")):
+        segs = []
+        for p in parts:
+            shp = tuple(int(v) for v in p["s_" + k])
+            a = p["m_" + k]
+            a = np.unpackbits(a)[:int(np.prod(shp))].astype(bool) if k[:4] != "pool" else a
+            segs.append(a.reshape(shp))
+        cat = np.concatenate(segs, axis=2)
+        masks[k] = torch.from_numpy(cat) if cat.dtype == np.bool_ else torch.from_numpy(cat.astype(np.int64))
+    ref_grads = _oracle_grads(st, x, y, masks)
+    grads = {k: torch.from_numpy(parts[0]["g_" + k]) for k in ref_grads[0]}
     _compare("config4 path: 1x5x16x512^2 depth-sharded world 2 (bf16x6)", lg,
-             float(parts[0]["loss"]), grads, ref_logits, ref_loss, ref_grads)
+             float(parts[0]["loss"]), grads, ref_logits, ref_loss, ref_grads,
+             scales=_mag_scales(st, ref_grads[0]))
 
 
 # ------------------------------------------------------------ configs[4] (Swin)
@@ -201,11 +283,14 @@ def test_config5_swin_128_matches_oracle():
     torch.set_num_threads(_threads())
     S.ACT_MASKS = engine_act_masks(m, x.shape)
     try:
-        P = S.params_from_state(st)
-        rl, rloss = S.fwd_bwd(P, x, y, cfg)
+        refs = []
+        for dt in (torch.float64, torch.float32):
+            P = S.params_from_state(st, dtype=dt)
+            rl, rloss = S.fwd_bwd(P, x.to(dt), y, cfg)
+            refs.append((rl.detach().float(), float(rloss), {k: v.grad for k, v in P.items()}))
     finally:
         S.ACT_MASKS = None
     named = dict(m.named_parameters())
-    grads = {k: named[k].grad for k in P}
+    grads = {k: named[k].grad for k in refs[0][2]}
     _compare("config5 SwinUNETR 2x1x128^3 (bf16x6)", logits.detach().cpu(), float(loss), grads,
-             rl.detach(), float(rloss), {k: v.grad for k, v in P.items()})
+             refs[0][0], refs[0][1], (refs[0][2], refs[1][2]))

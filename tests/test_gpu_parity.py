@@ -127,6 +127,10 @@ def _block_names(cfg):
 
 
 def engine_lrelu_masks(core, d):
+    return engine_branch_masks(core, d["x"].shape, state_of(d), cfg_of(d["meta"]))
+
+
+def engine_branch_masks(core, xshape, st, cfg):
     """Sign pattern of every LeakyReLU input, and the argmax of every max-pool
     window, as the ENGINE saw them (the pools: from its saved pool inputs; ties
     resolved first-max like the engine and torch).  The LeakyReLUs: the engine's
@@ -135,18 +139,16 @@ def engine_lrelu_masks(core, d):
     (|r| ~ 0) can take the other slope (1 vs 0.01) -- a legitimate fp32 outcome
     the reference could equally produce.  Feeding the engine's pattern to the
     oracle removes these knife-edge flips from the gradient comparison."""
-    cfg = cfg_of(d["meta"])
-    B = d["x"].shape[0]
+    B = xshape[0]
     plan = core._plan
-    st = state_of(d)
     masks = {}
     for blk, a, b in _block_names(cfg):
         for tag, key in ((a, "y1"), (b, "y2")):
             y = plan.saved(f"{blk}.{key}").double().cpu()
             C = y.shape[1]
-            Dd = d["x"].shape[2]
+            Dd = xshape[2]
             lvl = {"enc1": 0, "dec1": 0, "enc2": 1, "dec2": 1, "enc3": 2, "dec3": 2, "bott": 3}[blk]
-            Hh_, Ww = d["x"].shape[3] >> lvl, d["x"].shape[4] >> lvl
+            Hh_, Ww = xshape[3] >> lvl, xshape[4] >> lvl
             y = y.view(B, Dd, Hh_, Ww, C).permute(0, 4, 1, 2, 3)
             g = torch.from_numpy(st[f"{blk}.{tag}.1.weight"]).double()
             bb = torch.from_numpy(st[f"{blk}.{tag}.1.bias"]).double()
@@ -164,9 +166,9 @@ def engine_lrelu_masks(core, d):
                 print(f"  {blk}.{tag}: {nd} knife-edge signs (engine affine vs fp64 IN)")
             masks[f"{blk}.{tag}"] = m
     # max-pool windows: the engine's own first-max argmax over its pool inputs
-    Dd = d["x"].shape[2]
+    Dd = xshape[2]
     for k, blk in enumerate(("enc1", "enc2", "enc3")):
-        Hh_, Ww = d["x"].shape[3] >> k, d["x"].shape[4] >> k
+        Hh_, Ww = xshape[3] >> k, xshape[4] >> k
         y = plan.saved(f"{blk}.out").double().cpu()
         C = y.shape[1]
         y = y.view(B, Dd, Hh_, Ww, C).permute(0, 4, 1, 2, 3)
