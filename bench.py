@@ -451,7 +451,7 @@ def main():
     ap.add_argument("--hw", type=int, default=512)
     ap.add_argument("--cpu-depth", type=int, default=32)
     ap.add_argument("--cpu-steps", type=int, default=3)
-    ap.add_argument("--pmc", default=str(ROOT / "profiles" / "r01_pmc_conv.json"),
+    ap.add_argument("--pmc", default=str(ROOT / "profiles" / "r02_pmc_conv.json"),
                     help="optional per-launch HBM traffic summary from rocprofv3 --pmc")
     args = ap.parse_args()
 
@@ -558,7 +558,7 @@ def main():
             "compulsory_bytes_per_launch": cb / max(1, nl),
             "traffic_over_compulsory": (traffic / (cb / nl)) if (traffic and nl and cb) else None,
             "traffic_note": ("PMC HBM bytes per launch of this kernel (2 x FETCH_SIZE + WRITE_SIZE, "
-                             "profiles/r01_pmc_conv.json, same bench config)"),
+                             "profiles/r02_pmc_conv.json, same bench config)"),
             "per_class_ms_per_step": {k: v[0] / args.steps for k, v in prof.items()},
             "per_class_tflops": {k: (v[1] / (v[0] * 1e-3) / 1e12 if v[0] > 0 else None)
                                  for k, v in prof.items() if k not in plan.MEM_CLASSES},

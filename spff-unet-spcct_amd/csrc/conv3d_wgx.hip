@@ -26,6 +26,10 @@
 #include <type_traits>
 #include <vector>
 
+#ifndef SPFF_XCDMAP
+#define SPFF_XCDMAP 1  // 0: split-fastest block order (A/B diagnostics)
+#endif
+
 namespace spff {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -94,7 +98,16 @@ __global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x(
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, h = g >> 1, q = (lane & 15) >> 2, pq = lane & 3;
-  const int split = blockIdx.x, ci_base = blockIdx.y * CI, co0 = blockIdx.z * WX_CO;
+  // XCD-aware order: blocks b and b + 8 share an XCD, so XCD group b % 8 runs the
+  // (ci, co) blocks of one voxel range back to back -- every x / dy tile is fetched
+  // from HBM once and re-read by the other channel blocks from that XCD's L2
+  const int nci = kpad / CI, ncb = nci * (npad / WX_CO);
+  const int rk = blockIdx.x >> 3;
+  const int nsp8 = gridDim.x / ncb;
+  const int cb = SPFF_XCDMAP ? rk % ncb : (int)(blockIdx.x / nsp8);
+  const int split = SPFF_XCDMAP ? (rk / ncb) * 8 + (blockIdx.x & 7) : (int)(blockIdx.x % nsp8);
+  if (split * tps >= ntiles) return;  // padding block (uniform)
+  const int ci_base = (cb % nci) * CI, co0 = (cb / nci) * WX_CO;
   const int D = vol.D, H = vol.H, W = vol.W;
 
   // blocks of this wave: wave, wave + 4, ...; nj of them (uniform per wave)
@@ -122,11 +135,13 @@ __global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x(
 
   float4 hreg[NH], yreg[NY];
   auto fetch = [&](int tile) {
+    // depth-fastest tile order: a split's consecutive tiles share two of their three
+    // halo planes, which the previous tile has just brought into L2
     int t = tile;
+    const int d0 = t % D; t /= D;
     const int twi = t % tilesW; t /= tilesW;
-    const int thi = t % tilesH; t /= tilesH;
-    const int d0 = t % D;
-    const int b = t / D;
+    const int thi = t % tilesH;
+    const int b = t / tilesH;
     const int h0 = thi * WX_TH, w0 = twi * WX_TW;
 #pragma unroll
     for (int k = 0; k < NH; ++k) {
@@ -339,7 +354,7 @@ hipError_t conv3d_wgrad_x(const Src2& x, const float* dy, int lddy, float* dw, V
   if (lddy % 4) return hipErrorInvalidValue;
   WxPlan p = wx_plan(vol, Cin, Cout);
   const WxTable tb = make_table(KD, p.ci);
-  dim3 grid(p.nsplit, p.kpad / p.ci, p.npad / WX_CO);
+  dim3 grid(8 * cdiv(p.nsplit, 8) * (p.kpad / p.ci) * (p.npad / WX_CO));
 #define SPFF_WX(KD_, CI_, NS_, NJ_)                                                            \
   hipLaunchKernelGGL((k_conv3d_wgrad_x<KD_, CI_, NS_, NJ_>), grid, dim3(256), 0, s, x, dy,     \
                      lddy, ws, vol, Cin, p.kpad, Cout, p.npad, p.tilesH, p.tilesW, p.ntiles,   \

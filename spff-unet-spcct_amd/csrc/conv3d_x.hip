@@ -45,6 +45,9 @@
 #ifndef SPFF_XDIAG
 #define SPFF_XDIAG 0  // timing diagnostics only: 1 = no restaging, 2 = no MFMA loop
 #endif
+#ifndef SPFF_XCDMAP
+#define SPFF_XCDMAP 1  // 0: tile-fastest block order (A/B diagnostics)
+#endif
 #ifndef SPFF_XIGLP
 #define SPFF_XIGLP -1
 #endif
@@ -142,7 +145,7 @@ template <int BN, int KD, int NS, int MB, int NW>
 __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
     Src2 x, const uint4* __restrict__ wp, Dst2 y, Vol vol, int Cin, int nkc, int Cout, int npad,
     int tilesD, int tilesH, int tilesW, float* __restrict__ part, int kps,
-    float* __restrict__ stats) {
+    float* __restrict__ stats, int ntiles) {
   constexpr int XT_THREADS = NW * 64;
   constexpr int TD = XT_D, TH = NW * MB, TW = XT_W;
   constexpr int HH = TH + 2, HWD = TW + 2;
@@ -162,15 +165,25 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int khalf = lane >> 5, l32 = lane & 31;
-  int t = blockIdx.x;
+  // XCD-aware order: blocks b and b + 8 share an XCD (and its L2), so XCD group
+  // b % 8 walks a contiguous run of tiles, the npad / BN output-channel blocks of a
+  // tile back to back -- neighbouring tiles' halos and a tile's input for its other
+  // channel blocks are then L2 hits instead of HBM re-reads
+  const int nnb = npad / BN;
+  const int per = (ntiles + 7) >> 3;
+  const int grp = blockIdx.x & 7, rk = blockIdx.x >> 3;
+  const int tile = SPFF_XCDMAP ? grp * per + rk / nnb : (int)(blockIdx.x % (8 * per));
+  const int nbk = SPFF_XCDMAP ? rk % nnb : (int)(blockIdx.x / (8 * per));
+  if (tile >= ntiles) return;  // padding block (uniform: the whole workgroup)
+  int t = tile;
   const int twi = t % tilesW; t /= tilesW;
   const int thi = t % tilesH; t /= tilesH;
   const int tdi = t % tilesD;
   const int b = t / tilesD;
   const int d0 = tdi * TD, h0 = thi * TH, w0 = twi * TW;
-  const int n0 = blockIdx.y * BN;
+  const int n0 = nbk * BN;
   const int D = vol.D, H = vol.H, W = vol.W;
-  const uint4* wsrc = wp + (int64_t)blockIdx.y * nkc * NWU;
+  const uint4* wsrc = wp + (int64_t)nbk * nkc * NWU;
 
   // voxel of MFMA row r in 32-row block q (q = wave*MB + mb)
   auto vrow = [](int q, int r, int& td, int& th, int& tw) {
@@ -422,13 +435,13 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
         for (int w = 0; w < NW; ++w) q += sred[(w * NB + nb) * 32 + l32];
         const int n = n0 + nb * 32 + l32;
         if (n < Cout) {
-          stats[((int64_t)blockIdx.x * npad + n) * 2 + 0] = tsum[nb];
-          stats[((int64_t)blockIdx.x * npad + n) * 2 + 1] = q;
+          stats[((int64_t)tile * npad + n) * 2 + 0] = tsum[nb];
+          stats[((int64_t)tile * npad + n) * 2 + 1] = q;
         }
       }
     }
-    if (tid == 0 && blockIdx.y == 0)
-      stats[(int64_t)gridDim.x * npad * 2 + blockIdx.x] = cnt;
+    if (tid == 0 && nbk == 0)
+      stats[(int64_t)ntiles * npad * 2 + tile] = cnt;
   }
 }
 
@@ -520,9 +533,10 @@ static hipError_t launch_fwd_x(const Src2& x, const uint4* wx, const Dst2& y, Vo
     attr = true;
   }
   const int tilesD = cdiv(vol.D, XT_D), tilesH = cdiv(vol.H, NW * MB), tilesW = cdiv(vol.W, XT_W);
-  dim3 grid(vol.B * tilesD * tilesH * tilesW, npad / BN, part ? nsplit : 1);
+  const int ntiles = vol.B * tilesD * tilesH * tilesW;
+  dim3 grid(8 * cdiv(ntiles, 8) * (npad / BN), 1, part ? nsplit : 1);
   hipLaunchKernelGGL(kern, grid, dim3(NW * 64), shm, s, x, wx, y, vol, K, nkc, N, npad, tilesD,
-                     tilesH, tilesW, part, part ? kps : nkc, part ? nullptr : stats);
+                     tilesH, tilesW, part, part ? kps : nkc, part ? nullptr : stats, ntiles);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || !part) return e;
   const int64_t total = nvox(vol) * N;
