@@ -41,12 +41,16 @@
 
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 
 #ifndef SPFF_XDIAG
 #define SPFF_XDIAG 0  // timing diagnostics only: 1 = no restaging, 2 = no MFMA loop
 #endif
 #ifndef SPFF_XCDMAP
 #define SPFF_XCDMAP 1  // 0: tile-fastest block order (A/B diagnostics)
+#endif
+#ifndef SPFF_X16
+#define SPFF_X16 1  // 1: v_mfma_f32_16x16x32_bf16 tap-quad schedule, 0: 32x32x16 tap pairs
 #endif
 #ifndef SPFF_XIGLP
 #define SPFF_XIGLP -1
@@ -58,6 +62,7 @@
 namespace spff {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
@@ -141,7 +146,52 @@ constexpr size_t xt_lds_bytes() {
 }
 }  // namespace
 
-template <int BN, int KD, int NS, int MB, int NW>
+// 16x16x32 tap-quad schedule (X16): k = 4 lane groups x 8 channels, lane group g
+// at its own tap.  A ds_read_b128 lane group mixes rows {0-3, 12-15} of k-group
+// 0 (2) with rows 4-11 of k-group 1 (3): with the rows of a block mapped to the
+// W-row's voxels as rows 4-11 -> even w, the rest -> odd w, every such group
+// covers 16 distinct 16-byte bank quads as long as the two taps' halo offsets
+// differ by an EVEN number of positions, i.e. have the same kw parity (offset
+// = (kd HH + kh) HWD + kw with even HH, HWD).  Pairs are therefore formed within
+// the even-kw and within the odd-kw taps; a leftover tap pairs with the zero
+// padding row (weight index T), which reads its partner's position.
+template <int KD>
+struct XQuads {
+  int nq = 0;
+  signed char tap[32] = {};  // weight row per slot (T = the zero padding row)
+  signed char src[32] = {};  // tap whose halo offset the slot reads
+};
+template <int KD>
+__host__ __device__ constexpr XQuads<KD> x_quads() {
+  XQuads<KD> q{};
+  constexpr int T = KD * 9;
+  int ev[27] = {}, od[27] = {}, ne = 0, no = 0;
+  for (int t = 0; t < T; ++t) {
+    if ((t % 3) % 2 == 0) ev[ne++] = t;
+    else od[no++] = t;
+  }
+  int pa[32] = {}, pb[32] = {}, np = 0;
+  for (int i = 0; i + 1 < ne; i += 2) { pa[np] = ev[i]; pb[np] = ev[i + 1]; ++np; }
+  for (int i = 0; i + 1 < no; i += 2) { pa[np] = od[i]; pb[np] = od[i + 1]; ++np; }
+  if (ne % 2) { pa[np] = ev[ne - 1]; pb[np] = -1; ++np; }
+  if (no % 2) { pa[np] = od[no - 1]; pb[np] = -1; ++np; }
+  if (np % 2) { pa[np] = -2; pb[np] = -2; ++np; }  // (pad, pad)
+  q.nq = np / 2;
+  for (int i = 0; i < np; ++i) {
+    const int a = pa[i], b = pb[i];
+    q.tap[2 * i] = (signed char)(a >= 0 ? a : T);
+    q.src[2 * i] = (signed char)(a >= 0 ? a : 0);
+    q.tap[2 * i + 1] = (signed char)(b >= 0 ? b : T);
+    q.src[2 * i + 1] = (signed char)(b >= 0 ? b : (a >= 0 ? a : 0));
+  }
+  return q;
+}
+// MFMA row r (0..15) of a 16-row block -> w within the W-row (see x_quads)
+__device__ __forceinline__ int x16_w(int r) {
+  return (r >= 4 && r < 12) ? 2 * (r - 4) : (r < 4 ? 2 * r + 1 : 2 * r - 15);
+}
+
+template <int BN, int KD, int NS, int MB, int NW, bool X16>
 __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
     Src2 x, const uint4* __restrict__ wp, Dst2 y, Vol vol, int Cin, int nkc, int Cout, int npad,
     int tilesD, int tilesH, int tilesW, float* __restrict__ part, int kps,
@@ -150,13 +200,20 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
   constexpr int TD = XT_D, TH = NW * MB, TW = XT_W;
   constexpr int HH = TH + 2, HWD = TW + 2;
   constexpr int NPOS = xt_npos<KD, TH>();
-  constexpr int T = KD * 9, T2 = xt_t2<KD>(), NJ = T2 / 2;
-  constexpr int NB = BN / 32;
+  constexpr int T = KD * 9, T2 = xt_t2<KD>();
+  // MFMA blocking: 32x32x16 -- MB 32-row blocks x BN/32 col blocks per wave, a k-step
+  // per tap pair; 16x16x32 -- 2 MB 16-row blocks x BN/16, a k-step per tap quad
+  constexpr int RB = X16 ? 2 * MB : MB, CB = X16 ? BN / 16 : BN / 32;
+  constexpr int NCOL = X16 ? 16 : 32, NREG = X16 ? 4 : 16;
+  constexpr XQuads<KD> QT = x_quads<KD>();
+  constexpr int NJ = X16 ? QT.nq : T2 / 2;
+  using AccT = typename std::conditional<X16, f32x4, f32x16>::type;
   constexpr int NHX = NPOS * 2;  // halo float4 per chunk (8 channels = 2 float4)
   constexpr int RH = (NHX + XT_THREADS - 1) / XT_THREADS;
   constexpr int NWU = NS * T2 * BN;  // pre-split weight units (16 B) per chunk
   static_assert(NWU % 64 == 0, "weight image must be whole 1 KiB DMA pieces");
-  constexpr int SPJ = (RH + (NJ - NJ / 2) - 1) / (NJ - NJ / 2);  // halo float4 split per tap pair
+  static_assert(!X16 || TD * TH == NW * RB, "X16: one W-row per 16-row block");
+  constexpr int SPJ = (RH + (NJ - NJ / 2) - 1) / (NJ - NJ / 2);  // halo float4 split per k-step
   constexpr int NPC = NWU / 64;
   extern __shared__ uint4 lds4[];
   uint4* Xs = lds4;               // [NS][NPOS]
@@ -164,7 +221,8 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
-  const int khalf = lane >> 5, l32 = lane & 31;
+  const int khalf = lane >> 5, l32 = lane & 31, kg = lane >> 4, l16 = lane & 15;
+  const int lcol = X16 ? l16 : l32;
   // XCD-aware order: blocks b and b + 8 share an XCD (and its L2), so XCD group
   // b % 8 walks a contiguous run of tiles, the npad / BN output-channel blocks of a
   // tile back to back -- neighbouring tiles' halos and a tile's input for its other
@@ -185,27 +243,37 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
   const int D = vol.D, H = vol.H, W = vol.W;
   const uint4* wsrc = wp + (int64_t)nbk * nkc * NWU;
 
-  // voxel of MFMA row r in 32-row block q (q = wave*MB + mb)
+  // voxel of MFMA row r in row block q (q = wave*RB + rb)
   auto vrow = [](int q, int r, int& td, int& th, int& tw) {
-    td = q / (TH / 2);
-    th = 2 * (q % (TH / 2)) + (r >> 4);
-    tw = r < 16 ? r : ((r + 14) & 15);
+    if constexpr (X16) {
+      td = q / TH;
+      th = q % TH;
+      tw = x16_w(r);
+    } else {
+      td = q / (TH / 2);
+      th = 2 * (q % (TH / 2)) + (r >> 4);
+      tw = r < 16 ? r : ((r + 14) & 15);
+    }
   };
-  int hpos[MB];
+  // output register r of this lane -> MFMA row
+  auto orow = [&](int r) {
+    return X16 ? 4 * kg + r : (r & 3) + 8 * (r >> 2) + 4 * khalf;
+  };
+  int hpos[RB];
 #pragma unroll
-  for (int mb = 0; mb < MB; ++mb) {
+  for (int rb = 0; rb < RB; ++rb) {
     int td, th, tw;
-    vrow(wave * MB + mb, l32, td, th, tw);
-    hpos[mb] = (td * HH + th) * HWD + tw;
+    vrow(wave * RB + rb, X16 ? l16 : l32, td, th, tw);
+    hpos[rb] = (td * HH + th) * HWD + tw;
   }
 
-  f32x16 acc[MB][NB];
+  AccT acc[RB][CB];
 #pragma unroll
-  for (int mb = 0; mb < MB; ++mb)
+  for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
-    for (int nb = 0; nb < NB; ++nb)
+    for (int cb = 0; cb < CB; ++cb)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[mb][nb][r] = 0.f;
+      for (int r = 0; r < NREG; ++r) acc[rb][cb][r] = 0.f;
 
   // halo of the next chunk: fp32 loads in flight during this chunk's first
   // MFMAs, split into bf16 planes half-way through it (VALU beside the MFMAs),
@@ -269,6 +337,7 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
                                          16, 0, 0);
     }
   };
+  auto toff_of = [](int tp) { return ((tp / 9) * HH + (tp / 3) % 3) * HWD + tp % 3; };
 
   // split-K (small volumes): this workgroup reduces chunks [kc0, kc1) only and
   // writes fp32 partial sums that k_splitk_reduce adds in a fixed order
@@ -285,9 +354,9 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
       // sign-alternating accumulation: odd chunks carry negated weights, so the
       // accumulator holds (-1)^kc x the partial sum; flip it at every chunk boundary
 #pragma unroll
-      for (int mb = 0; mb < MB; ++mb)
+      for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
-        for (int nb = 0; nb < NB; ++nb) acc[mb][nb] = -acc[mb][nb];
+        for (int cb = 0; cb < CB; ++cb) acc[rb][cb] = -acc[rb][cb];
       __syncthreads();
     }
     if (SPFF_XDIAG != 1 || kc == kc0) stash(kc);
@@ -296,7 +365,7 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
 #pragma unroll
     for (int j = 0; j < (SPFF_XDIAG == 2 ? 0 : NJ); ++j) {
       if constexpr (SPFF_XIGLP >= 0) __builtin_amdgcn_iglp_opt(SPFF_XIGLP);
-      // split one prefetched halo float4 per tap pair from the middle of the
+      // split one prefetched halo float4 per k-step from the middle of the
       // chunk on; the fences keep this VALU (and its vmcnt wait) in place
       // while MFMAs and LDS reads may still move across
       if (j >= NJ / 2 && (j - NJ / 2) * SPJ < RH) {
@@ -306,72 +375,104 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
           if ((j - NJ / 2) * SPJ + u < RH) split_one((j - NJ / 2) * SPJ + u);
         __builtin_amdgcn_sched_barrier(0x10C);
       }
-      // lane half h takes tap 2j+h; the padding tap (>= T) reads a valid
-      // position against a zero weight row
-      const int tp0 = 2 * j, tp1 = (2 * j + 1 < T) ? 2 * j + 1 : T - 1;
-      const int toff0 = ((tp0 / 9) * HH + (tp0 / 3) % 3) * HWD + tp0 % 3;
-      const int toff1 = ((tp1 / 9) * HH + (tp1 / 3) % 3) * HWD + tp1 % 3;
-      const int toff = khalf ? toff1 : toff0;
-      const int wtap = 2 * j + khalf;
-      bf16x8 a[MB][NS], bm[NB][NS];
+      if constexpr (X16) {
+        // lane group kg takes slot 4j + kg of the quad schedule
+        const int s01 = kg & 1;
+        const int sa = 4 * j + (kg & 2);
+        const int toff = s01 ? toff_of(QT.src[sa + 1]) : toff_of(QT.src[sa]);
+        const int wtap = s01 ? QT.tap[sa + 1] : QT.tap[sa];
+        bf16x8 a[RB][NS], bm[CB][NS];
 #pragma unroll
-      for (int p = 0; p < NS; ++p) {
+        for (int p = 0; p < NS; ++p) {
 #pragma unroll
-        for (int mb = 0; mb < MB; ++mb)
-          a[mb][p] = __builtin_bit_cast(bf16x8, Xs[p * NPOS + hpos[mb] + toff]);
+          for (int rb = 0; rb < RB; ++rb)
+            a[rb][p] = __builtin_bit_cast(bf16x8, Xs[p * NPOS + hpos[rb] + toff]);
 #pragma unroll
-        for (int nb = 0; nb < NB; ++nb)
-          bm[nb][p] = __builtin_bit_cast(bf16x8, Ws[(p * T2 + wtap) * BN + nb * 32 + l32]);
-      }
-#pragma unroll
-      for (int mb = 0; mb < MB; ++mb)
-#pragma unroll
-        for (int nb = 0; nb < NB; ++nb) {
-          f32x16 c = acc[mb][nb];
-          if constexpr (NS == 3) {
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mb][1], bm[nb][1], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mb][0], bm[nb][2], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mb][2], bm[nb][0], c, 0, 0, 0);
-          }
-          if constexpr (NS >= 2) {
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mb][0], bm[nb][1], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mb][1], bm[nb][0], c, 0, 0, 0);
-          }
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mb][0], bm[nb][0], c, 0, 0, 0);
-          acc[mb][nb] = c;
+          for (int cb = 0; cb < CB; ++cb)
+            bm[cb][p] = __builtin_bit_cast(bf16x8, Ws[(p * T2 + wtap) * BN + cb * 16 + l16]);
         }
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+          for (int cb = 0; cb < CB; ++cb) {
+            f32x4 c = acc[rb][cb];
+            if constexpr (NS == 3) {
+              c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb][1], bm[cb][1], c, 0, 0, 0);
+              c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb][0], bm[cb][2], c, 0, 0, 0);
+              c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb][2], bm[cb][0], c, 0, 0, 0);
+            }
+            if constexpr (NS >= 2) {
+              c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb][0], bm[cb][1], c, 0, 0, 0);
+              c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb][1], bm[cb][0], c, 0, 0, 0);
+            }
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb][0], bm[cb][0], c, 0, 0, 0);
+            acc[rb][cb] = c;
+          }
+      } else {
+        // lane half h takes tap 2j+h; the padding tap (>= T) reads a valid
+        // position against a zero weight row
+        const int tp0 = 2 * j, tp1 = (2 * j + 1 < T) ? 2 * j + 1 : T - 1;
+        const int toff = khalf ? toff_of(tp1) : toff_of(tp0);
+        const int wtap = 2 * j + khalf;
+        bf16x8 a[RB][NS], bm[CB][NS];
+#pragma unroll
+        for (int p = 0; p < NS; ++p) {
+#pragma unroll
+          for (int rb = 0; rb < RB; ++rb)
+            a[rb][p] = __builtin_bit_cast(bf16x8, Xs[p * NPOS + hpos[rb] + toff]);
+#pragma unroll
+          for (int cb = 0; cb < CB; ++cb)
+            bm[cb][p] = __builtin_bit_cast(bf16x8, Ws[(p * T2 + wtap) * BN + cb * 32 + l32]);
+        }
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+          for (int cb = 0; cb < CB; ++cb) {
+            f32x16 c = acc[rb][cb];
+            if constexpr (NS == 3) {
+              c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[rb][1], bm[cb][1], c, 0, 0, 0);
+              c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[rb][0], bm[cb][2], c, 0, 0, 0);
+              c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[rb][2], bm[cb][0], c, 0, 0, 0);
+            }
+            if constexpr (NS >= 2) {
+              c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[rb][0], bm[cb][1], c, 0, 0, 0);
+              c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[rb][1], bm[cb][0], c, 0, 0, 0);
+            }
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[rb][0], bm[cb][0], c, 0, 0, 0);
+            acc[rb][cb] = c;
+          }
+      }
     }
   }
 
   if ((kc1 - 1) & 1) {
 #pragma unroll
-    for (int mb = 0; mb < MB; ++mb)
+    for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
-      for (int nb = 0; nb < NB; ++nb) acc[mb][nb] = -acc[mb][nb];
+      for (int cb = 0; cb < CB; ++cb) acc[rb][cb] = -acc[rb][cb];
   }
 
 // ---- epilogue: C[i][j], row i = voxel (vrow mapping), col j = out channel ----
 #pragma unroll
-  for (int mb = 0; mb < MB; ++mb) {
+  for (int rb = 0; rb < RB; ++rb) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int i = (r & 3) + 8 * (r >> 2) + 4 * khalf;
+    for (int r = 0; r < NREG; ++r) {
       int td, th, tw;
-      vrow(wave * MB + mb, i, td, th, tw);
+      vrow(wave * RB + rb, orow(r), td, th, tw);
       const int gd = d0 + td, gh = h0 + th, gw = w0 + tw;
       if (gd >= D || gh >= H || gw >= W) continue;
       const int64_t vox = (((int64_t)b * D + gd) * H + gh) * W + gw;
 #pragma unroll
-      for (int nb = 0; nb < NB; ++nb) {
-        const int n = n0 + nb * 32 + l32;
+      for (int cb = 0; cb < CB; ++cb) {
+        const int n = n0 + cb * NCOL + lcol;
         if (n >= Cout) continue;
         if (part) {
           part[((int64_t)blockIdx.z * ((int64_t)vol.B * D * H * W) + vox) * npad + n] =
-              acc[mb][nb][r];
+              acc[rb][cb][r];
           continue;
         }
         float* p = n < y.split ? y.p0 + vox * y.ld0 + n : y.p1 + vox * y.ld1 + (n - y.split);
-        *p = acc[mb][nb][r];
+        *p = acc[rb][cb][r];
       }
     }
   }
@@ -382,60 +483,66 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
   // by k_in_stats_fin (Chan).  stats[(tile*npad + n)*2 + {0,1}], count[tile].
   if (stats) {
     __syncthreads();  // every wave is past its last LDS operand read
-    float* sred = reinterpret_cast<float*>(lds4);  // [NW][NB][32]
+    float* sred = reinterpret_cast<float*>(lds4);  // [NW][CB][NCOL]
     const int nd = min(D - d0, TD), nh = min(H - h0, TH), nwv = min(W - w0, TW);
     const float cnt = (float)(nd * nh * nwv);
-    bool ok[MB][16];
+    bool ok[RB][NREG];
 #pragma unroll
-    for (int mb = 0; mb < MB; ++mb)
+    for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
+      for (int r = 0; r < NREG; ++r) {
         int td, th, tw;
-        vrow(wave * MB + mb, (r & 3) + 8 * (r >> 2) + 4 * khalf, td, th, tw);
-        ok[mb][r] = d0 + td < D && h0 + th < H && w0 + tw < W;
+        vrow(wave * RB + rb, orow(r), td, th, tw);
+        ok[rb][r] = d0 + td < D && h0 + th < H && w0 + tw < W;
       }
-    float tsum[NB], mu[NB];
+    // lanes holding the same column: 32x32 -- l and l+32; 16x16 -- l, l+16, l+32, l+48
+    auto colsum = [&](float v) {
+      v += __shfl_xor(v, 32);
+      if constexpr (X16) v += __shfl_xor(v, 16);
+      return v;
+    };
+    float tsum[CB], mu[CB];
 #pragma unroll
-    for (int nb = 0; nb < NB; ++nb) {
+    for (int cb = 0; cb < CB; ++cb) {
       float sacc = 0.f;
 #pragma unroll
-      for (int mb = 0; mb < MB; ++mb)
+      for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) sacc += ok[mb][r] ? acc[mb][nb][r] : 0.f;
-      sacc += __shfl_xor(sacc, 32);
-      if (!khalf) sred[(wave * NB + nb) * 32 + l32] = sacc;
+        for (int r = 0; r < NREG; ++r) sacc += ok[rb][r] ? acc[rb][cb][r] : 0.f;
+      sacc = colsum(sacc);
+      if (lane < NCOL) sred[(wave * CB + cb) * NCOL + lcol] = sacc;
     }
     __syncthreads();
 #pragma unroll
-    for (int nb = 0; nb < NB; ++nb) {
+    for (int cb = 0; cb < CB; ++cb) {
       float t = 0.f;
-      for (int w = 0; w < NW; ++w) t += sred[(w * NB + nb) * 32 + l32];
-      tsum[nb] = t;
-      mu[nb] = t / cnt;
+      for (int w = 0; w < NW; ++w) t += sred[(w * CB + cb) * NCOL + lcol];
+      tsum[cb] = t;
+      mu[cb] = t / cnt;
     }
     __syncthreads();
 #pragma unroll
-    for (int nb = 0; nb < NB; ++nb) {
+    for (int cb = 0; cb < CB; ++cb) {
       float qacc = 0.f;
 #pragma unroll
-      for (int mb = 0; mb < MB; ++mb)
+      for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float dl = acc[mb][nb][r] - mu[nb];
-          qacc += ok[mb][r] ? dl * dl : 0.f;
+        for (int r = 0; r < NREG; ++r) {
+          const float dl = acc[rb][cb][r] - mu[cb];
+          qacc += ok[rb][r] ? dl * dl : 0.f;
         }
-      qacc += __shfl_xor(qacc, 32);
-      if (!khalf) sred[(wave * NB + nb) * 32 + l32] = qacc;
+      qacc = colsum(qacc);
+      if (lane < NCOL) sred[(wave * CB + cb) * NCOL + lcol] = qacc;
     }
     __syncthreads();
-    if (wave == 0 && !khalf) {
+    if (wave == 0 && lane < NCOL) {
 #pragma unroll
-      for (int nb = 0; nb < NB; ++nb) {
+      for (int cb = 0; cb < CB; ++cb) {
         float q = 0.f;
-        for (int w = 0; w < NW; ++w) q += sred[(w * NB + nb) * 32 + l32];
-        const int n = n0 + nb * 32 + l32;
+        for (int w = 0; w < NW; ++w) q += sred[(w * CB + cb) * NCOL + lcol];
+        const int n = n0 + cb * NCOL + lcol;
         if (n < Cout) {
-          stats[((int64_t)tile * npad + n) * 2 + 0] = tsum[nb];
+          stats[((int64_t)tile * npad + n) * 2 + 0] = tsum[cb];
           stats[((int64_t)tile * npad + n) * 2 + 1] = q;
         }
       }
@@ -524,7 +631,7 @@ static hipError_t launch_fwd_x(const Src2& x, const uint4* wx, const Dst2& y, Vo
                                int nsplit = 1, int kps = 0, float* stats = nullptr) {
   constexpr size_t shm = xt_lds_bytes<BN, KD, NS, NW * MB>();
   static_assert(shm <= (NW == 8 ? 160 : 80) * 1024, "LDS budget");
-  auto kern = k_conv3d_fwd_x<BN, KD, NS, MB, NW>;
+  auto kern = k_conv3d_fwd_x<BN, KD, NS, MB, NW, SPFF_X16 != 0>;
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
