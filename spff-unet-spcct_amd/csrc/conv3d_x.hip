@@ -291,14 +291,17 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
       const int q = i & 1, pos = (i < NHX ? i : 0) >> 1;
       const int hw = pos % HWD, t2 = pos / HWD, hh = t2 % HH, hd = t2 / HH;
       const int gd = d0 + hd - KD / 2, gh = h0 + hh - 1, gw = w0 + hw - 1;
-      const int c = kc * 8 + 4 * q;
       const bool ok = i < NHX && (unsigned)(gd + vol.dh) < (unsigned)(D + 2 * vol.dh) &&
-                      (unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W && c < Cin;
+                      (unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W &&
+                      kc * 8 + 4 * q < Cin;
       const int64_t vox = ok ? (((int64_t)b * D + gd) * H + gh) * W + gw : 0;
-      const int cc = ok ? c : 0;
-      const float* p =
-          cc < x.split ? x.p0 + vox * x.ld0 + cc : x.p1 + vox * x.ld1 + (cc - x.split);
-      hreg[k] = *reinterpret_cast<const float4*>(p);
+      // two-source select on the operands (v_cndmask), not on two address
+      // expressions (which the compiler turns into divergent branches)
+      const int c = ok ? kc * 8 + 4 * q : 0;
+      const bool s0 = c < x.split;
+      const float* src = s0 ? x.p0 : x.p1;
+      const int64_t ld = s0 ? x.ld0 : x.ld1;
+      hreg[k] = *reinterpret_cast<const float4*>(src + vox * ld + (s0 ? c : c - x.split));
       hvalid |= ok ? (1u << k) : 0u;
     }
   };

@@ -92,6 +92,11 @@ struct UpL {
   int Cin, Cout, lvl_low;
   int64_t w, b;
   size_t pk, out;
+  // _cat trilinear fallback (models.py:687-691): 2 x the low level's H / W differs from
+  // the skip's (odd extents floor in the pools).  raw = the up-conv output at 2H x 2W
+  // (resized into out); in the backward it holds the resized-back gradient.
+  bool rs = false;
+  size_t raw = 0;
 };
 
 }  // namespace
@@ -232,10 +237,8 @@ int build_plan(spff_plan* p) {
   if (c.base < 8 || (c.base & (c.base - 1)))
     return fail(SPFF_EINVAL, "base must be a power of two >= 8");
   if (c.ksd != 1 && c.ksd != 3) return fail(SPFF_EINVAL, "ksd must be 1 or 3");
-  if (c.height % 8 || c.width % 8 || c.height < 8 || c.width < 8)
-    return fail(SPFF_ESHAPE,
-                "H and W must be multiples of 8 (three (1,2,2) pools without the trilinear _cat "
-                "fallback of models.py:689-690)");
+  if (c.height < 8 || c.width < 8)
+    return fail(SPFF_ESHAPE, "H and W must be >= 8 (three (1,2,2) pools)");
   if (c.in_ch > 64) return fail(SPFF_EINVAL, "in_ch > 64 not supported");
   if (c.math < SPFF_MATH_F32 || c.math > SPFF_MATH_BF16X3)
     return fail(SPFF_EINVAL, "math must be one of SPFF_MATH_*");
@@ -293,6 +296,9 @@ int build_plan(spff_plan* p) {
     U.Cin = upc[u][0];
     U.Cout = upc[u][1];
     U.lvl_low = upc[u][2] + 1;
+    const Vol& vl = p->vol[U.lvl_low];
+    const Vol& vh = p->vol[U.lvl_low - 1];
+    U.rs = 2 * vl.H != vh.H || 2 * vl.W != vh.W;
     U.w = p->reg(std::string(upn[u]) + ".weight", {U.Cin, U.Cout, 1, 2, 2});
     U.b = p->reg(std::string(upn[u]) + ".bias", {U.Cout});
     reg_block(p, p->blk[4 + u]);
@@ -376,6 +382,7 @@ int build_plan(spff_plan* p) {
     const Vol& vh = p->vol[U.lvl_low - 1];
     if (!p->lean) U.out = p->alloc_halo(nvox(vh) * U.Cout * sizeof(float), slice(vh, U.Cout));
     U.pk = p->alloc(upconv_pack_floats(U.Cin, U.Cout) * sizeof(float));
+    if (U.rs) U.raw = p->alloc(nvox(p->vol[U.lvl_low]) * 4 * U.Cout * sizeof(float));
     wg = std::max(wg, upconv_wgrad_ws_bytes(p->vol[U.lvl_low], U.Cin, U.Cout));
   }
   p->head_pk = p->alloc(head_pack_floats(f, p->K) * sizeof(float));
@@ -586,6 +593,23 @@ int fwd_block(spff_plan* p, Blk& b, const Src2& in) {
 
 Src2 src2(const float* a, const float* b, int C) { return Src2{a, b, C, C, C}; }
 
+// up-conv of `in` into U.out at the skip's resolution (through U.raw and the _cat
+// trilinear resize when the pooled extents were odd)
+int upconv_out(spff_plan* p, const UpL& U, const float* in) {
+  const Vol& low = p->vol[U.lvl_low];
+  PROF(p, 3, 2.0 * nvox(low) * U.Cin * 4.0 * U.Cout,
+       upconv_fwd(in, p->F(U.pk), p->P(U.b), p->F(U.rs ? U.raw : U.out), low, U.Cin, U.Cout,
+                  p->st));
+  if (U.rs) {
+    const Vol& vh = p->vol[U.lvl_low - 1];
+    Vol vr = low;
+    vr.H *= 2;
+    vr.W *= 2;
+    HIPCK(resize_hw_fwd(p->F(U.raw), p->F(U.out), vr, vh.H, vh.W, U.Cout, p->st));
+  }
+  return SPFF_OK;
+}
+
 // block output out = lrelu(y2 * al2 + de2) [* P + Q] into dst (lean recompute)
 int recompute_out(spff_plan* p, const Blk& b, float* dst) {
   const Vol& v = p->vol[b.lvl];
@@ -606,9 +630,7 @@ int lean_dec_input(spff_plan* p, int bi, Src2* in) {
   const Blk& prev = B[bi - 1];
   UpL& U = p->up[bi - 4];
   if (bi - 1 >= 4) CK(recompute_out(p, prev, p->F(prev.out)));
-  PROF(p, 3, 2.0 * nvox(p->vol[U.lvl_low]) * U.Cin * 4.0 * U.Cout,
-       upconv_fwd(p->F(prev.out), p->F(U.pk), p->P(U.b), p->F(U.out), p->vol[U.lvl_low], U.Cin,
-                  U.Cout, p->st));
+  CK(upconv_out(p, U, p->F(prev.out)));
   CK(recompute_out(p, skip, p->F(p->G_out)));
   *in = src2(p->F(U.out), p->F(p->G_out), d.C);
   return halo_src(p, *in, p->vol[d.lvl]);
@@ -737,8 +759,7 @@ int forward(spff_plan* p, const float* x, float* logits) {
     float* pk = p->F(U.pk);
     HIPCK(upconv_pack(p->P(U.w), pk, pk + upconv_pack_dgrad_offset(U.Cin, U.Cout), U.Cin, U.Cout,
                       p->st));
-    PROF(p, 3, 2.0 * nvox(p->vol[U.lvl_low]) * U.Cin * 4.0 * U.Cout,
-         upconv_fwd(prev, pk, p->P(U.b), p->F(U.out), p->vol[U.lvl_low], U.Cin, U.Cout, p->st));
+    CK(upconv_out(p, U, prev));
     Blk& d = B[4 + u];
     const Blk& skip = B[2 - u];
     CK(fwd_block(p, d, src2(p->F(U.out), p->F(skip.out), U.Cout)));
@@ -777,13 +798,22 @@ int backward(spff_plan* p, const float* dl) {
     if (p->dbg_stop == k + 1) return SPFF_OK;
     const float* upin = (ui == 0) ? p->F(B[3].out) : p->F(B[bi - 1].out);
     const Vol& low = p->vol[U.lvl_low];
+    const float* gup = p->F(p->G_dx);
+    if (U.rs) {  // back through the _cat resize to the up-conv's 2H x 2W grid
+      Vol vr = low;
+      vr.H *= 2;
+      vr.W *= 2;
+      HIPCK(resize_hw_bwd(p->F(p->G_dx), p->F(U.raw), vr, p->vol[lvl].H, p->vol[lvl].W, C,
+                          p->st));
+      gup = p->F(U.raw);
+    }
     PROF(p, 3, 2.0 * nvox(low) * U.Cin * 4.0 * U.Cout,
-         upconv_wgrad(upin, p->F(p->G_dx), C, p->DP(U.w), p->DP(U.b), low, U.Cin, U.Cout,
+         upconv_wgrad(upin, gup, C, p->DP(U.w), p->DP(U.b), low, U.Cin, U.Cout,
                       p->F(p->wg_ws), p->st));
     CK(grad_ready(p, U.w, U.b + U.Cout));
     float* pk = p->F(U.pk);
     PROF(p, 3, 2.0 * nvox(low) * U.Cin * 4.0 * U.Cout,
-         upconv_dgrad(p->F(p->G_dx), C, pk + upconv_pack_dgrad_offset(U.Cin, U.Cout),
+         upconv_dgrad(gup, C, pk + upconv_pack_dgrad_offset(U.Cin, U.Cout),
                       p->F(p->G_out), low, U.Cin, U.Cout, p->st));
   }
   // bottleneck + encoder

@@ -1,6 +1,8 @@
 // Layout conversion, MaxPool3d((1,2,2)) forward/backward and small utilities.
 // Reference: MaxPool3d(P=(1,2,2)) models.py:661-665 (pool only in H,W: F6).
 #include "spff_internal.h"
+
+#include <algorithm>
 #include <math.h>
 
 namespace spff {
@@ -113,6 +115,114 @@ hipError_t maxpool_bwd_add(const float* dp, const uint8_t* idx, const float* dsk
   return hipGetLastError();
 }
 
+// ------------------------------------------------ _cat trilinear fallback --
+// ATen upsample_trilinear3d, align_corners=False, output size given: per axis
+// scale = in / out (fp32), src = scale (o + 0.5) - 0.5 clamped at 0, i0 = (int) src,
+// i1 = i0 + (i0 < in - 1), l1 = src - i0, l0 = 1 - l1.  Depth in == out makes the
+// depth source index exactly d (weights 1, 0), so only (h, w) interpolate.  The
+// value is accumulated as ATen's CPU kernel nests it: h outer, w inner.
+__device__ __forceinline__ void lin_src(int o, int in, int out, int& i0, int& i1, float& l0,
+                                        float& l1) {
+  const float scale = (float)in / (float)out;
+  float src = scale * ((float)o + 0.5f) - 0.5f;
+  src = src < 0.f ? 0.f : src;
+  i0 = (int)src;
+  if (i0 > in - 1) i0 = in - 1;
+  i1 = i0 + (i0 < in - 1 ? 1 : 0);
+  l1 = src - (float)i0;
+  l0 = 1.f - l1;
+}
+
+__global__ void k_resize_hw_fwd(const float* __restrict__ x, float* __restrict__ y, Vol in,
+                                int Ho, int Wo, int C) {
+  const int C4 = C / 4;
+  const int64_t total = (int64_t)in.B * in.D * Ho * Wo * C4;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C4) * 4;
+    int64_t t = i / C4;
+    const int wo = (int)(t % Wo); t /= Wo;
+    const int ho = (int)(t % Ho); t /= Ho;  // t = b*D + d
+    int h0, h1, w0, w1;
+    float lh0, lh1, lw0, lw1;
+    lin_src(ho, in.H, Ho, h0, h1, lh0, lh1);
+    lin_src(wo, in.W, Wo, w0, w1, lw0, lw1);
+    const float* r0 = x + ((t * in.H + h0) * in.W) * C + c;
+    const float* r1 = x + ((t * in.H + h1) * in.W) * C + c;
+    const float4 a = *reinterpret_cast<const float4*>(r0 + (int64_t)w0 * C);
+    const float4 b = *reinterpret_cast<const float4*>(r0 + (int64_t)w1 * C);
+    const float4 e = *reinterpret_cast<const float4*>(r1 + (int64_t)w0 * C);
+    const float4 f = *reinterpret_cast<const float4*>(r1 + (int64_t)w1 * C);
+    float4 o;
+    o.x = (a.x * lw0 + b.x * lw1) * lh0 + (e.x * lw0 + f.x * lw1) * lh1;
+    o.y = (a.y * lw0 + b.y * lw1) * lh0 + (e.y * lw0 + f.y * lw1) * lh1;
+    o.z = (a.z * lw0 + b.z * lw1) * lh0 + (e.z * lw0 + f.z * lw1) * lh1;
+    o.w = (a.w * lw0 + b.w * lw1) * lh0 + (e.w * lw0 + f.w * lw1) * lh1;
+    *reinterpret_cast<float4*>(y + (i / C4) * C + c) = o;
+  }
+}
+
+// output rows o in [lo, hi] that can read input row i (scale = in / out <= ~1)
+__device__ __forceinline__ void lin_range(int i, int in, int out, int& lo, int& hi) {
+  const float inv = (float)out / (float)in;
+  lo = max(0, (int)floorf(((float)i - 1.f + 0.5f) * inv - 0.5f) - 1);
+  hi = min(out - 1, (int)ceilf(((float)i + 1.f + 0.5f) * inv - 0.5f) + 1);
+}
+
+// dx[i] = sum over the outputs that read input (h, w) of lambda_h lambda_w dy, gathered
+// in (ho, h0-then-h1, wo, w0-then-w1) order -- deterministic, no atomics
+__global__ void k_resize_hw_bwd(const float* __restrict__ dy, float* __restrict__ dx, Vol in,
+                                int Ho, int Wo, int C) {
+  const int C4 = C / 4;
+  const int64_t total = (int64_t)in.B * in.D * in.H * in.W * C4;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C4) * 4;
+    int64_t t = i / C4;
+    const int wi = (int)(t % in.W); t /= in.W;
+    const int hi = (int)(t % in.H); t /= in.H;
+    int hlo, hhi, wlo, whi;
+    lin_range(hi, in.H, Ho, hlo, hhi);
+    lin_range(wi, in.W, Wo, wlo, whi);
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int ho = hlo; ho <= hhi; ++ho) {
+      int h0, h1, w0, w1;
+      float lh0, lh1, lw0, lw1;
+      lin_src(ho, in.H, Ho, h0, h1, lh0, lh1);
+      for (int hs = 0; hs < 2; ++hs) {
+        if ((hs ? h1 : h0) != hi) continue;
+        const float lh = hs ? lh1 : lh0;
+        for (int wo = wlo; wo <= whi; ++wo) {
+          lin_src(wo, in.W, Wo, w0, w1, lw0, lw1);
+          const float4 g = *reinterpret_cast<const float4*>(
+              dy + ((t * Ho + ho) * (int64_t)Wo + wo) * C + c);
+          for (int ws = 0; ws < 2; ++ws) {
+            if ((ws ? w1 : w0) != wi) continue;
+            const float wgt = lh * (ws ? lw1 : lw0);
+            acc.x += g.x * wgt; acc.y += g.y * wgt; acc.z += g.z * wgt; acc.w += g.w * wgt;
+          }
+        }
+      }
+    }
+    *reinterpret_cast<float4*>(dx + (i / C4) * C + c) = acc;
+  }
+}
+
+hipError_t resize_hw_fwd(const float* x, float* y, Vol in, int Ho, int Wo, int C, hipStream_t s) {
+  const int64_t total = (int64_t)in.B * in.D * Ho * Wo * (C / 4);
+  const int grid = (int)std::min<int64_t>((total + 255) / 256, 16384);
+  hipLaunchKernelGGL(k_resize_hw_fwd, dim3(grid), dim3(256), 0, s, x, y, in, Ho, Wo, C);
+  return hipGetLastError();
+}
+
+hipError_t resize_hw_bwd(const float* dy, float* dx, Vol in, int Ho, int Wo, int C,
+                         hipStream_t s) {
+  const int64_t total = (int64_t)in.B * in.D * in.H * in.W * (C / 4);
+  const int grid = (int)std::min<int64_t>((total + 255) / 256, 16384);
+  hipLaunchKernelGGL(k_resize_hw_bwd, dim3(grid), dim3(256), 0, s, dy, dx, in, Ho, Wo, C);
+  return hipGetLastError();
+}
+
 // --------------------------------------------------------- maxpool 2x2x2 --
 // nn.MaxPool3d(2) (reference Cicek3DUNet pool1..pool4, models.py:728-731):
 // scan (dd, dh, dw) in row-major order, replace on strictly greater or NaN, so
@@ -211,18 +321,7 @@ hipError_t maxpool3_bwd_add(const float* dp, const uint8_t* idx, const float* ds
 // models.py:153-163): the H/W factors are exactly 1 (source index = output
 // index, weights 1 and 0), so it is linear interpolation along D with ATen's
 // source index: src = max(0, (Din/Dout)*(d + 0.5) - 0.5) in fp32,
-// i0 = floor(src), i1 = min(i0 + 1, Din - 1), w1 = src - i0, w0 = 1 - w1.
-__device__ __forceinline__ void lin_src(int d, int Din, int Dout, int& i0, int& i1, float& w0,
-                                        float& w1) {
-  const float scale = (float)Din / (float)Dout;
-  float src = scale * ((float)d + 0.5f) - 0.5f;
-  src = src < 0.f ? 0.f : src;
-  i0 = (int)src;
-  if (i0 > Din - 1) i0 = Din - 1;
-  i1 = i0 + (i0 < Din - 1 ? 1 : 0);
-  w1 = src - (float)i0;
-  w0 = 1.f - w1;
-}
+// i0 = floor(src), i1 = min(i0 + 1, Din - 1), w1 = src - i0, w0 = 1 - w1 (lin_src above).
 
 // input: x [B][C][Din][H][W] (reference layout) -> y [B][Dout][H][W][ldy]
 // (channel-last, channels C..ldy-1 zero) in one pass

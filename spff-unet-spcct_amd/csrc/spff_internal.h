@@ -260,6 +260,11 @@ hipError_t maxpool_fwd(const float* x, float* y, uint8_t* idx, Vol in, int C, hi
 hipError_t maxpool_bwd_add(const float* dp, const uint8_t* idx, const float* dskip, int ldskip,
                            float* dx, Vol in, int C, hipStream_t s);
 hipError_t scale_by_dev(float* x, int64_t n, const float* scale, hipStream_t s);
+// the decoder's _cat fallback (models.py:687-691): F.interpolate(up, skip size, trilinear,
+// align_corners=False) from (D, Hi, Wi) to (D, Ho, Wo) -- the D factor is exactly 1 --
+// and its backward (gather form, fixed order).  Channel-last, ld = C (multiple of 4).
+hipError_t resize_hw_fwd(const float* x, float* y, Vol in, int Ho, int Wo, int C, hipStream_t s);
+hipError_t resize_hw_bwd(const float* dy, float* dx, Vol in, int Ho, int Wo, int C, hipStream_t s);
 // MaxPool3d(2) (full 2x2x2), first-max ties; idx = (dd*2+dh)*2+dw
 hipError_t maxpool3_fwd(const float* x, float* y, uint8_t* idx, Vol in, int C, hipStream_t s);
 hipError_t maxpool3_bwd_add(const float* dp, const uint8_t* idx, const float* dskip, int ldskip,

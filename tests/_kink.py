@@ -52,7 +52,8 @@ class _Hooks:
         k = self.npool % 3
         self.npool += 1
         B_, C_, D_, H_, W_ = t.shape
-        v = t.reshape(B_, C_, D_, H_ // 2, 2, W_ // 2, 2).permute(0, 1, 2, 3, 5, 4, 6)
+        v = t[..., :H_ // 2 * 2, :W_ // 2 * 2].reshape(B_, C_, D_, H_ // 2, 2, W_ // 2, 2)
+        v = v.permute(0, 1, 2, 3, 5, 4, 6)
         v = v.reshape(B_, C_, D_, H_ // 2, W_ // 2, 4)
         self.record[f"pool{k + 1}"] = v.detach().clone()
         idx = v.detach().argmax(-1)
@@ -170,7 +171,8 @@ class forced_branches:
         k = self.npool % 3
         self.npool += 1
         B_, C_, D_, H_, W_ = t.shape
-        v = t.reshape(B_, C_, D_, H_ // 2, 2, W_ // 2, 2).permute(0, 1, 2, 3, 5, 4, 6)
+        v = t[..., :H_ // 2 * 2, :W_ // 2 * 2].reshape(B_, C_, D_, H_ // 2, 2, W_ // 2, 2)
+        v = v.permute(0, 1, 2, 3, 5, 4, 6)
         v = v.reshape(B_, C_, D_, H_ // 2, W_ // 2, 4)
         return v.gather(-1, self.masks[f"pool{k + 1}"].unsqueeze(-1)).squeeze(-1)
 

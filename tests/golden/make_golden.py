@@ -372,6 +372,18 @@ def main():
         meta=dict(variant="SPFF-UNet", in_ch=1, base=8, K=13, seed=5, jitter=0.25, lit=False),
         data=_run_case(torch, Hh, ns_core(1, 13, 8), x, y, 13, 5, 0.25, True, False))
 
+    # --- Fx4: H, W not multiples of 8 (18 x 20): the trilinear _cat fallback of
+    # models.py:687-691 runs at level 1 (H 9 vs 2x4) and level 2 (W 5 vs 2x2) ---
+    rng = np.random.default_rng(66)
+    x = rng.standard_normal((1, 5, 4, 18, 20)).astype(np.float32)
+    y = _labels(rng, (1, 4, 18, 20), 9)
+    cases["fx4_ragged_hw"] = dict(
+        meta=dict(variant="SPFF-UNet", in_ch=5, base=8, K=9, seed=11, jitter=0.25, lit=False),
+        data=_run_case(torch, Hh, ns_core(5, 9, 8), x, y, 9, 11, 0.25, True, False))
+    if only and only.startswith("fx4"):
+        _write(cases, only)
+        return
+
     # --- Fx-ablations: the other SPCT-family registry variants, base=8 ---
     abl = {
         "E_SP_UNet": dict(efilm=True, fgate=False, se=True, specse=True),

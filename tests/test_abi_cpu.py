@@ -49,7 +49,9 @@ def test_plan_layout_matches_reference_state_dict():
 
 def test_plan_rejects_bad_shapes():
     with pytest.raises(E.SpffError):
-        E.Plan(1, 1, 5, 60, 64, 13)   # H not a multiple of 8
+        E.Plan(1, 1, 5, 4, 64, 13)    # H < 8: three (1,2,2) pools
+    # H, W not multiples of 8 take the _cat trilinear fallback (models.py:687-691)
+    E.Plan(1, 1, 5, 60, 66, 13)
     with pytest.raises(E.SpffError):
         E.Plan(1, 1, 5, 64, 64, 40)   # K > 32
     with pytest.raises(E.SpffError):

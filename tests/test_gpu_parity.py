@@ -172,7 +172,8 @@ def engine_branch_masks(core, xshape, st, cfg):
         y = plan.saved(f"{blk}.out").double().cpu()
         C = y.shape[1]
         y = y.view(B, Dd, Hh_, Ww, C).permute(0, 4, 1, 2, 3)
-        v = y.reshape(B, C, Dd, Hh_ // 2, 2, Ww // 2, 2).permute(0, 1, 2, 3, 5, 4, 6)
+        v = y[..., :Hh_ // 2 * 2, :Ww // 2 * 2].reshape(B, C, Dd, Hh_ // 2, 2, Ww // 2, 2)
+        v = v.permute(0, 1, 2, 3, 5, 4, 6)
         masks[f"pool{k + 1}"] = v.reshape(B, C, Dd, Hh_ // 2, Ww // 2, 4).argmax(-1).contiguous()
     return masks
 
@@ -195,7 +196,8 @@ def oracle_grads(d, masks):
         npool[0] += 1
         idx = masks[f"pool{k + 1}"]
         B_, C_, D_, H_, W_ = t.shape
-        v = t.reshape(B_, C_, D_, H_ // 2, 2, W_ // 2, 2).permute(0, 1, 2, 3, 5, 4, 6)
+        v = t[..., :H_ // 2 * 2, :W_ // 2 * 2].reshape(B_, C_, D_, H_ // 2, 2, W_ // 2, 2)
+        v = v.permute(0, 1, 2, 3, 5, 4, 6)
         v = v.reshape(B_, C_, D_, H_ // 2, W_ // 2, 4)
         if t.dtype == torch.float64:
             nflip[0] += int((v.detach().argmax(-1) != idx).sum())
