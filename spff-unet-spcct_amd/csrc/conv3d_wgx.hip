@@ -134,6 +134,7 @@ __global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x(
     for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
 
   float4 hreg[NH], yreg[NY];
+  float4 xal = make_float4(1.f, 1.f, 1.f, 1.f), xde = make_float4(0.f, 0.f, 0.f, 0.f);
   auto fetch = [&](int tile) {
     // depth-fastest tile order: a split's consecutive tiles share two of their three
     // halo planes, which the previous tile has just brought into L2
@@ -143,6 +144,14 @@ __global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x(
     const int thi = t % tilesH;
     const int b = t / tilesH;
     const int h0 = thi * WX_TH, w0 = twi * WX_TW;
+    if (x.al) {  // fused input activation: this tile's batch, this thread's 4 channels
+      // (256 threads, CQ | 256: the thread's channel group is the same for every k)
+      const int c = ci_base + 4 * (tid % CQ);
+      if (c < Cin) {
+        xal = *reinterpret_cast<const float4*>(x.al + (int64_t)b * x.ld0 + c);
+        xde = *reinterpret_cast<const float4*>(x.de + (int64_t)b * x.ld0 + c);
+      }
+    }
 #pragma unroll
     for (int k = 0; k < NH; ++k) {
       const int i = tid + 256 * k;
@@ -153,11 +162,17 @@ __global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x(
         const int gd = d0 + hd - KD / 2, gh = h0 + hh - 1, gw = w0 + hw - 1;
         const int c = ci_base + 4 * c4;
         if ((unsigned)(gd + vol.dh) < (unsigned)(D + 2 * vol.dh) && (unsigned)gh < (unsigned)H &&
-            (unsigned)gw < (unsigned)W && c < Cin) {
+            (unsigned)gw < (unsigned)W && c < Cin && !((gd < 0 && x.zlo) || (gd >= D && x.zhi))) {
           const int64_t vox = (((int64_t)b * D + gd) * H + gh) * W + gw;
           const float* p =
               c < x.split ? x.p0 + vox * x.ld0 + c : x.p1 + vox * x.ld1 + (c - x.split);
           v = *reinterpret_cast<const float4*>(p);
+          if (x.al) {
+            v.x = v.x * xal.x + xde.x; v.x = v.x > 0.f ? v.x : 0.01f * v.x;
+            v.y = v.y * xal.y + xde.y; v.y = v.y > 0.f ? v.y : 0.01f * v.y;
+            v.z = v.z * xal.z + xde.z; v.z = v.z > 0.f ? v.z : 0.01f * v.z;
+            v.w = v.w * xal.w + xde.w; v.w = v.w > 0.f ? v.w : 0.01f * v.w;
+          }
         }
       }
       hreg[k] = v;

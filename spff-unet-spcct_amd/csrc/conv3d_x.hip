@@ -281,8 +281,10 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
   float4 hreg[RH];
   uint2 hs[RH][NS];
   unsigned hvalid = 0;  // bit k: hreg[k] is in bounds (else it is zeroed at the split)
+  int fkc = 0;          // chunk of the registers in flight
   auto fetch = [&](int kc) {
     hvalid = 0;
+    fkc = kc;
 #pragma unroll
     for (int k = 0; k < RH; ++k) {
       const int i = tid + XT_THREADS * k;
@@ -293,7 +295,7 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
       const int gd = d0 + hd - KD / 2, gh = h0 + hh - 1, gw = w0 + hw - 1;
       const bool ok = i < NHX && (unsigned)(gd + vol.dh) < (unsigned)(D + 2 * vol.dh) &&
                       (unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W &&
-                      kc * 8 + 4 * q < Cin;
+                      kc * 8 + 4 * q < Cin && !((gd < 0 && x.zlo) || (gd >= D && x.zhi));
       const int64_t vox = ok ? (((int64_t)b * D + gd) * H + gh) * W + gw : 0;
       // two-source select on the operands (v_cndmask), not on two address
       // expressions (which the compiler turns into divergent branches)
@@ -307,11 +309,30 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
   };
   auto split_one = [&](int k) {
     const bool ok = (hvalid >> k) & 1u;
+    float4 v = hreg[k];
+    // fused input activation (zero padding stays zero: applied to valid only).  Compiled
+    // for the 32-wide tiles only: the level-0 convs (C = 32) carry 55 % of the fused
+    // bytes, and in the 64-wide kernel the extra registers spill (256 VGPRs)
+    if constexpr (BN == 32) if (x.al) {
+      // the chunk's 8 (al, de) pairs are workgroup-uniform (scalar loads); a thread's 4
+      // channels are the lower or upper half (XT_THREADS is even: q = tid & 1 for all k)
+      const float* ap = x.al + (int64_t)b * x.ld0 + fkc * 8;
+      const float* dp = x.de + (int64_t)b * x.ld0 + fkc * 8;
+      const bool hi = tid & 1;
+      float r[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float a = hi ? ap[4 + j] : ap[j], e = hi ? dp[4 + j] : dp[j];
+        const float t = r[j] * a + e;
+        r[j] = fmaxf(t, 0.01f * t);  // = lrelu(t, 0.01) (t > 0 ? t : 0.01 t) for finite t
+      }
+      v = make_float4(r[0], r[1], r[2], r[3]);
+    }
     unsigned short s0[NS], s1[NS], s2[NS], s3[NS];
-    split_bf16<NS>(ok ? hreg[k].x : 0.f, s0);
-    split_bf16<NS>(ok ? hreg[k].y : 0.f, s1);
-    split_bf16<NS>(ok ? hreg[k].z : 0.f, s2);
-    split_bf16<NS>(ok ? hreg[k].w : 0.f, s3);
+    split_bf16<NS>(ok ? v.x : 0.f, s0);
+    split_bf16<NS>(ok ? v.y : 0.f, s1);
+    split_bf16<NS>(ok ? v.z : 0.f, s2);
+    split_bf16<NS>(ok ? v.w : 0.f, s3);
 #pragma unroll
     for (int p = 0; p < NS; ++p) {
       hs[k][p].x = (unsigned)s0[p] | ((unsigned)s1[p] << 16);
@@ -634,6 +655,7 @@ static hipError_t launch_fwd_x(const Src2& x, const uint4* wx, const Dst2& y, Vo
                                int nsplit = 1, int kps = 0, float* stats = nullptr) {
   constexpr size_t shm = xt_lds_bytes<BN, KD, NS, NW * MB>();
   static_assert(shm <= (NW == 8 ? 160 : 80) * 1024, "LDS budget");
+  if (x.al && BN != 32) return hipErrorInvalidValue;  // fused activation: 32-wide tiles only
   auto kern = k_conv3d_fwd_x<BN, KD, NS, MB, NW, SPFF_X16 != 0>;
   static bool attr = false;
   if (!attr) {
@@ -691,6 +713,9 @@ bool use_split(Vol vol, int math, bool dgrad) {
 }
 }  // namespace
 bool debug_split_wgrad() { return (debug_split_dir() & 4) != 0; }
+bool conv3d_fuses_act(int math, int C) {
+  return math != SPFF_MATH_F32 && debug_split_dir() == 7 && C == 32;
+}
 namespace {
 // split-K for launches that would not fill the chip (the deep levels of the
 // 3DUNet: 2 x 12 x 12 and 1 x 6 x 6 voxels with 256-512 channels): the input

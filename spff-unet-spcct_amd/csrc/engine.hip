@@ -85,6 +85,7 @@ struct Blk {
   size_t mean1, rstd1, al1, de1, mean2, rstd2, al2, de2;
   size_t Sa, t, bt, hid, s1, g1s, sg2, p, h, e, P, Q;
   size_t spec = 0;  // sharded plans: full-depth s1 spectrum [B][L][2] (fp64)
+  bool fa = false;  // conv2 reads y1 through the IN affine (a1 never stored)
   bool tail() const { return efilm || fgate || post_se || post_spec; }
 };
 
@@ -281,6 +282,7 @@ int build_plan(spff_plan* p) {
     b.novel = b.efilm || b.fgate;
     b.post_se = i < 4 && c.use_se;
     b.post_spec = i < 4 && c.use_specse;
+    b.fa = conv3d_fuses_act(c.math, b.C);
     conv_dims(b.c1, b.Cin, b.C);
     conv_dims(b.c2, b.C, b.C);
   }
@@ -330,10 +332,11 @@ int build_plan(spff_plan* p) {
     Blk& b = p->blk[i];
     const Vol& v = p->vol[b.lvl];
     const size_t act = nvox(v) * b.C * sizeof(float);
-    b.y1 = p->alloc(act);
+    // with the fused input activation conv2 reads y1 (halo'd when sharded), not a1
+    b.y1 = b.fa ? p->alloc_halo(act, slice(v, b.C)) : p->alloc(act);
     b.y2 = p->alloc(act);
     if (!p->lean) {
-      b.a1 = p->alloc_halo(act, slice(v, b.C));
+      if (!b.fa) b.a1 = p->alloc_halo(act, slice(v, b.C));
       b.out = p->alloc_halo(act, slice(v, b.C));
     } else if (i == 3) {
       b.out = p->alloc(act);  // the bottleneck output (up3's input) is kept: 1/64 size
@@ -535,6 +538,18 @@ int in_bwd(spff_plan* p, const Vol& v, int C, int64_t gamma, int64_t beta) {
   return SPFF_OK;
 }
 
+// conv2's input: a1 = lrelu(IN(y1)) -- read from y1 through the IN affine when the
+// conv kernels fuse it (a1 is then never stored), else the materialised a1
+Src2 act_src(const spff_plan* p, const Blk& b) {
+  if (!b.fa) return src1(p->F(b.a1), b.C);
+  Src2 s = src1(p->F(b.y1), b.C);
+  s.al = p->F(b.al1);
+  s.de = p->F(b.de1);
+  s.zlo = p->co.on() && p->co.rank == 0;
+  s.zhi = p->co.on() && p->co.rank == p->co.world - 1;
+  return s;
+}
+
 int fwd_block(spff_plan* p, Blk& b, const Src2& in) {
   const Vol& v = p->vol[b.lvl];
   const int C = b.C, KD = p->KD;
@@ -553,14 +568,16 @@ int fwd_block(spff_plan* p, Blk& b, const Src2& in) {
                               p->F(b.mean1), p->F(b.rstd1), p->F(b.al1), p->F(b.de1), p->st));
   else
     CK(in_stats(p, v, C, b.y1, b.mean1, b.rstd1, b.al1, b.de1, b.g1, b.b1));
-  PROFB(p, 5, 0.0, 8.0 * (double)nvox(v) * C,
-        act_apply(p->F(b.y1), p->F(b.a1), p->F(b.al1), p->F(b.de1), nullptr, nullptr, v, C,
-                  p->st));
+  if (!b.fa)
+    PROFB(p, 5, 0.0, 8.0 * (double)nvox(v) * C,
+          act_apply(p->F(b.y1), p->F(b.a1), p->F(b.al1), p->F(b.de1), nullptr, nullptr, v, C,
+                    p->st));
   HIPCK(conv3d_pack(p->P(b.c2.w), p->F(p->wt), v, KD, C, C, false, math, p->st));
-  CK(halo(p, p->F(b.a1), v, C));
+  const Src2 in2 = act_src(p, b);
+  CK(halo(p, in2.p0, v, C));
   const bool fuse2 = !p->co.on() && conv3d_fuses_stats(v, KD, C, C, math);
   PROFB(p, 0, 2.0 * V * C * C * T, cbytes(V, C, C, T),
-       conv3d_run(src1(p->F(b.a1), C), p->F(p->wt), dst1(p->F(b.y2), C), v, KD, C, C, false,
+       conv3d_run(in2, p->F(p->wt), dst1(p->F(b.y2), C), v, KD, C, C, false,
                   math, p->st, p->F(p->wg_ws), fuse2 ? p->F(p->cst) : nullptr));
   if (fuse2)
     HIPCK(conv3d_in_stats_fin(p->F(p->cst), v, KD, C, C, p->P(b.g2), p->P(b.b2), p->F(b.mean2),
@@ -687,15 +704,15 @@ int bwd_block(spff_plan* p, Blk& b, const float* dout, const Dst2* dx, const Src
                        p->F(b.de2), p->P(b.g2), A, Bc, p->F(p->kk1), p->F(p->kk2), v, C, p->st));
   }
   const double V = (double)nvox(v), T = 9.0 * KD;
-  const float* a1 = p->F(b.a1);
-  if (p->lean) {  // a1 = lrelu(IN(y1)) again, into the buffer da1 overwrites next
+  Src2 a1 = act_src(p, b);  // (fused: y1 and its halo as the forward left them)
+  if (p->lean && !b.fa) {  // a1 = lrelu(IN(y1)) again, into the buffer da1 overwrites next
     PROFB(p, 5, 0.0, 8.0 * (double)nvox(v) * C,
           act_apply(p->F(b.y1), da1, p->F(b.al1), p->F(b.de1), nullptr, nullptr, v, C, p->st));
     CK(halo(p, da1, v, C));
-    a1 = da1;
+    a1 = src1(da1, C);
   }
   PROFB(p, 2, 2.0 * V * C * C * T, cbytes(V, C, C, T),
-       conv3d_wgrad(src1(a1, C), dy2, C, p->DP(b.c2.w), v, KD, C, C, p->cfg.math,
+       conv3d_wgrad(a1, dy2, C, p->DP(b.c2.w), v, KD, C, C, p->cfg.math,
                     p->F(p->wg_ws), p->st));
   const int math = p->cfg.math;
   HIPCK(conv3d_pack(p->P(b.c2.w), p->F(p->wt), v, KD, C, C, true, math, p->st));
@@ -951,7 +968,11 @@ int spff_saved_tensor(const spff_plan* p, void* ws, const char* name, const floa
     const Blk& b = p->blk[i];
     const Vol& v = p->vol[b.lvl];
     if (n == b.name + ".y1") return ret(b.y1, v, b.C);
-    if (n == b.name + ".a1") return ret(b.a1, v, b.C);
+    if (n == b.name + ".a1") {
+      if (b.fa)
+        return fail(SPFF_EINVAL, "a1 is not stored: conv2 applies lrelu(IN(y1)) as it loads y1");
+      return ret(b.a1, v, b.C);
+    }
     if (n == b.name + ".y2") return ret(b.y2, v, b.C);
     if (n == b.name + ".out") return ret(b.out, v, b.C);
     // per-(b,c) normalisation of the IN that follows conv 1 / 2: r = y*al + de

@@ -17,6 +17,13 @@ int set_error(int code, const char* msg);
 // without materialising torch.cat (reference _cat, models.py:687-691).
 struct Src2 {
   const float* p0; const float* p1; int ld0, ld1, split;
+  // Optional input activation of source 0, applied as the conv loads it:
+  // lrelu(x * al[b*ld0 + c] + de[b*ld0 + c], 0.01).  A block's second conv reads its
+  // first conv's raw output y1 through the InstanceNorm affine this way, so
+  // a1 = lrelu(IN(y1)) is never written to HBM (split-bf16 conv kernels only).
+  const float* al = nullptr;
+  const float* de = nullptr;
+  int zlo = 0, zhi = 0;  // depth-sharded: the d = -1 / d = D halo slice is zero padding
 };
 struct Dst2 {
   float* p0; float* p1; int ld0, ld1, split;
@@ -75,6 +82,9 @@ hipError_t conv3d_wgrad(const Src2& x, const float* dy, int lddy, float* dw, Vol
                         int Cin, int Cout, int math, float* ws, hipStream_t s);
 size_t conv3d_wgrad_x_ws_bytes(Vol vol, int KD, int Cin, int Cout);
 bool debug_split_wgrad();  // SPFF_DEBUG_SPLIT (conv3d_x.hip)
+// the split-bf16 fwd and wgrad kernels apply Src2::al / de to a C-channel conv input of
+// a C -> C conv (conv3d_x.hip: the 32-wide tiles, so C == 32)
+bool conv3d_fuses_act(int math, int C);
 hipError_t conv3d_wgrad_x(const Src2& x, const float* dy, int lddy, float* dw, Vol vol, int KD,
                           int Cin, int Cout, int math, float* ws, hipStream_t s);
 // fixed-order sum of the [nsplit][T][kpad][npad] partial slabs into dw[Cout][Cin][T]
