@@ -589,7 +589,7 @@ def main():
                            f"{Dl * world} x {HW} x {HW} volume depth-sharded into {world} x "
                            f"{Dl}-slice slabs (BASELINE configs[3] at 8 GPUs), K={K}, base {args.base}",
                "global_batch": 1, "shape": [1, args.in_ch, Dl * world, HW, HW],
-               "parallelism": f"depth{world}", "memory_layout": plan.memory,
+               "parallelism": f"depth{world}", "memory_layout": plan.layout,
                "workspace_GiB": plan.ws_bytes / 2 ** 30}
         metric = ("voxels/sec fwd+bwd, SPFF-UNet 5-ch volume depth-sharded (512^3 at 8 GPUs)"
                   if not args.strong else

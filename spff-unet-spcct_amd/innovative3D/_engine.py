@@ -235,6 +235,10 @@ class Plan:
         cfg.math = MATH_NAMES[math]
         cfg.memory_mode = MEMORY_MODES[memory]
         self.memory = memory
+        # the layout the engine resolves (engine.hip build_plan: lean from 2^26 voxels on auto)
+        self.layout = ("lean" if memory == "lean" or
+                       (memory == "auto" and batch * depth * height * width >= 1 << 26)
+                       else "full")
         cfg.shard_world, cfg.shard_rank = int(shard_world), int(shard_rank)
         self.math = math
         self.shard = (int(shard_world), int(shard_rank))

@@ -72,7 +72,7 @@ def test_full_volume_512_fits_one_mi355x():
     (2.7 GB), labels (1.1 GB), logits and dlogits (7.0 GB each) and the flat params."""
     p = E.Plan(1, 5, 512, 512, 512, 13)
     V = 512 ** 3
-    assert p.memory == "auto"
+    assert p.memory == "auto" and p.layout == "lean"
     assert p.ws_bytes / V <= 1750, p.ws_bytes / V
     assert p.ws_bytes + V * (5 * 4 + 8 + 2 * 13 * 4) < 250 * 2 ** 30
     full = E.Plan(1, 5, 512, 512, 512, 13, memory="full")
