@@ -29,10 +29,14 @@
 #ifndef SPFF_XCDMAP
 #define SPFF_XCDMAP 1  // 0: split-fastest block order (A/B diagnostics)
 #endif
+#ifndef SPFF_WX16
+#define SPFF_WX16 1  // 1: v_mfma_f32_16x16x32_bf16 wgrad (k_conv3d_wgrad_x16), 0: 32x32x16
+#endif
 
 namespace spff {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short i16x4 __attribute__((ext_vector_type(4)));
 
@@ -291,6 +295,242 @@ __global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x(
   }
 }
 
+// ------------------------------------------------- 16x16x32 wgrad (X16) --
+// Same tiles, staging and partial slabs as k_conv3d_wgrad_x; the MFMA is
+// v_mfma_f32_16x16x32_bf16: rows = 16 (tap, channel) -- one tap x 16 channels
+// (CI 16) or two taps x 8 (CI 8), so 27 x 16 = 432 rows are 27 blocks with no
+// padding, 7 / 7 / 7 / 6 over the 4 waves (the 32-row schedule pads to 448 and
+// gives one wave 128 rows) -- cols = 16 Cout (two col blocks of the 32),
+// k = 32 voxels = two W-rows of the 1 x 8 x 16 tile.
+// k-group g (lanes 16g..16g+15) takes W-row 2ks + (g >> 1), w = 8s + 4(g & 1) + q
+// for read s = 0, 1 and transpose row q: a 32-lane half then reads 8 consecutive
+// halo positions (conflict-free on the channel-last [pos][CI] image), and B reads
+// 8 consecutive voxels of the dy image whose 16-byte chunks are XOR-swizzled by
+// voxel bit 2 (chunk ^= ((v >> 2) & 1) << 1) so those 8 rows of 64 B hit 64
+// distinct banks.
+template <int KD, int CI, int NS, int NJMAX>
+__global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x16(
+    Src2 x, const float* __restrict__ dy, int lddy, float* __restrict__ part, Vol vol, int Cin,
+    int kpad, int Cout, int npad, int tilesH, int tilesW, int ntiles, int tps, int nblk) {
+  constexpr int HD = KD, HH = WX_TH + 2, HWD = WX_TW + 2;
+  constexpr int NPOS = HD * HH * HWD;
+  constexpr int T = KD * 9;
+  constexpr int CQ = CI / 4;                              // float4 per halo position
+  constexpr int NH = (NPOS * CQ + 255) / 256;              // halo float4 per thread
+  constexpr int NY = WX_TV * (WX_CO / 4) / 256;            // dy float4 per thread (= 4)
+  constexpr int NCB = WX_CO / 16;                          // 16-wide col blocks (2)
+  __shared__ __attribute__((aligned(16))) unsigned short Xs[NS * NPOS * CI];
+  __shared__ __attribute__((aligned(16))) unsigned short Ys[NS * WX_TV * WX_CO];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, q = (lane & 15) >> 2, pq = lane & 3;
+  const int nci = kpad / CI, ncb = nci * (npad / WX_CO);
+  const int rk = blockIdx.x >> 3;
+  const int nsp8 = gridDim.x / ncb;
+  const int cbk = SPFF_XCDMAP ? rk % ncb : (int)(blockIdx.x / nsp8);
+  const int split = SPFF_XCDMAP ? (rk / ncb) * 8 + (blockIdx.x & 7) : (int)(blockIdx.x % nsp8);
+  if (split * tps >= ntiles) return;  // padding block (uniform)
+  const int ci_base = (cbk % nci) * CI, co0 = (cbk / nci) * WX_CO;
+  const int D = vol.D, H = vol.H, W = vol.W;
+
+  // row blocks of this wave: wave, wave + 4, ...; nj of them (uniform per wave)
+  const int nj = (nblk - wave + 3) / 4;
+  // lane-constant A address (elements; plane 0, k-step 0, read 0) per block: transpose
+  // column block pq = rows 4pq..4pq+3 of the block = tap (16 blk + 4pq) / CI, channels
+  // (16 blk + 4pq) % CI ..; transpose row q = voxel (W-row g >> 1, w 4(g & 1) + q)
+  int aoff[NJMAX];
+#pragma unroll
+  for (int j = 0; j < NJMAX; ++j) {
+    const int r0 = 16 * (wave + 4 * j) + 4 * pq;
+    int t = r0 / CI;
+    const int ch0 = r0 % CI;
+    if (t >= T) t = 0;  // padding rows: any valid address (never stored)
+    const int kd = t / 9, kh = (t / 3) % 3, kw = t % 3;
+    aoff[j] = ((kd * HH + kh + (g >> 1)) * HWD + kw + 4 * (g & 1) + q) * CI + ch0;
+  }
+  // B: voxel (W-row g >> 1, w 4(g & 1) + q), co 16 cb + 4 pq, chunk-swizzled
+  const int bsw = (g & 1) << 1;
+  const int bv = (g >> 1) * WX_TW + 4 * (g & 1) + q;
+  int boff[NCB];
+#pragma unroll
+  for (int cb = 0; cb < NCB; ++cb)
+    boff[cb] = bv * WX_CO + (((2 * cb + (pq >> 1)) ^ bsw) << 3) + 4 * (pq & 1);
+
+  f32x4 acc[NJMAX][NCB];
+#pragma unroll
+  for (int j = 0; j < NJMAX; ++j)
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[j][cb][r] = 0.f;
+
+  float4 hreg[NH], yreg[NY];
+  float4 xal = make_float4(1.f, 1.f, 1.f, 1.f), xde = make_float4(0.f, 0.f, 0.f, 0.f);
+  auto fetch = [&](int tile) {
+    int t = tile;
+    const int d0 = t % D; t /= D;
+    const int twi = t % tilesW; t /= tilesW;
+    const int thi = t % tilesH;
+    const int b = t / tilesH;
+    const int h0 = thi * WX_TH, w0 = twi * WX_TW;
+    if (x.al) {
+      const int c = ci_base + 4 * (tid % CQ);
+      if (c < Cin) {
+        xal = *reinterpret_cast<const float4*>(x.al + (int64_t)b * x.ld0 + c);
+        xde = *reinterpret_cast<const float4*>(x.de + (int64_t)b * x.ld0 + c);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NH; ++k) {
+      const int i = tid + 256 * k;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (i < NPOS * CQ) {
+        const int c4 = i % CQ, pos = i / CQ;
+        const int hw = pos % HWD, t2 = pos / HWD, hh = t2 % HH, hd = t2 / HH;
+        const int gd = d0 + hd - KD / 2, gh = h0 + hh - 1, gw = w0 + hw - 1;
+        const int c = ci_base + 4 * c4;
+        if ((unsigned)(gd + vol.dh) < (unsigned)(D + 2 * vol.dh) && (unsigned)gh < (unsigned)H &&
+            (unsigned)gw < (unsigned)W && c < Cin && !((gd < 0 && x.zlo) || (gd >= D && x.zhi))) {
+          const int64_t vox = (((int64_t)b * D + gd) * H + gh) * W + gw;
+          const float* p =
+              c < x.split ? x.p0 + vox * x.ld0 + c : x.p1 + vox * x.ld1 + (c - x.split);
+          v = *reinterpret_cast<const float4*>(p);
+          if (x.al) {
+            v.x = v.x * xal.x + xde.x; v.x = v.x > 0.f ? v.x : 0.01f * v.x;
+            v.y = v.y * xal.y + xde.y; v.y = v.y > 0.f ? v.y : 0.01f * v.y;
+            v.z = v.z * xal.z + xde.z; v.z = v.z > 0.f ? v.z : 0.01f * v.z;
+            v.w = v.w * xal.w + xde.w; v.w = v.w > 0.f ? v.w : 0.01f * v.w;
+          }
+        }
+      }
+      hreg[k] = v;
+    }
+#pragma unroll
+    for (int k = 0; k < NY; ++k) {
+      const int i = tid + 256 * k;
+      const int c4 = i % (WX_CO / 4), kv = i / (WX_CO / 4);
+      const int gh = h0 + kv / WX_TW, gw = w0 + kv % WX_TW;
+      const int c = co0 + 4 * c4;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (gh < H && gw < W && c < Cout) {
+        const int64_t vox = (((int64_t)b * D + d0) * H + gh) * W + gw;
+        v = *reinterpret_cast<const float4*>(dy + vox * lddy + c);
+      }
+      yreg[k] = v;
+    }
+  };
+  auto stash = [&](bool negate) {
+#pragma unroll
+    for (int k = 0; k < NH; ++k) {
+      const int i = tid + 256 * k;
+      if (i < NPOS * CQ) {
+        uint2 o[NS];
+        split4<NS>(hreg[k], o);
+#pragma unroll
+        for (int p = 0; p < NS; ++p)
+          *reinterpret_cast<uint2*>(Xs + p * NPOS * CI + 4 * i) = o[p];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NY; ++k) {
+      const int i = tid + 256 * k;
+      const int c4 = i % (WX_CO / 4), kv = i / (WX_CO / 4);
+      uint2 o[NS];
+      const float4 yv = negate ? make_float4(-yreg[k].x, -yreg[k].y, -yreg[k].z, -yreg[k].w)
+                               : yreg[k];
+      split4<NS>(yv, o);
+      const int off = kv * WX_CO + (((c4 >> 1) ^ (((kv >> 2) & 1) << 1)) << 3) + 4 * (c4 & 1);
+#pragma unroll
+      for (int p = 0; p < NS; ++p)
+        *reinterpret_cast<uint2*>(Ys + p * WX_TV * WX_CO + off) = o[p];
+    }
+  };
+
+  auto compute = [&](auto NJc) {
+    constexpr int NJ = decltype(NJc)::value;
+#pragma unroll 2
+    for (int ks = 0; ks < WX_TH / 2; ++ks) {
+      bf16x8 bq[NCB][NS];
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb)
+#pragma unroll
+        for (int p = 0; p < NS; ++p) {
+          const unsigned short* yb = Ys + p * WX_TV * WX_CO + 2 * ks * WX_TW * WX_CO + boff[cb];
+          bq[cb][p] = frag(tr_read(yb), tr_read(yb + 8 * WX_CO));
+        }
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        bf16x8 aq[NS];
+#pragma unroll
+        for (int p = 0; p < NS; ++p) {
+          const unsigned short* xb = Xs + p * NPOS * CI + 2 * ks * HWD * CI + aoff[j];
+          aq[p] = frag(tr_read(xb), tr_read(xb + 8 * CI));
+        }
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb) {
+          f32x4 c = acc[j][cb];
+          if constexpr (NS == 3) {
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq[1], bq[cb][1], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq[0], bq[cb][2], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq[2], bq[cb][0], c, 0, 0, 0);
+          }
+          if constexpr (NS >= 2) {
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq[0], bq[cb][1], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq[1], bq[cb][0], c, 0, 0, 0);
+          }
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq[0], bq[cb][0], c, 0, 0, 0);
+          acc[j][cb] = c;
+        }
+      }
+    }
+  };
+
+  const int tbeg = split * tps;
+  const int tend = min(ntiles, tbeg + tps);
+  if (tbeg < tend) fetch(tbeg);
+  for (int tile = tbeg; tile < tend; ++tile) {
+    // sign-alternating accumulation (conv3d_x.hip)
+    if (tile != tbeg) {
+#pragma unroll
+      for (int j = 0; j < NJMAX; ++j)
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb) acc[j][cb] = -acc[j][cb];
+    }
+    __syncthreads();  // previous compute done reading LDS
+    stash(((tile - tbeg) & 1) != 0);
+    __syncthreads();
+    if (tile + 1 < tend) fetch(tile + 1);
+    if (nj == NJMAX) compute(std::integral_constant<int, NJMAX>{});
+    else if constexpr (NJMAX > 1) compute(std::integral_constant<int, NJMAX - 1>{});
+  }
+
+  if (tend > tbeg && ((tend - 1 - tbeg) & 1)) {
+#pragma unroll
+    for (int j = 0; j < NJMAX; ++j)
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb) acc[j][cb] = -acc[j][cb];
+  }
+
+  // partial slab [split][tap][kpad][npad]: output row 4 g + r of block blk = tap
+  // (16 blk + row) / CI, channel (16 blk + row) % CI; col = co 16 cb + (lane & 15)
+#pragma unroll
+  for (int j = 0; j < NJMAX; ++j) {
+    const int blk = wave + 4 * j;
+    if (j >= nj || blk >= nblk) continue;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 16 * blk + 4 * g + r;
+      const int t = row / CI;
+      if (t >= T) continue;
+      const int ci = ci_base + row % CI;
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb)
+        part[(((int64_t)split * T + t) * kpad + ci) * npad + co0 + 16 * cb + (lane & 15)] =
+            acc[j][cb][r];
+    }
+  }
+}
+
 // ------------------------------------------------------------------ host --
 namespace {
 // halo position offset of a tap inside the 1 x 8 x 16 tile's halo
@@ -375,6 +615,26 @@ hipError_t conv3d_wgrad_x(const Src2& x, const float* dy, int lddy, float* dw, V
                      lddy, ws, vol, Cin, p.kpad, Cout, p.npad, p.tilesH, p.tilesW, p.ntiles,   \
                      p.tps, tb)
   const bool x3 = math == SPFF_MATH_BF16X3;
+  if (SPFF_WX16) {
+    // 16-row blocks: nblk = ceil(T CI / 16); NJMAX = ceil(nblk / 4):
+    // KD3/CI16 27 -> 7, KD3/CI8 14 -> 4, KD1/CI16 9 -> 3, KD1/CI8 5 -> 2
+    const int nblk = cdiv(KD * 9 * p.ci, 16);
+#define SPFF_WX16(KD_, CI_, NS_, NJ_)                                                          \
+  hipLaunchKernelGGL((k_conv3d_wgrad_x16<KD_, CI_, NS_, NJ_>), grid, dim3(256), 0, s, x, dy,   \
+                     lddy, ws, vol, Cin, p.kpad, Cout, p.npad, p.tilesH, p.tilesW, p.ntiles,   \
+                     p.tps, nblk)
+    if (KD == 3) {
+      if (p.ci == 16) { if (x3) SPFF_WX16(3, 16, 2, 7); else SPFF_WX16(3, 16, 3, 7); }
+      else            { if (x3) SPFF_WX16(3, 8, 2, 4);  else SPFF_WX16(3, 8, 3, 4); }
+    } else {
+      if (p.ci == 16) { if (x3) SPFF_WX16(1, 16, 2, 3); else SPFF_WX16(1, 16, 3, 3); }
+      else            { if (x3) SPFF_WX16(1, 8, 2, 2);  else SPFF_WX16(1, 8, 3, 2); }
+    }
+#undef SPFF_WX16
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return conv3d_wgrad_reduce(ws, dw, p.nsplit, KD * 9, p.kpad, p.npad, Cin, Cout, s);
+  }
   // NJMAX = ceil(nblk / 4): KD3/CI16 14 blocks -> 4, KD3/CI8 7 -> 2, KD1/CI16 5 -> 2, KD1/CI8 3 -> 1
   if (KD == 3) {
     if (p.ci == 16) { if (x3) SPFF_WX(3, 16, 2, 4); else SPFF_WX(3, 16, 3, 4); }
