@@ -316,7 +316,8 @@ __global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x16(
   constexpr int NPOS = HD * HH * HWD;
   constexpr int T = KD * 9;
   constexpr int CQ = CI / 4;                              // float4 per halo position
-  constexpr int NH = (NPOS * CQ + 255) / 256;              // halo float4 per thread
+  constexpr int PPOS = HH * HWD;                           // positions per depth plane
+  constexpr int NP = (PPOS * CQ + 255) / 256;              // plane float4 per thread
   constexpr int NY = WX_TV * (WX_CO / 4) / 256;            // dy float4 per thread (= 4)
   constexpr int NCB = WX_CO / 16;                          // 16-wide col blocks (2)
   __shared__ __attribute__((aligned(16))) unsigned short Xs[NS * NPOS * CI];
@@ -364,30 +365,34 @@ __global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x16(
 #pragma unroll
       for (int r = 0; r < 4; ++r) acc[j][cb][r] = 0.f;
 
-  float4 hreg[NH], yreg[NY];
+  // Rolling depth-plane halo: tiles run depth-fastest, so tile d0 + 1 of the same
+  // (b, h, w) column needs only ONE new plane (gd = d0 + 1 + KD / 2) beside the KD - 1
+  // it shares with tile d0.  Plane gd lives in slot (gd + 3) % KD of the halo image; the
+  // register pipeline carries one plane (+ dy) per tile, and a column's first tile
+  // stages its other KD - 1 planes synchronously.
+  float4 hreg[NP], yreg[NY];
   float4 xal = make_float4(1.f, 1.f, 1.f, 1.f), xde = make_float4(0.f, 0.f, 0.f, 0.f);
-  auto fetch = [&](int tile) {
+  struct TileXY { int d0, b, h0, w0; };
+  auto tile_xy = [&](int tile) {
+    TileXY r;
     int t = tile;
-    const int d0 = t % D; t /= D;
+    r.d0 = t % D; t /= D;
     const int twi = t % tilesW; t /= tilesW;
     const int thi = t % tilesH;
-    const int b = t / tilesH;
-    const int h0 = thi * WX_TH, w0 = twi * WX_TW;
-    if (x.al) {
-      const int c = ci_base + 4 * (tid % CQ);
-      if (c < Cin) {
-        xal = *reinterpret_cast<const float4*>(x.al + (int64_t)b * x.ld0 + c);
-        xde = *reinterpret_cast<const float4*>(x.de + (int64_t)b * x.ld0 + c);
-      }
-    }
+    r.b = t / tilesH;
+    r.h0 = thi * WX_TH;
+    r.w0 = twi * WX_TW;
+    return r;
+  };
+  auto load_plane = [&](const TileXY& tx, int gd, float4 (&r)[NP]) {
 #pragma unroll
-    for (int k = 0; k < NH; ++k) {
+    for (int k = 0; k < NP; ++k) {
       const int i = tid + 256 * k;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (i < NPOS * CQ) {
+      if (i < PPOS * CQ) {
         const int c4 = i % CQ, pos = i / CQ;
-        const int hw = pos % HWD, t2 = pos / HWD, hh = t2 % HH, hd = t2 / HH;
-        const int gd = d0 + hd - KD / 2, gh = h0 + hh - 1, gw = w0 + hw - 1;
+        const int hw = pos % HWD, hh = pos / HWD;
+        const int b = tx.b, gh = tx.h0 + hh - 1, gw = tx.w0 + hw - 1;
         const int c = ci_base + 4 * c4;
         if ((unsigned)(gd + vol.dh) < (unsigned)(D + 2 * vol.dh) && (unsigned)gh < (unsigned)H &&
             (unsigned)gw < (unsigned)W && c < Cin && !((gd < 0 && x.zlo) || (gd >= D && x.zhi))) {
@@ -403,8 +408,34 @@ __global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x16(
           }
         }
       }
-      hreg[k] = v;
+      r[k] = v;
     }
+  };
+  auto store_plane = [&](int gd, const float4 (&r)[NP]) {
+    unsigned short* dst = Xs + ((gd + 3) % KD) * PPOS * CI;
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+      const int i = tid + 256 * k;
+      if (i < PPOS * CQ) {
+        uint2 o[NS];
+        split4<NS>(r[k], o);
+#pragma unroll
+        for (int p = 0; p < NS; ++p)
+          *reinterpret_cast<uint2*>(dst + p * NPOS * CI + 4 * i) = o[p];
+      }
+    }
+  };
+  auto fetch = [&](int tile) {
+    const TileXY tx = tile_xy(tile);
+    if (x.al) {
+      const int c = ci_base + 4 * (tid % CQ);
+      if (c < Cin) {
+        xal = *reinterpret_cast<const float4*>(x.al + (int64_t)tx.b * x.ld0 + c);
+        xde = *reinterpret_cast<const float4*>(x.de + (int64_t)tx.b * x.ld0 + c);
+      }
+    }
+    load_plane(tx, tx.d0 + KD / 2, hreg);
+    const int b = tx.b, d0 = tx.d0, h0 = tx.h0, w0 = tx.w0;
 #pragma unroll
     for (int k = 0; k < NY; ++k) {
       const int i = tid + 256 * k;
@@ -419,18 +450,8 @@ __global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x16(
       yreg[k] = v;
     }
   };
-  auto stash = [&](bool negate) {
-#pragma unroll
-    for (int k = 0; k < NH; ++k) {
-      const int i = tid + 256 * k;
-      if (i < NPOS * CQ) {
-        uint2 o[NS];
-        split4<NS>(hreg[k], o);
-#pragma unroll
-        for (int p = 0; p < NS; ++p)
-          *reinterpret_cast<uint2*>(Xs + p * NPOS * CI + 4 * i) = o[p];
-      }
-    }
+  auto stash = [&](int d0, bool negate) {
+    store_plane(d0 + KD / 2, hreg);
 #pragma unroll
     for (int k = 0; k < NY; ++k) {
       const int i = tid + 256 * k;
@@ -446,8 +467,16 @@ __global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x16(
     }
   };
 
-  auto compute = [&](auto NJc) {
+  auto compute = [&](auto NJc, int d0) {
     constexpr int NJ = decltype(NJc)::value;
+    // aoff[j] addresses plane kd as slot kd; tap kd reads gd = d0 + kd - KD / 2, in slot
+    // (kd + rot) % KD with rot = (d0 - KD / 2 + 3) % KD
+    constexpr int PL = PPOS * CI;
+    const int rot = (d0 - KD / 2 + 3) % KD;
+    int ab[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+      ab[j] = aoff[j] + (aoff[j] >= (KD - rot) * PL ? (rot - KD) * PL : rot * PL);
 #pragma unroll 2
     for (int ks = 0; ks < WX_TH / 2; ++ks) {
       bf16x8 bq[NCB][NS];
@@ -463,7 +492,7 @@ __global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x16(
         bf16x8 aq[NS];
 #pragma unroll
         for (int p = 0; p < NS; ++p) {
-          const unsigned short* xb = Xs + p * NPOS * CI + 2 * ks * HWD * CI + aoff[j];
+          const unsigned short* xb = Xs + p * NPOS * CI + 2 * ks * HWD * CI + ab[j];
           aq[p] = frag(tr_read(xb), tr_read(xb + 8 * CI));
         }
 #pragma unroll
@@ -497,11 +526,22 @@ __global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x16(
         for (int cb = 0; cb < NCB; ++cb) acc[j][cb] = -acc[j][cb];
     }
     __syncthreads();  // previous compute done reading LDS
-    stash(((tile - tbeg) & 1) != 0);
+    const int d0 = tile % D;
+    if (KD > 1 && (tile == tbeg || d0 == 0)) {
+      // first tile of a column: its other planes d0 - KD / 2 .. d0 + KD / 2 - 1
+      const TileXY tx = tile_xy(tile);
+#pragma unroll
+      for (int hd = 0; hd < KD - 1; ++hd) {
+        float4 r[NP];
+        load_plane(tx, d0 + hd - KD / 2, r);
+        store_plane(d0 + hd - KD / 2, r);
+      }
+    }
+    stash(d0, ((tile - tbeg) & 1) != 0);
     __syncthreads();
     if (tile + 1 < tend) fetch(tile + 1);
-    if (nj == NJMAX) compute(std::integral_constant<int, NJMAX>{});
-    else if constexpr (NJMAX > 1) compute(std::integral_constant<int, NJMAX - 1>{});
+    if (nj == NJMAX) compute(std::integral_constant<int, NJMAX>{}, d0);
+    else if constexpr (NJMAX > 1) compute(std::integral_constant<int, NJMAX - 1>{}, d0);
   }
 
   if (tend > tbeg && ((tend - 1 - tbeg) & 1)) {

@@ -49,6 +49,9 @@
 #ifndef SPFF_XCDMAP
 #define SPFF_XCDMAP 1  // 0: tile-fastest block order (A/B diagnostics)
 #endif
+#ifndef SPFF_X32T
+#define SPFF_X32T 1  // 1: 32-wide tiles are 4 x 16 x 16 voxels (MB 4), 0: 2 x 16 x 16 (MB 2)
+#endif
 #ifndef SPFF_X16
 #define SPFF_X16 1  // 1: v_mfma_f32_16x16x32_bf16 tap-quad schedule, 0: 32x32x16 tap pairs
 #endif
@@ -131,19 +134,23 @@ __global__ void k_conv_pack_x(const float* __restrict__ w, uint4* __restrict__ w
 // ------------------------------------------------------------ fwd / dgrad --
 namespace {
 constexpr int XT_D = 2, XT_H = 16, XT_W = 16, XT_THREADS = 512;
-// NW waves x MB 32-row blocks per wave: tile 2 x (NW MB) x 16 voxels
-template <int KD, int TH>
+// NW waves x MB 32-row blocks per wave: tile TD x TH x 16 voxels with TD TH = 2 NW MB
+// (TD = 2 except the 32-wide 16x16x32 tiles, SPFF_X32T: 4 x 16 x 16)
+template <int KD, int TD, int TH>
 __host__ __device__ constexpr int xt_npos() {
-  return (XT_D + KD - 1) * (TH + 2) * (XT_W + 2);
+  return (TD + KD - 1) * (TH + 2) * (XT_W + 2);
 }
 template <int KD>
 __host__ __device__ constexpr int xt_t2() {
   return (KD * 9 + 1) & ~1;
 }
-template <int BN, int KD, int NS, int TH>
+template <int BN, int KD, int NS, int TD, int TH>
 constexpr size_t xt_lds_bytes() {
-  return (size_t)NS * (xt_npos<KD, TH>() + xt_t2<KD>() * BN) * 16;
+  return (size_t)NS * (xt_npos<KD, TD, TH>() + xt_t2<KD>() * BN) * 16;
 }
+// tile depth of a BN-wide launch (host side: launches, fused-statistics layout)
+constexpr int xt_td(int BN) { return (BN == 32 && SPFF_X16 && SPFF_X32T) ? 4 : XT_D; }
+constexpr int xt_mb(int BN) { return (BN == 32 && SPFF_X16 && SPFF_X32T) ? 4 : 2; }
 }  // namespace
 
 // 16x16x32 tap-quad schedule (X16): k = 4 lane groups x 8 channels, lane group g
@@ -191,15 +198,16 @@ __device__ __forceinline__ int x16_w(int r) {
   return (r >= 4 && r < 12) ? 2 * (r - 4) : (r < 4 ? 2 * r + 1 : 2 * r - 15);
 }
 
-template <int BN, int KD, int NS, int MB, int NW, bool X16>
+template <int BN, int KD, int NS, int MB, int NW, bool X16, int TD>
 __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
     Src2 x, const uint4* __restrict__ wp, Dst2 y, Vol vol, int Cin, int nkc, int Cout, int npad,
     int tilesD, int tilesH, int tilesW, float* __restrict__ part, int kps,
     float* __restrict__ stats, int ntiles) {
   constexpr int XT_THREADS = NW * 64;
-  constexpr int TD = XT_D, TH = NW * MB, TW = XT_W;
+  constexpr int TH = X16 ? 2 * NW * MB / TD : NW * MB, TW = XT_W;
+  static_assert(X16 || TD == 2, "32x32x16 schedule: 2-deep tiles");
   constexpr int HH = TH + 2, HWD = TW + 2;
-  constexpr int NPOS = xt_npos<KD, TH>();
+  constexpr int NPOS = xt_npos<KD, TD, TH>();
   constexpr int T = KD * 9, T2 = xt_t2<KD>();
   // MFMA blocking: 32x32x16 -- MB 32-row blocks x BN/32 col blocks per wave, a k-step
   // per tap pair; 16x16x32 -- 2 MB 16-row blocks x BN/16, a k-step per tap quad
@@ -405,33 +413,42 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
         const int sa = 4 * j + (kg & 2);
         const int toff = s01 ? toff_of(QT.src[sa + 1]) : toff_of(QT.src[sa]);
         const int wtap = s01 ? QT.tap[sa + 1] : QT.tap[sa];
-        bf16x8 a[RB][NS], bm[CB][NS];
+        // row blocks in groups of RBH (the 4 x 16 x 16 tiles' 8 row blocks: two groups,
+        // so only half of the A fragments are live at a time)
+        constexpr int RBH = RB > 4 ? 4 : RB;
+        bf16x8 bm[CB][NS];
 #pragma unroll
-        for (int p = 0; p < NS; ++p) {
-#pragma unroll
-          for (int rb = 0; rb < RB; ++rb)
-            a[rb][p] = __builtin_bit_cast(bf16x8, Xs[p * NPOS + hpos[rb] + toff]);
+        for (int p = 0; p < NS; ++p)
 #pragma unroll
           for (int cb = 0; cb < CB; ++cb)
             bm[cb][p] = __builtin_bit_cast(bf16x8, Ws[(p * T2 + wtap) * BN + cb * 16 + l16]);
-        }
 #pragma unroll
-        for (int rb = 0; rb < RB; ++rb)
+        for (int rg = 0; rg < RB; rg += RBH) {
+        bf16x8 a[RBH][NS];
+#pragma unroll
+        for (int p = 0; p < NS; ++p)
+#pragma unroll
+          for (int rh = 0; rh < RBH; ++rh)
+            a[rh][p] = __builtin_bit_cast(bf16x8, Xs[p * NPOS + hpos[rg + rh] + toff]);
+#pragma unroll
+        for (int rh = 0; rh < RBH; ++rh)
 #pragma unroll
           for (int cb = 0; cb < CB; ++cb) {
+            const int rb = rg + rh;
             f32x4 c = acc[rb][cb];
             if constexpr (NS == 3) {
-              c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb][1], bm[cb][1], c, 0, 0, 0);
-              c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb][0], bm[cb][2], c, 0, 0, 0);
-              c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb][2], bm[cb][0], c, 0, 0, 0);
+              c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rh][1], bm[cb][1], c, 0, 0, 0);
+              c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rh][0], bm[cb][2], c, 0, 0, 0);
+              c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rh][2], bm[cb][0], c, 0, 0, 0);
             }
             if constexpr (NS >= 2) {
-              c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb][0], bm[cb][1], c, 0, 0, 0);
-              c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb][1], bm[cb][0], c, 0, 0, 0);
+              c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rh][0], bm[cb][1], c, 0, 0, 0);
+              c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rh][1], bm[cb][0], c, 0, 0, 0);
             }
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb][0], bm[cb][0], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rh][0], bm[cb][0], c, 0, 0, 0);
             acc[rb][cb] = c;
           }
+        }
       } else {
         // lane half h takes tap 2j+h; the padding tap (>= T) reads a valid
         // position against a zero weight row
@@ -649,14 +666,16 @@ __global__ void k_splitk_reduce(const float* __restrict__ part, int nsplit, int6
   }
 }
 
-template <int BN, int KD, int NS, int MB, int NW = 8>
+template <int BN, int KD, int NS, int MB = xt_mb(BN), int NW = 8, int TD = xt_td(BN)>
 static hipError_t launch_fwd_x(const Src2& x, const uint4* wx, const Dst2& y, Vol vol, int K,
                                int nkc, int N, int npad, hipStream_t s, float* part = nullptr,
                                int nsplit = 1, int kps = 0, float* stats = nullptr) {
-  constexpr size_t shm = xt_lds_bytes<BN, KD, NS, NW * MB>();
+  constexpr int TH = SPFF_X16 ? 2 * NW * MB / TD : NW * MB;
+  static_assert(NW == 8 || TD == XT_D, "xt_ntiles assumes 8 waves for other tile depths");
+  constexpr size_t shm = xt_lds_bytes<BN, KD, NS, TD, TH>();
   static_assert(shm <= (NW == 8 ? 160 : 80) * 1024, "LDS budget");
   if (x.al && BN != 32) return hipErrorInvalidValue;  // fused activation: 32-wide tiles only
-  auto kern = k_conv3d_fwd_x<BN, KD, NS, MB, NW, SPFF_X16 != 0>;
+  auto kern = k_conv3d_fwd_x<BN, KD, NS, MB, NW, SPFF_X16 != 0, TD>;
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
@@ -664,7 +683,7 @@ static hipError_t launch_fwd_x(const Src2& x, const uint4* wx, const Dst2& y, Vo
     if (e != hipSuccess) return e;
     attr = true;
   }
-  const int tilesD = cdiv(vol.D, XT_D), tilesH = cdiv(vol.H, NW * MB), tilesW = cdiv(vol.W, XT_W);
+  const int tilesD = cdiv(vol.D, TD), tilesH = cdiv(vol.H, TH), tilesW = cdiv(vol.W, XT_W);
   const int ntiles = vol.B * tilesD * tilesH * tilesW;
   dim3 grid(8 * cdiv(ntiles, 8) * (npad / BN), 1, part ? nsplit : 1);
   hipLaunchKernelGGL(kern, grid, dim3(NW * 64), shm, s, x, wx, y, vol, K, nkc, N, npad, tilesD,
@@ -716,6 +735,11 @@ bool debug_split_wgrad() { return (debug_split_dir() & 4) != 0; }
 bool conv3d_fuses_act(int math, int C) {
   return math != SPFF_MATH_F32 && debug_split_dir() == 7 && C == 32;
 }
+// tiles of a BN-wide launch (the fused IN statistics are per (tile, out channel))
+static int64_t xt_ntiles(Vol vol, int BN) {
+  const int td = xt_td(BN), th = SPFF_X16 ? 2 * 8 * xt_mb(BN) / td : 8 * xt_mb(BN);
+  return (int64_t)vol.B * cdiv(vol.D, td) * cdiv(vol.H, th) * cdiv(vol.W, XT_W);
+}
 namespace {
 // split-K for launches that would not fill the chip (the deep levels of the
 // 3DUNet: 2 x 12 x 12 and 1 x 6 x 6 voxels with 256-512 channels): the input
@@ -726,8 +750,7 @@ struct SplitK {
 SplitK splitk_plan(Vol vol, const XDims& d) {
   SplitK k;
   k.kps = d.nkc;
-  const int64_t wgs = (int64_t)vol.B * cdiv(vol.D, XT_D) * cdiv(vol.H, XT_H) * cdiv(vol.W, XT_W) *
-                      (d.npad / d.BN);
+  const int64_t wgs = xt_ntiles(vol, d.BN) * (d.npad / d.BN);
   if (wgs >= 256 || d.nkc < 4) return k;
   int ns = (int)std::min<int64_t>(d.nkc / 2, (512 + wgs - 1) / wgs);
   ns = std::max(1, ns);
@@ -770,19 +793,19 @@ hipError_t conv3d_pack(const float* w, void* wpack, Vol vol, int KD, int Cin_w, 
 template <int NS>
 static hipError_t run_x(const Src2& x, const uint4* wu, const Dst2& y, Vol vol, int KD,
                         const XDims& d, hipStream_t s, float* ws, float* stats) {
-  // (MB = 4, 1024-voxel tiles for Cout <= 32, fits LDS but spills 91 VGPRs at NS = 3)
+  // (32x32x16, MB = 4, 2 x 32 x 16 tiles for Cout <= 32: fits LDS but spills 91 VGPRs)
   // (NW = 4 waves, 2 x 8 x 16 tiles, BN 32, two workgroups per CU: measured 6 % slower)
   SplitK k = ws ? splitk_plan(vol, d) : SplitK{1, d.nkc};
   float* part = k.nsplit > 1 ? ws : nullptr;
   if (d.BN == 64)
     return KD == 3
-               ? launch_fwd_x<64, 3, NS, 2>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s, part,
+               ? launch_fwd_x<64, 3, NS>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s, part,
                                                 k.nsplit, k.kps, stats)
-               : launch_fwd_x<64, 1, NS, 2>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s, part,
+               : launch_fwd_x<64, 1, NS>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s, part,
                                                 k.nsplit, k.kps, stats);
-  return KD == 3 ? launch_fwd_x<32, 3, NS, 2>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s,
+  return KD == 3 ? launch_fwd_x<32, 3, NS>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s,
                                                   part, k.nsplit, k.kps, stats)
-                 : launch_fwd_x<32, 1, NS, 2>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s,
+                 : launch_fwd_x<32, 1, NS>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s,
                                                   part, k.nsplit, k.kps, stats);
 }
 
@@ -797,13 +820,9 @@ size_t conv3d_splitk_bytes(Vol vol, int KD, int Cin, int Cout) {
   return b;
 }
 
-// fused IN statistics: per (tile, out channel) {sum, M2} + a count per tile
-static int64_t xt_ntiles(Vol vol) {
-  return (int64_t)vol.B * cdiv(vol.D, XT_D) * cdiv(vol.H, XT_H) * cdiv(vol.W, XT_W);
-}
 size_t conv3d_stats_bytes(Vol vol, int KD, int Cin, int Cout) {
   const XDims d = xdims(KD, Cin, Cout, false);
-  return (size_t)xt_ntiles(vol) * (2 * d.npad + 1) * sizeof(float);
+  return (size_t)xt_ntiles(vol, d.BN) * (2 * d.npad + 1) * sizeof(float);
 }
 bool conv3d_fuses_stats(Vol vol, int KD, int Cin, int Cout, int math) {
   const XDims d = xdims(KD, Cin, Cout, false);
@@ -813,7 +832,7 @@ hipError_t conv3d_in_stats_fin(const float* stats, Vol vol, int KD, int Cin, int
                                const float* gamma, const float* beta, float* mean, float* rstd,
                                float* al, float* de, hipStream_t s) {
   const XDims d = xdims(KD, Cin, Cout, false);
-  const int64_t nt = xt_ntiles(vol);
+  const int64_t nt = xt_ntiles(vol, d.BN);
   hipLaunchKernelGGL(k_in_stats_fin, dim3(vol.B * Cout), dim3(256), 0, s, stats, (int)nt,
                      (int)(nt / vol.B), d.npad, Cout, gamma, beta, mean, rstd, al, de);
   return hipGetLastError();
