@@ -616,7 +616,7 @@ int upconv_out(spff_plan* p, const UpL& U, const float* in) {
   const Vol& low = p->vol[U.lvl_low];
   PROF(p, 3, 2.0 * nvox(low) * U.Cin * 4.0 * U.Cout,
        upconv_fwd(in, p->F(U.pk), p->P(U.b), p->F(U.rs ? U.raw : U.out), low, U.Cin, U.Cout,
-                  p->st));
+                  p->st, 4, p->cfg.math));
   if (U.rs) {
     const Vol& vh = p->vol[U.lvl_low - 1];
     Vol vr = low;
@@ -785,7 +785,7 @@ int forward(spff_plan* p, const float* x, float* logits) {
   float* hp = p->F(p->head_pk);
   HIPCK(head_pack(p->P(p->out_w), hp, hp + head_pack_dgrad_offset(f, p->K), f, p->K, p->st));
   PROF(p, 3, 2.0 * nvox(p->vol[0]) * f * p->K,
-       head_fwd(prev, hp, p->P(p->out_b), logits, nvox(p->vol[0]), f, p->K, p->st));
+       head_fwd(prev, hp, p->P(p->out_b), logits, nvox(p->vol[0]), f, p->K, p->st, p->cfg.math));
   return SPFF_OK;
 }
 
@@ -800,7 +800,7 @@ int backward(spff_plan* p, const float* dl) {
   CK(grad_ready(p, p->out_w, p->out_b + p->K));
   PROF(p, 3, 2.0 * V0 * f * p->K,
        head_dgrad(dl, hp + head_pack_dgrad_offset(f, p->K), p->F(p->G_out), V0, f, p->K,
-                  p->st));
+                  p->st, p->cfg.math));
   // decoder: dec1 (B[6]) <- up1 (up[2]) <- dec2 ... ; skip grads go to dskip[l]
   for (int k = 0; k < 3; ++k) {
     const int bi = 6 - k;          // dec1, dec2, dec3
@@ -831,7 +831,7 @@ int backward(spff_plan* p, const float* dl) {
     float* pk = p->F(U.pk);
     PROF(p, 3, 2.0 * nvox(low) * U.Cin * 4.0 * U.Cout,
          upconv_dgrad(gup, C, pk + upconv_pack_dgrad_offset(U.Cin, U.Cout),
-                      p->F(p->G_out), low, U.Cin, U.Cout, p->st));
+                      p->F(p->G_out), low, U.Cin, U.Cout, p->st, 4, p->cfg.math));
   }
   // bottleneck + encoder
   {

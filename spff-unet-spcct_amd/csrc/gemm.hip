@@ -13,6 +13,26 @@ namespace spff {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+// SPFF_GEMM_SPLIT=0 (A/B diagnostics): the fp32 MFMA GEMMs for every math
+#ifndef SPFF_GEMM_SPLIT
+#define SPFF_GEMM_SPLIT 1
+#endif
+__host__ __device__ inline int64_t cdiv64d(int64_t a, int64_t b) { return (a + b - 1) / b; }
+static int num_cus() {
+  static int n = [] {
+    int dev = 0, c = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 256;
+    return c > 0 ? c : 256;
+  }();
+  return n;
+}
+// SPFF_GEMM_PERSIST=0 (A/B diagnostics): one row tile per workgroup
+#ifndef SPFF_GEMM_PERSIST
+#define SPFF_GEMM_PERSIST 1
+#endif
+static inline bool gemm_split(int math) { return SPFF_GEMM_SPLIT && math == SPFF_MATH_BF16X6; }
 static inline int64_t cdiv64(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 // ------------------------------------------------------------- functors --
@@ -261,12 +281,224 @@ __global__ __launch_bounds__(256, 2) void k_gemm(AL A, const float* __restrict__
   }
 }
 
+// ------------------------------------------------- C = A.B, split bf16 --
+// The same tile (128 rows x BN cols, K in chunks of 32, 4 waves x 32 rows) on
+// v_mfma_f32_16x16x32_bf16 with the exact 3-plane bf16 split of both operands and
+// the 6 leading cross products (conv3d_x.hip): ~2.7x fewer MFMA
+// cycles than the fp32 MFMA, which bound the up-conv GEMMs (K = 64..128).
+// A is split as it is staged, row-major per plane (16-B k-chunk XOR (row bit 3)<<1:
+// conflict-free ds_read_b128 A fragments); B (the fp32 packed weight) likewise,
+// k-major per plane with 32-B column units XOR-swizzled by k so that the
+// ds_read_b64_tr_b16 B fragments (4 k-rows x 16 cols per 16 lanes) are conflict-free.
+// Sign alternation: odd chunks stage -B and the accumulator is negated at every
+// chunk boundary (the bf16 MFMA's rounding then cancels across chunks).
+typedef float f32x4g __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8g __attribute__((ext_vector_type(8)));
+typedef short i16x4g __attribute__((ext_vector_type(4)));
+typedef short i16x8g __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) i16x4g lds_i16x4g;
+__device__ __forceinline__ void gsplit4(float4 v, uint2 (&o)[3]) {
+  float r[4] = {v.x, v.y, v.z, v.w};
+  unsigned short h[4][3];
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      const __bf16 b = (__bf16)r[e];
+      h[e][p] = __builtin_bit_cast(unsigned short, b);
+      r[e] -= (float)b;
+    }
+#pragma unroll
+  for (int p = 0; p < 3; ++p) {
+    o[p].x = (unsigned)h[0][p] | ((unsigned)h[1][p] << 16);
+    o[p].y = (unsigned)h[2][p] | ((unsigned)h[3][p] << 16);
+  }
+}
+// 32-B column-unit swizzle of B row k (BN / 16 units per row, 128 / BN rows per 256 B)
+template <int BN>
+__device__ __forceinline__ int gx_bsw(int k) {
+  constexpr int L = BN == 128 ? 0 : BN == 64 ? 1 : 2;
+  return ((k & 3) >> L) | (((k >> 3) & 1) << (2 - L));
+}
+template <class AL, class CS, int BN>
+__global__ __launch_bounds__(256, 2) void k_gemm_x(AL A, const float* __restrict__ B, CS C,
+                                                   int kpad, int npad) {
+  constexpr int CB = BN / 16, NRB = BN / 32;  // 16-wide col blocks; B float4 per thread
+  constexpr int APL = G_BM * G_BK, BPL = G_BK * BN;  // bf16 per plane
+  __shared__ __attribute__((aligned(16))) unsigned short As[3 * APL];
+  __shared__ __attribute__((aligned(16))) unsigned short Bs[3 * BPL];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, l16 = lane & 15;
+  // persistent over row tiles blockIdx.x, + gridDim.x, ...: the next tile's first
+  // chunk is fetched during the current tile's last MFMAs and its epilogue, so HBM
+  // reads stay in flight across tiles (K = 32..128 is only 1-4 chunks per tile)
+  const int64_t ntl = cdiv64d(A.M, G_BM);
+  int64_t tl = blockIdx.x;
+  if (tl >= ntl) return;
+  const int n0 = blockIdx.y * BN;
+  const int nkc = kpad / G_BK;
+  const int aq = tid & 7, arow = tid >> 3;
+  f32x4g acc[2][CB];
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+    for (int cb = 0; cb < CB; ++cb) acc[rb][cb] = f32x4g{0.f, 0.f, 0.f, 0.f};
+  float4 ra[4], rb[NRB];
+  int64_t ah[4];
+  auto prep_rows = [&](int64_t t) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) ah[j] = A.prep(t * G_BM + arow + 32 * j);
+  };
+  prep_rows(tl);
+  auto fetch = [&](int k0) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) ra[j] = A.load4(ah[j], k0 + 4 * aq);
+#pragma unroll
+    for (int j = 0; j < NRB; ++j) {
+      const int i = tid + 256 * j, r = i / (BN / 4), c4 = i % (BN / 4);
+      rb[j] = *reinterpret_cast<const float4*>(B + (int64_t)(k0 + r) * npad + n0 + 4 * c4);
+    }
+  };
+  auto stash = [&](bool neg) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int m = arow + 32 * j;
+      uint2 o[3];
+      gsplit4(ra[j], o);
+      const int off = m * G_BK + 8 * ((aq >> 1) ^ ((m & 8) >> 2)) + 4 * (aq & 1);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) *reinterpret_cast<uint2*>(As + p * APL + off) = o[p];
+    }
+#pragma unroll
+    for (int j = 0; j < NRB; ++j) {
+      const int i = tid + 256 * j, r = i / (BN / 4), c4 = i % (BN / 4);
+      float4 v = rb[j];
+      if (neg) v = make_float4(-v.x, -v.y, -v.z, -v.w);
+      uint2 o[3];
+      gsplit4(v, o);
+      const int off = r * BN + 16 * ((c4 >> 2) ^ gx_bsw<BN>(r)) + 4 * (c4 & 3);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) *reinterpret_cast<uint2*>(Bs + p * BPL + off) = o[p];
+    }
+  };
+  // A fragment: row 16 rb + l16 of this wave's 32, k-chunk g (8 bf16 = 16 B)
+  int aoff[2];
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb) {
+    const int m = wave * 32 + rb * 16 + l16;
+    aoff[rb] = m * G_BK + 8 * (g ^ ((m & 8) >> 2));
+  }
+  // B fragment (transposed reads): lane 4q + p of k-group g addresses k-row 8 g + q
+  // (and + 4), columns 16 cb + 4 p
+  const int q = l16 >> 2, pp = l16 & 3;
+  const int kr0 = 8 * g + q, kr1 = kr0 + 4;
+  fetch(0);
+  bool first = true;
+  for (;;) {
+  const int64_t m0 = tl * G_BM;
+  const int64_t tn = tl + gridDim.x;
+  for (int kc = 0; kc < nkc; ++kc) {
+    if (kc) {
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+        for (int cb = 0; cb < CB; ++cb) acc[rb][cb] = -acc[rb][cb];
+    }
+    if (!first) __syncthreads();  // every wave is past its reads of the previous chunk
+    first = false;
+    stash(kc & 1);
+    __syncthreads();
+    {  // one fetch site: the next chunk of this tile, or the first of the next tile
+      const bool last = kc + 1 == nkc;
+      if (last && tn < ntl) prep_rows(tn);
+      if (!last || tn < ntl) fetch(last ? 0 : (kc + 1) * G_BK);
+    }
+    bf16x8g a[2][3];
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        a[rb][p] = *reinterpret_cast<const bf16x8g*>(As + p * APL + aoff[rb]);
+#pragma unroll
+    for (int cb = 0; cb < CB; ++cb) {
+      bf16x8g b[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        const unsigned short* b0 = Bs + p * BPL + kr0 * BN + 16 * (cb ^ gx_bsw<BN>(kr0)) + 4 * pp;
+        const unsigned short* b1 = Bs + p * BPL + kr1 * BN + 16 * (cb ^ gx_bsw<BN>(kr1)) + 4 * pp;
+        const i16x4g lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4g*)b0);
+        const i16x4g hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4g*)b1);
+        const i16x8g v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        b[p] = __builtin_bit_cast(bf16x8g, v);
+      }
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) {
+        f32x4g c = acc[rb][cb];
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb][1], b[1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb][0], b[2], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb][2], b[0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb][0], b[1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb][1], b[0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb][0], b[0], c, 0, 0, 0);
+        acc[rb][cb] = c;
+      }
+    }
+  }
+  const float sg = ((nkc - 1) & 1) ? -1.f : 1.f;
+  int64_t cc[CB];
+  float bv[CB];
+#pragma unroll
+  for (int cb = 0; cb < CB; ++cb) {
+    cc[cb] = C.col(n0 + cb * 16 + l16);
+    bv[cb] = C.bias_of(n0 + cb * 16 + l16);
+  }
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t rh = C.prep(m0 + wave * 32 + rb * 16 + 4 * g + r);
+      if (rh < 0) continue;
+#pragma unroll
+      for (int cb = 0; cb < CB; ++cb)
+        if (cc[cb] >= 0) C.put(rh + cc[cb], sg * acc[rb][cb][r] + bv[cb]);
+    }
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+    for (int cb = 0; cb < CB; ++cb) acc[rb][cb] = f32x4g{0.f, 0.f, 0.f, 0.f};
+  if (tn >= ntl) break;
+  tl = tn;
+  }
+}
+
+// persistent row tiles: as many workgroups as fit the chip at once
+template <int BN, class AL, class CS>
+static void launch_gemm_x(const AL& A, const float* B, const CS& C, dim3 grid, int kpad, int npad,
+                          hipStream_t s) {
+  auto kern = k_gemm_x<AL, CS, BN>;
+  static int per_cu = 0;
+  if (!per_cu &&
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0) != hipSuccess)
+    per_cu = 2;
+  per_cu = std::max(per_cu, 1);
+  const int64_t cap = std::max<int64_t>(1, (int64_t)per_cu * num_cus() / std::max(1, (int)grid.y));
+  const dim3 gx((unsigned)(SPFF_GEMM_PERSIST ? std::min<int64_t>(grid.x, cap) : grid.x), grid.y);
+  hipLaunchKernelGGL(kern, gx, dim3(256), 0, s, A, B, C, kpad, npad);
+}
+
+// split = true: k_gemm_x (split bf16, SPFF_MATH_BF16X6); false: fp32 MFMA k_gemm
 template <class AL, class CS>
 static hipError_t launch_gemm(const AL& A, const float* B, const CS& C, int64_t M, int kpad,
-                              int npad, hipStream_t s) {
+                              int npad, hipStream_t s, bool split = false) {
   if (kpad % G_BK || npad % 32 || M >= (int64_t(1) << 31)) return hipErrorInvalidValue;
   const int BN = npad % 128 == 0 ? 128 : npad % 64 == 0 ? 64 : 32;
   dim3 grid((unsigned)cdiv64(M, G_BM), npad / BN);
+  if (split) {
+    if (BN == 128) launch_gemm_x<128>(A, B, C, grid, kpad, npad, s);
+    else if (BN == 64) launch_gemm_x<64>(A, B, C, grid, kpad, npad, s);
+    else launch_gemm_x<32>(A, B, C, grid, kpad, npad, s);
+    return hipGetLastError();
+  }
   if (BN == 128)
     hipLaunchKernelGGL((k_gemm<AL, CS, 128>), grid, dim3(256), 0, s, A, B, C, kpad, npad);
   else if (BN == 64)
@@ -631,19 +863,19 @@ hipError_t upconv_pack(const float* w, float* wf, float* wd, int Cin, int Cout, 
 }
 
 hipError_t upconv_fwd(const float* x, const float* wf, const float* bias, float* y, Vol low,
-                      int Cin, int Cout, hipStream_t s, int ns) {
+                      int Cin, int Cout, hipStream_t s, int ns, int math) {
   const int64_t M = nvox(low);
   LoadRowsVec A{x, Cin, Cin, M};
   StoreUp C{y, Cout, bias, low.D, low.H, low.W, M, ns};
-  return launch_gemm(A, wf, C, M, up_f_kpad(Cin), up_f_npad(Cout, ns), s);
+  return launch_gemm(A, wf, C, M, up_f_kpad(Cin), up_f_npad(Cout, ns), s, gemm_split(math));
 }
 
 hipError_t upconv_dgrad(const float* dy, int lddy, const float* wd, float* dx, Vol low, int Cin,
-                        int Cout, hipStream_t s, int ns) {
+                        int Cout, hipStream_t s, int ns, int math) {
   const int64_t M = nvox(low);
   LoadUpGather A{dy, lddy, Cout, low.D, low.H, low.W, M, ns};
   StoreRows C{dx, Cin, Cin, nullptr, M};
-  return launch_gemm(A, wd, C, M, up_d_kpad(Cout, ns), up_d_npad(Cin), s);
+  return launch_gemm(A, wd, C, M, up_d_kpad(Cout, ns), up_d_npad(Cin), s, gemm_split(math));
 }
 
 size_t upconv_wgrad_ws_bytes(Vol low, int Cin, int Cout, int ns) {
@@ -684,10 +916,10 @@ static inline int head_dk(int K) { return cdiv(K, G_BK) * G_BK; }
 static inline int head_dn(int Cin) { return cdiv(Cin, 32) * 32; }
 
 hipError_t head_fwd(const float* x, const float* wf, const float* b, float* y, int64_t V, int Cin,
-                    int K, hipStream_t s) {
+                    int K, hipStream_t s, int math) {
   LoadRowsVec A{x, Cin, Cin, V};
   StoreRows C{y, K, K, b, V};
-  return launch_gemm(A, wf, C, V, head_fk(Cin), head_fn(K), s);
+  return launch_gemm(A, wf, C, V, head_fk(Cin), head_fn(K), s, gemm_split(math));
 }
 
 hipError_t head_pack(const float* w, float* wf, float* wd, int Cin, int K, hipStream_t s) {
@@ -710,10 +942,10 @@ size_t upconv_pack_dgrad_offset(int Cin, int Cout, int ns) {
 }
 
 hipError_t head_dgrad(const float* dy, const float* wd, float* dx, int64_t V, int Cin, int K,
-                      hipStream_t s) {
+                      hipStream_t s, int math) {
   LoadRowsScalar A{dy, K, K, V};
   StoreRows C{dx, Cin, Cin, nullptr, V};
-  return launch_gemm(A, wd, C, V, head_dk(K), head_dn(Cin), s);
+  return launch_gemm(A, wd, C, V, head_dk(K), head_dn(Cin), s, gemm_split(math));
 }
 
 size_t head_wgrad_ws_bytes(int64_t V, int Cin, int K) { return xty_ws_bytes(V, Cin, K); }

@@ -97,10 +97,12 @@ hipError_t conv3d_wgrad_reduce(const float* part, float* dw, int nsplit, int T, 
 // ns = 8).  Reference weight W[Cin][Cout][1 or 2][2][2].
 hipError_t upconv_pack(const float* w, float* wf, float* wd, int Cin, int Cout, hipStream_t s,
                        int ns = 4);
+// (math = SPFF_MATH_BF16X6: the split-bf16 MFMA GEMM; otherwise the fp32 MFMA one)
 hipError_t upconv_fwd(const float* x, const float* wf, const float* bias, float* y,
-                      Vol low, int Cin, int Cout, hipStream_t s, int ns = 4);
+                      Vol low, int Cin, int Cout, hipStream_t s, int ns = 4,
+                      int math = SPFF_MATH_F32);
 hipError_t upconv_dgrad(const float* dy, int lddy, const float* wd, float* dx, Vol low,
-                        int Cin, int Cout, hipStream_t s, int ns = 4);
+                        int Cin, int Cout, hipStream_t s, int ns = 4, int math = SPFF_MATH_F32);
 size_t upconv_wgrad_ws_bytes(Vol low, int Cin, int Cout, int ns = 4);
 hipError_t upconv_wgrad(const float* x, const float* dy, int lddy, float* dw, float* db,
                         Vol low, int Cin, int Cout, float* ws, hipStream_t s, int ns = 4);
@@ -111,9 +113,9 @@ hipError_t head_pack(const float* w, float* wf, float* wd, int Cin, int K, hipSt
 size_t head_pack_floats(int Cin, int K);
 size_t head_pack_dgrad_offset(int Cin, int K);
 hipError_t head_fwd(const float* x, const float* wf, const float* b, float* y, int64_t V,
-                    int Cin, int K, hipStream_t s);
+                    int Cin, int K, hipStream_t s, int math = SPFF_MATH_F32);
 hipError_t head_dgrad(const float* dy, const float* wd, float* dx, int64_t V, int Cin, int K,
-                      hipStream_t s);
+                      hipStream_t s, int math = SPFF_MATH_F32);
 size_t head_wgrad_ws_bytes(int64_t V, int Cin, int K);
 hipError_t head_wgrad(const float* x, const float* dy, float* dw, float* db, int64_t V,
                       int Cin, int K, float* ws, hipStream_t s);

@@ -335,7 +335,7 @@ int forward(spff_unet3d* p, const float* x, float* logits, bool training) {
     UHIPCK(upconv_pack(p->P(U.w), pk, pk + upconv_pack_dgrad_offset(U.Cin, U.Cout, NSUB), U.Cin,
                        U.Cout, p->st, NSUB));
     UHIPCK(upconv_fwd(prev, pk, p->P(U.b), p->F(U.out), p->vol[U.lvl_low], U.Cin, U.Cout, p->st,
-                      NSUB));
+                      NSUB, p->cfg.math));
     UBlk& d = B[5 + u];
     const UBlk& skip = B[3 - u];
     // torch.cat([up(x), skip], dim=1) read in place through the two-source view
@@ -345,7 +345,7 @@ int forward(spff_unet3d* p, const float* x, float* logits, bool training) {
   float* hp = p->F(p->head_pk);
   UHIPCK(head_pack(p->P(p->out_w), hp, hp + head_pack_dgrad_offset(f, p->K), f, p->K, p->st));
   float* lt = p->Dt != c.depth ? p->F(p->logit_t) : logits;
-  UHIPCK(head_fwd(prev, hp, p->P(p->out_b), lt, nvox(v0), f, p->K, p->st));
+  UHIPCK(head_fwd(prev, hp, p->P(p->out_b), lt, nvox(v0), f, p->K, p->st, p->cfg.math));
   if (p->Dt != c.depth)  // _resize_logits_depth_like (models.py:159-163)
     UHIPCK(resize_d_rows(lt, logits, c.batch, p->K, p->Dt, c.depth, c.height, c.width, p->st));
   p->last_training = training;
@@ -367,7 +367,7 @@ int backward(spff_unet3d* p, const float* dl) {
   UHIPCK(head_wgrad(p->F(B[8].out), d16, p->DP(p->out_w), p->DP(p->out_b), V0, f, p->K,
                     p->F(p->wg_ws), p->st));
   UHIPCK(head_dgrad(d16, hp + head_pack_dgrad_offset(f, p->K), p->F(p->G_out), V0, f, p->K,
-                    p->st));
+                    p->st, p->cfg.math));
   for (int k = 0; k < NUP; ++k) {  // dec1 <- up1 <- dec2 ... <- up4
     const int bi = 8 - k, ui = 3 - k;
     UBlk& d = B[bi];
@@ -381,7 +381,7 @@ int backward(spff_unet3d* p, const float* dl) {
                         U.Cout, p->F(p->wg_ws), p->st, NSUB));
     float* pk = p->F(U.pk);
     UHIPCK(upconv_dgrad(p->F(p->G_dx), C, pk + upconv_pack_dgrad_offset(U.Cin, U.Cout, NSUB),
-                        p->F(p->G_out), low, U.Cin, U.Cout, p->st, NSUB));
+                        p->F(p->G_out), low, U.Cin, U.Cout, p->st, NSUB, p->cfg.math));
   }
   {
     Dst2 dx = dst1(p->F(p->G_dx), 8 * f);
