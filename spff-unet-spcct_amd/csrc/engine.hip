@@ -826,7 +826,7 @@ int backward(spff_plan* p, const float* dl) {
     }
     PROF(p, 3, 2.0 * nvox(low) * U.Cin * 4.0 * U.Cout,
          upconv_wgrad(upin, gup, C, p->DP(U.w), p->DP(U.b), low, U.Cin, U.Cout,
-                      p->F(p->wg_ws), p->st));
+                      p->F(p->wg_ws), p->st, 4, p->cfg.math));
     CK(grad_ready(p, U.w, U.b + U.Cout));
     float* pk = p->F(U.pk);
     PROF(p, 3, 2.0 * nvox(low) * U.Cin * 4.0 * U.Cout,

@@ -568,6 +568,136 @@ __global__ __launch_bounds__(256) void k_atb(XL X, YL Y, float* __restrict__ par
   }
 }
 
+// ------------------------------------------------ C = X^T . Y, split bf16 --
+// k_atb on v_mfma_f32_16x16x32_bf16 with the exact 3-plane split (see k_gemm_x):
+// the same 64 x 64 output tile per workgroup (4 waves 2 x 2, each 32 x 32 = 2 x 2
+// blocks), voxel chunks of 64 = two k-steps.  X and Y are staged voxel-major per
+// plane ([m][64 cols], 32-B column units XOR-swizzled by m, gx_bsw<64>) and both
+// MFMA operands are gathered with ds_read_b64_tr_b16 (m is the reduction axis of
+// both).  Odd chunks stage -Y and the accumulator is negated at every chunk
+// boundary.  The bias column sums are taken in fp32 from the staged registers.
+template <class XL, class YL>
+__global__ __launch_bounds__(256, 2) void k_atb_x(XL X, YL Y, float* __restrict__ part,
+                                                  float* __restrict__ csum, int64_t M, int64_t rps,
+                                                  int k1pad, int npad) {
+  constexpr int PL = T_BM * 64;  // bf16 per plane
+  __shared__ __attribute__((aligned(16))) unsigned short Xs[3 * PL];
+  __shared__ __attribute__((aligned(16))) unsigned short Ys[3 * PL];
+  __shared__ float4 cred[16][16];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, l16 = lane & 15, q = l16 >> 2, pp = l16 & 3;
+  const int split = blockIdx.x, k10 = blockIdx.y * 64, n0 = blockIdx.z * 64;
+  const int wr = wave >> 1, wc = wave & 1;
+  const bool do_cs = blockIdx.y == 0;
+  f32x4g acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4g{0.f, 0.f, 0.f, 0.f};
+  float4 cs = make_float4(0.f, 0.f, 0.f, 0.f);  // columns n0 + 4 (tid & 15) .. + 3
+  const int sq = tid & 15, sr = tid >> 4;      // staging: col quad, row (+ 16 j)
+  float4 xr[4], yr[4];
+  const int64_t mb = (int64_t)split * rps, me = min(M, mb + rps);
+  auto fetch = [&](int64_t m0) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t m = m0 + sr + 16 * j;
+      const bool ok = m < me;
+      xr[j] = ok ? X.load4(X.prep(m), k10 + 4 * sq) : make_float4(0.f, 0.f, 0.f, 0.f);
+      yr[j] = ok ? Y.load4(Y.prep(m), n0 + 4 * sq) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto stash = [&](bool neg) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int m = sr + 16 * j;
+      const int off = m * 64 + 16 * ((sq >> 2) ^ gx_bsw<64>(m)) + 4 * (sq & 3);
+      uint2 o[3];
+      gsplit4(xr[j], o);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) *reinterpret_cast<uint2*>(Xs + p * PL + off) = o[p];
+      float4 y = yr[j];
+      if (do_cs) { cs.x += y.x; cs.y += y.y; cs.z += y.z; cs.w += y.w; }
+      if (neg) y = make_float4(-y.x, -y.y, -y.z, -y.w);
+      gsplit4(y, o);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) *reinterpret_cast<uint2*>(Ys + p * PL + off) = o[p];
+    }
+  };
+  // operand of row block i (16 columns of X or Y at c0 + 16 i): lane 4q + p of k-group
+  // g addresses voxel rows 32 ks + 8 g + q (and + 4), columns c0 + 16 i + 4 p
+  auto frag = [&](const unsigned short* img, int ks, int unit) {
+    const int r0 = 32 * ks + 8 * g + q, r1 = r0 + 4;
+    const unsigned short* a0 = img + r0 * 64 + 16 * (unit ^ gx_bsw<64>(r0)) + 4 * pp;
+    const unsigned short* a1 = img + r1 * 64 + 16 * (unit ^ gx_bsw<64>(r1)) + 4 * pp;
+    const i16x4g lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4g*)a0);
+    const i16x4g hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4g*)a1);
+    const i16x8g v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8g, v);
+  };
+  if (mb < me) fetch(mb);
+  int kc = 0;
+  for (int64_t m0 = mb; m0 < me; m0 += T_BM, ++kc) {
+    if (kc) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = -acc[i][j];
+      __syncthreads();
+    }
+    stash(kc & 1);
+    __syncthreads();
+    if (m0 + T_BM < me) fetch(m0 + T_BM);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8g a[2][3], b[2][3];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          a[i][p] = frag(Xs + p * PL, ks, 2 * wr + i);
+          b[i][p] = frag(Ys + p * PL, ks, 2 * wc + i);
+        }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          f32x4g c = acc[i][j];
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][1], b[j][1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[j][2], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][2], b[j][0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[j][1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][1], b[j][0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[j][0], c, 0, 0, 0);
+          acc[i][j] = c;
+        }
+    }
+  }
+  const float sg = (kc > 0 && ((kc - 1) & 1)) ? -1.f : 1.f;
+  // C[k1][n]: lane holds rows k10 + 32 wr + 16 i + 4 g + r, column n0 + 32 wc + 16 j + l16
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        part[((int64_t)split * k1pad + k10 + 32 * wr + 16 * i + 4 * g + r) * npad + n0 + 32 * wc +
+             16 * j + l16] = sg * acc[i][j][r];
+  if (do_cs) {
+    cred[sr][sq] = cs;
+    __syncthreads();
+    if (tid < 64) {
+      const int c4 = tid >> 2, e = tid & 3;
+      float v = 0.f;
+      for (int r = 0; r < 16; ++r) {
+        const float4 t = cred[r][c4];
+        v += e == 0 ? t.x : e == 1 ? t.y : e == 2 ? t.z : t.w;
+      }
+      csum[(int64_t)split * npad + n0 + tid] = v;
+    }
+  }
+}
+
 // ------------------------------------------------ C = X^T . Y, streaming --
 // Weight gradients of the up-convs and the head: part[split][k1][n] = sum over
 // the split's voxels of X[v][k1] * Y[v][n] (+ csum[split][n] = sum Y[v][n]).
@@ -793,7 +923,8 @@ static hipError_t launch_xty(const float* X, int ldx, int K1, const float* Y, in
 
 template <class XL, class YL>
 static hipError_t launch_atb(const XL& X, const YL& Y, int64_t M, int K1, int N, int Cout,
-                             int mode, float* dw, float* db, float* ws, hipStream_t s) {
+                             int mode, float* dw, float* db, float* ws, hipStream_t s,
+                             bool split = false) {
   if (M >= (int64_t(1) << 31)) return hipErrorInvalidValue;
   const int k1pad = cdiv(K1, 64) * 64, npad = cdiv(N, 64) * 64;
   const int nout = (k1pad / 64) * (npad / 64);
@@ -804,8 +935,12 @@ static hipError_t launch_atb(const XL& X, const YL& Y, int64_t M, int K1, int N,
   float* part = ws;
   float* csum = ws + nsplit * k1pad * npad;
   dim3 grid((unsigned)nsplit, k1pad / 64, npad / 64);
-  hipLaunchKernelGGL((k_atb<XL, YL>), grid, dim3(256), 0, s, X, Y, part, csum, M, rps, k1pad,
-                     npad);
+  if (split)
+    hipLaunchKernelGGL((k_atb_x<XL, YL>), grid, dim3(256), 0, s, X, Y, part, csum, M, rps, k1pad,
+                       npad);
+  else
+    hipLaunchKernelGGL((k_atb<XL, YL>), grid, dim3(256), 0, s, X, Y, part, csum, M, rps, k1pad,
+                       npad);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const int nwb = cdiv(k1pad * npad, 32);
@@ -883,13 +1018,14 @@ size_t upconv_wgrad_ws_bytes(Vol low, int Cin, int Cout, int ns) {
 }
 
 hipError_t upconv_wgrad(const float* x, const float* dy, int lddy, float* dw, float* db, Vol low,
-                        int Cin, int Cout, float* ws, hipStream_t s, int ns) {
+                        int Cin, int Cout, float* ws, hipStream_t s, int ns, int math) {
   // (the streaming k_xty measured 15 % slower here: the up-conv gather needs a
   //  per-voxel index division, and 64 x 64 LDS tiles reuse X and Y better)
   const int64_t M = nvox(low);
   LoadRowsVec X{x, Cin, Cin, M};
   LoadUpGather Y{dy, lddy, Cout, low.D, low.H, low.W, M, ns};
-  return launch_atb(X, Y, M, Cin, ns * Cout, Cout, ns == 8 ? 2 : 0, dw, db, ws, s);
+  return launch_atb(X, Y, M, Cin, ns * Cout, Cout, ns == 8 ? 2 : 0, dw, db, ws, s,
+                    gemm_split(math));
 }
 
 // ------------------------------------------------------------------- head --

@@ -105,7 +105,8 @@ hipError_t upconv_dgrad(const float* dy, int lddy, const float* wd, float* dx, V
                         int Cin, int Cout, hipStream_t s, int ns = 4, int math = SPFF_MATH_F32);
 size_t upconv_wgrad_ws_bytes(Vol low, int Cin, int Cout, int ns = 4);
 hipError_t upconv_wgrad(const float* x, const float* dy, int lddy, float* dw, float* db,
-                        Vol low, int Cin, int Cout, float* ws, hipStream_t s, int ns = 4);
+                        Vol low, int Cin, int Cout, float* ws, hipStream_t s, int ns = 4,
+                        int math = SPFF_MATH_F32);
 size_t upconv_pack_floats(int Cin, int Cout, int ns = 4);
 size_t upconv_pack_dgrad_offset(int Cin, int Cout, int ns = 4);
 // 1x1x1 conv head: y[v][K] = x[v][:Cin] . W[K][Cin] + b  (wf/wd from head_pack)

@@ -378,7 +378,7 @@ int backward(spff_unet3d* p, const float* dl) {
                   Src2{p->F(U.out), p->F(B[lvl].out), C, C, C}));
     const Vol& low = p->vol[U.lvl_low];
     UHIPCK(upconv_wgrad(p->F(B[bi - 1].out), p->F(p->G_dx), C, p->DP(U.w), p->DP(U.b), low, U.Cin,
-                        U.Cout, p->F(p->wg_ws), p->st, NSUB));
+                        U.Cout, p->F(p->wg_ws), p->st, NSUB, p->cfg.math));
     float* pk = p->F(U.pk);
     UHIPCK(upconv_dgrad(p->F(p->G_dx), C, pk + upconv_pack_dgrad_offset(U.Cin, U.Cout, NSUB),
                         p->F(p->G_out), low, U.Cin, U.Cout, p->st, NSUB, p->cfg.math));
