@@ -12,6 +12,10 @@
 // per-(b,c,d) coefficients P, Q (gates.hip).  Saved for backward: y1, a1, y2,
 // out and the (b,c)/(b,c,d) statistics -- everything else is recomputed.
 #include "spff_internal.h"
+
+#ifndef SPFF_RED_FUSE
+#define SPFF_RED_FUSE 1  // 0 (A/B diagnostics): separate tail and IN-backward reductions
+#endif
 #include "spff.h"
 
 #include <cmath>
@@ -115,8 +119,8 @@ struct spff_plan {
   int64_t out_w = -1, out_b = -1;
   size_t head_pk = 0;
   size_t x_cl = 0, pool[3] = {0, 0, 0}, pidx[3] = {0, 0, 0};
-  size_t red_ws = 0, red_out = 0, gscr = 0, Abuf = 0, Bbuf = 0, kk1 = 0, kk2 = 0, wg_ws = 0,
-         wt = 0, cst = 0;
+  size_t red_ws = 0, red_out = 0, red_out4 = 0, gscr = 0, Abuf = 0, Bbuf = 0, kk1 = 0, kk2 = 0,
+         wg_ws = 0, wt = 0, cst = 0;
   size_t G_out = 0, G_dy2 = 0, G_da1 = 0, G_dx = 0, dskip[3] = {0, 0, 0};
   size_t part_d = 0;  // sharded plans: fp64 IN partials [B][C][2]
   size_t total = 0;
@@ -327,7 +331,7 @@ int build_plan(spff_plan* p) {
   const Vol& v0 = p->vol[0];
   const auto slice = [&](const Vol& v, int C) { return (size_t)v.H * v.W * C * sizeof(float); };
   p->x_cl = p->alloc_halo(nvox(v0) * p->ldx * sizeof(float), slice(v0, p->ldx));
-  size_t red_ws = 0, red_out = 0, gs = 0, bcd = 0, wg = 0, wt = 0, cst = 0;
+  size_t red_ws = 0, red_out = 0, red_out4 = 0, gs = 0, bcd = 0, wg = 0, wt = 0, cst = 0;
   for (int i = 0; i < 7; ++i) {
     Blk& b = p->blk[i];
     const Vol& v = p->vol[b.lvl];
@@ -360,8 +364,10 @@ int build_plan(spff_plan* p) {
       b.hid = p->alloc((size_t)32 * D * 4);
       if (world > 1) b.spec = p->alloc((size_t)B * (p->co.D_glob / 2 + 1) * 2 * sizeof(double));
     }
-    red_ws = std::max(red_ws, slab_reduce_ws_bytes(v, b.C, 2));
+    red_ws = std::max(red_ws, slab_reduce_ws_bytes(v, b.C, b.tail() && SPFF_RED_FUSE ? 6 : 2));
     red_out = std::max(red_out, (size_t)B * b.C * D * 2 * sizeof(float));
+    if (b.tail() && SPFF_RED_FUSE)
+      red_out4 = std::max(red_out4, (size_t)B * b.C * D * 4 * sizeof(float));
     gs = std::max(gs, world > 1 ? gates_sh_scratch_bytes(v, b.C, p->co.D_glob)
                                 : gates_scratch_bytes(v, b.C));
     bcd = std::max(bcd, bcdz);
@@ -392,6 +398,7 @@ int build_plan(spff_plan* p) {
   wg = std::max(wg, head_wgrad_ws_bytes(nvox(v0), f, p->K));
   p->red_ws = p->alloc(red_ws);
   p->red_out = p->alloc(red_out);
+  p->red_out4 = p->alloc(red_out4);
   p->gscr = p->alloc(gs);
   p->Abuf = p->alloc(bcd);
   p->Bbuf = p->alloc(bcd);
@@ -666,8 +673,14 @@ int bwd_block(spff_plan* p, Blk& b, const float* dout, const Dst2* dx, const Src
     a.g = dout;
     a.al = p->F(b.al2);
     a.de = p->F(b.de2);
+    a.mean = p->F(b.mean2);
+    a.rstd = p->F(b.rstd2);
+    // (SPFF_RED_FUSE: the IN-backward sums of y2 in the same pass, RED_BWD_TAIL6)
     PROFB(p, 4, 0.0, 8.0 * (double)nvox(v) * C,
-        slab_reduce(RED_BWD_TAIL, a, v, C, p->F(p->red_out), p->F(p->red_ws), p->st));
+          SPFF_RED_FUSE ? slab_reduce(RED_BWD_TAIL6, a, v, C, p->F(p->red_out), p->F(p->red_ws),
+                                      p->st, p->F(p->red_out4))
+                        : slab_reduce(RED_BWD_TAIL, a, v, C, p->F(p->red_out), p->F(p->red_ws),
+                                      p->st));
     GateParams gp = gate_params(p, b);
     GateSaved sv = gate_saved(p, b);
     GateGrads gg;
@@ -696,8 +709,12 @@ int bwd_block(spff_plan* p, Blk& b, const float* dout, const Dst2* dx, const Src
     RedArgs a{};
     a.y = p->F(b.y2); a.g = dout; a.mean = p->F(b.mean2); a.rstd = p->F(b.rstd2);
     a.al = p->F(b.al2); a.de = p->F(b.de2); a.A = A; a.Bc = Bc;
-    PROFB(p, 4, 0.0, 8.0 * (double)nvox(v) * C,
-        slab_reduce(RED_BWD_IN, a, v, C, p->F(p->red_out), p->F(p->red_ws), p->st));
+    if (b.tail() && SPFF_RED_FUSE)
+      HIPCK(in_sums_from_tail(p->F(p->red_out4), A, Bc, p->F(p->red_out),
+                              (int64_t)v.B * C * v.D, p->st));
+    else
+      PROFB(p, 4, 0.0, 8.0 * (double)nvox(v) * C,
+            slab_reduce(RED_BWD_IN, a, v, C, p->F(p->red_out), p->F(p->red_ws), p->st));
     CK(in_bwd(p, v, C, b.g2, b.b2));
     PROFB(p, 6, 0.0, 12.0 * (double)nvox(v) * C,
           in_bwd_apply(p->F(b.y2), dout, dy2, p->F(b.mean2), p->F(b.rstd2), p->F(b.al2),

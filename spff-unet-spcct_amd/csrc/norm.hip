@@ -71,13 +71,16 @@ __global__ __launch_bounds__(256) void k_slab_reduce(RedArgs a, Vol vol, int C, 
       const int bc = b * C + c + j;
       p0[j] = 0.f; p1[j] = 0.f; p2[j] = 1.f; p3[j] = 0.f;
       if (OP == RED_SQDEV) p0[j] = a.mean[bc];
-      if (OP == RED_ACT || OP == RED_BWD_TAIL || OP == RED_BWD_IN) { p0[j] = a.al[bc]; p1[j] = a.de[bc]; }
+      if (OP == RED_ACT || OP == RED_BWD_TAIL || OP == RED_BWD_IN || OP == RED_BWD_TAIL6) {
+        p0[j] = a.al[bc];
+        p1[j] = a.de[bc];
+      }
       if (OP == RED_BWD_IN) {
         if (a.A) { p2[j] = a.A[(int64_t)bc * vol.D + d]; p3[j] = a.Bc[(int64_t)bc * vol.D + d]; }
       }
     }
     float mu[4], rs[4];
-    if (OP == RED_BWD_IN) {
+    if (OP == RED_BWD_IN || OP == RED_BWD_TAIL6) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) { mu[j] = a.mean[b * C + c + j]; rs[j] = a.rstd[b * C + c + j]; }
     }
@@ -88,7 +91,7 @@ __global__ __launch_bounds__(256) void k_slab_reduce(RedArgs a, Vol vol, int C, 
       const float4 yv = *reinterpret_cast<const float4*>(a.y + off);
       const float ys[4] = {yv.x, yv.y, yv.z, yv.w};
       float gs[4] = {0.f, 0.f, 0.f, 0.f};
-      if (OP == RED_BWD_TAIL || OP == RED_BWD_IN) {
+      if (OP == RED_BWD_TAIL || OP == RED_BWD_IN || OP == RED_BWD_TAIL6) {
         const float4 gv = *reinterpret_cast<const float4*>(a.g + off);
         gs[0] = gv.x; gs[1] = gv.y; gs[2] = gv.z; gs[3] = gv.w;
       }
@@ -104,6 +107,16 @@ __global__ __launch_bounds__(256) void k_slab_reduce(RedArgs a, Vol vol, int C, 
         } else if (OP == RED_BWD_TAIL) {
           acc[0][j] += gs[j];
           acc[NQ - 1][j] += gs[j] * lrelu(ys[j] * p0[j] + p1[j], a.neg);
+        } else if (OP == RED_BWD_TAIL6) {
+          const float r = ys[j] * p0[j] + p1[j];
+          const float sl = slope(r, a.neg), gsl = gs[j] * sl;
+          const float xh = (ys[j] - mu[j]) * rs[j];
+          acc[0][j] += gs[j];
+          acc[1][j] += gs[j] * lrelu(r, a.neg);
+          acc[2][j] += gsl;
+          acc[3][j] += sl;
+          acc[4][j] += gsl * xh;
+          acc[5][j] += sl * xh;
         } else {  // RED_BWD_IN
           const float r = ys[j] * p0[j] + p1[j];
           const float dr = (gs[j] * p2[j] + p3[j]) * slope(r, a.neg);
@@ -137,9 +150,10 @@ __global__ __launch_bounds__(256) void k_slab_reduce(RedArgs a, Vol vol, int C, 
   }
 }
 
-// combine splits: out[b][c][d][q] = sum_split ws[bd][split][c][q]
+// combine splits: out[b][c][d][q] = sum_split ws[bd][split][c][q]; with out2, q >= 2 go to
+// out2[b][c][d][q - 2] (nq - 2 wide) and out holds q 0, 1
 __global__ void k_slab_combine(const float* __restrict__ ws, float* __restrict__ out, Vol vol,
-                               int C, int nq, int nsplit) {
+                               int C, int nq, int nsplit, float* __restrict__ out2) {
   const int total = vol.B * vol.D * C * nq;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
     const int q = i % nq;
@@ -149,8 +163,30 @@ __global__ void k_slab_combine(const float* __restrict__ ws, float* __restrict__
     float s = 0.f;
 #pragma unroll 4
     for (int k = 0; k < nsplit; ++k) s += ws[(((int64_t)bd * nsplit + k) * C + c) * nq + q];
-    out[(((int64_t)b * C + c) * vol.D + d) * nq + q] = s;
+    const int64_t slab = ((int64_t)b * C + c) * vol.D + d;
+    if (!out2) out[slab * nq + q] = s;
+    else if (q < 2) out[slab * 2 + q] = s;
+    else out2[slab * (nq - 2) + (q - 2)] = s;
   }
+}
+
+__global__ void k_in_sums_from_tail(const float* __restrict__ t4, const float* __restrict__ A,
+                                    const float* __restrict__ Bc, float* __restrict__ out,
+                                    int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float4 t = reinterpret_cast<const float4*>(t4)[i];
+    const float a = A[i], bc = Bc[i];
+    out[2 * i] = a * t.x + bc * t.y;
+    out[2 * i + 1] = a * t.z + bc * t.w;
+  }
+}
+hipError_t in_sums_from_tail(const float* t4, const float* A, const float* Bc, float* out,
+                             int64_t n, hipStream_t s) {
+  hipLaunchKernelGGL(k_in_sums_from_tail,
+                     dim3((unsigned)std::min<int64_t>((n + 255) / 256, 4096)), dim3(256), 0, s, t4,
+                     A, Bc, out, n);
+  return hipGetLastError();
 }
 
 size_t slab_reduce_ws_bytes(Vol vol, int C, int nq) {
@@ -159,7 +195,8 @@ size_t slab_reduce_ws_bytes(Vol vol, int C, int nq) {
 }
 
 hipError_t slab_reduce(RedOp op, const RedArgs& a, Vol vol, int C, float* out, float* ws,
-                       hipStream_t s) {
+                       hipStream_t s, float* out2) {
+  if ((op == RED_BWD_TAIL6) != (out2 != nullptr)) return hipErrorInvalidValue;
   if (C % 4 || C > 1024) return hipErrorInvalidValue;
   RedPlan p = red_plan(vol, C);
   dim3 grid(p.nsplit, vol.B * vol.D);
@@ -170,12 +207,13 @@ hipError_t slab_reduce(RedOp op, const RedArgs& a, Vol vol, int C, float* out, f
     case RED_ACT: hipLaunchKernelGGL((k_slab_reduce<RED_ACT, 1>), grid, dim3(256), 0, s, a, vol, C, ws, p.nsplit, p.chunk); break;
     case RED_BWD_TAIL: nq = 2; hipLaunchKernelGGL((k_slab_reduce<RED_BWD_TAIL, 2>), grid, dim3(256), 0, s, a, vol, C, ws, p.nsplit, p.chunk); break;
     case RED_BWD_IN: nq = 2; hipLaunchKernelGGL((k_slab_reduce<RED_BWD_IN, 2>), grid, dim3(256), 0, s, a, vol, C, ws, p.nsplit, p.chunk); break;
+    case RED_BWD_TAIL6: nq = 6; hipLaunchKernelGGL((k_slab_reduce<RED_BWD_TAIL6, 6>), grid, dim3(256), 0, s, a, vol, C, ws, p.nsplit, p.chunk); break;
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const int total = vol.B * vol.D * C * nq;
   hipLaunchKernelGGL(k_slab_combine, dim3(std::min(cdiv(total, 256), 4096)), dim3(256), 0, s, ws,
-                     out, vol, C, nq, p.nsplit);
+                     out, vol, C, nq, p.nsplit, out2);
   return hipGetLastError();
 }
 

@@ -157,6 +157,11 @@ enum RedOp {
   RED_ACT = 2,        // q0 = lrelu(y*al + de)              (aux0 = alpha, aux1 = delta)
   RED_BWD_TAIL = 3,   // q0 = g, q1 = g*lrelu(y*al+de)      (g = dout)
   RED_BWD_IN = 4,     // r = y*al+de; dr = (g*A+Bc)*slope(r); q0 = dr, q1 = dr*xhat
+  // RED_BWD_TAIL and the gated block's RED_BWD_IN in one pass: dr = (g A + Bc) s with
+  // A, Bc per (b,c,d), so its sums factor as A S(g s) + Bc S(s) and A S(g s xhat) +
+  // Bc S(s xhat).  out = [q0 g, q1 g*a]; out2 = [S(g s), S(s), S(g s xhat), S(s xhat)]
+  // (s = slope(r)); in_sums_from_tail() turns out2 into RED_BWD_IN's [B][C][D][2]
+  RED_BWD_TAIL6 = 5,
 };
 struct RedArgs {
   const float* y; const float* g;     // y: [V][C] (ld = C), g: [V][C] (ld = C)
@@ -168,7 +173,10 @@ struct RedArgs {
 // out: [B][C][D][nq] fp32, summed over h,w in a fixed order.
 size_t slab_reduce_ws_bytes(Vol vol, int C, int nq);
 hipError_t slab_reduce(RedOp op, const RedArgs& a, Vol vol, int C, float* out, float* ws,
-                       hipStream_t s);
+                       hipStream_t s, float* out2 = nullptr);
+// out[i] = {A t4[i][0] + Bc t4[i][1], A t4[i][2] + Bc t4[i][3]} for the n = B C D slabs
+hipError_t in_sums_from_tail(const float* t4, const float* A, const float* Bc, float* out,
+                             int64_t n, hipStream_t s);
 // stats: from per-(b,c,d) sums -> mean[b,c] ; from sqdev sums -> rstd, alpha, delta
 hipError_t in_mean(const float* sums, float* mean, Vol vol, int C, hipStream_t s);
 hipError_t in_rstd(const float* sqsums, const float* gamma, const float* beta,
