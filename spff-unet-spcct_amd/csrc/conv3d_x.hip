@@ -50,7 +50,9 @@
 #define SPFF_XCDMAP 1  // 0: tile-fastest block order (A/B diagnostics)
 #endif
 #ifndef SPFF_X32T
-#define SPFF_X32T 1  // 1: 32-wide tiles are 4 x 16 x 16 voxels (MB 4), 0: 2 x 16 x 16 (MB 2)
+// 1: 32-wide tiles are 4 x 16 x 16 voxels (MB 4), 0: 2 x 16 x 16 (MB 2).  Measured: 4-deep
+// tiles conv_fwd -0.25 ms/step but the 32-wide launches' HBM traffic 2.23 -> 3.61 GB
+#define SPFF_X32T 0
 #endif
 #ifndef SPFF_X16
 #define SPFF_X16 1  // 1: v_mfma_f32_16x16x32_bf16 tap-quad schedule, 0: 32x32x16 tap pairs
