@@ -49,9 +49,12 @@
 #ifndef SPFF_XCDMAP
 #define SPFF_XCDMAP 1  // 0: tile-fastest block order (A/B diagnostics)
 #endif
+#ifndef SPFF_XDFAST
+#define SPFF_XDFAST 1  // 1: tiles depth-fastest (per batch sample), 0: W-fastest
+#endif
 #ifndef SPFF_X32T
-// 1: 32-wide tiles are 4 x 16 x 16 voxels (MB 4), 0: 2 x 16 x 16 (MB 2).  Measured: 4-deep
-// tiles conv_fwd -0.25 ms/step but the 32-wide launches' HBM traffic 2.23 -> 3.61 GB
+// 1: 32-wide tiles are 4 x 16 x 16 voxels (MB 4), 0: 2 x 16 x 16 (MB 2).  Measured (with the
+// depth-fastest order): 4-deep tiles -0.45 ms/step, but the 32-wide launches read 1.42 -> 2.35 GB
 #define SPFF_X32T 0
 #endif
 #ifndef SPFF_X16
@@ -244,10 +247,19 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
   const int nbk = SPFF_XCDMAP ? rk % nnb : (int)(blockIdx.x / (8 * per));
   if (tile >= ntiles) return;  // padding block (uniform: the whole workgroup)
   int t = tile;
-  const int twi = t % tilesW; t /= tilesW;
-  const int thi = t % tilesH; t /= tilesH;
-  const int tdi = t % tilesD;
-  const int b = t / tilesD;
+  int twi, thi, tdi;
+  if (SPFF_XDFAST) {
+    // depth-fastest: the ~32 tiles an XCD runs at once are D-neighbours, whose halos
+    // share KD - 1 planes -- those are L2 hits instead of a later HBM re-read
+    tdi = t % tilesD; t /= tilesD;
+    twi = t % tilesW; t /= tilesW;
+    thi = t % tilesH; t /= tilesH;
+  } else {
+    twi = t % tilesW; t /= tilesW;
+    thi = t % tilesH; t /= tilesH;
+    tdi = t % tilesD; t /= tilesD;
+  }
+  const int b = t;
   const int d0 = tdi * TD, h0 = thi * TH, w0 = twi * TW;
   const int n0 = nbk * BN;
   const int D = vol.D, H = vol.H, W = vol.W;
