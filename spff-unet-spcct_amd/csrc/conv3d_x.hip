@@ -207,7 +207,7 @@ template <int BN, int KD, int NS, int MB, int NW, bool X16, int TD>
 __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
     Src2 x, const uint4* __restrict__ wp, Dst2 y, Vol vol, int Cin, int nkc, int Cout, int npad,
     int tilesD, int tilesH, int tilesW, float* __restrict__ part, int kps,
-    float* __restrict__ stats, int ntiles) {
+    float* __restrict__ stats, int ntiles, int td0, int tds) {
   constexpr int XT_THREADS = NW * 64;
   constexpr int TH = X16 ? 2 * NW * MB / TD : NW * MB, TW = XT_W;
   static_assert(X16 || TD == 2, "32x32x16 schedule: 2-deep tiles");
@@ -260,6 +260,7 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
     tdi = t % tilesD; t /= tilesD;
   }
   const int b = t;
+  tdi = td0 + tdi * tds;  // depth-tile subset (sharded halo overlap): td0 + k tds, k < tilesD
   const int d0 = tdi * TD, h0 = thi * TH, w0 = twi * TW;
   const int n0 = nbk * BN;
   const int D = vol.D, H = vol.H, W = vol.W;
@@ -683,7 +684,8 @@ __global__ void k_splitk_reduce(const float* __restrict__ part, int nsplit, int6
 template <int BN, int KD, int NS, int MB = xt_mb(BN), int NW = 8, int TD = xt_td(BN)>
 static hipError_t launch_fwd_x(const Src2& x, const uint4* wx, const Dst2& y, Vol vol, int K,
                                int nkc, int N, int npad, hipStream_t s, float* part = nullptr,
-                               int nsplit = 1, int kps = 0, float* stats = nullptr) {
+                               int nsplit = 1, int kps = 0, float* stats = nullptr,
+                               int dpart = 0) {
   constexpr int TH = SPFF_X16 ? 2 * NW * MB / TD : NW * MB;
   static_assert(NW == 8 || TD == XT_D, "xt_ntiles assumes 8 waves for other tile depths");
   constexpr size_t shm = xt_lds_bytes<BN, KD, NS, TD, TH>();
@@ -697,11 +699,17 @@ static hipError_t launch_fwd_x(const Src2& x, const uint4* wx, const Dst2& y, Vo
     if (e != hipSuccess) return e;
     attr = true;
   }
-  const int tilesD = cdiv(vol.D, TD), tilesH = cdiv(vol.H, TH), tilesW = cdiv(vol.W, XT_W);
+  const int tilesH = cdiv(vol.H, TH), tilesW = cdiv(vol.W, XT_W);
+  // dpart 1: the interior depth tiles 1 .. n-2 (no halo slice read), 2: the first and last
+  const int tdn = cdiv(vol.D, TD);
+  if (dpart && (tdn < 3 || part || stats)) return hipErrorInvalidValue;
+  const int tilesD = dpart == 1 ? tdn - 2 : dpart == 2 ? 2 : tdn;
+  const int td0 = dpart == 1 ? 1 : 0, tds = dpart == 2 ? tdn - 1 : 1;
   const int ntiles = vol.B * tilesD * tilesH * tilesW;
   dim3 grid(8 * cdiv(ntiles, 8) * (npad / BN), 1, part ? nsplit : 1);
   hipLaunchKernelGGL(kern, grid, dim3(NW * 64), shm, s, x, wx, y, vol, K, nkc, N, npad, tilesD,
-                     tilesH, tilesW, part, part ? kps : nkc, part ? nullptr : stats, ntiles);
+                     tilesH, tilesW, part, part ? kps : nkc, part ? nullptr : stats, ntiles, td0,
+                     tds);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || !part) return e;
   const int64_t total = nvox(vol) * N;
@@ -806,7 +814,7 @@ hipError_t conv3d_pack(const float* w, void* wpack, Vol vol, int KD, int Cin_w, 
 
 template <int NS>
 static hipError_t run_x(const Src2& x, const uint4* wu, const Dst2& y, Vol vol, int KD,
-                        const XDims& d, hipStream_t s, float* ws, float* stats) {
+                        const XDims& d, hipStream_t s, float* ws, float* stats, int dpart) {
   // (32x32x16, MB = 4, 2 x 32 x 16 tiles for Cout <= 32: fits LDS but spills 91 VGPRs)
   // (NW = 4 waves, 2 x 8 x 16 tiles, BN 32, two workgroups per CU: measured 6 % slower)
   SplitK k = ws ? splitk_plan(vol, d) : SplitK{1, d.nkc};
@@ -814,13 +822,13 @@ static hipError_t run_x(const Src2& x, const uint4* wu, const Dst2& y, Vol vol, 
   if (d.BN == 64)
     return KD == 3
                ? launch_fwd_x<64, 3, NS>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s, part,
-                                                k.nsplit, k.kps, stats)
+                                                k.nsplit, k.kps, stats, dpart)
                : launch_fwd_x<64, 1, NS>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s, part,
-                                                k.nsplit, k.kps, stats);
+                                                k.nsplit, k.kps, stats, dpart);
   return KD == 3 ? launch_fwd_x<32, 3, NS>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s,
-                                                  part, k.nsplit, k.kps, stats)
+                                                  part, k.nsplit, k.kps, stats, dpart)
                  : launch_fwd_x<32, 1, NS>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s,
-                                                  part, k.nsplit, k.kps, stats);
+                                                  part, k.nsplit, k.kps, stats, dpart);
 }
 
 
@@ -834,6 +842,11 @@ size_t conv3d_splitk_bytes(Vol vol, int KD, int Cin, int Cout) {
   return b;
 }
 
+bool conv3d_splits_depth(Vol vol, int KD, int Cin_w, int Cout_w, bool dgrad, int math) {
+  const XDims d = xdims(KD, Cin_w, Cout_w, dgrad);
+  return KD == 3 && use_split(vol, math, dgrad) && splitk_plan(vol, d).nsplit == 1 &&
+         cdiv(vol.D, xt_td(d.BN)) >= 3;
+}
 size_t conv3d_stats_bytes(Vol vol, int KD, int Cin, int Cout) {
   const XDims d = xdims(KD, Cin, Cout, false);
   return (size_t)xt_ntiles(vol, d.BN) * (2 * d.npad + 1) * sizeof(float);
@@ -854,14 +867,16 @@ hipError_t conv3d_in_stats_fin(const float* stats, Vol vol, int KD, int Cin, int
 
 hipError_t conv3d_run(const Src2& x, const void* wpack, const Dst2& y, Vol vol, int KD,
                       int Cin_w, int Cout_w, bool dgrad, int math, hipStream_t s, float* ws,
-                      float* stats) {
+                      float* stats, int dpart) {
   const XDims d = xdims(KD, Cin_w, Cout_w, dgrad);
   if (stats && (dgrad || !conv3d_fuses_stats(vol, KD, Cin_w, Cout_w, math)))
     return hipErrorInvalidValue;
+  if (dpart && !conv3d_splits_depth(vol, KD, Cin_w, Cout_w, dgrad, math))
+    return hipErrorInvalidValue;
   if (use_split(vol, math, dgrad)) {
     const uint4* wu = static_cast<const uint4*>(wpack);
-    return math == SPFF_MATH_BF16X3 ? run_x<2>(x, wu, y, vol, KD, d, s, ws, stats)
-                                    : run_x<3>(x, wu, y, vol, KD, d, s, ws, stats);
+    return math == SPFF_MATH_BF16X3 ? run_x<2>(x, wu, y, vol, KD, d, s, ws, stats, dpart)
+                                    : run_x<3>(x, wu, y, vol, KD, d, s, ws, stats, dpart);
   }
   return conv3d_fwd(x, static_cast<const float*>(wpack), y, vol, KD, d.K, rup(d.K, 8), d.N,
                     rup(d.N, conv3d_bn(d.N)), s);

@@ -141,6 +141,10 @@ struct spff_plan {
   const float* prm = nullptr;
   float* dprm = nullptr;
   hipStream_t st = nullptr;
+  // depth-sharded plans: side stream + events of the halo exchange that overlaps the
+  // interior depth tiles of the next convolution (conv_halo)
+  hipStream_t st2 = nullptr;
+  hipEvent_t ev_in = nullptr, ev_halo = nullptr;
 
   float* F(size_t off) const { return reinterpret_cast<float*>(ws + off); }
   const float* P(int64_t off) const { return off < 0 ? nullptr : prm + off; }
@@ -482,19 +486,55 @@ GateSaved gate_saved(const spff_plan* p, const Blk& b) {
 }
 
 // one D-slice halo per side for a conv input of a depth-sharded plan (no-op otherwise)
-int halo(spff_plan* p, const float* interior, const Vol& v, int C) {
+int halo(spff_plan* p, const float* interior, const Vol& v, int C, hipStream_t st = nullptr) {
   if (!v.dh) return SPFF_OK;
+  if (!st) st = p->st;
   const int64_t sl = (int64_t)v.H * v.W * C;
   float* in = const_cast<float*>(interior);
-  if (p->co.rank == 0) HIPCK(hipMemsetAsync(in - sl, 0, sl * sizeof(float), p->st));
+  if (p->co.rank == 0) HIPCK(hipMemsetAsync(in - sl, 0, sl * sizeof(float), st));
   if (p->co.rank == p->co.world - 1)
-    HIPCK(hipMemsetAsync(in + v.D * sl, 0, sl * sizeof(float), p->st));
-  if (p->co.halo(p->co.ctx, in, sl, v.D, p->st) != 0) return fail(SPFF_EHIP, "halo exchange failed");
+    HIPCK(hipMemsetAsync(in + v.D * sl, 0, sl * sizeof(float), st));
+  if (p->co.halo(p->co.ctx, in, sl, v.D, st) != 0) return fail(SPFF_EHIP, "halo exchange failed");
   return SPFF_OK;
 }
-int halo_src(spff_plan* p, const Src2& x, const Vol& v) {
-  CK(halo(p, x.p0, v, x.ld0));
-  if (x.p1 != x.p0) CK(halo(p, x.p1, v, x.ld1));
+int halo_src(spff_plan* p, const Src2& x, const Vol& v, hipStream_t st = nullptr) {
+  CK(halo(p, x.p0, v, x.ld0, st));
+  if (x.p1 != x.p0) CK(halo(p, x.p1, v, x.ld1, st));
+  return SPFF_OK;
+}
+// halo exchange of x + the 3x3x3 convolution reading it.  Depth-sharded plans whose
+// conv can split its depth tiles run the exchange on the side stream st2 while the
+// interior depth tiles (which read no halo slice) compute on st, then the first and
+// last depth tiles after it; otherwise exchange, then convolve.  cls / flops / bytes:
+// the PROFB record of the launch (the interior launch carries the FLOPs, the
+// boundary one adds its time to the same class).
+int conv_halo(spff_plan* p, int cls, double flops, double bytes, const Src2& x, const Dst2& y,
+              const Vol& v, int Cin_w, int Cout_w, bool dgrad, float* stats) {
+  const int KD = p->KD, math = p->cfg.math;
+  const bool ovl = v.dh && !stats && conv3d_splits_depth(v, KD, Cin_w, Cout_w, dgrad, math);
+  if (!ovl) {
+    CK(halo_src(p, x, v));
+    PROFB(p, cls, flops, bytes,
+          conv3d_run(x, p->F(p->wt), y, v, KD, Cin_w, Cout_w, dgrad, math, p->st, p->F(p->wg_ws),
+                     stats));
+    return SPFF_OK;
+  }
+  if (!p->st2) {
+    HIPCK(hipStreamCreateWithFlags(&p->st2, hipStreamNonBlocking));
+    HIPCK(hipEventCreateWithFlags(&p->ev_in, hipEventDisableTiming));
+    HIPCK(hipEventCreateWithFlags(&p->ev_halo, hipEventDisableTiming));
+  }
+  HIPCK(hipEventRecord(p->ev_in, p->st));  // x is final
+  HIPCK(hipStreamWaitEvent(p->st2, p->ev_in, 0));
+  CK(halo_src(p, x, v, p->st2));
+  HIPCK(hipEventRecord(p->ev_halo, p->st2));
+  PROFB(p, cls, flops, bytes,
+        conv3d_run(x, p->F(p->wt), y, v, KD, Cin_w, Cout_w, dgrad, math, p->st, p->F(p->wg_ws),
+                   nullptr, 1));
+  HIPCK(hipStreamWaitEvent(p->st, p->ev_halo, 0));
+  PROFB(p, cls, 0.0, 0.0,
+        conv3d_run(x, p->F(p->wt), y, v, KD, Cin_w, Cout_w, dgrad, math, p->st, p->F(p->wg_ws),
+                   nullptr, 2));
   return SPFF_OK;
 }
 
@@ -562,14 +602,12 @@ int fwd_block(spff_plan* p, Blk& b, const Src2& in) {
   const int C = b.C, KD = p->KD;
   const int math = p->cfg.math;
   HIPCK(conv3d_pack(p->P(b.c1.w), p->F(p->wt), v, KD, b.Cin, C, false, math, p->st));
-  CK(halo_src(p, in, v));
   const double V = (double)nvox(v), T = 9.0 * KD;
   // InstanceNorm statistics fused into the conv epilogue where the split kernel
   // runs unsharded without split-K; otherwise the two slab_reduce passes
   const bool fuse1 = !p->co.on() && conv3d_fuses_stats(v, KD, b.Cin, C, math);
-  PROFB(p, 0, 2.0 * V * b.Cin * C * T, cbytes(V, b.Cin, C, T),
-       conv3d_run(in, p->F(p->wt), dst1(p->F(b.y1), C), v, KD, b.Cin, C, false, math, p->st,
-                  p->F(p->wg_ws), fuse1 ? p->F(p->cst) : nullptr));
+  CK(conv_halo(p, 0, 2.0 * V * b.Cin * C * T, cbytes(V, b.Cin, C, T), in, dst1(p->F(b.y1), C), v,
+               b.Cin, C, false, fuse1 ? p->F(p->cst) : nullptr));
   if (fuse1)
     HIPCK(conv3d_in_stats_fin(p->F(p->cst), v, KD, b.Cin, C, p->P(b.g1), p->P(b.b1),
                               p->F(b.mean1), p->F(b.rstd1), p->F(b.al1), p->F(b.de1), p->st));
@@ -581,11 +619,9 @@ int fwd_block(spff_plan* p, Blk& b, const Src2& in) {
                     p->st));
   HIPCK(conv3d_pack(p->P(b.c2.w), p->F(p->wt), v, KD, C, C, false, math, p->st));
   const Src2 in2 = act_src(p, b);
-  CK(halo(p, in2.p0, v, C));
   const bool fuse2 = !p->co.on() && conv3d_fuses_stats(v, KD, C, C, math);
-  PROFB(p, 0, 2.0 * V * C * C * T, cbytes(V, C, C, T),
-       conv3d_run(in2, p->F(p->wt), dst1(p->F(b.y2), C), v, KD, C, C, false,
-                  math, p->st, p->F(p->wg_ws), fuse2 ? p->F(p->cst) : nullptr));
+  CK(conv_halo(p, 0, 2.0 * V * C * C * T, cbytes(V, C, C, T), in2, dst1(p->F(b.y2), C), v, C, C,
+               false, fuse2 ? p->F(p->cst) : nullptr));
   if (fuse2)
     HIPCK(conv3d_in_stats_fin(p->F(p->cst), v, KD, C, C, p->P(b.g2), p->P(b.b2), p->F(b.mean2),
                               p->F(b.rstd2), p->F(b.al2), p->F(b.de2), p->st));
@@ -733,9 +769,8 @@ int bwd_block(spff_plan* p, Blk& b, const float* dout, const Dst2* dx, const Src
                     p->F(p->wg_ws), p->st));
   const int math = p->cfg.math;
   HIPCK(conv3d_pack(p->P(b.c2.w), p->F(p->wt), v, KD, C, C, true, math, p->st));
-  CK(halo(p, dy2, v, C));
-  PROFB(p, 1, 2.0 * V * C * C * T, cbytes(V, C, C, T),
-       conv3d_run(src1(dy2, C), p->F(p->wt), dst1(da1, C), v, KD, C, C, true, math, p->st, p->F(p->wg_ws)));
+  CK(conv_halo(p, 1, 2.0 * V * C * C * T, cbytes(V, C, C, T), src1(dy2, C), dst1(da1, C), v, C, C,
+               true, nullptr));
   {
     RedArgs a{};
     a.y = p->F(b.y1); a.g = da1; a.mean = p->F(b.mean1); a.rstd = p->F(b.rstd1);
@@ -754,9 +789,8 @@ int bwd_block(spff_plan* p, Blk& b, const float* dout, const Dst2* dx, const Src
                     p->st));
   if (dx) {
     HIPCK(conv3d_pack(p->P(b.c1.w), p->F(p->wt), v, KD, b.Cin, C, true, math, p->st));
-    CK(halo(p, da1, v, C));
-    PROFB(p, 1, 2.0 * V * b.Cin * C * T, cbytes(V, b.Cin, C, T),
-          conv3d_run(src1(da1, C), p->F(p->wt), *dx, v, KD, b.Cin, C, true, math, p->st, p->F(p->wg_ws)));
+    CK(conv_halo(p, 1, 2.0 * V * b.Cin * C * T, cbytes(V, b.Cin, C, T), src1(da1, C), *dx, v,
+                 b.Cin, C, true, nullptr));
   }
   return SPFF_OK;
 }
@@ -916,6 +950,9 @@ void spff_plan_destroy(spff_plan* p) {
     (void)hipEventDestroy(r.b);
   }
   if (p->pe_dev) (void)hipFree(p->pe_dev);
+  if (p->ev_in) (void)hipEventDestroy(p->ev_in);
+  if (p->ev_halo) (void)hipEventDestroy(p->ev_halo);
+  if (p->st2) (void)hipStreamDestroy(p->st2);
   delete p;
 }
 

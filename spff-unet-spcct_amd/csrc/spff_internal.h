@@ -65,9 +65,13 @@ hipError_t conv3d_pack(const float* w, void* wpack, Vol vol, int KD, int Cin_w, 
 // writes per-tile InstanceNorm partials (>= conv3d_stats_bytes) that
 // conv3d_in_stats_fin turns into mean / rstd / al / de, replacing the two
 // slab_reduce passes of the unfused path.
+// dpart (depth-sharded halo overlap, when conv3d_splits_depth): 1 = only the interior
+// depth tiles, whose 3x3x3 stencil reads no halo slice; 2 = only the first and last
+// depth tiles; 0 = all.  1 and 2 together write exactly what 0 writes.
 hipError_t conv3d_run(const Src2& x, const void* wpack, const Dst2& y, Vol vol, int KD,
                       int Cin_w, int Cout_w, bool dgrad, int math, hipStream_t s,
-                      float* ws = nullptr, float* stats = nullptr);
+                      float* ws = nullptr, float* stats = nullptr, int dpart = 0);
+bool conv3d_splits_depth(Vol vol, int KD, int Cin_w, int Cout_w, bool dgrad, int math);
 bool conv3d_fuses_stats(Vol vol, int KD, int Cin, int Cout, int math);
 size_t conv3d_stats_bytes(Vol vol, int KD, int Cin, int Cout);
 hipError_t conv3d_in_stats_fin(const float* stats, Vol vol, int KD, int Cin, int Cout,

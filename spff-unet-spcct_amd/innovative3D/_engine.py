@@ -302,9 +302,15 @@ class Plan:
 
         def _halo(ctx, interior, sl, d_local, stream):
             try:
-                ws = self._ws
                 slab = view(interior - 4 * sl, (d_local + 2) * sl, torch.float32)
-                impl.halo(slab, int(sl), int(d_local))
+                cur = torch.cuda.current_stream(slab.device)
+                if stream and stream != cur.cuda_stream:
+                    # the engine's side stream (halo exchange overlapping the interior
+                    # depth tiles of the next convolution): issue the exchange there
+                    with torch.cuda.stream(torch.cuda.ExternalStream(stream, device=slab.device)):
+                        impl.halo(slab, int(sl), int(d_local))
+                else:
+                    impl.halo(slab, int(sl), int(d_local))
                 return 0
             except Exception as e:  # noqa: BLE001
                 self.coll_error = e

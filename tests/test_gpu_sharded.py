@@ -3,7 +3,9 @@ shard_rank + spff_coll) on ONE GPU: 2 and 4 ranks, each its own process and
 plan, exchange halos and all-reduce through host-staged gloo
 (innovative3D.sharded.TorchDepthColl).  Their gathered logits, the loss and
 the all-reduced gradients must match the unsharded engine on the same volume.
-Marked gpu."""
+The 16-deep case gives each of 2 ranks 4 depth tiles, so the split-bf16 convs run
+the halo exchange on the engine's side stream beside their interior depth tiles
+(engine.hip conv_halo).  Marked gpu."""
 import os
 import socket
 
@@ -17,6 +19,10 @@ pytestmark = pytest.mark.gpu
 K, BASE, SHAPE = 5, 8, (1, 5, 8, 32, 32)
 
 
+def _shape(depth):
+    return (SHAPE[0], SHAPE[1], depth, SHAPE[3], SHAPE[4])
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -25,12 +31,12 @@ def _free_port():
     return p
 
 
-def _model(math_mode):
+def _model(math_mode, depth=SHAPE[2]):
     import innovative3D.models as M
     from innovative3D.weightgen import synth_state
     core = M.build_spct_energyfilm_fourier(num_classes=K, base=BASE, in_channels=SHAPE[1])
     for b in core._blocks():
-        b.fgate._ensure_mask(SHAPE[2], "cpu")
+        b.fgate._ensure_mask(depth, "cpu")
     st = synth_state([(k, tuple(v.shape)) for k, v in core.state_dict().items()], seed=5)
     # a non-trivial FourierGate (mask / scale) so the sharded spectra matter
     for k in st:
@@ -42,13 +48,13 @@ def _model(math_mode):
     return core
 
 
-def _data():
+def _data(depth=SHAPE[2]):
     from innovative3D.synthetic import synthetic_batch
-    x, y = synthetic_batch(*SHAPE, num_classes=K, ignore_frac=0.05, seed=11)
+    x, y = synthetic_batch(*_shape(depth), num_classes=K, ignore_frac=0.05, seed=11)
     return x, y
 
 
-def _worker(rank, world, port, math_mode, out):
+def _worker(rank, world, port, math_mode, out, depth):
     import pathlib
     import sys
     root = pathlib.Path(__file__).resolve().parents[1]
@@ -58,9 +64,9 @@ def _worker(rank, world, port, math_mode, out):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.cuda.set_device(0)
-    core = _model(math_mode)
-    x, y = _data()
-    off, d = shard_bounds(SHAPE[2], world, rank)
+    core = _model(math_mode, depth)
+    x, y = _data(depth)
+    off, d = shard_bounds(depth, world, rank)
     step = DepthShardedSPFF(core, K, 255)
     loss, conf = step.step(x[:, :, off:off + d].contiguous().cuda(), y[:, off:off + d].contiguous().cuda())
     torch.cuda.synchronize()
@@ -72,23 +78,23 @@ def _worker(rank, world, port, math_mode, out):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("math_mode", ["f32", "bf16x6"])
-@pytest.mark.parametrize("world", [2, 4])
-def test_depth_sharded_engine_matches_unsharded(tmp_path, world, math_mode):
+@pytest.mark.parametrize("world,math_mode,depth", [
+    (2, "f32", 8), (4, "f32", 8), (2, "bf16x6", 8), (4, "bf16x6", 8), (2, "bf16x6", 16)])
+def test_depth_sharded_engine_matches_unsharded(tmp_path, world, math_mode, depth):
     import innovative3D.helpers as Hh
-    core = _model(math_mode)
-    x, y = _data()
+    core = _model(math_mode, depth)
+    x, y = _data(depth)
     logits = core(x.cuda())
     loss, conf = Hh.ce_dice_with_confusion(logits, y.cuda(), K, 255)
     loss.backward()
     ref = logits.detach().cpu().numpy()
     grads = {k: p.grad.cpu().numpy() for k, p in core.named_parameters() if p.grad is not None}
     out = str(tmp_path / "sh")
-    mp.spawn(_worker, args=(world, _free_port(), math_mode, out), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), math_mode, out, depth), nprocs=world, join=True)
     parts = [np.load(f"{out}.{r}.npz") for r in range(world)]
     lg = np.concatenate([p["logits"] for p in parts], axis=2)
     e = float(np.abs(lg - ref).max())
-    print(f"world {world} {math_mode}: max|dlogit| {e:.2e}, loss {float(parts[0]['loss']):.7f} "
+    print(f"world {world} {math_mode} D {depth}: max|dlogit| {e:.2e}, loss {float(parts[0]['loss']):.7f} "
           f"vs {float(loss):.7f}")
     assert e <= 1e-4 * float(np.abs(ref).max())
     assert abs(float(parts[0]["loss"]) - float(loss)) <= 1e-5 * abs(float(loss))
