@@ -94,6 +94,14 @@ struct StoreRows {  // C[m][n] -> p[m*ld + n] (+bias[n]), n < nmax
   __device__ int64_t col(int n) const { return n < nmax ? n : -1; }
   __device__ float bias_of(int n) const { return (bias && n < nmax) ? bias[n] : 0.f; }
   __device__ void put(int64_t idx, float v) const { p[idx] = v; }
+  // 16-B column quads (k_gemm_x<..., V4 = true>): columns n .. n+3, n % 4 == 0
+  static constexpr bool kVec = true;
+  __host__ __device__ bool vec_ok() const { return (ld & 3) == 0 && (nmax & 3) == 0; }
+  __device__ float4 bias4(int n) const {
+    return (bias && n < nmax) ? *reinterpret_cast<const float4*>(bias + n)
+                              : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  __device__ void put4(int64_t idx, float4 v) const { *reinterpret_cast<float4*>(p + idx) = v; }
 };
 struct StoreUp {  // C[m][n], n = ij*Cout + co -> y[high(m,ij)*Cout + co] + bias[co]
   float* p; int Cout; const float* bias; int D, Hl, Wl; int64_t M; int nsub;
@@ -107,6 +115,13 @@ struct StoreUp {  // C[m][n], n = ij*Cout + co -> y[high(m,ij)*Cout + co] + bias
   }
   __device__ float bias_of(int n) const { return n < nsub * Cout ? bias[n % Cout] : 0.f; }
   __device__ void put(int64_t idx, float v) const { p[idx] = v; }
+  static constexpr bool kVec = true;
+  __host__ __device__ bool vec_ok() const { return (Cout & 3) == 0; }
+  __device__ float4 bias4(int n) const {
+    return n < nsub * Cout ? *reinterpret_cast<const float4*>(bias + n % Cout)
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  __device__ void put4(int64_t idx, float4 v) const { *reinterpret_cast<float4*>(p + idx) = v; }
 };
 
 // --- Linear-layer functors (SwinUNETR path, swin.hip) ---
@@ -159,6 +174,10 @@ struct StoreRowsRes {  // y[m][n] = res[m][n] + v + bias[n]   (residual add)
     const int n = (int)(idx & 0xffff);
     p[m * ld + n] = (res ? res[m * ldr + n] : 0.f) + v;
   }
+  static constexpr bool kVec = false;
+  __host__ __device__ bool vec_ok() const { return false; }
+  __device__ float4 bias4(int) const { return make_float4(0.f, 0.f, 0.f, 0.f); }
+  __device__ void put4(int64_t, float4) const {}
 };
 __device__ __forceinline__ float gelu_erf(float x) {
   return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
@@ -176,6 +195,10 @@ struct StoreGelu {  // pre[m][n] = v + bias[n]; act[m][n] = gelu(pre)  (nn.GELU,
     pre[idx] = v;
     act[idx] = gelu_erf(v);
   }
+  static constexpr bool kVec = false;
+  __host__ __device__ bool vec_ok() const { return false; }
+  __device__ float4 bias4(int) const { return make_float4(0.f, 0.f, 0.f, 0.f); }
+  __device__ void put4(int64_t, float4) const {}
 };
 struct StoreGeluBwd {  // dpre[m][n] = v * gelu'(pre[m][n])
   float* p; const float* pre; int ld, nmax; int64_t M;
@@ -183,6 +206,10 @@ struct StoreGeluBwd {  // dpre[m][n] = v * gelu'(pre[m][n])
   __device__ int64_t col(int n) const { return n < nmax ? n : -1; }
   __device__ float bias_of(int) const { return 0.f; }
   __device__ void put(int64_t idx, float v) const { p[idx] = v * gelu_erf_grad(pre[idx]); }
+  static constexpr bool kVec = false;
+  __host__ __device__ bool vec_ok() const { return false; }
+  __device__ float4 bias4(int) const { return make_float4(0.f, 0.f, 0.f, 0.f); }
+  __device__ void put4(int64_t, float4) const {}
 };
 struct StoreDst2 {  // C[m][n] -> dst (two-source channel view), optionally accumulated
   Dst2 y; int nmax; int acc; int64_t M;
@@ -195,6 +222,10 @@ struct StoreDst2 {  // C[m][n] -> dst (two-source channel view), optionally accu
     float* q = n < y.split ? y.p0 + m * y.ld0 + n : y.p1 + m * y.ld1 + (n - y.split);
     *q = acc ? *q + v : v;
   }
+  static constexpr bool kVec = false;
+  __host__ __device__ bool vec_ok() const { return false; }
+  __device__ float4 bias4(int) const { return make_float4(0.f, 0.f, 0.f, 0.f); }
+  __device__ void put4(int64_t, float4) const {}
 };
 
 // ---------------------------------------------------------------- C = A.B --
@@ -320,7 +351,7 @@ __device__ __forceinline__ int gx_bsw(int k) {
   constexpr int L = BN == 128 ? 0 : BN == 64 ? 1 : 2;
   return ((k & 3) >> L) | (((k >> 3) & 1) << (2 - L));
 }
-template <class AL, class CS, int BN>
+template <class AL, class CS, int BN, bool V4>
 __global__ __launch_bounds__(256, 2) void k_gemm_x(AL A, const float* __restrict__ B, CS C,
                                                    int kpad, int npad) {
   constexpr int CB = BN / 16, NRB = BN / 32;  // 16-wide col blocks; B float4 per thread
@@ -431,37 +462,63 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x(AL A, const float* __restrict
         const i16x8g v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         b[p] = __builtin_bit_cast(bf16x8g, v);
       }
+      // V4: operands swapped (B^T . A^T), so the lane holds 4 consecutive output COLUMNS
+      // of one row, stored as one 16-B write (the epilogue is store-issue bound otherwise);
+      // else the lane holds 4 rows of one column (row-contiguous lanes for narrow pitches)
+      auto mf = [](const bf16x8g& x, const bf16x8g& y, f32x4g c) {
+        return V4 ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(y, x, c, 0, 0, 0)
+                  : __builtin_amdgcn_mfma_f32_16x16x32_bf16(x, y, c, 0, 0, 0);
+      };
 #pragma unroll
       for (int rb = 0; rb < 2; ++rb) {
         f32x4g c = acc[rb][cb];
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb][1], b[1], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb][0], b[2], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb][2], b[0], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb][0], b[1], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb][1], b[0], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb][0], b[0], c, 0, 0, 0);
+        c = mf(a[rb][1], b[1], c);
+        c = mf(a[rb][0], b[2], c);
+        c = mf(a[rb][2], b[0], c);
+        c = mf(a[rb][0], b[1], c);
+        c = mf(a[rb][1], b[0], c);
+        c = mf(a[rb][0], b[0], c);
         acc[rb][cb] = c;
       }
     }
   }
   const float sg = ((nkc - 1) & 1) ? -1.f : 1.f;
-  int64_t cc[CB];
-  float bv[CB];
+  if constexpr (V4) {
+    // lane: row 16 rb + l16 of the wave's 32, columns n0 + 16 cb + 4 g + (0..3)
+    int64_t rh[2];
 #pragma unroll
-  for (int cb = 0; cb < CB; ++cb) {
-    cc[cb] = C.col(n0 + cb * 16 + l16);
-    bv[cb] = C.bias_of(n0 + cb * 16 + l16);
-  }
+    for (int rb = 0; rb < 2; ++rb) rh[rb] = C.prep(m0 + wave * 32 + rb * 16 + l16);
 #pragma unroll
-  for (int rb = 0; rb < 2; ++rb)
+    for (int cb = 0; cb < CB; ++cb) {
+      const int n = n0 + cb * 16 + 4 * g;
+      const int64_t c0 = C.col(n);  // the quad is valid or not as a whole (vec_ok)
+      const float4 bq = C.bias4(n);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int64_t rh = C.prep(m0 + wave * 32 + rb * 16 + 4 * g + r);
-      if (rh < 0) continue;
-#pragma unroll
-      for (int cb = 0; cb < CB; ++cb)
-        if (cc[cb] >= 0) C.put(rh + cc[cb], sg * acc[rb][cb][r] + bv[cb]);
+      for (int rb = 0; rb < 2; ++rb)
+        if (rh[rb] >= 0 && c0 >= 0)
+          C.put4(rh[rb] + c0, make_float4(sg * acc[rb][cb][0] + bq.x, sg * acc[rb][cb][1] + bq.y,
+                                          sg * acc[rb][cb][2] + bq.z, sg * acc[rb][cb][3] + bq.w));
     }
+  } else {
+    // lane: rows 16 rb + 4 g + (0..3), column n0 + 16 cb + l16
+    int64_t cc[CB];
+    float bv[CB];
+#pragma unroll
+    for (int cb = 0; cb < CB; ++cb) {
+      cc[cb] = C.col(n0 + cb * 16 + l16);
+      bv[cb] = C.bias_of(n0 + cb * 16 + l16);
+    }
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t rh = C.prep(m0 + wave * 32 + rb * 16 + 4 * g + r);
+        if (rh < 0) continue;
+#pragma unroll
+        for (int cb = 0; cb < CB; ++cb)
+          if (cc[cb] >= 0) C.put(rh + cc[cb], sg * acc[rb][cb][r] + bv[cb]);
+      }
+  }
 #pragma unroll
   for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
@@ -472,10 +529,10 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x(AL A, const float* __restrict
 }
 
 // persistent row tiles: as many workgroups as fit the chip at once
-template <int BN, class AL, class CS>
+template <int BN, bool V4, class AL, class CS>
 static void launch_gemm_x(const AL& A, const float* B, const CS& C, dim3 grid, int kpad, int npad,
                           hipStream_t s) {
-  auto kern = k_gemm_x<AL, CS, BN>;
+  auto kern = k_gemm_x<AL, CS, BN, V4>;
   static int per_cu = 0;
   if (!per_cu &&
       hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0) != hipSuccess)
@@ -494,9 +551,14 @@ static hipError_t launch_gemm(const AL& A, const float* B, const CS& C, int64_t 
   const int BN = npad % 128 == 0 ? 128 : npad % 64 == 0 ? 64 : 32;
   dim3 grid((unsigned)cdiv64(M, G_BM), npad / BN);
   if (split) {
-    if (BN == 128) launch_gemm_x<128>(A, B, C, grid, kpad, npad, s);
-    else if (BN == 64) launch_gemm_x<64>(A, B, C, grid, kpad, npad, s);
-    else launch_gemm_x<32>(A, B, C, grid, kpad, npad, s);
+    // 16-B stores of column quads where the output functor and its pitch allow
+    const bool v4 = CS::kVec && C.vec_ok();
+    if (BN == 128) v4 ? launch_gemm_x<128, true>(A, B, C, grid, kpad, npad, s)
+                      : launch_gemm_x<128, false>(A, B, C, grid, kpad, npad, s);
+    else if (BN == 64) v4 ? launch_gemm_x<64, true>(A, B, C, grid, kpad, npad, s)
+                          : launch_gemm_x<64, false>(A, B, C, grid, kpad, npad, s);
+    else v4 ? launch_gemm_x<32, true>(A, B, C, grid, kpad, npad, s)
+            : launch_gemm_x<32, false>(A, B, C, grid, kpad, npad, s);
     return hipGetLastError();
   }
   if (BN == 128)
