@@ -73,8 +73,11 @@ typedef struct spff_cfg {
 #define SPFF_MEM_LEAN 2
 
 /* The shard group's collectives, implemented by the caller (e.g. RCCL through
- * torch.distributed) and called by the engine in stream order on the stream of
- * the current spff_forward / spff_backward.  Return 0 on success.
+ * torch.distributed) and called by the engine in stream order on the stream
+ * argument: the stream of the current spff_forward / spff_backward, or -- for a
+ * halo that overlaps a convolution's interior depth tiles -- the plan's side
+ * stream, which the engine has made wait for the data and whose completion the
+ * main stream waits for.  Issue the work on the stream given.  Return 0 on success.
  *   allreduce: in-place sum over the group of n elements at device pointer buf
  *              (dtype 0 = fp32, 1 = fp64).
  *   halo:      interior points at slice 0 of a [d_local][slice_floats] slab
