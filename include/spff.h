@@ -65,8 +65,17 @@ typedef struct spff_cfg {
    * rest in the backward (~1.7 KB per voxel: one 5 x 512^3 volume fits one MI355X;
    * +~3 % step time); SPFF_MEM_AUTO (0) = lean from 2^26 voxels per plan. */
   int memory_mode;
-  int reserved[4];                          /* zero */
+  /* the axis a sharded plan (shard_world > 1) splits: SPFF_SHARD_DEPTH (0) -- above;
+   * SPFF_SHARD_HEIGHT (1) -- the registry layout [B, 1, 5, H, W]: this
+   * plan holds global rows [shard_rank * height, (shard_rank + 1) * height) of a volume
+   * of height shard_world * height; height and width multiples of 8 (the three (1,2,2)
+   * pools stay rank-local), any batch.  Same collectives table. */
+  int shard_axis;
+  int reserved[3];                          /* zero */
 } spff_cfg;
+
+#define SPFF_SHARD_DEPTH 0
+#define SPFF_SHARD_HEIGHT 1
 
 #define SPFF_MEM_AUTO 0
 #define SPFF_MEM_FULL 1

@@ -123,8 +123,14 @@ struct spff_plan {
          wg_ws = 0, wt = 0, cst = 0;
   size_t G_out = 0, G_dy2 = 0, G_da1 = 0, G_dx = 0, dskip[3] = {0, 0, 0};
   size_t part_d = 0;  // sharded plans: fp64 IN partials [B][C][2]
+  // height-sharded plans (spff_cfg.shard_axis = SPFF_SHARD_HEIGHT, hshard.hip): the
+  // row-padded conv input / output, the boundary-row staging slab, and the gate
+  // parameter gradients of ranks other than 0 (the gates are evaluated replicated)
+  bool hsh = false;
+  int hmul = 1;  // global / local rows
+  size_t hxp = 0, hyp = 0, hst = 0, gdum = 0;
   size_t total = 0;
-  Coll co;             // depth-sharding group (world 1: unsharded)
+  Coll co;             // sharding group (world 1: unsharded)
   bool coll_set = false;
   spff_grad_ready_fn grad_fn = nullptr;  // data-parallel gradient-ready hook
   void* grad_ctx = nullptr;
@@ -257,19 +263,26 @@ int build_plan(spff_plan* p) {
             (c.memory_mode == SPFF_MEM_AUTO &&
              (int64_t)c.batch * c.depth * c.height * c.width >= (int64_t(1) << 26));
   const int world = c.shard_world > 1 ? c.shard_world : 1;
+  const bool hsh = world > 1 && c.shard_axis == SPFF_SHARD_HEIGHT;
   if (world > 1) {
-    if (c.batch != 1) return fail(SPFF_EINVAL, "depth-sharded plans take batch == 1");
+    if (c.shard_axis != SPFF_SHARD_DEPTH && c.shard_axis != SPFF_SHARD_HEIGHT)
+      return fail(SPFF_EINVAL, "shard_axis must be SPFF_SHARD_DEPTH or SPFF_SHARD_HEIGHT");
+    if (!hsh && c.batch != 1) return fail(SPFF_EINVAL, "depth-sharded plans take batch == 1");
+    if (hsh && (c.height % 8 || c.width % 8))
+      return fail(SPFF_ESHAPE, "height-sharded plans take local height and width multiples of 8");
     if (c.shard_rank < 0 || c.shard_rank >= world) return fail(SPFF_EINVAL, "bad shard_rank");
   }
+  p->hsh = hsh;
+  p->hmul = hsh ? world : 1;
   p->co.world = world;
   p->co.rank = world > 1 ? c.shard_rank : 0;
-  p->co.D_glob = c.depth * world;
-  p->co.d_off = p->co.rank * c.depth;
+  p->co.D_glob = hsh ? c.depth : c.depth * world;
+  p->co.d_off = hsh ? 0 : p->co.rank * c.depth;
   p->f = c.base;
   p->KD = c.ksd;
   p->K = c.num_classes;
   p->ldx = rup(c.in_ch, 8);
-  const int dh = (world > 1 && c.ksd == 3) ? 1 : 0;
+  const int dh = (world > 1 && !hsh && c.ksd == 3) ? 1 : 0;
   for (int l = 0; l < 4; ++l) {
     p->vol[l] = Vol{c.batch, c.depth, c.height >> l, c.width >> l};
     p->vol[l].dh = dh;
@@ -336,6 +349,7 @@ int build_plan(spff_plan* p) {
   const auto slice = [&](const Vol& v, int C) { return (size_t)v.H * v.W * C * sizeof(float); };
   p->x_cl = p->alloc_halo(nvox(v0) * p->ldx * sizeof(float), slice(v0, p->ldx));
   size_t red_ws = 0, red_out = 0, red_out4 = 0, gs = 0, bcd = 0, wg = 0, wt = 0, cst = 0;
+  size_t hx = 0, hst = 0, gd = 0;
   for (int i = 0; i < 7; ++i) {
     Blk& b = p->blk[i];
     const Vol& v = p->vol[b.lvl];
@@ -366,14 +380,27 @@ int build_plan(spff_plan* p) {
       b.t = p->alloc((size_t)b.C * D * 4);
       b.bt = p->alloc((size_t)b.C * D * 4);
       b.hid = p->alloc((size_t)32 * D * 4);
-      if (world > 1) b.spec = p->alloc((size_t)B * (p->co.D_glob / 2 + 1) * 2 * sizeof(double));
+      if (world > 1 && !hsh)
+        b.spec = p->alloc((size_t)B * (p->co.D_glob / 2 + 1) * 2 * sizeof(double));
     }
     red_ws = std::max(red_ws, slab_reduce_ws_bytes(v, b.C, b.tail() && SPFF_RED_FUSE ? 6 : 2));
     red_out = std::max(red_out, (size_t)B * b.C * D * 2 * sizeof(float));
     if (b.tail() && SPFF_RED_FUSE)
       red_out4 = std::max(red_out4, (size_t)B * b.C * D * 4 * sizeof(float));
-    gs = std::max(gs, world > 1 ? gates_sh_scratch_bytes(v, b.C, p->co.D_glob)
-                                : gates_scratch_bytes(v, b.C));
+    gs = std::max(gs, world > 1 && !hsh ? gates_sh_scratch_bytes(v, b.C, p->co.D_glob)
+                                        : gates_scratch_bytes(v, b.C));
+    if (hsh) {  // row-padded conv operands (input, output / zero-row dy) and staging
+      Vol vp = v;
+      vp.H += 2;
+      const int lmax = rup(std::max(b.Cin, b.C), 8);
+      hx = std::max(hx, hpad_floats(v, lmax));
+      hst = std::max(hst, hstage_floats(v, lmax));
+      wg = std::max(wg, conv3d_wgrad_ws_bytes(vp, p->KD, b.Cin, b.C));
+      wg = std::max(wg, conv3d_wgrad_ws_bytes(vp, p->KD, b.C, b.C));
+      wg = std::max(wg, conv3d_splitk_bytes(vp, p->KD, b.Cin, b.C));
+      wg = std::max(wg, conv3d_splitk_bytes(vp, p->KD, b.C, b.C));
+      gd = std::max(gd, (size_t)(b.pr1 - (b.b2 + b.C)) + (size_t)(b.se1 - b.se0));
+    }
     bcd = std::max(bcd, bcdz);
     wg = std::max(wg, conv3d_wgrad_ws_bytes(v, p->KD, b.Cin, b.C));
     wg = std::max(wg, conv3d_wgrad_ws_bytes(v, p->KD, b.C, b.C));
@@ -443,6 +470,12 @@ int build_plan(spff_plan* p) {
     for (int u = 0; u < 3; ++u) p->up[u].out = p->G_dx;
   }
   if (world > 1) p->part_d = p->alloc((size_t)B * 8 * f * 2 * sizeof(double));
+  if (hsh) {
+    p->hxp = p->alloc(hx * sizeof(float));
+    p->hyp = p->alloc(hx * sizeof(float));
+    p->hst = p->alloc(hst * sizeof(float));
+    p->gdum = p->alloc(std::max<size_t>(gd, 1) * sizeof(float));
+  }
 
   host_pe(p->co.D_glob, p->pe_host);  // global depths; a slab reads columns d_off + d  // uploaded on the first forward (plan creation needs no GPU)
   return SPFF_OK;
@@ -502,6 +535,55 @@ int halo_src(spff_plan* p, const Src2& x, const Vol& v, hipStream_t st = nullptr
   if (x.p1 != x.p0) CK(halo(p, x.p1, v, x.ld1, st));
   return SPFF_OK;
 }
+// ---- height-sharded plans (hshard.hip): every 3x3x3 conv runs on a row-padded copy ----
+Vol conv_vol(const spff_plan* p, Vol v) {
+  if (p->hsh) v.H += 2;
+  return v;
+}
+// x row-padded into xp (pitch rup(cin, 8)); exch: rows 0 / H + 1 = the neighbours'
+// boundary rows through spff_coll.halo (zero at the global ends), else zero rows
+int hpad_src(spff_plan* p, const Src2& x, const Vol& v, int cin, float* xp, bool exch) {
+  const int ldp = rup(cin, 8);
+  float* stg = exch ? p->F(p->hst) : nullptr;
+  HIPCK(hpad(x, cin, xp, stg, v, ldp, p->st));
+  if (!exch) return SPFF_OK;
+  const int64_t S = (int64_t)v.B * v.D * v.W * ldp;
+  if (p->co.halo(p->co.ctx, stg + S, S, 2, p->st) != 0)
+    return fail(SPFF_EHIP, "halo exchange failed");
+  HIPCK(hfill(xp, stg, v, ldp, p->co.rank == 0, p->co.rank == p->co.world - 1, p->st));
+  return SPFF_OK;
+}
+int conv_h(spff_plan* p, int cls, double flops, double bytes, const Src2& x, const Dst2& y,
+           const Vol& v, int Cin_w, int Cout_w, bool dgrad) {
+  const int cin = dgrad ? Cout_w : Cin_w, cout = dgrad ? Cin_w : Cout_w;
+  float* xp = p->F(p->hxp);
+  float* yp = p->F(p->hyp);
+  CK(hpad_src(p, x, v, cin, xp, true));
+  PROFB(p, cls, flops, bytes,
+        conv3d_run(src1(xp, rup(cin, 8)), p->F(p->wt), dst1(yp, cout), conv_vol(p, v), p->KD,
+                   Cin_w, Cout_w, dgrad, p->cfg.math, p->st, p->F(p->wg_ws), nullptr));
+  HIPCK(hunpad(yp, y, cout, v, p->st));
+  return SPFF_OK;
+}
+// weight gradient of a 3x3x3 conv (height-sharded: over the padded volume, dy with
+// zero rows 0 / H + 1, so only the local output rows contribute)
+int conv_wgrad(spff_plan* p, double flops, double bytes, const Src2& x, const float* dy, float* dw,
+               const Vol& v, int Cin, int Cout) {
+  if (!p->hsh) {
+    PROFB(p, 2, flops, bytes,
+          conv3d_wgrad(x, dy, Cout, dw, v, p->KD, Cin, Cout, p->cfg.math, p->F(p->wg_ws), p->st));
+    return SPFF_OK;
+  }
+  float* xp = p->F(p->hxp);
+  float* dp = p->F(p->hyp);
+  CK(hpad_src(p, x, v, Cin, xp, true));
+  CK(hpad_src(p, src1(dy, Cout), v, Cout, dp, false));
+  PROFB(p, 2, flops, bytes,
+        conv3d_wgrad(src1(xp, rup(Cin, 8)), dp, rup(Cout, 8), dw, conv_vol(p, v), p->KD, Cin, Cout,
+                     p->cfg.math, p->F(p->wg_ws), p->st));
+  return SPFF_OK;
+}
+
 // halo exchange of x + the 3x3x3 convolution reading it.  Depth-sharded plans whose
 // conv can split its depth tiles run the exchange on the side stream st2 while the
 // interior depth tiles (which read no halo slice) compute on st, then the first and
@@ -510,6 +592,7 @@ int halo_src(spff_plan* p, const Src2& x, const Vol& v, hipStream_t st = nullptr
 // boundary one adds its time to the same class).
 int conv_halo(spff_plan* p, int cls, double flops, double bytes, const Src2& x, const Dst2& y,
               const Vol& v, int Cin_w, int Cout_w, bool dgrad, float* stats) {
+  if (p->hsh) return conv_h(p, cls, flops, bytes, x, y, v, Cin_w, Cout_w, dgrad);
   const int KD = p->KD, math = p->cfg.math;
   const bool ovl = v.dh && !stats && conv3d_splits_depth(v, KD, Cin_w, Cout_w, dgrad, math);
   if (!ovl) {
@@ -544,7 +627,7 @@ int in_stats(spff_plan* p, const Vol& v, int C, size_t y, size_t mean, size_t rs
   a.y = p->F(y);
   const bool sh = p->co.on();
   double* pd = sh ? p->D64(p->part_d) : nullptr;
-  const double N = (double)p->co.D_glob * v.H * v.W;
+  const double N = (double)p->co.D_glob * v.H * p->hmul * v.W;
   PROFB(p, 4, 0.0, 4.0 * (double)nvox(v) * C,
         slab_reduce(RED_SUM, a, v, C, p->F(p->red_out), p->F(p->red_ws), p->st));
   if (sh) {  // per-(b,c) sums over the slab -> group sum -> global mean
@@ -581,7 +664,7 @@ int in_bwd(spff_plan* p, const Vol& v, int C, int64_t gamma, int64_t beta) {
   HIPCK(in_bwd_dgb(pd, p->DP(gamma), p->DP(beta), v.B, C, p->st));  // local partial grads
   HIPCK(p->co.sum_f64(pd, (int64_t)v.B * C * 2, p->st));
   HIPCK(in_bwd_fin(pd, p->F(p->kk1), p->F(p->kk2), v.B * C,
-                   (double)p->co.D_glob * v.H * v.W, p->st));
+                   (double)p->co.D_glob * v.H * p->hmul * v.W, p->st));
   return SPFF_OK;
 }
 
@@ -636,7 +719,12 @@ int fwd_block(spff_plan* p, Blk& b, const Src2& in) {
         slab_reduce(RED_ACT, a, v, C, p->F(b.Sa), p->F(p->red_ws), p->st));
     GateParams gp = gate_params(p, b);
     GateSaved sv = gate_saved(p, b);
-    if (p->co.on())
+    if (p->hsh) {  // partial (h, w) sums of the local rows -> global; gates replicated
+      HIPCK(p->co.sum_f32(p->F(b.Sa), (int64_t)v.B * C * v.D, p->st));
+      Vol vg = v;
+      vg.H *= p->hmul;
+      HIPCK(gates_fwd(gp, p->F(b.Sa), sv, vg, C, p->F(p->gscr), p->st));
+    } else if (p->co.on())
       HIPCK(gates_fwd_sh(gp, p->F(b.Sa), sv, v, C, p->F(p->gscr), p->co, p->st));
     else
       HIPCK(gates_fwd(gp, p->F(b.Sa), sv, v, C, p->F(p->gscr), p->st));
@@ -696,6 +784,25 @@ int lean_dec_input(spff_plan* p, int bi, Src2* in) {
   return halo_src(p, *in, p->vol[d.lvl]);
 }
 
+// height-sharded ranks other than 0: the block's replicated gate parameter gradients go
+// to scratch and their dparams ranges are zeroed (the flat gradient is SUM-reduced)
+int hsh_gate_grads(spff_plan* p, const Blk& b, GateGrads& gg) {
+  if (p->co.rank == 0) return SPFF_OK;
+  const int64_t g0 = b.b2 + b.C, span = b.pr1 - g0;
+  float* dum = p->F(p->gdum);
+  auto mv = [&](float*& q, int64_t off, bool se) {
+    if (q) q = se ? dum + span + (off - b.se0) : dum + (off - g0);
+  };
+  mv(gg.fw0, b.fw0, false); mv(gg.fb0, b.fb0, false); mv(gg.fw2, b.fw2, false);
+  mv(gg.fb2, b.fb2, false); mv(gg.mask, b.mask, false); mv(gg.mag, b.mag, false);
+  mv(gg.sw0, b.sw0, true); mv(gg.sb0, b.sb0, true); mv(gg.sw2, b.sw2, true);
+  mv(gg.sb2, b.sb2, true);
+  if (span > 0) HIPCK(hipMemsetAsync(p->DP(g0), 0, span * sizeof(float), p->st));
+  if (b.se1 > b.se0)
+    HIPCK(hipMemsetAsync(p->DP(b.se0), 0, (b.se1 - b.se0) * sizeof(float), p->st));
+  return SPFF_OK;
+}
+
 int bwd_block(spff_plan* p, Blk& b, const float* dout, const Dst2* dx, const Src2& in_saved,
               int dec_bi = -1) {
   const Vol& v = p->vol[b.lvl];
@@ -730,7 +837,16 @@ int bwd_block(spff_plan* p, Blk& b, const float* dout, const Dst2* dx, const Src
     gg.sb0 = b.post_se ? p->DP(b.sb0) : nullptr;
     gg.sw2 = b.post_se ? p->DP(b.sw2) : nullptr;
     gg.sb2 = b.post_se ? p->DP(b.sb2) : nullptr;
-    if (p->co.on())
+    if (p->hsh) {
+      // the per-(b,c,d) sums of dout, dout*a2 summed over the group; every rank then
+      // derives the same A, Bc and gate parameter gradients -- rank 0 keeps the latter
+      HIPCK(p->co.sum_f32(p->F(p->red_out), (int64_t)v.B * C * v.D * 2, p->st));
+      CK(hsh_gate_grads(p, b, gg));
+      Vol vg = v;
+      vg.H *= p->hmul;
+      HIPCK(gates_bwd(gp, sv, p->F(b.Sa), p->F(p->red_out), gg, p->F(p->Abuf), p->F(p->Bbuf), vg,
+                      C, p->F(p->gscr), p->st));
+    } else if (p->co.on())
       HIPCK(gates_bwd_sh(gp, sv, p->F(b.Sa), p->F(p->red_out), gg, p->F(p->Abuf), p->F(p->Bbuf),
                          v, C, p->F(p->gscr), p->co, p->st));
     else
@@ -764,9 +880,7 @@ int bwd_block(spff_plan* p, Blk& b, const float* dout, const Dst2* dx, const Src
     CK(halo(p, da1, v, C));
     a1 = src1(da1, C);
   }
-  PROFB(p, 2, 2.0 * V * C * C * T, cbytes(V, C, C, T),
-       conv3d_wgrad(a1, dy2, C, p->DP(b.c2.w), v, KD, C, C, p->cfg.math,
-                    p->F(p->wg_ws), p->st));
+  CK(conv_wgrad(p, 2.0 * V * C * C * T, cbytes(V, C, C, T), a1, dy2, p->DP(b.c2.w), v, C, C));
   const int math = p->cfg.math;
   HIPCK(conv3d_pack(p->P(b.c2.w), p->F(p->wt), v, KD, C, C, true, math, p->st));
   CK(conv_halo(p, 1, 2.0 * V * C * C * T, cbytes(V, C, C, T), src1(dy2, C), dst1(da1, C), v, C, C,
@@ -784,9 +898,8 @@ int bwd_block(spff_plan* p, Blk& b, const float* dout, const Dst2* dx, const Src
                        C, p->st));
   }
   if (p->lean && dec_bi >= 0) CK(lean_dec_input(p, dec_bi, &in));
-  PROFB(p, 2, 2.0 * V * b.Cin * C * T, cbytes(V, b.Cin, C, T),
-       conv3d_wgrad(in, da1, C, p->DP(b.c1.w), v, KD, b.Cin, C, p->cfg.math, p->F(p->wg_ws),
-                    p->st));
+  CK(conv_wgrad(p, 2.0 * V * b.Cin * C * T, cbytes(V, b.Cin, C, T), in, da1, p->DP(b.c1.w), v,
+                b.Cin, C));
   if (dx) {
     HIPCK(conv3d_pack(p->P(b.c1.w), p->F(p->wt), v, KD, b.Cin, C, true, math, p->st));
     CK(conv_halo(p, 1, 2.0 * V * b.Cin * C * T, cbytes(V, b.Cin, C, T), src1(da1, C), *dx, v,

@@ -222,7 +222,7 @@ hipError_t bn_eval(const float* rmean, const float* rvar, const float* gamma, co
 hipError_t bn_bwd_stats(const float* sums, float* dgamma, float* dbeta, float* k1, float* k2,
                         Vol vol, int C, hipStream_t s, int eval = 0);
 
-// Depth sharding: the shard group's collectives, supplied by the caller through
+// Depth / height sharding: the shard group's collectives, supplied by the caller through
 // spff_coll (include/spff.h).  world == 1: unsharded, every call is a no-op.
 struct Coll {
   int world = 1, rank = 0, d_off = 0, D_glob = 0;
@@ -233,6 +233,10 @@ struct Coll {
   hipError_t sum_f64(double* buf, int64_t n, hipStream_t s) const {
     if (!on()) return hipSuccess;
     return allreduce(ctx, buf, n, 1, s) == 0 ? hipSuccess : hipErrorUnknown;
+  }
+  hipError_t sum_f32(float* buf, int64_t n, hipStream_t s) const {
+    if (!on()) return hipSuccess;
+    return allreduce(ctx, buf, n, 0, s) == 0 ? hipSuccess : hipErrorUnknown;
   }
 };
 
@@ -277,6 +281,19 @@ hipError_t gates_bwd_sh(const GateParams& gp, const GateSaved& sv, const float* 
                         const float* Sg, GateGrads& gg, float* A, float* Bc, Vol vol, int C,
                         float* scratch, const Coll& co, hipStream_t s);
 size_t gates_sh_scratch_bytes(Vol vol, int C, int D_glob);
+
+// ------------------------------------------------------- height sharding --
+// (hshard.hip) row-padded conv inputs of a height-sharded plan: xp = [B][D][H + 2][W][ldp]
+// with rows 1 .. H from x (Src2: two sources, source-0 activation), rows 0 / H + 1 zero;
+// stage (optional) = [recv_lo | send_lo | send_hi | recv_hi] slab of B D W ldp floats each:
+// hpad writes the send rows, the caller exchanges them (spff_coll.halo at d_local = 2),
+// hfill copies the received rows into rows 0 / H + 1 (zlo / zhi: global end, zero).
+size_t hpad_floats(Vol v, int ldp);
+size_t hstage_floats(Vol v, int ldp);
+hipError_t hpad(const Src2& x, int cin, float* xp, float* stage, Vol v, int ldp, hipStream_t s);
+hipError_t hfill(float* xp, const float* stage, Vol v, int ldp, int zlo, int zhi, hipStream_t s);
+// y (local rows) <- rows 1 .. H of a conv output over the padded volume (pitch C)
+hipError_t hunpad(const float* yp, const Dst2& y, int C, Vol v, hipStream_t s);
 
 // ------------------------------------------------------------------ misc --
 hipError_t ncdhw_to_ndhwc(const float* x, float* y, Vol vol, int C, int ldy, hipStream_t s);

@@ -30,7 +30,7 @@ class spff_cfg(ctypes.Structure):
         ("base", ctypes.c_int), ("ksd", ctypes.c_int), ("use_efilm", ctypes.c_int),
         ("use_fgate", ctypes.c_int), ("use_se", ctypes.c_int), ("use_specse", ctypes.c_int),
         ("math", ctypes.c_int), ("shard_world", ctypes.c_int), ("shard_rank", ctypes.c_int),
-        ("memory_mode", ctypes.c_int), ("reserved", ctypes.c_int * 4),
+        ("memory_mode", ctypes.c_int), ("shard_axis", ctypes.c_int), ("reserved", ctypes.c_int * 3),
     ]
 
 
@@ -224,7 +224,7 @@ class Plan:
 
     def __init__(self, batch, in_ch, depth, height, width, num_classes, base=32, ksd=3,
                  efilm=True, fgate=True, se=True, specse=True, device=None, math=None,
-                 shard_world=1, shard_rank=0, memory=None):
+                 shard_world=1, shard_rank=0, memory=None, shard_axis=0):
         math = default_math() if math is None else math
         if math not in MATH_NAMES:
             raise SpffError(f"math={math!r}: expected one of {sorted(MATH_NAMES)}")
@@ -240,8 +240,10 @@ class Plan:
                        (memory == "auto" and batch * depth * height * width >= 1 << 26)
                        else "full")
         cfg.shard_world, cfg.shard_rank = int(shard_world), int(shard_rank)
+        # 0 = SPFF_SHARD_DEPTH (BASELINE config 4), 1 = SPFF_SHARD_HEIGHT (registry layout)
+        cfg.shard_axis = int(shard_axis)
         self.math = math
-        self.shard = (int(shard_world), int(shard_rank))
+        self.shard = (int(shard_world), int(shard_rank), int(shard_axis))
         cfg.batch, cfg.in_ch, cfg.depth, cfg.height, cfg.width = batch, in_ch, depth, height, width
         cfg.num_classes, cfg.base, cfg.ksd = num_classes, base, ksd
         cfg.use_efilm, cfg.use_fgate, cfg.use_se, cfg.use_specse = (int(bool(efilm)), int(bool(fgate)),
@@ -451,18 +453,23 @@ def release_plans(owner=None) -> None:
         _OWNER_PLANS.pop(owner, None)
 
 
+def shard_key(shard) -> Tuple[int, int, int]:
+    """(world, rank[, axis]) -> (world, rank, axis); axis 0 = depth, 1 = height"""
+    sh = tuple(int(v) for v in shard)
+    return sh if len(sh) == 3 else (sh[0], sh[1], 0)
+
+
 def get_plan(owner=None, tag: str = "", **kw) -> Plan:
     """The plan of ``owner`` (an nn.Module) for tag ``tag`` and this shape/flag set."""
     key = (kw["batch"], kw["in_ch"], kw["depth"], kw["height"], kw["width"], kw["num_classes"],
            kw.get("base", 32), kw.get("ksd", 3), bool(kw.get("efilm", True)),
            bool(kw.get("fgate", True)), bool(kw.get("se", True)), bool(kw.get("specse", True)),
-           kw.get("math") or default_math(), tuple(kw.get("shard", (1, 0))),
+           kw.get("math") or default_math(), shard_key(kw.get("shard", (1, 0))),
            kw.get("memory") or default_memory())
 
     def make():
         kk = dict(kw)
-        sh = kk.pop("shard", (1, 0))
-        kk["shard_world"], kk["shard_rank"] = sh
+        kk["shard_world"], kk["shard_rank"], kk["shard_axis"] = shard_key(kk.pop("shard", (1, 0)))
         return Plan(**kk)
     return _owned_plan(owner, tag, key, make)
 

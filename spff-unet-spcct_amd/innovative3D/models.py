@@ -264,12 +264,13 @@ class UNet3D_SpectralCore(nn.Module):
         if C != self.in_channels:
             raise ValueError(f"expected {self.in_channels} input channels, got {C}")
         efilm, fgate = self._flags()
-        # depth sharding (innovative3D.sharded): x is this rank's D-slab of a
-        # volume of depth D * world; the FourierGate acts on the full depth
-        shard = tuple(getattr(self, "shard", (1, 0)))
+        # sharding (innovative3D.sharded): x is this rank's D-slab of a volume of
+        # depth D * world (axis 0), or its H-slab of a volume of height H * world
+        # (axis 1, the registry layout); the FourierGate acts on the full depth
+        shard = E.shard_key(getattr(self, "shard", (1, 0)))
         if fgate:
             for b in self._blocks():
-                b.fgate._ensure_mask(D * shard[0], x.device)
+                b.fgate._ensure_mask(D * (shard[0] if shard[2] == 0 else 1), x.device)
         plan = E.get_plan(batch=B, in_ch=C, depth=D, height=H, width=W,
                           num_classes=self.num_classes, base=self.base, ksd=self.ksd,
                           efilm=efilm, fgate=fgate, se=self.use_se, specse=self.use_specse,

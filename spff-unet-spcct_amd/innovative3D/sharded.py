@@ -12,6 +12,17 @@ slab and calls back, in stream order, for the only cross-slab couplings:
     partial rfft spectra of the FourierGate (forward s1, backward dw) and the
     SE gradient contraction -- ``allreduce``.
 
+Height sharding (``HeightShardedSPFF``; SURVEY.md §8(e): "in the registry
+layout (D = 5), shard H instead, in multiples of 8 rows") splits the registry
+input [B, 1, 5, H, W] into row slabs of a multiple of 8 rows, so the three
+(1,2,2) pools and the up-convolutions stay rank-local.  The engine
+(spff_cfg.shard_axis = SPFF_SHARD_HEIGHT) exchanges one boundary ROW per side
+before every 3x3x3 convolution through the same ``halo`` callback (a staging
+slab of two rows per side), all-reduces the InstanceNorm moments as above, and
+all-reduces the per-(b, c, d) gate sums (fp32), after which the EnergyFiLM /
+FourierGate / SpectralSE / SE algebra is evaluated replicated (rank 0 keeps its
+parameter gradients).  Any batch size.
+
 The loss is normalised by the GLOBAL valid-voxel count and the flat weight
 gradient is all-reduced once per step, as in innovative3D.distributed.  The
 algorithm is pinned against the unsharded oracle by tests/test_sharded_cpu.py
@@ -82,6 +93,14 @@ class TorchDepthColl:
             op.wait()
 
 
+def height_bounds(H: int, world: int, rank: int):
+    """(offset, rows) of rank's slab of a height-H volume (H / world a multiple of 8)."""
+    if H % (8 * world):
+        raise ValueError(f"height {H} does not split into {world} slabs of a multiple of 8 rows")
+    h = H // world
+    return rank * h, h
+
+
 def shard_bounds(D: int, world: int, rank: int):
     """(offset, depth) of rank's slab of a depth-D volume (D divisible by world)."""
     if D % world:
@@ -96,11 +115,13 @@ class DepthShardedSPFF:
     Returns (loss, confusion) with the hard-Dice term from the all-reduced
     confusion, i.e. the values of the unsharded step."""
 
+    axis = 0  # SPFF_SHARD_DEPTH
+
     def __init__(self, core: torch.nn.Module, num_classes: int, ignore_index: int = 255,
                  group=None, coll=None):
         self.core, self.K, self.ignore, self.group = core, int(num_classes), ignore_index, group
         self.coll = coll or TorchDepthColl(group)
-        core.shard = (self.coll.world, self.coll.rank)
+        core.shard = (self.coll.world, self.coll.rank, self.axis)
         core.shard_coll = self.coll
         self.params = [p for p in core.parameters()]
 
@@ -117,3 +138,11 @@ class DepthShardedSPFF:
         # the global value: summed CE shares + 0.5 * Dice of the summed confusion
         loss, _ce, conf_g = Dd.global_loss(ce, conf, self.K, group=self.group)
         return loss, conf_g
+
+
+class HeightShardedSPFF(DepthShardedSPFF):
+    """``step(x_slab, y_slab)`` on this rank's H-slab (``height_bounds``) of a
+    registry-layout batch [B, 1, 5, H, W] / labels [B, 5, H, W]; same return
+    values as the unsharded step."""
+
+    axis = 1  # SPFF_SHARD_HEIGHT

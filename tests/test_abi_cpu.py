@@ -81,3 +81,22 @@ def test_full_volume_512_fits_one_mi355x():
     assert head.ws_bytes == E.Plan(2, 5, 128, 128, 128, 13, memory="full").ws_bytes
     with pytest.raises(E.SpffError):
         E.Plan(1, 5, 8, 32, 32, 5, memory="small")
+
+
+def test_height_sharded_plan_shapes():
+    """SPFF_SHARD_HEIGHT (registry layout [B, 1, 5, H, W]): local rows and
+    width multiples of 8, any batch; the plan carries the row-padded conv operands on top
+    of the unsharded layout of its slab, but no depth halos."""
+    whole = E.Plan(1, 1, 5, 512, 512, 13)
+    for world in (2, 4, 8):
+        h = 512 // world
+        p = E.Plan(2, 1, 5, h, 512, 13, shard_world=world, shard_rank=world - 1, shard_axis=1)
+        assert p.nfloats == whole.nfloats  # same parameters (the FourierGate at D = 5)
+        unsh = E.Plan(2, 1, 5, h, 512, 13)
+        assert unsh.ws_bytes < p.ws_bytes < 1.6 * unsh.ws_bytes
+    with pytest.raises(E.SpffError):
+        E.Plan(1, 1, 5, 60, 512, 13, shard_world=2, shard_rank=0, shard_axis=1)  # 60 rows
+    with pytest.raises(E.SpffError):
+        E.Plan(1, 1, 5, 64, 512, 13, shard_world=2, shard_rank=0, shard_axis=2)  # bad axis
+    with pytest.raises(E.SpffError):  # depth sharding keeps batch 1
+        E.Plan(2, 1, 8, 64, 64, 13, shard_world=2, shard_rank=0, shard_axis=0)

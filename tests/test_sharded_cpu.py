@@ -1,6 +1,6 @@
-"""Depth sharding (BASELINE config 4) on CPU with gloo:
-world sizes 2 and 4 run the depth-sharded restatement (oracle/spff_sharded.py)
-on slabs of one volume; the gathered logits, the loss and the all-reduced
+"""Depth sharding (BASELINE config 4) and height sharding of
+the registry layout on CPU with gloo: world sizes 2 and 4 run the sharded
+restatement (oracle/spff_sharded.py) on slabs of one volume; the gathered logits, the loss and the all-reduced
 gradients must equal the unsharded oracle's (fp64, 1e-9).  This pins the
 exchange plan the engine's sharded plans implement: conv halos, distributed
 InstanceNorm / SE statistics, the FourierGate all-gather, global-D EFiLM
@@ -26,7 +26,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, name, out_path):
+def _worker(rank, world, port, name, out_path, axis=2):
     import pathlib
     import sys
     root = pathlib.Path(__file__).resolve().parents[1]
@@ -41,10 +41,9 @@ def _worker(rank, world, port, name, out_path):
     d = load(name)
     cfg = cfg_of(d["meta"])
     P = O.params_from_state(state_of(d), dtype=torch.float64)
-    D = d["x"].shape[2]
-    sh = S.Shard(D, rank, world)
-    x = torch.from_numpy(d["x"][:, :, sh.off:sh.off + sh.D_loc]).double()
-    y = torch.from_numpy(d["labels"][:, sh.off:sh.off + sh.D_loc])
+    sh = S.Shard(d["x"].shape[axis], rank, world, axis)
+    x = torch.from_numpy(d["x"]).double().narrow(axis, sh.off, sh.D_loc).contiguous()
+    y = torch.from_numpy(d["labels"]).narrow(axis - 1, sh.off, sh.D_loc).contiguous()
     with torch.no_grad():
         lg = S.forward(P, x, cfg, sh)
     loss, ce, dice = S.fwd_bwd(P, x, y, cfg, sh)
@@ -54,9 +53,13 @@ def _worker(rank, world, port, name, out_path):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("name,world", [("fx3_fgate_even_b2", 2), ("fx3_fgate_even_b2", 4),
-                                        ("fx2_ns_base8", 2), ("fx2_ns_base8", 4)])
-def test_depth_sharded_equals_unsharded(tmp_path, name, world):
+@pytest.mark.parametrize("name,world,axis", [
+    ("fx3_fgate_even_b2", 2, 2), ("fx3_fgate_even_b2", 4, 2),
+    ("fx2_ns_base8", 2, 2), ("fx2_ns_base8", 4, 2),
+    # height sharding of the registry layout [B, 1, 5, H, W]
+    ("fx1_registry_k13", 2, 3), ("fx1_registry_k13", 4, 3), ("fx3b_fgate_odd_b2", 2, 3),
+    ("fx2_ns_base8", 2, 3)])
+def test_sharded_equals_unsharded(tmp_path, name, world, axis):
     from oracle import spff_oracle as O
     d = load(name)
     cfg = cfg_of(d["meta"])
@@ -69,9 +72,9 @@ def test_depth_sharded_equals_unsharded(tmp_path, name, world):
     dice = O.macro_dice_loss(O.confusion(logits.detach(), y, K, 255), K)
     ce.backward()
     out = str(tmp_path / "sh")
-    mp.spawn(_worker, args=(world, _free_port(), name, out), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), name, out, axis), nprocs=world, join=True)
     parts = [np.load(f"{out}.{r}.npz") for r in range(world)]
-    lg = np.concatenate([p["logits"] for p in parts], axis=2)
+    lg = np.concatenate([p["logits"] for p in parts], axis=axis)
     ref = logits.detach().numpy()
     assert np.abs(lg - ref).max() <= 1e-9 * np.abs(ref).max()
     assert abs(float(parts[0]["ce"]) - float(ce)) <= 1e-12 * abs(float(ce))
