@@ -32,6 +32,8 @@ for _p in (str(ROOT), str(ROOT / "spff-unet-spcct_amd")):
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
+from build_ext import build_record  # noqa: E402  (source digest the library was built from)
+
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 = f32 vector peak
 # dense bf16 MFMA: 256 CUs x 4 SIMDs x 1024 flop/clk (32x32x16 in 32 cycles) x 2.4 GHz
 BF16_MFMA_PEAK_TFLOPS = 256 * 4 * 1024 * 2.4e9 / 1e12
@@ -433,11 +435,13 @@ def main():
     ap.add_argument("--math", choices=("f32", "bf16x6", "bf16x3"), default="bf16x6",
                     help="conv arithmetic: bf16x6 = fp32 operands split exactly into 3 bf16 "
                          "planes, 6 products, fp32 accumulate (fp32 accuracy class; default)")
-    ap.add_argument("--workload", choices=("patch128", "volume512", "unet3d", "swin"),
+    ap.add_argument("--workload", choices=("patch128", "volume512", "registry", "unet3d", "swin"),
                     default="patch128",
                     help="patch128 = the headline (BASELINE configs[1]): batch data parallelism; "
                          "volume512 = BASELINE configs[3]: one 5 x (64 N) x 512 x 512 volume "
                          "depth-sharded over the N ranks (64-slice slab per rank, RCCL halos); "
+                         "registry = one batch of --batch registry-layout volumes 1 x 5 x hw x hw "
+                         "height-sharded over the N ranks (hw / N rows each; strong scaling); "
                          "unet3d = BASELINE configs[2]: the 3DUNet variant, batch 4 x 1 x 5 x 96^2; "
                          "swin = BASELINE configs[4]: the SwinUNETR variant, batch 2 x 1 x 128^3")
     ap.add_argument("--slab-depth", type=int, default=64)
@@ -473,7 +477,20 @@ def main():
 
     K = args.classes
     sharded = args.workload == "volume512"
-    if sharded:  # weak scaling: a fixed slab per rank, global depth = slab * world;
+    registry = args.workload == "registry"
+    if registry:  # the registry layout [B, 1, 5, H, W] sharded along H
+        from innovative3D.sharded import HeightShardedSPFF, height_bounds
+        B, HW = args.batch, args.hw
+        off, Hl = height_bounds(HW, world, rank)
+        core, st = build_model(K, args.base, 1, 5, device)
+        core.math = args.math
+        core.memory = args.memory
+        x, y = synthetic_batch(B, 1, 5, HW, HW, K, ignore_frac=0.01, seed=0)
+        x = x[:, :, :, off:off + Hl].contiguous().to(device)
+        y = y[:, :, off:off + Hl].contiguous().to(device)
+        runner = HeightShardedSPFF(core, K, 255) if world > 1 else DataParallelSPFF(core, K, 255)
+        vox_step = B * 5 * Hl * HW
+    elif sharded:  # weak scaling: a fixed slab per rank, global depth = slab * world;
         # --strong: one volume of --volume-depth slices, D / world per rank
         from innovative3D.sharded import DepthShardedSPFF
         B, HW = 1, args.hw
@@ -584,7 +601,14 @@ def main():
                  "input tensor per voxel, incl. the split combine); act_apply = IN/gate apply "
                  "(8*C B/voxel); in_bwd_apply = IN backward apply (12*C B/voxel); HIP events "
                  "on the engine stream")}
-    if sharded:
+    if registry:
+        cfg = {"workload": f"SPFF-UNet fwd+ce_plus_macro_dice+bwd, batch {B} x 1ch x 5 x {HW} x "
+                           f"{HW} (registry layout) height-sharded into {world} x {Hl}-row slabs, "
+                           f"K={K}, base {args.base}",
+               "global_batch": B, "shape": [B, 1, 5, HW, HW], "parallelism": f"height{world}"}
+        metric = f"voxels/sec fwd+bwd, SPFF-UNet registry layout {B}x1x5x{HW}x{HW}, " \
+                 "height-sharded over N GPUs (strong scaling)"
+    elif sharded:
         cfg = {"workload": f"SPFF-UNet fwd+ce_plus_macro_dice+bwd, one 1 x {args.in_ch}ch x "
                            f"{Dl * world} x {HW} x {HW} volume depth-sharded into {world} x "
                            f"{Dl}-slice slabs (BASELINE configs[3] at 8 GPUs), K={K}, base {args.base}",
@@ -605,17 +629,19 @@ def main():
         "metric": metric,
         "value": value, "unit": "voxels/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-        "scaling": "strong" if (sharded and args.strong) else "weak", "vs_baseline": None,
+        "scaling": "strong" if ((sharded and args.strong) or registry) else "weak",
+        "vs_baseline": None,
         "dtype": "f32", "conv_math": args.math,
         "data": "synthetic (x~N(0,1), labels U[0,K) with 1% ignore=255; weights from weightgen seed 0)",
         "config": cfg,
         "loss": float(loss.item()),
         "roofline": roof,
         "cpu_baseline": None,
+        "build": build_record(),
     }
     if world > 1:
         out["ranks"] = rank_report(elapsed_local, args.steps, device)
-    if rank == 0 and world == 1 and args.cpu_baseline == "auto" and not sharded:
+    if rank == 0 and world == 1 and args.cpu_baseline == "auto" and not (sharded or registry):
         out["cpu_baseline"] = cpu_baseline(st, K, args.base, x_cpu, y_cpu, args.cpu_depth,
                                            args.cpu_steps)
         out["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]

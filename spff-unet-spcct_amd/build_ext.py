@@ -4,11 +4,15 @@
 
 Objects are compiled in parallel with hipcc, then linked into
 ``spff-unet-spcct_amd/innovative3D/_lib/libspff_hip.so``.  Rebuilds only when
-a source/header is newer than the library.
+the sha256 of the sources, headers and flags differs from the one recorded
+beside the library at its build (``libspff_hip.build.json``; bench.py reports
+both digests, so a stale binary cannot ship unnoticed).
 """
 from __future__ import annotations
 
 import concurrent.futures as cf
+import hashlib
+import json
 import os
 import pathlib
 import shutil
@@ -38,12 +42,38 @@ def sources():
     return sorted(CSRC.glob("*.hip"))
 
 
+STAMP = OUT_DIR / "libspff_hip.build.json"
+
+
+def _portable_flags():
+    """the compile flags without the (checkout-dependent) include paths"""
+    return [f for f in FLAGS if not f.startswith("-I")]
+
+
+def source_digest() -> str:
+    """sha256 over every translation unit, header and the compile flags"""
+    h = hashlib.sha256(" ".join(_portable_flags()).encode())
+    for p in sorted(list(sources()) + list(CSRC.glob("*.h")) + list(INC.glob("*.h"))):
+        h.update(p.name.encode())
+        h.update(p.read_bytes())
+    return h.hexdigest()
+
+
+def build_record() -> dict:
+    """{"lib_sources_sha256": digest the library was built from (None: unknown),
+    "tree_sources_sha256": digest of the sources now, "fresh": equal}"""
+    built = None
+    try:
+        built = json.loads(STAMP.read_text()).get("sources_sha256")
+    except Exception:
+        pass
+    now = source_digest()
+    return {"lib": str(LIB.relative_to(ROOT)), "lib_sources_sha256": built,
+            "tree_sources_sha256": now, "fresh": bool(LIB.exists() and built == now)}
+
+
 def _stale() -> bool:
-    if not LIB.exists():
-        return True
-    t = LIB.stat().st_mtime
-    deps = list(sources()) + list(CSRC.glob("*.h")) + list(INC.glob("*.h")) + [pathlib.Path(__file__)]
-    return any(p.stat().st_mtime > t for p in deps)
+    return not build_record()["fresh"]
 
 
 def build(force: bool = False, verbose: bool = True) -> pathlib.Path:
@@ -70,6 +100,8 @@ def build(force: bool = False, verbose: bool = True) -> pathlib.Path:
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stderr[-4000:]}")
     os.replace(tmp, LIB)
+    STAMP.write_text(json.dumps({"sources_sha256": source_digest(), "arch": ARCH,
+                                 "flags": _portable_flags(), "hipcc": hipcc}))
     if verbose:
         print(f"[spff] built {LIB.relative_to(ROOT)}")
     return LIB

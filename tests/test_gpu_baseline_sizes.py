@@ -48,19 +48,19 @@ def _threads():
     return max(1, min(16, n, int(os.environ.get("OMP_NUM_THREADS", "16") or 16)))
 
 
-def _spff_state(D):
+def _spff_state(D, in_ch=5):
     import innovative3D.models as M
     from innovative3D.weightgen import synth_state
-    core = M.build_spct_energyfilm_fourier(num_classes=K13, base=32, in_channels=5)
+    core = M.build_spct_energyfilm_fourier(num_classes=K13, base=32, in_channels=in_ch)
     for b in core._blocks():
         b.fgate._ensure_mask(D, "cpu")
     st = synth_state([(k, tuple(v.shape)) for k, v in core.state_dict().items()], seed=0)
     return core, st
 
 
-def _oracle_cfg():
+def _oracle_cfg(in_ch=5):
     from oracle import spff_oracle as O
-    return O.SpffCfg(in_ch=5, num_classes=K13, base=32)
+    return O.SpffCfg(in_ch=in_ch, num_classes=K13, base=32)
 
 
 def _oracle_forward(st, x, y):
@@ -70,7 +70,7 @@ def _oracle_forward(st, x, y):
     P = O.params_from_state({k: v for k, v in st.items() if not k.endswith("._mask")},
                             requires_grad=False)
     with torch.no_grad():
-        logits = O.forward(P, x, _oracle_cfg())
+        logits = O.forward(P, x, _oracle_cfg(x.shape[1]))
         loss, _ce, _dice = O.ce_plus_macro_dice(logits, y, K13)
     return logits, float(loss)
 
@@ -87,7 +87,7 @@ def _oracle_grads(st, x, y, masks):
         P = O.params_from_state({k: v for k, v in st.items() if not k.endswith("._mask")},
                                 dtype=dt)
         with forced_branches(masks):
-            O.fwd_bwd(P, x.to(dt), y, _oracle_cfg())
+            O.fwd_bwd(P, x.to(dt), y, _oracle_cfg(x.shape[1]))
         out.append({k: v.grad.clone() for k, v in P.items()})
         del P
     return out
@@ -95,7 +95,7 @@ def _oracle_grads(st, x, y, masks):
 
 def _engine_masks(core, xshape, st):
     from test_gpu_parity import engine_branch_masks
-    return engine_branch_masks(core, xshape, st, _oracle_cfg())
+    return engine_branch_masks(core, xshape, st, _oracle_cfg(xshape[1]))
 
 
 def _mag_scales(st, g64s):
@@ -254,6 +254,80 @@ def test_config4_sharded_512_matches_oracle(tmp_path):
     ref_grads = _oracle_grads(st, x, y, masks)
     grads = {k: torch.from_numpy(parts[0]["g_" + k]) for k in ref_grads[0]}
     _compare("config4 path: 1x5x16x512^2 depth-sharded world 2 (bf16x6)", lg,
+             float(parts[0]["loss"]), grads, ref_logits, ref_loss, ref_grads,
+             scales=_mag_scales(st, ref_grads[0]))
+
+
+# ------------------------- registry layout height-sharded (SURVEY §8(e), 512 x 512)
+HS_SHAPE = (1, 1, 5, 512, 512)
+
+
+def _hs_data():
+    from innovative3D.synthetic import synthetic_batch
+    return synthetic_batch(*HS_SHAPE, num_classes=K13, ignore_frac=0.01, seed=6)
+
+
+def _hs_worker(rank, world, port, out):
+    import pathlib
+    import sys
+    root = pathlib.Path(__file__).resolve().parents[1]
+    sys.path[:0] = [str(root), str(root / "tests"), str(root / "spff-unet-spcct_amd")]
+    from test_gpu_baseline_sizes import _engine_masks, _hs_data, _spff_state
+    from innovative3D.sharded import HeightShardedSPFF, height_bounds
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    core, st = _spff_state(HS_SHAPE[2], in_ch=1)
+    core.load_state_dict({k: torch.from_numpy(v) for k, v in st.items()})
+    core = core.to(DEV)
+    core.math = "bf16x6"
+    x, y = _hs_data()
+    off, h = height_bounds(HS_SHAPE[3], world, rank)
+    step = HeightShardedSPFF(core, K13, 255)
+    loss, conf = step.step(x[:, :, :, off:off + h].contiguous().to(DEV),
+                           y[:, :, off:off + h].contiguous().to(DEV))
+    torch.cuda.synchronize()
+    # this rank's LeakyReLU signs (global IN affine) / pool argmaxes over its rows
+    masks = _engine_masks(core, HS_SHAPE[:3] + (h, HS_SHAPE[4]), st)
+    mk = {}
+    for k, m in masks.items():
+        a = m.numpy()
+        mk["m_" + k] = np.packbits(a) if a.dtype == np.bool_ else a.astype(np.uint8)
+        mk["s_" + k] = np.array(a.shape)
+    np.savez(f"{out}.{rank}.npz", logits=step.last_logits.cpu().numpy(), loss=float(loss), **mk,
+             **({"g_" + k: p.grad.cpu().numpy() for k, p in core.named_parameters(remove_duplicate=False)
+                 if p.grad is not None and not k.endswith("._mask")} if rank == 0 else {}))
+    del step, core
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(900)
+def test_registry_height_sharded_512_matches_oracle(tmp_path):
+    """One registry-layout volume 1 x 1 x 5 x 512 x 512 (K = 13, base 32) split into two
+    256-row slabs (spff_cfg.shard_axis = SPFF_SHARD_HEIGHT) vs the UNSHARDED oracle."""
+    out = str(tmp_path / "hs")
+    world = 2
+    mp.spawn(_hs_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    parts = [np.load(f"{out}.{r}.npz") for r in range(world)]
+    lg = torch.from_numpy(np.concatenate([p["logits"] for p in parts], axis=3))
+    _core, st = _spff_state(HS_SHAPE[2], in_ch=1)
+    x, y = _hs_data()
+    ref_logits, ref_loss = _oracle_forward(st, x, y)
+    masks = {}
+    for k in (f[2:] for f in parts[0].files if f.startswith("m_")):
+        segs = []
+        for p in parts:
+            shp = tuple(int(v) for v in p["s_" + k])
+            a = p["m_" + k]
+            a = np.unpackbits(a)[:int(np.prod(shp))].astype(bool) if k[:4] != "pool" else a
+            segs.append(a.reshape(shp))
+        cat = np.concatenate(segs, axis=3)   # [B, C, D, H, W]: the row slabs
+        masks[k] = torch.from_numpy(cat) if cat.dtype == np.bool_ else torch.from_numpy(cat.astype(np.int64))
+    ref_grads = _oracle_grads(st, x, y, masks)
+    grads = {k: torch.from_numpy(parts[0]["g_" + k]) for k in ref_grads[0]}
+    _compare("registry 1x1x5x512^2 height-sharded world 2 (bf16x6)", lg,
              float(parts[0]["loss"]), grads, ref_logits, ref_loss, ref_grads,
              scales=_mag_scales(st, ref_grads[0]))
 

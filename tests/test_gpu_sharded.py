@@ -7,8 +7,10 @@ The 16-deep case gives each of 2 ranks 4 depth tiles, so the split-bf16 convs ru
 the halo exchange on the engine's side stream beside their interior depth tiles
 (engine.hip conv_halo).  The height-sharded cases split the registry layout
 [B, 1, 5, H, W] into row slabs (spff_cfg.shard_axis = SPFF_SHARD_HEIGHT,
-innovative3D.sharded.HeightShardedSPFF), including one full-size 5 x 512 x 512
-registry volume.  Marked gpu."""
+innovative3D.sharded.HeightShardedSPFF); the full-size 1 x 1 x 5 x 512 x 512 registry
+volume is checked against the kink-consistent oracle in test_gpu_baseline_sizes.py
+(at 1.3 M voxels LeakyReLU / pool knife-edge flips move whole gradient tensors, so an
+engine-vs-engine comparison there is not meaningful).  Marked gpu."""
 import os
 import socket
 
@@ -21,7 +23,7 @@ import torch.multiprocessing as mp
 pytestmark = pytest.mark.gpu
 K, BASE, SHAPE = 5, 8, (1, 5, 8, 32, 32)
 # height-sharded cases: (batch, H, W, K, base) of the registry layout [B, 1, 5, H, W]
-HCASES = {"small": (2, 32, 64, 5, 8), "registry512": (1, 512, 512, 13, 32)}
+HCASES = {"small": (2, 32, 64, 5, 8)}
 
 
 def _shape(depth):
@@ -150,8 +152,7 @@ def test_depth_sharded_engine_matches_unsharded(tmp_path, world, math_mode, dept
 
 
 @pytest.mark.parametrize("world,math_mode,case", [
-    (2, "f32", "small"), (4, "f32", "small"), (2, "bf16x6", "small"), (4, "bf16x6", "small"),
-    (2, "bf16x6", "registry512")])
+    (2, "f32", "small"), (4, "f32", "small"), (2, "bf16x6", "small"), (4, "bf16x6", "small")])
 def test_height_sharded_engine_matches_unsharded(tmp_path, world, math_mode, case):
     import innovative3D.helpers as Hh
     B, H, W, k, base = HCASES[case]
