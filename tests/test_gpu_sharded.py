@@ -67,7 +67,7 @@ def _hdata(case):
     return synthetic_batch(B, 1, 5, H, W, num_classes=k, ignore_frac=0.05, seed=13)
 
 
-def _hworker(rank, world, port, math_mode, out, case):
+def _hworker(rank, world, port, math_mode, out, case, memory=None):
     import pathlib
     import sys
     root = pathlib.Path(__file__).resolve().parents[1]
@@ -79,6 +79,7 @@ def _hworker(rank, world, port, math_mode, out, case):
     torch.cuda.set_device(0)
     B, H, W, k, base = HCASES[case]
     core = _model(math_mode, 5, k, base, 1)
+    core.memory = memory
     x, y = _hdata(case)
     off, h = height_bounds(H, world, rank)
     step = HeightShardedSPFF(core, k, 255)
@@ -151,9 +152,12 @@ def test_depth_sharded_engine_matches_unsharded(tmp_path, world, math_mode, dept
     assert not bad, bad
 
 
-@pytest.mark.parametrize("world,math_mode,case", [
-    (2, "f32", "small"), (4, "f32", "small"), (2, "bf16x6", "small"), (4, "bf16x6", "small")])
-def test_height_sharded_engine_matches_unsharded(tmp_path, world, math_mode, case):
+@pytest.mark.parametrize("world,math_mode,case,memory", [
+    (2, "f32", "small", None), (4, "f32", "small", None), (2, "bf16x6", "small", None),
+    (4, "bf16x6", "small", None),
+    # the lean saved-activation layout (recomputed block outputs / decoder inputs)
+    (2, "bf16x6", "small", "lean")])
+def test_height_sharded_engine_matches_unsharded(tmp_path, world, math_mode, case, memory):
     import innovative3D.helpers as Hh
     B, H, W, k, base = HCASES[case]
     core = _model(math_mode, 5, k, base, 1)
@@ -167,13 +171,14 @@ def test_height_sharded_engine_matches_unsharded(tmp_path, world, math_mode, cas
     del core, logits, loss
     torch.cuda.empty_cache()
     out = str(tmp_path / "hsh")
-    mp.spawn(_hworker, args=(world, _free_port(), math_mode, out, case), nprocs=world, join=True)
+    mp.spawn(_hworker, args=(world, _free_port(), math_mode, out, case, memory), nprocs=world,
+             join=True)
     parts = [np.load(f"{out}.{r}.npz") for r in range(world)]
     lg = np.concatenate([p["logits"] for p in parts], axis=3)
     assert lg.shape == ref.shape, (lg.shape, ref.shape)
     e = float(np.abs(lg - ref).max())
     nflip = int((lg.argmax(1) != ref.argmax(1)).sum())
-    print(f"H-shard world {world} {math_mode} {case}: max|dlogit| {e:.2e}, argmax flips {nflip}, "
+    print(f"H-shard world {world} {math_mode} {case} {memory or 'auto'}: max|dlogit| {e:.2e}, argmax flips {nflip}, "
           f"loss {float(parts[0]['loss']):.7f} vs {loss_ref:.7f}")
     assert e <= 1e-4 * float(np.abs(ref).max())
     assert abs(float(parts[0]["loss"]) - loss_ref) <= 1e-5 * abs(loss_ref)
