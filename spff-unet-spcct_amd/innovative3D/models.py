@@ -280,7 +280,7 @@ class UNet3D_SpectralCore(nn.Module):
         if shard[0] > 1:
             coll = getattr(self, "shard_coll", None)
             if coll is None:
-                raise E.SpffError("depth-sharded module: set .shard_coll (innovative3D.sharded)")
+                raise E.SpffError("sharded module: set .shard_coll (innovative3D.sharded)")
             if getattr(plan, "coll_impl", None) is not coll:
                 plan.set_coll(coll)
         return plan
