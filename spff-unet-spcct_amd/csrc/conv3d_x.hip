@@ -44,7 +44,9 @@
 #include <type_traits>
 
 #ifndef SPFF_XDIAG
-#define SPFF_XDIAG 0  // timing diagnostics only: 1 = no restaging, 2 = no MFMA loop
+#define SPFF_XDIAG 0  // timing diagnostics only: 1 = no restaging, 2 = no MFMA loop,
+                      // 3 = halo restaged but weights staged once, 4 = weights restaged,
+                      // halo staged once (results wrong: kernel timing only)
 #endif
 #ifndef SPFF_XCDMAP
 #define SPFF_XCDMAP 1  // 0: tile-fastest block order (A/B diagnostics)
@@ -362,9 +364,10 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
       hs[k][p].y = (unsigned)s2[p] | ((unsigned)s3[p] << 16);
     }
   };
-  auto stash = [&](int kc) {
+  auto stash = [&](int kc, bool first) {
 #pragma unroll
     for (int k = 0; k < RH; ++k) {
+      if (SPFF_XDIAG == 4 && !first) break;
       const int i = tid + XT_THREADS * k;
       if (i < NHX) {
 #pragma unroll
@@ -377,6 +380,7 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
     const uint4* src = wsrc + (int64_t)kc * NWU + lane;
 #pragma unroll
     for (int k = 0; k < (NPC + NW - 1) / NW; ++k) {
+      if (SPFF_XDIAG == 3 && !first) break;
       const int pc = wave + k * NW;
       if (k * NW + NW <= NPC || pc < NPC)
         __builtin_amdgcn_global_load_lds((const void*)(src + pc * 64),
@@ -406,7 +410,7 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
         for (int cb = 0; cb < CB; ++cb) acc[rb][cb] = -acc[rb][cb];
       __syncthreads();
     }
-    if (SPFF_XDIAG != 1 || kc == kc0) stash(kc);
+    if (SPFF_XDIAG != 1 || kc == kc0) stash(kc, kc == kc0);
     __syncthreads();  // (vmcnt(0): the weight DMA has landed)
     if (kc + 1 < kc1) fetch(kc + 1);
 #pragma unroll
