@@ -62,6 +62,13 @@
 #ifndef SPFF_X16
 #define SPFF_X16 1  // 1: v_mfma_f32_16x16x32_bf16 tap-quad schedule, 0: 32x32x16 tap pairs
 #endif
+#ifndef SPFF_X32NW
+// waves per 32-wide workgroup: 8 (one 2 x 16 x 16 tile, one workgroup per CU) or 4 (a
+// 2 x 8 x 16 tile in 78 KB of LDS, two workgroups per CU: one's chunk-boundary staging
+// overlaps the other's MFMAs -- the level-0 launches 6-8 % faster, -0.46 ms/step A/B; not
+// the default: the depth-sharded 2 x 8-deep GPU test fails with it, cause not found yet)
+#define SPFF_X32NW 8
+#endif
 #ifndef SPFF_XIGLP
 #define SPFF_XIGLP -1
 #endif
@@ -158,6 +165,8 @@ constexpr size_t xt_lds_bytes() {
 // tile depth of a BN-wide launch (host side: launches, fused-statistics layout)
 constexpr int xt_td(int BN) { return (BN == 32 && SPFF_X16 && SPFF_X32T) ? 4 : XT_D; }
 constexpr int xt_mb(int BN) { return (BN == 32 && SPFF_X16 && SPFF_X32T) ? 4 : 2; }
+// waves of a BN-wide workgroup (4-wave 32-wide tiles: SPFF_X32NW, 2-deep tiles only)
+constexpr int xt_nw(int BN) { return (BN == 32 && SPFF_X16 && !SPFF_X32T) ? SPFF_X32NW : 8; }
 }  // namespace
 
 // 16x16x32 tap-quad schedule (X16): k = 4 lane groups x 8 channels, lane group g
@@ -685,7 +694,7 @@ __global__ void k_splitk_reduce(const float* __restrict__ part, int nsplit, int6
   }
 }
 
-template <int BN, int KD, int NS, int MB = xt_mb(BN), int NW = 8, int TD = xt_td(BN)>
+template <int BN, int KD, int NS, int MB = xt_mb(BN), int NW = xt_nw(BN), int TD = xt_td(BN)>
 static hipError_t launch_fwd_x(const Src2& x, const uint4* wx, const Dst2& y, Vol vol, int K,
                                int nkc, int N, int npad, hipStream_t s, float* part = nullptr,
                                int nsplit = 1, int kps = 0, float* stats = nullptr,
@@ -763,7 +772,8 @@ bool conv3d_fuses_act(int math, int C) {
 }
 // tiles of a BN-wide launch (the fused IN statistics are per (tile, out channel))
 static int64_t xt_ntiles(Vol vol, int BN) {
-  const int td = xt_td(BN), th = SPFF_X16 ? 2 * 8 * xt_mb(BN) / td : 8 * xt_mb(BN);
+  const int nw = xt_nw(BN);
+  const int td = xt_td(BN), th = SPFF_X16 ? 2 * nw * xt_mb(BN) / td : nw * xt_mb(BN);
   return (int64_t)vol.B * cdiv(vol.D, td) * cdiv(vol.H, th) * cdiv(vol.W, XT_W);
 }
 namespace {

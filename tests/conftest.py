@@ -12,3 +12,38 @@ for p in (str(ROOT), str(PKG)):
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device)")
     config.addinivalue_line("markers", "slow: long-running test")
+
+
+# Heartbeat for long tests (the baseline-size parity tests spend minutes in the CPU
+# oracle without output): every 60 s a line on the terminal and in
+# gpurun_out/heartbeat.log, so a long but live test is not mistaken for a hung one.
+import threading  # noqa: E402
+import time  # noqa: E402
+
+import pytest  # noqa: E402
+
+
+@pytest.fixture(autouse=True)
+def _heartbeat(request):
+    tr = request.config.pluginmanager.getplugin("terminalreporter")
+    stop = threading.Event()
+    t0 = time.time()
+    name = request.node.nodeid
+    out = ROOT / "gpurun_out"
+
+    def beat():
+        while not stop.wait(60.0):
+            msg = f"[heartbeat] {name} running {time.time() - t0:.0f} s"
+            try:
+                if tr is not None:
+                    tr.write_line(msg)
+                if out.is_dir():
+                    with open(out / "heartbeat.log", "a") as f:
+                        f.write(msg + "\n")
+            except Exception:
+                pass
+
+    th = threading.Thread(target=beat, daemon=True)
+    th.start()
+    yield
+    stop.set()
