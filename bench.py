@@ -12,7 +12,7 @@ runs its own batch, the valid-voxel count is all-reduced before the loss so
 the CE mean is the global one, and the flat gradient is all-reduced (RCCL).
 Rank 0 prints one JSON line.  The CPU baseline (rank 0, N=1) times the CPU
 oracle (oracle/spff_oracle.py, PyTorch-CPU restatement of the reference path)
-on a bounded sample of the same workload on the host cores.
+on the same batch on the host cores (all physical cores the process is allotted).
 """
 from __future__ import annotations
 
@@ -80,59 +80,159 @@ def host_cpu_info():
         pass
     aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
     omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    cg = cgroup_cpu_allotment()
+    allot = [aff] + [v for v in (cg.get("quota_cpus"), cg.get("cpuset_cpus")) if v]
     return {"physical_cores": len(phys) or None, "logical_cpus": logical or os.cpu_count(),
-            "affinity_cpus": aff, "omp_num_threads": omp or None}
+            "affinity_cpus": aff, "omp_num_threads": omp or None, "cgroup": cg,
+            "allotment_cpus": min(allot)}
+
+
+def _cpulist_len(s):
+    """number of CPUs in a kernel cpu-list string such as '0-15,32-47'"""
+    n = 0
+    for part in s.strip().split(","):
+        if not part:
+            continue
+        a, _, b = part.partition("-")
+        n += (int(b) - int(a) + 1) if b else 1
+    return n
+
+
+def cgroup_cpu_allotment():
+    """This process's CPU allotment from its cgroup, walking from its own cgroup up to the
+    root (the tightest limit wins): v2 `cpu.max` (quota / period) and
+    `cpuset.cpus.effective`, or v1 `cpu.cfs_quota_us / cpu.cfs_period_us` and
+    `cpuset.effective_cpus`.  Raw strings are kept as the record."""
+    rec = {"version": None, "quota_cpus": None, "cpuset_cpus": None, "raw": {}}
+    try:
+        lines = open("/proc/self/cgroup").read().split("\n")
+    except OSError:
+        return rec
+    base = pathlib.Path("/sys/fs/cgroup")
+    v2 = [ln.split(":", 2)[2] for ln in lines if ln.startswith("0::")]
+    quotas, cpusets = [], []
+    if v2 and (base / "cgroup.controllers").exists():
+        rec["version"] = 2
+        p = base / v2[0].lstrip("/")
+        chain = [p] + list(p.parents)
+        for d in chain:
+            if not str(d).startswith(str(base)):
+                break
+            try:
+                q, per = (d / "cpu.max").read_text().split()[:2]
+                rec["raw"].setdefault("cpu.max", []).append(f"{d}: {q} {per}")
+                if q != "max":
+                    quotas.append(int(q) / int(per))
+            except (OSError, ValueError):
+                pass
+            try:
+                s = (d / "cpuset.cpus.effective").read_text().strip()
+                if s:
+                    rec["raw"].setdefault("cpuset.cpus.effective", []).append(f"{d}: {s}")
+                    cpusets.append(_cpulist_len(s))
+            except (OSError, ValueError):
+                pass
+    else:
+        rec["version"] = 1
+        for ln in lines:
+            parts = ln.split(":", 2)
+            if len(parts) < 3:
+                continue
+            ctrls, path = parts[1].split(","), parts[2].lstrip("/")
+            for c in ctrls:
+                root = base / (c if (base / c).exists() else parts[1])
+                d = root / path
+                for dd in [d] + list(d.parents):
+                    if not str(dd).startswith(str(root)):
+                        break
+                    try:
+                        if c == "cpu":
+                            q = int((dd / "cpu.cfs_quota_us").read_text())
+                            per = int((dd / "cpu.cfs_period_us").read_text())
+                            rec["raw"].setdefault("cfs", []).append(f"{dd}: {q} {per}")
+                            if q > 0:
+                                quotas.append(q / per)
+                        elif c == "cpuset":
+                            s = (dd / "cpuset.effective_cpus").read_text().strip()
+                            rec["raw"].setdefault("cpuset", []).append(f"{dd}: {s}")
+                            if s:
+                                cpusets.append(_cpulist_len(s))
+                    except (OSError, ValueError):
+                        pass
+    if quotas:
+        rec["quota_cpus"] = max(1, int(min(quotas)))
+    if cpusets:
+        rec["cpuset_cpus"] = min(cpusets)
+    return rec
 
 
 def baseline_threads():
-    """All physical cores, bounded by this process's CPU share (affinity /
-    OMP_NUM_THREADS: the GPU box grants 16 CPUs per GPU)."""
+    """All physical cores the process may use ("the node's own host cores"):
+    min(physical cores, the process's real CPU allotment = affinity mask, cgroup quota,
+    cgroup cpuset).  OMP_NUM_THREADS is a per-GPU-share convention, not an allotment: it
+    is reported, and timed as a second labelled figure (`per_gpu_share`)."""
     h = host_cpu_info()
-    n = h["physical_cores"] or h["affinity_cpus"]
-    n = min(n, h["affinity_cpus"])
-    if h["omp_num_threads"]:
-        n = min(n, h["omp_num_threads"])
+    n = min(h["physical_cores"] or h["allotment_cpus"], h["allotment_cpus"])
     return max(1, n), h
 
 
 def cpu_baseline(st, K, base, x_cpu, y_cpu, depth, steps):
-    """Oracle (PyTorch-CPU restatement of the reference) fwd+loss+bwd on host cores, on a
-    bounded sample of the SAME inputs the GPU run uses: sample 0, depths [0, depth) of
-    config 2's batch (BASELINE.md 'CPU baseline timing': x ~ N(0,1) seed 0, labels with
-    1 % ignore).  voxels/s of the sample; the CPU cost is linear in the voxel count (a
-    fixed-work-per-voxel conv net), so this is the full batch's rate."""
+    """Oracle (PyTorch-CPU restatement of the reference) fwd+loss+bwd on the host cores, on
+    the SAME inputs the GPU run uses (BASELINE.md 'CPU baseline timing': x ~ N(0,1) seed 0,
+    labels with 1 % ignore): the WHOLE config-2 batch by default (depth = 0), so nothing is
+    extrapolated; `depth` > 0 restricts it to sample 0, depths [0, depth) (a debugging aid).
+    Threads = min(physical cores, the process's real allotment: affinity, cgroup quota and
+    cpuset; `baseline_threads`).  When OMP_NUM_THREADS (the box's per-GPU CPU share) is
+    smaller, the same batch is also timed on that many threads as `per_gpu_share`."""
     from oracle import spff_oracle as O
     threads, host = baseline_threads()
-    torch.set_num_threads(threads)
     in_ch = x_cpu.shape[1]
     cfg = O.SpffCfg(in_ch=in_ch, num_classes=K, base=base)
+    if depth and depth < x_cpu.shape[2]:
+        x = x_cpu[0:1, :, :depth].contiguous()
+        y = y_cpu[0:1, :depth].contiguous()
+    else:
+        x, y = x_cpu.contiguous(), y_cpu.contiguous()
+    D = x.shape[2]
     st_d = {k: v for k, v in st.items() if not k.endswith("._mask")}
     # masks for the sample depth (all ones, as in the reference, SURVEY F10)
     import numpy as np
     for k in list(st_d):
         if k.endswith("freq_mask"):
-            st_d[k] = np.ones((1, 1, depth // 2 + 1, 1, 1), np.float32)
+            st_d[k] = np.ones((1, 1, D // 2 + 1, 1, 1), np.float32)
     P = O.params_from_state(st_d)
-    x = x_cpu[0:1, :, :depth].contiguous()
-    y = y_cpu[0:1, :depth].contiguous()
-    H, W = x.shape[3], x.shape[4]
-    times = []
-    for i in range(steps + 1):
-        t0 = time.perf_counter()
-        O.fwd_bwd(P, x, y, cfg)
-        dt = time.perf_counter() - t0
-        if i > 0:
-            times.append(dt)
-    med = statistics.median(times)
-    vox = depth * H * W
-    full = x_cpu.shape[0] * x_cpu.shape[2] * H * W
-    return {"value": vox / med, "unit": "voxels/s", "cores": torch.get_num_threads(),
-            "kind": "port", "host": host,
-            "sample": f"oracle fwd+ce_plus_macro_dice+bwd on sample 0, depths 0..{depth - 1} of the "
-                      f"GPU run's own batch (synthetic_batch seed 0: 1x{in_ch}x{depth}x{H}x{W}, K={K}, "
-                      f"base {base}) = 1/{full // vox} of the headline voxels; median of {steps} "
-                      f"steps after 1 warm-up ({med:.2f} s/step; full batch extrapolated "
-                      f"{med * full / vox:.1f} s/step)"}
+    vox = x.shape[0] * D * x.shape[3] * x.shape[4]
+    full = x_cpu.shape[0] * x_cpu.shape[2] * x_cpu.shape[3] * x_cpu.shape[4]
+
+    def timed(nthreads, nsteps, warm):
+        torch.set_num_threads(nthreads)
+        times = []
+        for i in range(nsteps + warm):
+            t0 = time.perf_counter()
+            O.fwd_bwd(P, x, y, cfg)
+            if i >= warm:
+                times.append(time.perf_counter() - t0)
+        return statistics.median(times), times
+
+    med, times = timed(threads, steps, 1)
+    shape = "x".join(map(str, x.shape))
+    what = (f"the GPU run's whole batch ({shape}, synthetic_batch seed 0, K={K}, base {base}); "
+            "no extrapolation") if vox == full else (
+            f"sample 0, depths 0..{D - 1} of the GPU run's batch ({shape}) = 1/{full // vox} of "
+            "the headline voxels")
+    out = {"value": vox / med, "unit": "voxels/s", "cores": torch.get_num_threads(),
+           "kind": "port", "host": host, "s_per_step": times, "voxels_per_step": vox,
+           "threads_rule": "min(physical cores, allotment = min(affinity, cgroup quota, cgroup "
+                           "cpuset))",
+           "sample": f"oracle fwd+ce_plus_macro_dice+bwd on {what}; median of {steps} steps "
+                     f"after 1 warm-up ({med:.2f} s/step) on {torch.get_num_threads()} threads"}
+    share = host.get("omp_num_threads")
+    if share and share < threads:
+        med2, t2 = timed(share, 1, 1)
+        out["per_gpu_share"] = {"value": vox / med2, "cores": share, "s_per_step": t2,
+                                "note": "same batch on OMP_NUM_THREADS threads (the box's "
+                                        "per-GPU CPU share convention)"}
+    return out
 
 
 def unet3d_flops(B, D, H, W, K, f=32, cin=1):
@@ -453,10 +553,15 @@ def main():
     ap.add_argument("--memory", choices=("auto", "full", "lean"), default="auto",
                     help="saved-activation layout (include/spff.h SPFF_MEM_*)")
     ap.add_argument("--hw", type=int, default=512)
-    ap.add_argument("--cpu-depth", type=int, default=32)
-    ap.add_argument("--cpu-steps", type=int, default=3)
-    ap.add_argument("--pmc", default=str(ROOT / "profiles" / "r02_pmc_conv.json"),
-                    help="optional per-launch HBM traffic summary from rocprofv3 --pmc")
+    ap.add_argument("--coll-timeout", type=float, default=600.0,
+                    help="seconds before a collective is declared failed (process group timeout)")
+    ap.add_argument("--cpu-depth", type=int, default=0,
+                    help="0 (default) = time the CPU oracle on the whole batch; > 0 = sample 0, "
+                         "depths [0, cpu-depth) only")
+    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--pmc", default=str(ROOT / "profiles" / "r03_pmc_conv.json"),
+                    help="per-launch HBM traffic summary from rocprofv3 --pmc "
+                         "(scripts/pmc_traffic.py); used only when its workload key matches")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -465,7 +570,12 @@ def main():
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        # a dead or wedged peer fails the collective after this long instead of hanging the
+        # job (SURVEY §5 failure detection; the reference sets NCCL_ASYNC_ERROR_HANDLING)
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+        import datetime
+        dist.init_process_group("nccl", device_id=device,
+                                timeout=datetime.timedelta(seconds=args.coll_timeout))
 
     if args.workload == "unet3d":
         return bench_unet3d(args, world, rank, device)
@@ -554,12 +664,29 @@ def main():
     nl = prof["conv_fwd"][2] + prof["conv_dgrad"][2]
     cb = prof["conv_fwd"][3] + prof["conv_dgrad"][3]
     achieved = fl / (ms * 1e-3) / 1e12 if ms > 0 else None
-    traffic = None
+    # roofline.traffic: the PMC measurement is used only for the workload it was taken on
+    # (scripts/pmc_traffic.py stores the bench line's workload_key); otherwise null
+    if registry:
+        shape = [B, 1, 5, HW, HW]
+    elif sharded:
+        shape = [1, args.in_ch, Dl * world, HW, HW]
+    else:
+        shape = [B, args.in_ch, S, S, S]
+    wkey = {"workload": args.workload, "shape": shape, "classes": K, "base": args.base,
+            "math": args.math, "n_gpus": world, "memory_layout": plan.layout}
+    traffic, traffic_src = None, {"file": None, "matched": False}
     try:
         pm = json.loads(pathlib.Path(args.pmc).read_text())
-        traffic = pm.get("hbm_bytes_per_launch")
+        traffic_src["file"] = str(pathlib.Path(args.pmc).resolve().relative_to(ROOT))
+        if pm.get("workload_key") == wkey:
+            traffic = pm.get("hbm_bytes_per_launch")
+            traffic_src["matched"] = True
+            traffic_src["same_sources"] = (pm.get("lib_sources_sha256")
+                                           == build_record()["lib_sources_sha256"])
+        else:
+            traffic_src["pmc_workload_key"] = pm.get("workload_key")
     except Exception:
-        traffic = None
+        pass
     peak = MATH_PEAK[args.math]
     roof = {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
             "frac": (achieved / peak) if achieved else None, "traffic": traffic,
@@ -575,7 +702,9 @@ def main():
             "compulsory_bytes_per_launch": cb / max(1, nl),
             "traffic_over_compulsory": (traffic / (cb / nl)) if (traffic and nl and cb) else None,
             "traffic_note": ("PMC HBM bytes per launch of this kernel (2 x FETCH_SIZE + WRITE_SIZE, "
-                             "profiles/r02_pmc_conv.json, same bench config)"),
+                             "rocprofv3 --pmc passes of this same bench workload); null when the "
+                             "summary's workload key differs from this run's"),
+            "traffic_source": traffic_src,
             "per_class_ms_per_step": {k: v[0] / args.steps for k, v in prof.items()},
             "per_class_tflops": {k: (v[1] / (v[0] * 1e-3) / 1e12 if v[0] > 0 else None)
                                  for k, v in prof.items() if k not in plan.MEM_CLASSES},
@@ -634,6 +763,7 @@ def main():
         "dtype": "f32", "conv_math": args.math,
         "data": "synthetic (x~N(0,1), labels U[0,K) with 1% ignore=255; weights from weightgen seed 0)",
         "config": cfg,
+        "workload_key": wkey,
         "loss": float(loss.item()),
         "roofline": roof,
         "cpu_baseline": None,
@@ -645,6 +775,8 @@ def main():
         out["cpu_baseline"] = cpu_baseline(st, K, args.base, x_cpu, y_cpu, args.cpu_depth,
                                            args.cpu_steps)
         out["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
+        if "per_gpu_share" in out["cpu_baseline"]:
+            out["gpu_over_cpu_per_gpu_share"] = value / out["cpu_baseline"]["per_gpu_share"]["value"]
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -35,6 +35,7 @@ extern "C" {
 #define SPFF_EINVAL (-1)
 #define SPFF_EHIP (-2)
 #define SPFF_ESHAPE (-3)
+#define SPFF_ECOLL (-4) /* a shard-group collective callback (spff_coll) returned non-zero */
 
 /* arithmetic of the 3x3x3 conv contractions (spff_cfg.math):
  *   SPFF_MATH_F32     fp32 MFMA (v_mfma_f32_32x32x2_f32, an exact fp32 fma chain)

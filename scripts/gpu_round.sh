@@ -20,7 +20,7 @@ for step in "$@"; do
     bench512) timeout -k 10 900 python bench.py --workload volume512 --steps 3 --warmup 1 > gpurun_out/bench512.log 2>&1; rc=$? ;;
     benchfull) timeout -k 10 900 python bench.py > gpurun_out/bench.log 2>&1; rc=$? ;;
     prof) (cd "$GRAFT_REPO_ROOT" && timeout -k 10 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --cpu-baseline skip > gpurun_out/prof.log 2>&1); rc=$? ;;
-    pmc) (cd "$GRAFT_REPO_ROOT" && timeout -k 10 900 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 1 --warmup 1 --cpu-baseline skip > gpurun_out/pmc_fetch.log 2>&1 && timeout -k 10 900 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py --steps 1 --warmup 1 --cpu-baseline skip > gpurun_out/pmc_write.log 2>&1); rc=$? ;;
+    pmc) (cd "$GRAFT_REPO_ROOT" && timeout -k 10 900 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 1 --warmup 1 --cpu-baseline skip > gpurun_out/pmc_fetch.log 2>&1 && timeout -k 10 900 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py --steps 1 --warmup 1 --cpu-baseline skip > gpurun_out/pmc_write.log 2>&1 && python scripts/pmc_traffic.py gpurun_out/pmc_fetch/run_counter_collection.csv gpurun_out/pmc_write/run_counter_collection.csv gpurun_out/pmc_conv.json gpurun_out/pmc_hbm_per_kernel.csv --bench-log gpurun_out/pmc_fetch.log > gpurun_out/pmc_traffic.log 2>&1); rc=$? ;;
     kbench) timeout -k 10 300 python scripts/kbench.py > gpurun_out/kbench.log 2>&1; rc=$? ;;
     kbx) (timeout -k 10 300 python scripts/kbench.py --math bf16x6 > gpurun_out/kbx.log 2>&1 && timeout -k 10 300 python scripts/kbench.py --math bf16x3 >> gpurun_out/kbx.log 2>&1); rc=$? ;;
     train) timeout -k 10 600 python -m pytest tests/test_gpu_train.py -m gpu -q -s -p no:cacheprovider > gpurun_out/pytest_train.log 2>&1; rc=$? ;;

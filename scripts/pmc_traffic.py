@@ -5,7 +5,12 @@ MI355X_MICROARCH.md's gfx950 correction: FETCH_SIZE reports half the bytes of
 16-B/lane streaming reads, so traffic = 2 x FETCH_SIZE + WRITE_SIZE (both in KB).
 
     python scripts/pmc_traffic.py gpurun_out/pmc_fetch/run_counter_collection.csv \
-        gpurun_out/pmc_write/run_counter_collection.csv profiles/r01_pmc_conv.json
+        gpurun_out/pmc_write/run_counter_collection.csv profiles/r03_pmc_conv.json \
+        [per_kernel.csv] [--bench-log gpurun_out/pmc_fetch.log]
+
+--bench-log: the profiled bench.py run's output; its JSON line's `workload_key` and
+build digest are stored with the traffic, and bench.py uses the traffic only for a run
+with the same workload key (otherwise `roofline.traffic` is null).
 """
 import csv
 import json
@@ -23,6 +28,14 @@ def per_dispatch(path, counter):
     return out
 
 
+bench_line = None
+if "--bench-log" in sys.argv:
+    i = sys.argv.index("--bench-log")
+    for ln in open(sys.argv[i + 1]):
+        if ln.startswith("{") and '"workload_key"' in ln:
+            bench_line = json.loads(ln)
+    del sys.argv[i:i + 2]
+
 fetch = per_dispatch(sys.argv[1], "FETCH_SIZE")
 write = per_dispatch(sys.argv[2], "WRITE_SIZE")
 f_kb = [v for v, _ in fetch.values()]
@@ -35,6 +48,11 @@ res = {"kernel": KERNEL, "launches_fetch": len(f_kb), "launches_write": len(w_kb
        "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes, --kernel-trace), "
                  "bench.py --steps 1 --warmup 1; traffic = 2 x FETCH_SIZE + WRITE_SIZE (KB -> B), "
                  "averaged over the fwd+dgrad launches"}
+if bench_line is not None:
+    res["workload_key"] = bench_line["workload_key"]
+    res["lib_sources_sha256"] = bench_line.get("build", {}).get("lib_sources_sha256")
+    res["compulsory_bytes_per_launch"] = bench_line["roofline"]["compulsory_bytes_per_launch"]
+    res["traffic_over_compulsory"] = res["hbm_bytes_per_launch"] / res["compulsory_bytes_per_launch"]
 json.dump(res, open(sys.argv[3], "w"), indent=1)
 print(json.dumps(res, indent=1))
 

@@ -527,7 +527,7 @@ int halo(spff_plan* p, const float* interior, const Vol& v, int C, hipStream_t s
   if (p->co.rank == 0) HIPCK(hipMemsetAsync(in - sl, 0, sl * sizeof(float), st));
   if (p->co.rank == p->co.world - 1)
     HIPCK(hipMemsetAsync(in + v.D * sl, 0, sl * sizeof(float), st));
-  if (p->co.halo(p->co.ctx, in, sl, v.D, st) != 0) return fail(SPFF_EHIP, "halo exchange failed");
+  if (p->co.do_halo(in, sl, v.D, st) != 0) return fail(SPFF_ECOLL, "halo exchange failed");
   return SPFF_OK;
 }
 int halo_src(spff_plan* p, const Src2& x, const Vol& v, hipStream_t st = nullptr) {
@@ -548,8 +548,8 @@ int hpad_src(spff_plan* p, const Src2& x, const Vol& v, int cin, float* xp, bool
   HIPCK(hpad(x, cin, xp, stg, v, ldp, p->st));
   if (!exch) return SPFF_OK;
   const int64_t S = (int64_t)v.B * v.D * v.W * ldp;
-  if (p->co.halo(p->co.ctx, stg + S, S, 2, p->st) != 0)
-    return fail(SPFF_EHIP, "halo exchange failed");
+  if (p->co.do_halo(stg + S, S, 2, p->st) != 0)
+    return fail(SPFF_ECOLL, "halo exchange failed");
   HIPCK(hfill(xp, stg, v, ldp, p->co.rank == 0, p->co.rank == p->co.world - 1, p->st));
   return SPFF_OK;
 }
@@ -1087,6 +1087,16 @@ int spff_param_info(const spff_plan* p, int i, const char** name, int* ndim, int
 int64_t spff_param_floats(const spff_plan* p) { return p ? p->nparam : 0; }
 size_t spff_workspace_bytes(const spff_plan* p) { return p ? p->total : 0; }
 
+// a step that failed because a shard-group callback returned non-zero (e.g. a peer
+// that timed out) reports SPFF_ECOLL and which callback, whatever status the failing
+// kernel-level call surfaced
+static int coll_status(spff_plan* p, int rc, const char* what) {
+  if (rc == SPFF_OK || !p->co.failed) return rc;
+  return fail(SPFF_ECOLL, std::string(what) + ": shard-group collective (spff_coll." +
+                              p->co.failed + ") failed; the step's outputs are undefined (" +
+                              g_err + ")");
+}
+
 int spff_forward(spff_plan* p, const float* x, const float* params, float* logits, void* ws,
                  void* stream) {
   if (!p || !x || !params || !logits || !ws) return fail(SPFF_EINVAL, "null argument");
@@ -1097,7 +1107,8 @@ int spff_forward(spff_plan* p, const float* x, const float* params, float* logit
   if (p->co.on() && !p->coll_set)
     return fail(SPFF_EINVAL, "depth-sharded plan: call spff_plan_set_coll first");
   CK(ensure_pe(p));
-  return forward(p, x, logits);
+  p->co.failed = nullptr;
+  return coll_status(p, forward(p, x, logits), "spff_forward");
 }
 
 int spff_backward(spff_plan* p, const float* dlogits, const float* params, float* dparams,
@@ -1109,7 +1120,8 @@ int spff_backward(spff_plan* p, const float* dlogits, const float* params, float
   p->st = static_cast<hipStream_t>(stream);
   if (p->co.on() && !p->coll_set)
     return fail(SPFF_EINVAL, "depth-sharded plan: call spff_plan_set_coll first");
-  return backward(p, dlogits);
+  p->co.failed = nullptr;
+  return coll_status(p, backward(p, dlogits), "spff_backward");
 }
 
 int spff_saved_tensor(const spff_plan* p, void* ws, const char* name, const float** ptr,

@@ -229,14 +229,26 @@ struct Coll {
   void* ctx = nullptr;
   int (*allreduce)(void*, void*, int64_t, int, void*) = nullptr;
   int (*halo)(void*, float*, int64_t, int, void*) = nullptr;
+  // the first callback that failed during the current spff_forward / spff_backward
+  // ("allreduce" / "halo"; nullptr: none) -- the entry points report it as SPFF_ECOLL
+  mutable const char* failed = nullptr;
   bool on() const { return world > 1; }
   hipError_t sum_f64(double* buf, int64_t n, hipStream_t s) const {
     if (!on()) return hipSuccess;
-    return allreduce(ctx, buf, n, 1, s) == 0 ? hipSuccess : hipErrorUnknown;
+    if (allreduce(ctx, buf, n, 1, s) == 0) return hipSuccess;
+    if (!failed) failed = "allreduce";
+    return hipErrorUnknown;
   }
   hipError_t sum_f32(float* buf, int64_t n, hipStream_t s) const {
     if (!on()) return hipSuccess;
-    return allreduce(ctx, buf, n, 0, s) == 0 ? hipSuccess : hipErrorUnknown;
+    if (allreduce(ctx, buf, n, 0, s) == 0) return hipSuccess;
+    if (!failed) failed = "allreduce";
+    return hipErrorUnknown;
+  }
+  int do_halo(float* interior, int64_t slice_floats, int d_local, hipStream_t s) const {
+    const int r = halo(ctx, interior, slice_floats, d_local, s);
+    if (r != 0 && !failed) failed = "halo";
+    return r;
   }
 };
 

@@ -5,6 +5,7 @@ missing or the tensors are not on a ROCm device, every entry point raises.
 """
 from __future__ import annotations
 
+import collections
 import ctypes
 import os
 import pathlib
@@ -21,6 +22,14 @@ _lib_lock = threading.Lock()
 
 class SpffError(RuntimeError):
     pass
+
+
+class SpffCollError(SpffError):
+    """A shard-group collective (spff_coll callback: halo exchange or all-reduce) failed,
+    e.g. a peer rank died or timed out; the engine returned SPFF_ECOLL."""
+
+
+SPFF_ECOLL = -4
 
 
 class spff_cfg(ctypes.Structure):
@@ -342,9 +351,20 @@ class Plan:
                               dtype=torch.float32, device=x.device)
         ws = self.workspace(x.device)
         self.generation += 1
-        check(lib().spff_forward(self._h, _ptr(x), _ptr(flat), _ptr(out), _ptr(ws),
-                                 _stream(x.device)), "spff_forward")
+        self.coll_error = None
+        self._check(lib().spff_forward(self._h, _ptr(x), _ptr(flat), _ptr(out), _ptr(ws),
+                                       _stream(x.device)), "spff_forward")
         return out
+
+    def _check(self, rc: int, what: str) -> None:
+        """check(), raising SpffCollError chained to the callback's own exception when a
+        shard-group collective failed (SPFF_ECOLL)"""
+        if rc == SPFF_ECOLL:
+            msg = lib().spff_last_error()
+            err = getattr(self, "coll_error", None)
+            raise SpffCollError(f"{what} failed ({rc}): {msg.decode() if msg else ''}"
+                                + (f" -- {err!r}" if err is not None else "")) from err
+        check(rc, what)
 
     def backward(self, dlogits_cl: torch.Tensor, flat: torch.Tensor,
                  dflat: Optional[torch.Tensor] = None, grad_hook=None) -> torch.Tensor:
@@ -357,9 +377,10 @@ class Plan:
             dflat = torch.empty(self.nfloats, dtype=torch.float32, device=dlogits_cl.device)
         ws = self.workspace(dlogits_cl.device)
         L = lib()
+        self.coll_error = None
         if grad_hook is None:
-            check(L.spff_backward(self._h, _ptr(dlogits_cl), _ptr(flat), _ptr(dflat), _ptr(ws),
-                                  _stream(dlogits_cl.device)), "spff_backward")
+            self._check(L.spff_backward(self._h, _ptr(dlogits_cl), _ptr(flat), _ptr(dflat),
+                                        _ptr(ws), _stream(dlogits_cl.device)), "spff_backward")
             return dflat
         covered = [0]
         err = []
@@ -374,18 +395,27 @@ class Plan:
                 return 1
         fn = GRAD_READY_FN(_ready)
         grad_hook.begin(dflat)
-        check(L.spff_plan_set_grad_hook(self._h, fn, None), "spff_plan_set_grad_hook")
+        ok = False
         try:
-            rc = L.spff_backward(self._h, _ptr(dlogits_cl), _ptr(flat), _ptr(dflat), _ptr(ws),
-                                 _stream(dlogits_cl.device))
+            check(L.spff_plan_set_grad_hook(self._h, fn, None), "spff_plan_set_grad_hook")
+            try:
+                rc = L.spff_backward(self._h, _ptr(dlogits_cl), _ptr(flat), _ptr(dflat), _ptr(ws),
+                                     _stream(dlogits_cl.device))
+            finally:
+                L.spff_plan_set_grad_hook(self._h, GRAD_READY_FN(), None)
+            if err:
+                raise SpffError(f"gradient hook failed: {err[0]!r}") from err[0]
+            self._check(rc, "spff_backward")
+            if covered[0] != self.nfloats:
+                raise SpffError(f"gradient hook covered {covered[0]} of {self.nfloats} floats")
+            grad_hook.finish()
+            ok = True
         finally:
-            L.spff_plan_set_grad_hook(self._h, GRAD_READY_FN(), None)
-        if err:
-            raise SpffError(f"gradient hook failed: {err[0]!r}")
-        check(rc, "spff_backward")
-        if covered[0] != self.nfloats:
-            raise SpffError(f"gradient hook covered {covered[0]} of {self.nfloats} floats")
-        grad_hook.finish()
+            if not ok and hasattr(grad_hook, "abort"):
+                # join the bucket all-reduces already issued, so peers that issued the
+                # same ones complete them, then let the error propagate (the process
+                # group's timeout ends any collective a peer is left waiting in)
+                grad_hook.abort()
         return dflat
 
     PROF_CLASSES = ("conv_fwd", "conv_dgrad", "conv_wgrad", "gemm", "slab_reduce", "act_apply",
@@ -419,11 +449,26 @@ class Plan:
         return ws[off:off + 4 * n].view(torch.float32).view(nv.value, ch.value).clone()
 
 
-# Plans (and the workspace each pins: ~2.9 KB per voxel) belong to the module
-# that created them: one plan per (module, tag) -- a new shape replaces the old
-# plan -- dropped with the module (weak keys), or explicitly by release_plans().
+# Plans (and the workspace each pins: ~2.6 KB per voxel) belong to the module
+# that created them: a small LRU of shapes per (module, tag) -- so alternating
+# shapes (a partial last batch, validation at another size) do not rebuild and
+# re-allocate a multi-GB workspace on every switch -- dropped with the module (weak
+# keys), or explicitly by release_plans().  At most PLAN_CACHE plans per (module,
+# tag), and older ones are evicted first while their workspaces together would exceed
+# PLAN_CACHE_FRACTION of the device memory (a 5 x 512^3 plan alone is 211 GiB).
 _OWNER_PLANS: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
 _ANON_PLANS: Dict[tuple, object] = {}
+PLAN_CACHE = int(os.environ.get("SPFF_PLAN_CACHE", "3"))
+PLAN_CACHE_FRACTION = 0.4
+
+
+def _device_bytes() -> int:
+    try:
+        if torch.cuda.is_available():
+            return int(torch.cuda.get_device_properties(torch.cuda.current_device()).total_memory)
+    except Exception:  # noqa: BLE001
+        pass
+    return 64 << 30
 
 
 def _owned_plan(owner, tag: str, key: tuple, make):
@@ -435,12 +480,18 @@ def _owned_plan(owner, tag: str, key: tuple, make):
     if slots is None:
         slots = {}
         _OWNER_PLANS[owner] = slots
-    cur = slots.get(tag)
-    if cur is None or cur[0] != key:
-        slots.pop(tag, None)  # free the old plan's workspace before allocating a new one
-        cur = (key, make())
-        slots[tag] = cur
-    return cur[1]
+    lru = slots.setdefault(tag, collections.OrderedDict())
+    if key in lru:
+        lru.move_to_end(key)
+        return lru[key]
+    plan = make()  # host-side only: the workspace is allocated at first use
+    budget = PLAN_CACHE_FRACTION * _device_bytes()
+    while lru and (len(lru) >= PLAN_CACHE or
+                   sum(getattr(q, "ws_bytes", 0) for q in lru.values())
+                   + getattr(plan, "ws_bytes", 0) > budget):
+        lru.popitem(last=False)  # free the least recently used plan's workspace first
+    lru[key] = plan
+    return plan
 
 
 def release_plans(owner=None) -> None:

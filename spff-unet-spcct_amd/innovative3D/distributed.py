@@ -105,9 +105,21 @@ class GradBucketer:
         self.runs: List[List[int]] = []   # pending [start, end) runs, disjoint
         self.works = []
         self.launched: List[tuple] = []   # (start, end) of every issued all-reduce
+        self.begun = 0                    # begin() calls (DataParallelSPFF checks coverage)
 
     def begin(self, flat: torch.Tensor) -> None:
         self.flat, self.runs, self.works, self.launched = flat, [], [], []
+        self.begun += 1
+
+    def abort(self) -> None:
+        """Error exit of a backward that had begun: wait for the all-reduces already
+        issued (peers that issued the same ones can complete them) and drop the rest."""
+        works, self.works, self.runs = self.works, [], []
+        for w in works:
+            try:
+                w.wait()
+            except Exception:  # noqa: BLE001 -- the original error is what propagates
+                pass
 
     def _launch(self, a: int, b: int) -> None:
         self.launched.append((a, b))
@@ -139,10 +151,16 @@ class GradBucketer:
 
 
 class DataParallelSPFF:
-    """Minimal DDP for an SPFF module (Lit or core): ``step(x, y)`` runs
-    forward, the global-count loss, backward with the bucketed, overlapped
+    """Minimal DDP for an engine module (SPFF core or any Lit wrapper): ``step(x, y)``
+    runs forward, the global-count loss, backward with the bucketed, overlapped
     gradient all-reduce, and returns (loss, conf) of the GLOBAL batch -- the
-    values a single device would report for the concatenated batch."""
+    values a single device would report for the concatenated batch.
+
+    The bucketer is attached as ``grad_hook`` to EVERY submodule (the engine reads it
+    from whichever module calls its plan: the core, ``.backbone`` of the 3DUNet wrapper,
+    ``.model.model`` of the Swin wrapper).  If no plan took the hook during a step
+    (a backward that did not run through the engine), the gradients are all-reduced
+    after the backward instead, so ranks can never keep unreduced gradients."""
 
     def __init__(self, module: torch.nn.Module, num_classes: int, ignore_index: int = 255,
                  group=None, bucket_bytes: int = 4 << 20, overlap: bool = True):
@@ -151,13 +169,18 @@ class DataParallelSPFF:
         self.core = getattr(module, "model", module)
         self.bucketer = GradBucketer(group, bucket_bytes) if overlap else None
 
+    def _set_hook(self, hook) -> None:
+        for m in self.module.modules():
+            m.grad_hook = hook
+
     def step(self, x: torch.Tensor, y: torch.Tensor):
         from .helpers import ce_dice_parts
         for p in self.params:
             p.grad = None
         n = world(self.group)
         hook = self.bucketer if (n > 1 and self.bucketer is not None) else None
-        self.core.grad_hook = hook
+        begun = hook.begun if hook is not None else 0
+        self._set_hook(hook)
         try:
             logits = self.module(x)
             cnt = global_valid_count(y, self.ignore, self.group) if n > 1 else None
@@ -165,8 +188,8 @@ class DataParallelSPFF:
                                                count_override=cnt)
             loss_loc.backward()
         finally:
-            self.core.grad_hook = None
-        if n > 1 and hook is None:
+            self._set_hook(None)
+        if n > 1 and (hook is None or hook.begun == begun):
             allreduce_gradients(self.params, self.group)
         if n == 1:
             return loss_loc.detach(), conf

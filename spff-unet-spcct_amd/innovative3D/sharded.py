@@ -31,6 +31,8 @@ tests/test_gpu_sharded.py.
 """
 from __future__ import annotations
 
+import datetime
+
 import torch
 import torch.distributed as dist
 
@@ -41,21 +43,43 @@ class TorchDepthColl:
     """spff_coll over a torch.distributed group.  Device tensors go straight to
     the backend (RCCL: all_reduce and batched point-to-point send / recv on the
     current stream); ``host_staged`` (default for gloo) copies through host
-    memory, which lets several ranks share one GPU in tests."""
+    memory, which lets several ranks share one GPU in tests.
 
-    def __init__(self, group=None, host_staged=None):
+    Failure detection: a host-staged exchange waits at most ``timeout``
+    seconds for its peers and then raises, which the engine turns into a failed step
+    (SPFF_ECOLL -> innovative3D._engine.SpffCollError naming the collective and the
+    peer) instead of a hang.  Device (RCCL) collectives are stream-ordered -- blocking
+    the host on them would serialise the halo exchange the engine overlaps with the
+    interior tiles -- so they are bounded by the process group's own timeout
+    (init_process_group(timeout=...), with TORCH_NCCL_ASYNC_ERROR_HANDLING=1, as
+    bench.py / train.py set), whose watchdog fails the job when a peer stalls."""
+
+    def __init__(self, group=None, host_staged=None, timeout: float = 300.0):
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         self.host = (dist.get_backend(group) == "gloo") if host_staged is None else host_staged
+        self.timeout = datetime.timedelta(seconds=float(timeout))
 
     def _peer(self, r):
         return dist.get_global_rank(self.group, r) if self.group is not None else r
 
+    def _wait(self, works, what: str) -> None:
+        for w in works:
+            try:
+                ok = w.wait(timeout=self.timeout)
+            except Exception as e:  # noqa: BLE001
+                raise RuntimeError(f"rank {self.rank}: {what} did not complete within "
+                                   f"{self.timeout.total_seconds():.0f} s ({e})") from e
+            if ok is False:
+                raise RuntimeError(f"rank {self.rank}: {what} did not complete within "
+                                   f"{self.timeout.total_seconds():.0f} s")
+
     def allreduce(self, t: torch.Tensor) -> None:
         if self.host:
             c = t.cpu()
-            dist.all_reduce(c, group=self.group)
+            self._wait([dist.all_reduce(c, group=self.group, async_op=True)],
+                       f"all-reduce of {c.numel()} {str(c.dtype)[6:]} over {self.world} ranks")
             t.copy_(c)
         else:
             dist.all_reduce(t, group=self.group)
@@ -75,8 +99,8 @@ class TorchDepthColl:
             if r + 1 < w:
                 ops += [dist.P2POp(dist.isend, last_c, self._peer(r + 1), self.group),
                         dist.P2POp(dist.irecv, right_c, self._peer(r + 1), self.group)]
-            for op in dist.batch_isend_irecv(ops) if ops else []:
-                op.wait()
+            self._wait(dist.batch_isend_irecv(ops) if ops else [],
+                       f"halo exchange with ranks {[q for q in (r - 1, r + 1) if 0 <= q < w]}")
             if r > 0:
                 left.copy_(left_c)
             if r + 1 < w:
@@ -118,9 +142,9 @@ class DepthShardedSPFF:
     axis = 0  # SPFF_SHARD_DEPTH
 
     def __init__(self, core: torch.nn.Module, num_classes: int, ignore_index: int = 255,
-                 group=None, coll=None):
+                 group=None, coll=None, timeout: float = 300.0):
         self.core, self.K, self.ignore, self.group = core, int(num_classes), ignore_index, group
-        self.coll = coll or TorchDepthColl(group)
+        self.coll = coll or TorchDepthColl(group, timeout=timeout)
         core.shard = (self.coll.world, self.coll.rank, self.axis)
         core.shard_coll = self.coll
         self.params = [p for p in core.parameters()]

@@ -158,3 +158,82 @@ def test_dice_loss_from_confusion_t_matches_host():
         a = Hh.dice_loss_from_confusion(conf, K)
         b = float(Hh.dice_loss_from_confusion_t(torch.from_numpy(conf), K))
         assert abs(a - b) <= 1e-15
+
+
+def _worker_timeout(rank, world, port, out_path):
+    """rank 1 never joins the halo exchange: rank 0's host-staged TorchDepthColl must
+    raise within its deadline (SURVEY §5 failure detection) instead of hanging."""
+    import sys
+    import pathlib
+    import time
+    root = pathlib.Path(__file__).resolve().parents[1]
+    sys.path[:0] = [str(root / "tests"), str(root), str(root / "spff-unet-spcct_amd")]
+    from innovative3D.sharded import TorchDepthColl
+    import datetime
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=60))
+    coll = TorchDepthColl(timeout=2.0)
+    msg = ""
+    if rank == 0:
+        slab = torch.zeros(4 * 8)
+        t0 = time.time()
+        try:
+            coll.halo(slab, 8, 2)
+        except RuntimeError as e:
+            msg = str(e)
+        np.savez(out_path, msg=np.array(msg), dt=np.array(time.time() - t0))
+    else:
+        time.sleep(6.0)   # a stalled peer: never posts its side of the exchange
+    os._exit(0)           # skip the (now mismatched) process-group teardown
+
+
+def test_host_staged_halo_times_out(tmp_path):
+    out = str(tmp_path / "t.npz")
+    mp.spawn(_worker_timeout, args=(2, _free_port(), out), nprocs=2, join=True)
+    got = np.load(out)
+    assert "did not complete within 2 s" in str(got["msg"]), str(got["msg"])
+    assert float(got["dt"]) < 5.0
+
+
+def test_data_parallel_hooks_every_submodule_and_falls_back(monkeypatch):
+    """the grad hook must reach the module that calls the engine plan
+    (``.backbone``, ``.model.model``), and a step in which no plan took it must still
+    all-reduce the gradients (world > 1)."""
+    from innovative3D import distributed as Dd
+    import innovative3D.helpers as Hh
+
+    seen = []
+
+    class Inner(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.w = torch.nn.Parameter(torch.ones(3))
+
+        def forward(self, x):
+            seen.append(getattr(self, "grad_hook", None))
+            return x * self.w
+
+    class Outer(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.backbone = Inner()
+
+        def forward(self, x):
+            return self.backbone(x)
+
+    m = Outer()
+    calls = []
+    monkeypatch.setattr(Dd, "world", lambda group=None: 2)
+    monkeypatch.setattr(Dd, "global_valid_count", lambda *a, **k: None)
+    monkeypatch.setattr(Dd, "allreduce_gradients", lambda params, group=None: calls.append(1))
+    monkeypatch.setattr(Dd, "global_loss", lambda ce, conf, K, group=None: (ce, ce, conf))
+    monkeypatch.setattr(Hh, "ce_dice_parts",
+                        lambda lg, y, K, ig, count_override=None: (lg.sum(), None, lg.sum()))
+    dp = Dd.DataParallelSPFF(m, 3)
+    dp.step(torch.ones(3), None)
+    assert seen and seen[0] is dp.bucketer          # reached the nested module
+    assert getattr(m.backbone, "grad_hook", "x") is None   # and was removed afterwards
+    assert calls == [1]                              # no plan began the hook: fallback ran
+    assert torch.equal(m.backbone.w.grad, torch.ones(3))

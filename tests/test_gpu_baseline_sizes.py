@@ -114,10 +114,46 @@ def _mag_scales(st, g64s):
     return out
 
 
-def _compare(tag, lg, loss, grads, ref_logits, ref_loss, ref_grads, loss_rtol=1e-5, scales=None):
+def _compare_metrics(tag, conf, labels, ref_logits, nflips, K=K13):
+    """BASELINE metric's "macro-Dice parity": per_class_metrics_3d of the engine's
+    confusion (helpers.metrics_from_confusion) vs the reference semantics on the oracle's
+    argmax (oracle per_class_metrics_3d, helpers.py:668-725), and the hard macro-Dice
+    loss term (helpers.py:782-795).  Equal when no argmax flips; otherwise each flip moves
+    one voxel between two classes, which changes dice_c = 2tp/(2tp+fp+fn) of those two
+    classes by at most ~2/(2tp+fp+fn) each, so |d macro| <= 4 flips / min_c(2tp+fp+fn) /
+    (K-1) -- asserted with the bound printed."""
+    import innovative3D.models as M
+    from oracle import spff_oracle as O
+    conf = np.asarray(conf)
+    n = int(labels.numel())
+    met = M.metrics_from_confusion(conf, K, n)
+    ref_conf = O.confusion(ref_logits, labels, K, 255)
+    ref = O.metrics_from_confusion(ref_conf, K, n)
+    dl_e = O.macro_dice_loss(conf[:, :K], K)
+    dl_r = O.macro_dice_loss(ref_conf, K)
+    dmac = abs(met[3] - ref[3])
+    # 2 tp + fp + fn = row sum + column sum of the class
+    den = min(int(ref_conf[c, :].sum()) + int(ref_conf[:, c].sum()) for c in range(1, K))
+    bound = 4.0 * nflips / max(den - nflips, 1) / (K - 1)
+    print(f"{tag}: macro-Dice {met[3]:.10f} vs oracle {ref[3]:.10f} (|d| {dmac:.2e}, bound "
+          f"{bound:.2e} for {nflips} flips); hard-Dice loss term {dl_e:.10f} vs {dl_r:.10f}; "
+          f"micro-Dice {met[6]:.10f} vs {ref[6]:.10f}")
+    assert int(conf[:, K].sum()) == 0
+    if nflips == 0:
+        np.testing.assert_array_equal(conf[:, :K], ref_conf)
+        assert met[3] == ref[3] and dl_e == dl_r
+    else:
+        assert int(np.abs(conf[:, :K] - ref_conf).sum()) <= 2 * nflips
+        assert dmac <= bound and abs(dl_e - dl_r) <= bound
+        assert abs(met[6] - ref[6]) <= bound * (K - 1)
+
+
+def _compare(tag, lg, loss, grads, ref_logits, ref_loss, ref_grads, loss_rtol=1e-5, scales=None,
+             conf=None, labels=None):
     """``ref_grads`` = (fp64, fp32) kink-consistent oracle gradients: every engine
     gradient within max(1e-3, 4 x the fp32 oracle's own distance) relative L2 of fp64
-    (relative to ``scales[k]`` instead of |g64| where given)."""
+    (relative to ``scales[k]`` instead of |g64| where given).  ``conf`` (the engine's
+    [K, K+1] confusion) + ``labels``: also the metric tuple (_compare_metrics)."""
     err = float((lg - ref_logits).abs().max())
     am, am_ref = lg.argmax(1), ref_logits.argmax(1)
     flips = am != am_ref
@@ -130,6 +166,8 @@ def _compare(tag, lg, loss, grads, ref_logits, ref_loss, ref_grads, loss_rtol=1e
     assert err <= 1e-3
     assert not (flips & ~ties).any(), f"{int((flips & ~ties).sum())} argmax flips outside near-ties"
     assert abs(loss - ref_loss) <= loss_rtol * abs(ref_loss)
+    if conf is not None:
+        _compare_metrics(tag, conf, labels, ref_logits, int(flips.sum()))
     g64s, g32s = ref_grads
     rows, bad = [], []
     for k, g64 in g64s.items():
@@ -168,13 +206,14 @@ def test_config2_headline_matches_oracle(config2_oracle, mth):
     core = core.to(DEV)
     core.math = mth
     logits = core(x.to(DEV))
-    loss, _conf = Hh.ce_dice_with_confusion(logits, y.to(DEV), K13, 255)
+    loss, conf = Hh.ce_dice_with_confusion(logits, y.to(DEV), K13, 255)
     loss.backward()
     torch.cuda.synchronize()
     grads = {k: p.grad for k, p in core.named_parameters(remove_duplicate=False)}
     ref_grads = _oracle_grads(st, x, y, _engine_masks(core, tuple(x.shape), st))
     _compare(f"config2 2x5x128^3 {mth}", logits.detach().cpu(), float(loss), grads, ref_logits,
-             ref_loss, ref_grads, scales=_mag_scales(st, ref_grads[0]))
+             ref_loss, ref_grads, scales=_mag_scales(st, ref_grads[0]),
+             conf=conf.cpu().numpy(), labels=y)
 
 
 # ------------------------------------------------- configs[3] path (sharded)

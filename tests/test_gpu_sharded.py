@@ -5,7 +5,17 @@ plan, exchange halos and all-reduce through host-staged gloo
 the all-reduced gradients must match the unsharded engine on the same volume.
 The 16-deep case gives each of 2 ranks 4 depth tiles, so the split-bf16 convs run
 the halo exchange on the engine's side stream beside their interior depth tiles
-(engine.hip conv_halo).  The height-sharded cases split the registry layout
+(engine.hip conv_halo).
+
+Gradients are judged BRANCH-CONSISTENTLY: against the fp64 oracle run with the
+sharded engine's own LeakyReLU signs and max-pool argmaxes (each rank's slab,
+gathered; test_gpu_parity.engine_branch_masks / oracle_grads_st), not against the
+unsharded engine.  Two fp32 engines whose reductions sum in different orders may
+put a LeakyReLU input that sits on its kink on opposite sides, which moves a
+gradient tensor by up to 14 % at these tiny sizes (round 2: the 4-wave conv tiles'
+fused statistics order) -- a legitimate fp32 outcome, not a sharding error.  The
+logits, loss and confusion (robust to such flips) are still compared with the
+unsharded engine.  The height-sharded cases split the registry layout
 [B, 1, 5, H, W] into row slabs (spff_cfg.shard_axis = SPFF_SHARD_HEIGHT,
 innovative3D.sharded.HeightShardedSPFF); the full-size 1 x 1 x 5 x 512 x 512 registry
 volume is checked against the kink-consistent oracle in test_gpu_baseline_sizes.py
@@ -52,7 +62,51 @@ def _model(math_mode, depth=SHAPE[2], k=K, base=BASE, in_ch=SHAPE[1]):
     core.load_state_dict({k: torch.from_numpy(v) for k, v in st.items()})
     core = core.to("cuda")
     core.math = math_mode
+    core._synth_state = st
     return core
+
+
+def _cfg(k=K, base=BASE, in_ch=SHAPE[1]):
+    from oracle import spff_oracle as O
+    return O.SpffCfg(in_ch=in_ch, num_classes=k, base=base)
+
+
+def _save_masks(core, local_shape, cfg):
+    """this rank's LeakyReLU signs / pool argmaxes over its own slab (npz-ready)"""
+    from test_gpu_parity import engine_branch_masks
+    masks = engine_branch_masks(core, local_shape, core._synth_state, cfg)
+    mk = {}
+    for kk, m in masks.items():
+        a = m.numpy()
+        mk["m_" + kk] = np.packbits(a) if a.dtype == np.bool_ else a.astype(np.uint8)
+        mk["s_" + kk] = np.array(a.shape)
+    return mk
+
+
+def _gather_masks(parts, axis):
+    """the ranks' branch decisions concatenated along the sharded axis (2 = D, 3 = H)"""
+    masks = {}
+    for kk in (f[2:] for f in parts[0].files if f.startswith("m_")):
+        segs = []
+        for p in parts:
+            shp = tuple(int(v) for v in p["s_" + kk])
+            a = p["m_" + kk]
+            a = np.unpackbits(a)[:int(np.prod(shp))].astype(bool) if kk[:4] != "pool" else a
+            segs.append(a.reshape(shp))
+        cat = np.concatenate(segs, axis=axis)
+        masks[kk] = (torch.from_numpy(cat) if cat.dtype == np.bool_
+                     else torch.from_numpy(cat.astype(np.int64)))
+    return masks
+
+
+def _check_vs_oracle(parts, axis, st, cfg, x, y, mth):
+    """the sharded engine's gradients (rank 0; all ranks hold the same all-reduced
+    gradient) vs the fp64 oracle with the sharded engine's own branch decisions"""
+    from test_gpu_parity import check_grads, oracle_grads_st
+    masks = _gather_masks(parts, axis)
+    ref64, ref32, nflip, absb = oracle_grads_st(cfg, st, x.numpy(), y.numpy(), masks)
+    print(f"  branch decisions differing from the fp64 oracle's own: {nflip}")
+    check_grads({k: parts[0]["g_" + k] for k in ref64}, ref64, ref32, absb, st, mth)
 
 
 def _data(depth=SHAPE[2]):
@@ -71,7 +125,7 @@ def _hworker(rank, world, port, math_mode, out, case, memory=None):
     import pathlib
     import sys
     root = pathlib.Path(__file__).resolve().parents[1]
-    sys.path[:0] = [str(root), str(root / "spff-unet-spcct_amd")]
+    sys.path[:0] = [str(root), str(root / "tests"), str(root / "spff-unet-spcct_amd")]
     from innovative3D.sharded import HeightShardedSPFF, height_bounds
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -86,8 +140,9 @@ def _hworker(rank, world, port, math_mode, out, case, memory=None):
     loss, conf = step.step(x[:, :, :, off:off + h].contiguous().cuda(),
                            y[:, :, off:off + h].contiguous().cuda())
     torch.cuda.synchronize()
+    mk = _save_masks(core, (B, 1, 5, h, W), _cfg(k, base, 1))
     np.savez(f"{out}.{rank}.npz", logits=step.last_logits.cpu().numpy(), loss=float(loss),
-             conf=conf.cpu().numpy(),
+             conf=conf.cpu().numpy(), **mk,
              **{"g_" + kk: p.grad.cpu().numpy() for kk, p in core.named_parameters()
                 if p.grad is not None})
     dist.barrier()
@@ -98,7 +153,7 @@ def _worker(rank, world, port, math_mode, out, depth):
     import pathlib
     import sys
     root = pathlib.Path(__file__).resolve().parents[1]
-    sys.path[:0] = [str(root), str(root / "spff-unet-spcct_amd")]
+    sys.path[:0] = [str(root), str(root / "tests"), str(root / "spff-unet-spcct_amd")]
     from innovative3D.sharded import DepthShardedSPFF, shard_bounds
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -110,8 +165,9 @@ def _worker(rank, world, port, math_mode, out, depth):
     step = DepthShardedSPFF(core, K, 255)
     loss, conf = step.step(x[:, :, off:off + d].contiguous().cuda(), y[:, off:off + d].contiguous().cuda())
     torch.cuda.synchronize()
+    mk = _save_masks(core, (SHAPE[0], SHAPE[1], d, SHAPE[3], SHAPE[4]), _cfg())
     np.savez(f"{out}.{rank}.npz", logits=step.last_logits.cpu().numpy(), loss=float(loss),
-             conf=conf.cpu().numpy(),
+             conf=conf.cpu().numpy(), **mk,
              **{"g_" + k: p.grad.cpu().numpy() for k, p in core.named_parameters()
                 if p.grad is not None})
     dist.barrier()
@@ -123,6 +179,7 @@ def _worker(rank, world, port, math_mode, out, depth):
 def test_depth_sharded_engine_matches_unsharded(tmp_path, world, math_mode, depth):
     import innovative3D.helpers as Hh
     core = _model(math_mode, depth)
+    st = core._synth_state
     x, y = _data(depth)
     logits = core(x.cuda())
     loss, conf = Hh.ce_dice_with_confusion(logits, y.cuda(), K, 255)
@@ -138,18 +195,12 @@ def test_depth_sharded_engine_matches_unsharded(tmp_path, world, math_mode, dept
           f"vs {float(loss):.7f}")
     assert e <= 1e-4 * float(np.abs(ref).max())
     assert abs(float(parts[0]["loss"]) - float(loss)) <= 1e-5 * abs(float(loss))
-    np.testing.assert_array_equal(parts[0]["conf"], conf.cpu().numpy())
-    rows = []
-    for k, g in grads.items():
-        sc = max(float(np.abs(g).max()), 1e-30)
-        eg = float(np.abs(parts[0]["g_" + k] - g).max()) / sc
-        rows.append((eg, k))
+    nflip = int((lg.argmax(1) != ref.argmax(1)).sum())
+    assert int(np.abs(parts[0]["conf"] - conf.cpu().numpy()).sum()) <= 2 * nflip
+    for k in grads:
         for p in parts[1:]:
             np.testing.assert_array_equal(p["g_" + k], parts[0]["g_" + k])
-    rows.sort(reverse=True)
-    print("  " + ", ".join(f"{k} {v:.1e}" for v, k in rows[:5]))
-    bad = [(k, v) for v, k in rows if v > (5e-2 if k.endswith("mag_scale") else 2e-3)]
-    assert not bad, bad
+    _check_vs_oracle(parts, 2, st, _cfg(), x, y, math_mode)
 
 
 @pytest.mark.parametrize("world,math_mode,case,memory", [
@@ -161,6 +212,7 @@ def test_height_sharded_engine_matches_unsharded(tmp_path, world, math_mode, cas
     import innovative3D.helpers as Hh
     B, H, W, k, base = HCASES[case]
     core = _model(math_mode, 5, k, base, 1)
+    st = core._synth_state
     x, y = _hdata(case)
     logits = core(x.cuda())
     loss, conf = Hh.ce_dice_with_confusion(logits, y.cuda(), k, 255)
@@ -184,14 +236,7 @@ def test_height_sharded_engine_matches_unsharded(tmp_path, world, math_mode, cas
     assert abs(float(parts[0]["loss"]) - loss_ref) <= 1e-5 * abs(loss_ref)
     # the confusion counts match except where a logit within rounding of a tie flips
     assert int(np.abs(parts[0]["conf"] - conf_ref).sum()) <= 2 * nflip
-    rows = []
-    for kk, g in grads.items():
-        sc = max(float(np.abs(g).max()), 1e-30)
-        eg = float(np.abs(parts[0]["g_" + kk] - g).max()) / sc
-        rows.append((eg, kk))
+    for kk in grads:
         for p in parts[1:]:
             np.testing.assert_array_equal(p["g_" + kk], parts[0]["g_" + kk])
-    rows.sort(reverse=True)
-    print("  " + ", ".join(f"{kk} {v:.1e}" for v, kk in rows[:5]))
-    bad = [(kk, v) for v, kk in rows if v > (5e-2 if kk.endswith("mag_scale") else 2e-3)]
-    assert not bad, bad
+    _check_vs_oracle(parts, 3, st, _cfg(k, base, 1), x, y, math_mode)
