@@ -49,9 +49,60 @@ RedPlan red_plan(Vol vol, int C) {
 }
 }  // namespace
 
+#ifndef SPFF_RED_BATCH
+#define SPFF_RED_BATCH 4  // voxel rows loaded back to back per thread before accumulating
+#endif
+
+template <int OP, int NQ>
+__device__ __forceinline__ void red_accum(const RedArgs& a, const float (&ys)[4], const float (&gs)[4],
+                                          const float (&p0)[4], const float (&p1)[4],
+                                          const float (&p2)[4], const float (&p3)[4],
+                                          const float (&mu)[4], const float (&rs)[4],
+                                          float (&acc)[NQ][4]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (OP == RED_SUM) {
+      acc[0][j] += ys[j];
+    } else if (OP == RED_SQDEV) {
+      const float t = ys[j] - p0[j];
+      acc[0][j] += t * t;
+    } else if (OP == RED_ACT) {
+      acc[0][j] += lrelu(ys[j] * p0[j] + p1[j], a.neg);
+    } else if (OP == RED_BWD_TAIL) {
+      acc[0][j] += gs[j];
+      acc[NQ - 1][j] += gs[j] * lrelu(ys[j] * p0[j] + p1[j], a.neg);
+    } else if (OP == RED_BWD_TAIL6) {
+      const float r = ys[j] * p0[j] + p1[j];
+      const float sl = slope(r, a.neg), gsl = gs[j] * sl;
+      const float xh = (ys[j] - mu[j]) * rs[j];
+      acc[0][j] += gs[j];
+      acc[1][j] += gs[j] * lrelu(r, a.neg);
+      acc[2][j] += gsl;
+      acc[3][j] += sl;
+      acc[4][j] += gsl * xh;
+      acc[5][j] += sl * xh;
+    } else {  // RED_BWD_IN
+      const float r = ys[j] * p0[j] + p1[j];
+      const float dr = (gs[j] * p2[j] + p3[j]) * slope(r, a.neg);
+      const float xh = (ys[j] - mu[j]) * rs[j];
+      acc[0][j] += dr;
+      acc[NQ - 1][j] += dr * xh;
+    }
+  }
+}
+
+// One block per (split, b*D + d): the thread (vo, cq) streams channel quad cq of voxels
+// hb + vo, hb + vo + vpp, ... of the slab's chunk, SPFF_RED_BATCH rows loaded back to
+// back (several 16-B loads in flight per thread: the single-load loop held ~half the
+// bytes in flight the HBM needs), then the fixed-order reduction over vo: for power-of-
+// two quads per voxel (C = 4 .. 256) xor-shuffles inside each wave and the 4 wave sums
+// added in wave order through LDS (one barrier); otherwise (SwinUNETR's C = 12, 24, 48,
+// the 3DUNet's C = 512) the LDS tree.
 template <int OP, int NQ>
 __global__ __launch_bounds__(256) void k_slab_reduce(RedArgs a, Vol vol, int C, float* __restrict__ ws,
                                                      int nsplit, int chunk) {
+  constexpr bool TWO = OP == RED_BWD_TAIL || OP == RED_BWD_IN || OP == RED_BWD_TAIL6;
+  constexpr int NB = SPFF_RED_BATCH;
   const int bd = blockIdx.y;  // b*D + d
   const int split = blockIdx.x;
   const int b = bd / vol.D, d = bd % vol.D;
@@ -79,56 +130,61 @@ __global__ __launch_bounds__(256) void k_slab_reduce(RedArgs a, Vol vol, int C, 
         if (a.A) { p2[j] = a.A[(int64_t)bc * vol.D + d]; p3[j] = a.Bc[(int64_t)bc * vol.D + d]; }
       }
     }
-    float mu[4], rs[4];
+    float mu[4] = {0.f, 0.f, 0.f, 0.f}, rs[4] = {0.f, 0.f, 0.f, 0.f};
     if (OP == RED_BWD_IN || OP == RED_BWD_TAIL6) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) { mu[j] = a.mean[b * C + c + j]; rs[j] = a.rstd[b * C + c + j]; }
     }
     const int hb = split * chunk, he = min(HW, hb + chunk);
     const int64_t base = (int64_t)bd * HW;
-    for (int hw = hb + vo; hw < he; hw += vpp) {
-      const int64_t off = (base + hw) * C + c;
-      const float4 yv = *reinterpret_cast<const float4*>(a.y + off);
-      const float ys[4] = {yv.x, yv.y, yv.z, yv.w};
-      float gs[4] = {0.f, 0.f, 0.f, 0.f};
-      if (OP == RED_BWD_TAIL || OP == RED_BWD_IN || OP == RED_BWD_TAIL6) {
-        const float4 gv = *reinterpret_cast<const float4*>(a.g + off);
-        gs[0] = gv.x; gs[1] = gv.y; gs[2] = gv.z; gs[3] = gv.w;
+    for (int hw0 = hb + vo; hw0 < he; hw0 += NB * vpp) {
+      float4 yv[NB], gv[NB];
+#pragma unroll
+      for (int k = 0; k < NB; ++k) {
+        const int hw = hw0 + k * vpp;
+        const int64_t off = (base + (hw < he ? hw : hw0)) * C + c;
+        yv[k] = *reinterpret_cast<const float4*>(a.y + off);
+        if (TWO) gv[k] = *reinterpret_cast<const float4*>(a.g + off);
       }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if (OP == RED_SUM) {
-          acc[0][j] += ys[j];
-        } else if (OP == RED_SQDEV) {
-          const float t = ys[j] - p0[j];
-          acc[0][j] += t * t;
-        } else if (OP == RED_ACT) {
-          acc[0][j] += lrelu(ys[j] * p0[j] + p1[j], a.neg);
-        } else if (OP == RED_BWD_TAIL) {
-          acc[0][j] += gs[j];
-          acc[NQ - 1][j] += gs[j] * lrelu(ys[j] * p0[j] + p1[j], a.neg);
-        } else if (OP == RED_BWD_TAIL6) {
-          const float r = ys[j] * p0[j] + p1[j];
-          const float sl = slope(r, a.neg), gsl = gs[j] * sl;
-          const float xh = (ys[j] - mu[j]) * rs[j];
-          acc[0][j] += gs[j];
-          acc[1][j] += gs[j] * lrelu(r, a.neg);
-          acc[2][j] += gsl;
-          acc[3][j] += sl;
-          acc[4][j] += gsl * xh;
-          acc[5][j] += sl * xh;
-        } else {  // RED_BWD_IN
-          const float r = ys[j] * p0[j] + p1[j];
-          const float dr = (gs[j] * p2[j] + p3[j]) * slope(r, a.neg);
-          const float xh = (ys[j] - mu[j]) * rs[j];
-          acc[0][j] += dr;
-          acc[NQ - 1][j] += dr * xh;
-        }
+      for (int k = 0; k < NB; ++k) {
+        if (hw0 + k * vpp >= he) break;
+        const float ys[4] = {yv[k].x, yv[k].y, yv[k].z, yv[k].w};
+        float gs[4] = {0.f, 0.f, 0.f, 0.f};
+        if (TWO) { gs[0] = gv[k].x; gs[1] = gv[k].y; gs[2] = gv[k].z; gs[3] = gv[k].w; }
+        red_accum<OP, NQ>(a, ys, gs, p0, p1, p2, p3, mu, rs, acc);
       }
     }
   }
+  __shared__ float red[256 * 4 * (NQ > 4 ? NQ : 4)];
+  if ((tpv & (tpv - 1)) == 0 && tpv <= 64) {
+    // xor-shuffle tree over the wave's 64 / tpv voxel lanes (vpp = 256 / tpv, so every
+    // thread is active and the waves hold equal voxel-lane counts), then the waves in order
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float v = acc[q][j];
+        for (int o = tpv; o < 64; o <<= 1) v += __shfl_xor(v, o);
+        acc[q][j] = v;
+      }
+    if (lane < tpv) {
+#pragma unroll
+      for (int q = 0; q < NQ; ++q)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) red[((wv * NQ + q) * tpv + lane) * 4 + j] = acc[q][j];
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < NQ * tpv * 4; i += 256) {
+      const int j = i & 3, cqq = (i >> 2) % tpv, q = (i >> 2) / tpv;
+      float t = 0.f;
+      for (int w = 0; w < 4; ++w) t += red[((w * NQ + q) * tpv + cqq) * 4 + j];
+      ws[(((int64_t)bd * nsplit + split) * C + 4 * cqq + j) * NQ + q] = t;
+    }
+    return;
+  }
   // fixed-order LDS tree over the vpp voxel lanes
-  __shared__ float red[256 * 4];
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
 #pragma unroll

@@ -143,7 +143,7 @@ def _hworker(rank, world, port, math_mode, out, case, memory=None):
     mk = _save_masks(core, (B, 1, 5, h, W), _cfg(k, base, 1))
     np.savez(f"{out}.{rank}.npz", logits=step.last_logits.cpu().numpy(), loss=float(loss),
              conf=conf.cpu().numpy(), **mk,
-             **{"g_" + kk: p.grad.cpu().numpy() for kk, p in core.named_parameters()
+             **{"g_" + kk: p.grad.cpu().numpy() for kk, p in core.named_parameters(remove_duplicate=False)
                 if p.grad is not None})
     dist.barrier()
     dist.destroy_process_group()
@@ -168,7 +168,7 @@ def _worker(rank, world, port, math_mode, out, depth):
     mk = _save_masks(core, (SHAPE[0], SHAPE[1], d, SHAPE[3], SHAPE[4]), _cfg())
     np.savez(f"{out}.{rank}.npz", logits=step.last_logits.cpu().numpy(), loss=float(loss),
              conf=conf.cpu().numpy(), **mk,
-             **{"g_" + k: p.grad.cpu().numpy() for k, p in core.named_parameters()
+             **{"g_" + k: p.grad.cpu().numpy() for k, p in core.named_parameters(remove_duplicate=False)
                 if p.grad is not None})
     dist.barrier()
     dist.destroy_process_group()
@@ -185,7 +185,7 @@ def test_depth_sharded_engine_matches_unsharded(tmp_path, world, math_mode, dept
     loss, conf = Hh.ce_dice_with_confusion(logits, y.cuda(), K, 255)
     loss.backward()
     ref = logits.detach().cpu().numpy()
-    grads = {k: p.grad.cpu().numpy() for k, p in core.named_parameters() if p.grad is not None}
+    grads = {k: p.grad.cpu().numpy() for k, p in core.named_parameters(remove_duplicate=False) if p.grad is not None}
     out = str(tmp_path / "sh")
     mp.spawn(_worker, args=(world, _free_port(), math_mode, out, depth), nprocs=world, join=True)
     parts = [np.load(f"{out}.{r}.npz") for r in range(world)]
@@ -218,7 +218,7 @@ def test_height_sharded_engine_matches_unsharded(tmp_path, world, math_mode, cas
     loss, conf = Hh.ce_dice_with_confusion(logits, y.cuda(), k, 255)
     loss.backward()
     ref = logits.detach().cpu().numpy()            # [B, K, D, H, W]
-    grads = {kk: p.grad.cpu().numpy() for kk, p in core.named_parameters() if p.grad is not None}
+    grads = {kk: p.grad.cpu().numpy() for kk, p in core.named_parameters(remove_duplicate=False) if p.grad is not None}
     loss_ref, conf_ref = float(loss), conf.cpu().numpy()
     del core, logits, loss
     torch.cuda.empty_cache()
