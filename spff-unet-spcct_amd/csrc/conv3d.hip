@@ -123,13 +123,8 @@ __global__ __launch_bounds__(256) void k_conv3d_fwd(Src2 x, const float* __restr
         const int hw = pos % HWD, t2 = pos / HWD, hh = t2 % HH, hd = t2 / HH;
         const int gd = d0 + hd - KD / 2, gh = h0 + hh - 1, gw = w0 + hw - 1;
         const int c = c0 + 4 * q;
-        if ((unsigned)(gd + vol.dh) < (unsigned)(D + 2 * vol.dh) && (unsigned)gh < (unsigned)H &&
-            (unsigned)gw < (unsigned)W && c < Cin) {
-          const int64_t vox = (((int64_t)b * D + gd) * H + gh) * W + gw;
-          const float* p =
-              c < x.split ? x.p0 + vox * x.ld0 + c : x.p1 + vox * x.ld1 + (c - x.split);
-          v = *reinterpret_cast<const float4*>(p);
-        }
+        const float* p = src_at(x, vol, b, gd, gh, gw, c);
+        if (p && c < Cin) v = *reinterpret_cast<const float4*>(p);
       }
       hreg[k] = v;
     }
@@ -334,13 +329,8 @@ __global__ __launch_bounds__(256, 1) void k_conv3d_wgrad(Src2 x, const float* __
         const int hw = pos % HWD, t2 = pos / HWD, hh = t2 % HH, hd = t2 / HH;
         const int gd = d0 + hd - KD / 2, gh = h0 + hh - 1, gw = w0 + hw - 1;
         const int c = ci0 + 4 * q;
-        if ((unsigned)(gd + vol.dh) < (unsigned)(D + 2 * vol.dh) && (unsigned)gh < (unsigned)H &&
-            (unsigned)gw < (unsigned)W && c < Cin) {
-          const int64_t vox = (((int64_t)b * D + gd) * H + gh) * W + gw;
-          const float* p =
-              c < x.split ? x.p0 + vox * x.ld0 + c : x.p1 + vox * x.ld1 + (c - x.split);
-          v = *reinterpret_cast<const float4*>(p);
-        }
+        const float* p = src_at(x, vol, b, gd, gh, gw, c);
+        if (p && c < Cin) v = *reinterpret_cast<const float4*>(p);
       }
       hreg[k] = v;
     }

@@ -308,7 +308,9 @@ __global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x(
 // 8 consecutive voxels of the dy image whose 16-byte chunks are XOR-swizzled by
 // voxel bit 2 (chunk ^= ((v >> 2) & 1) << 1) so those 8 rows of 64 B hit 64
 // distinct banks.
-template <int KD, int CI, int NS, int NJMAX>
+// HR: height-sharded input (the stencil's rows h = -1 / h = H from Src2::rlo / rhi, as in
+// k_conv3d_fwd_x); a separate instantiation
+template <int KD, int CI, int NS, int NJMAX, bool HR>
 __global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x16(
     Src2 x, const float* __restrict__ dy, int lddy, float* __restrict__ part, Vol vol, int Cin,
     int kpad, int Cout, int npad, int tilesH, int tilesW, int ntiles, int tps, int nblk) {
@@ -394,11 +396,17 @@ __global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x16(
         const int hw = pos % HWD, hh = pos / HWD;
         const int b = tx.b, gh = tx.h0 + hh - 1, gw = tx.w0 + hw - 1;
         const int c = ci_base + 4 * c4;
-        if ((unsigned)(gd + vol.dh) < (unsigned)(D + 2 * vol.dh) && (unsigned)gh < (unsigned)H &&
+        bool hin = (unsigned)gh < (unsigned)H;
+        if constexpr (HR) hin = hin || (gh == -1 && x.rlo) || (gh == H && x.rhi);
+        if ((unsigned)(gd + vol.dh) < (unsigned)(D + 2 * vol.dh) && hin &&
             (unsigned)gw < (unsigned)W && c < Cin && !((gd < 0 && x.zlo) || (gd >= D && x.zhi))) {
           const int64_t vox = (((int64_t)b * D + gd) * H + gh) * W + gw;
           const float* p =
               c < x.split ? x.p0 + vox * x.ld0 + c : x.p1 + vox * x.ld1 + (c - x.split);
+          if constexpr (HR) {
+            if ((unsigned)gh >= (unsigned)H)
+              p = (gh < 0 ? x.rlo : x.rhi) + (((int64_t)b * D + gd) * W + gw) * x.ldr + c;
+          }
           v = *reinterpret_cast<const float4*>(p);
           if (x.al) {
             v.x = v.x * xal.x + xde.x; v.x = v.x > 0.f ? v.x : 0.01f * v.x;
@@ -660,9 +668,16 @@ hipError_t conv3d_wgrad_x(const Src2& x, const float* dy, int lddy, float* dw, V
     // KD3/CI16 27 -> 7, KD3/CI8 14 -> 4, KD1/CI16 9 -> 3, KD1/CI8 5 -> 2
     const int nblk = cdiv(KD * 9 * p.ci, 16);
 #define SPFF_WX16(KD_, CI_, NS_, NJ_)                                                          \
-  hipLaunchKernelGGL((k_conv3d_wgrad_x16<KD_, CI_, NS_, NJ_>), grid, dim3(256), 0, s, x, dy,   \
-                     lddy, ws, vol, Cin, p.kpad, Cout, p.npad, p.tilesH, p.tilesW, p.ntiles,   \
-                     p.tps, nblk)
+  do {                                                                                         \
+    if (x.rows())                                                                              \
+      hipLaunchKernelGGL((k_conv3d_wgrad_x16<KD_, CI_, NS_, NJ_, true>), grid, dim3(256), 0, s, \
+                         x, dy, lddy, ws, vol, Cin, p.kpad, Cout, p.npad, p.tilesH, p.tilesW,  \
+                         p.ntiles, p.tps, nblk);                                               \
+    else                                                                                       \
+      hipLaunchKernelGGL((k_conv3d_wgrad_x16<KD_, CI_, NS_, NJ_, false>), grid, dim3(256), 0,  \
+                         s, x, dy, lddy, ws, vol, Cin, p.kpad, Cout, p.npad, p.tilesH,         \
+                         p.tilesW, p.ntiles, p.tps, nblk);                                     \
+  } while (0)
     if (KD == 3) {
       if (p.ci == 16) { if (x3) SPFF_WX16(3, 16, 2, 7); else SPFF_WX16(3, 16, 3, 7); }
       else            { if (x3) SPFF_WX16(3, 8, 2, 4);  else SPFF_WX16(3, 8, 3, 4); }
@@ -676,6 +691,7 @@ hipError_t conv3d_wgrad_x(const Src2& x, const float* dy, int lddy, float* dw, V
     return conv3d_wgrad_reduce(ws, dw, p.nsplit, KD * 9, p.kpad, p.npad, Cin, Cout, s);
   }
   // NJMAX = ceil(nblk / 4): KD3/CI16 14 blocks -> 4, KD3/CI8 7 -> 2, KD1/CI16 5 -> 2, KD1/CI8 3 -> 1
+  if (x.rows()) return hipErrorInvalidValue;  // (32x32x16 diagnostics kernel: no row halo)
   if (KD == 3) {
     if (p.ci == 16) { if (x3) SPFF_WX(3, 16, 2, 4); else SPFF_WX(3, 16, 3, 4); }
     else            { if (x3) SPFF_WX(3, 8, 2, 2);  else SPFF_WX(3, 8, 3, 2); }

@@ -218,11 +218,14 @@ __device__ __forceinline__ int x16_w(int r) {
   return (r >= 4 && r < 12) ? 2 * (r - 4) : (r < 4 ? 2 * r + 1 : 2 * r - 15);
 }
 
-template <int BN, int KD, int NS, int MB, int NW, bool X16, int TD>
+// HR: height-sharded input -- stencil rows h = -1 / h = H read the neighbours' boundary
+// rows (Src2::rlo / rhi; zero where null) instead of zero padding (hshard.hip).  A
+// separate instantiation, so the unsharded kernels' register budget is unchanged.
+template <int BN, int KD, int NS, int MB, int NW, bool X16, int TD, bool HR>
 __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
     Src2 x, const uint4* __restrict__ wp, Dst2 y, Vol vol, int Cin, int nkc, int Cout, int npad,
     int tilesD, int tilesH, int tilesW, float* __restrict__ part, int kps,
-    float* __restrict__ stats, int ntiles, int td0, int tds) {
+    float* __restrict__ stats, int ntiles, int td0, int tds, int th0, int ths) {
   constexpr int XT_THREADS = NW * 64;
   constexpr int TH = X16 ? 2 * NW * MB / TD : NW * MB, TW = XT_W;
   static_assert(X16 || TD == 2, "32x32x16 schedule: 2-deep tiles");
@@ -276,6 +279,7 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
   }
   const int b = t;
   tdi = td0 + tdi * tds;  // depth-tile subset (sharded halo overlap): td0 + k tds, k < tilesD
+  if constexpr (HR) thi = th0 + thi * ths;  // H-tile subset (height-sharded overlap)
   const int d0 = tdi * TD, h0 = thi * TH, w0 = twi * TW;
   const int n0 = nbk * BN;
   const int D = vol.D, H = vol.H, W = vol.W;
@@ -331,8 +335,14 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
       const int q = i & 1, pos = (i < NHX ? i : 0) >> 1;
       const int hw = pos % HWD, t2 = pos / HWD, hh = t2 % HH, hd = t2 / HH;
       const int gd = d0 + hd - KD / 2, gh = h0 + hh - 1, gw = w0 + hw - 1;
-      const bool ok = i < NHX && (unsigned)(gd + vol.dh) < (unsigned)(D + 2 * vol.dh) &&
-                      (unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W &&
+      bool hin = (unsigned)gh < (unsigned)H;
+      bool hrow = false;
+      if constexpr (HR) {
+        hrow = (gh < 0 && x.rlo) || (gh >= H && x.rhi);
+        hin = hin || hrow;
+      }
+      const bool ok = i < NHX && (unsigned)(gd + vol.dh) < (unsigned)(D + 2 * vol.dh) && hin &&
+                      (unsigned)gw < (unsigned)W &&
                       kc * 8 + 4 * q < Cin && !((gd < 0 && x.zlo) || (gd >= D && x.zhi));
       const int64_t vox = ok ? (((int64_t)b * D + gd) * H + gh) * W + gw : 0;
       // two-source select on the operands (v_cndmask), not on two address
@@ -341,7 +351,14 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
       const bool s0 = c < x.split;
       const float* src = s0 ? x.p0 : x.p1;
       const int64_t ld = s0 ? x.ld0 : x.ld1;
-      hreg[k] = *reinterpret_cast<const float4*>(src + vox * ld + (s0 ? c : c - x.split));
+      int64_t off = vox * ld + (s0 ? c : c - x.split);
+      if constexpr (HR) {
+        if (hrow) {  // the neighbour's boundary row: [b][d][w][ldr], channel c
+          src = gh < 0 ? x.rlo : x.rhi;
+          off = (((int64_t)b * D + gd) * W + gw) * x.ldr + c;
+        }
+      }
+      hreg[k] = *reinterpret_cast<const float4*>(src + off);
       hvalid |= ok ? (1u << k) : 0u;
     }
   };
@@ -698,17 +715,17 @@ __global__ void k_splitk_reduce(const float* __restrict__ part, int nsplit, int6
   }
 }
 
-template <int BN, int KD, int NS, int MB = xt_mb(BN), int NW = xt_nw(BN), int TD = xt_td(BN)>
-static hipError_t launch_fwd_x(const Src2& x, const uint4* wx, const Dst2& y, Vol vol, int K,
-                               int nkc, int N, int npad, hipStream_t s, float* part = nullptr,
-                               int nsplit = 1, int kps = 0, float* stats = nullptr,
-                               int dpart = 0) {
+template <int BN, int KD, int NS, bool HR, int MB = xt_mb(BN), int NW = xt_nw(BN),
+          int TD = xt_td(BN)>
+static hipError_t launch_fwd_xh(const Src2& x, const uint4* wx, const Dst2& y, Vol vol, int K,
+                                int nkc, int N, int npad, hipStream_t s, float* part, int nsplit,
+                                int kps, float* stats, int dpart) {
   constexpr int TH = SPFF_X16 ? 2 * NW * MB / TD : NW * MB;
   static_assert(NW == 8 || TD == XT_D, "xt_ntiles assumes 8 waves for other tile depths");
   constexpr size_t shm = xt_lds_bytes<BN, KD, NS, TD, TH>();
   static_assert(shm <= (NW == 8 ? 160 : 80) * 1024, "LDS budget");
   if (x.al && BN != 32) return hipErrorInvalidValue;  // fused activation: 32-wide tiles only
-  auto kern = k_conv3d_fwd_x<BN, KD, NS, MB, NW, SPFF_X16 != 0, TD>;
+  auto kern = k_conv3d_fwd_x<BN, KD, NS, MB, NW, SPFF_X16 != 0, TD, HR>;
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
@@ -716,23 +733,37 @@ static hipError_t launch_fwd_x(const Src2& x, const uint4* wx, const Dst2& y, Vo
     if (e != hipSuccess) return e;
     attr = true;
   }
-  const int tilesH = cdiv(vol.H, TH), tilesW = cdiv(vol.W, XT_W);
-  // dpart 1: the interior depth tiles 1 .. n-2 (no halo slice read), 2: the first and last
+  const int thn = cdiv(vol.H, TH), tilesW = cdiv(vol.W, XT_W);
+  // dpart 1: the interior depth tiles 1 .. n-2 (no halo slice read), 2: the first and last;
+  // 3 / 4: the same for the H tiles (height-sharded: no boundary row read / the others)
   const int tdn = cdiv(vol.D, TD);
-  if (dpart && (tdn < 3 || part || stats)) return hipErrorInvalidValue;
+  if ((dpart == 1 || dpart == 2) && (tdn < 3 || part || stats)) return hipErrorInvalidValue;
+  if ((dpart == 3 || dpart == 4) && (thn < 3 || part || stats || !HR)) return hipErrorInvalidValue;
   const int tilesD = dpart == 1 ? tdn - 2 : dpart == 2 ? 2 : tdn;
   const int td0 = dpart == 1 ? 1 : 0, tds = dpart == 2 ? tdn - 1 : 1;
+  const int tilesH = dpart == 3 ? thn - 2 : dpart == 4 ? 2 : thn;
+  const int th0 = dpart == 3 ? 1 : 0, ths = dpart == 4 ? thn - 1 : 1;
   const int ntiles = vol.B * tilesD * tilesH * tilesW;
   dim3 grid(8 * cdiv(ntiles, 8) * (npad / BN), 1, part ? nsplit : 1);
   hipLaunchKernelGGL(kern, grid, dim3(NW * 64), shm, s, x, wx, y, vol, K, nkc, N, npad, tilesD,
                      tilesH, tilesW, part, part ? kps : nkc, part ? nullptr : stats, ntiles, td0,
-                     tds);
+                     tds, th0, ths);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || !part) return e;
   const int64_t total = nvox(vol) * N;
   hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)std::min<int64_t>((total + 255) / 256, 8192)),
                      dim3(256), 0, s, part, nsplit, nvox(vol), npad, N, y);
   return hipGetLastError();
+}
+template <int BN, int KD, int NS>
+static hipError_t launch_fwd_x(const Src2& x, const uint4* wx, const Dst2& y, Vol vol, int K,
+                               int nkc, int N, int npad, hipStream_t s, float* part = nullptr,
+                               int nsplit = 1, int kps = 0, float* stats = nullptr,
+                               int dpart = 0) {
+  return x.rows() ? launch_fwd_xh<BN, KD, NS, true>(x, wx, y, vol, K, nkc, N, npad, s, part,
+                                                    nsplit, kps, stats, dpart)
+                  : launch_fwd_xh<BN, KD, NS, false>(x, wx, y, vol, K, nkc, N, npad, s, part,
+                                                     nsplit, kps, stats, dpart);
 }
 
 namespace {
@@ -866,6 +897,12 @@ bool conv3d_splits_depth(Vol vol, int KD, int Cin_w, int Cout_w, bool dgrad, int
   return KD == 3 && use_split(vol, math, dgrad) && splitk_plan(vol, d).nsplit == 1 &&
          cdiv(vol.D, xt_td(d.BN)) >= 3;
 }
+bool conv3d_splits_height(Vol vol, int KD, int Cin_w, int Cout_w, bool dgrad, int math) {
+  const XDims d = xdims(KD, Cin_w, Cout_w, dgrad);
+  const int nw = xt_nw(d.BN);
+  const int th = SPFF_X16 ? 2 * nw * xt_mb(d.BN) / xt_td(d.BN) : nw * xt_mb(d.BN);
+  return use_split(vol, math, dgrad) && splitk_plan(vol, d).nsplit == 1 && cdiv(vol.H, th) >= 3;
+}
 size_t conv3d_stats_bytes(Vol vol, int KD, int Cin, int Cout) {
   const XDims d = xdims(KD, Cin, Cout, false);
   return (size_t)xt_ntiles(vol, d.BN) * (2 * d.npad + 1) * sizeof(float);
@@ -890,7 +927,10 @@ hipError_t conv3d_run(const Src2& x, const void* wpack, const Dst2& y, Vol vol, 
   const XDims d = xdims(KD, Cin_w, Cout_w, dgrad);
   if (stats && (dgrad || !conv3d_fuses_stats(vol, KD, Cin_w, Cout_w, math)))
     return hipErrorInvalidValue;
-  if (dpart && !conv3d_splits_depth(vol, KD, Cin_w, Cout_w, dgrad, math))
+  if ((dpart == 1 || dpart == 2) && !conv3d_splits_depth(vol, KD, Cin_w, Cout_w, dgrad, math))
+    return hipErrorInvalidValue;
+  if ((dpart == 3 || dpart == 4) &&
+      (!x.rows() || !conv3d_splits_height(vol, KD, Cin_w, Cout_w, dgrad, math)))
     return hipErrorInvalidValue;
   if (use_split(vol, math, dgrad)) {
     const uint4* wu = static_cast<const uint4*>(wpack);

@@ -124,11 +124,11 @@ struct spff_plan {
   size_t G_out = 0, G_dy2 = 0, G_da1 = 0, G_dx = 0, dskip[3] = {0, 0, 0};
   size_t part_d = 0;  // sharded plans: fp64 IN partials [B][C][2]
   // height-sharded plans (spff_cfg.shard_axis = SPFF_SHARD_HEIGHT, hshard.hip): the
-  // row-padded conv input / output, the boundary-row staging slab, and the gate
+  // boundary-row staging slab (the convs read the neighbours' rows in place) and the gate
   // parameter gradients of ranks other than 0 (the gates are evaluated replicated)
   bool hsh = false;
   int hmul = 1;  // global / local rows
-  size_t hxp = 0, hyp = 0, hst = 0, gdum = 0;
+  size_t hst = 0, gdum = 0;
   size_t total = 0;
   Coll co;             // sharding group (world 1: unsharded)
   bool coll_set = false;
@@ -349,7 +349,7 @@ int build_plan(spff_plan* p) {
   const auto slice = [&](const Vol& v, int C) { return (size_t)v.H * v.W * C * sizeof(float); };
   p->x_cl = p->alloc_halo(nvox(v0) * p->ldx * sizeof(float), slice(v0, p->ldx));
   size_t red_ws = 0, red_out = 0, red_out4 = 0, gs = 0, bcd = 0, wg = 0, wt = 0, cst = 0;
-  size_t hx = 0, hst = 0, gd = 0;
+  size_t hst = 0, gd = 0;
   for (int i = 0; i < 7; ++i) {
     Blk& b = p->blk[i];
     const Vol& v = p->vol[b.lvl];
@@ -389,16 +389,8 @@ int build_plan(spff_plan* p) {
       red_out4 = std::max(red_out4, (size_t)B * b.C * D * 4 * sizeof(float));
     gs = std::max(gs, world > 1 && !hsh ? gates_sh_scratch_bytes(v, b.C, p->co.D_glob)
                                         : gates_scratch_bytes(v, b.C));
-    if (hsh) {  // row-padded conv operands (input, output / zero-row dy) and staging
-      Vol vp = v;
-      vp.H += 2;
-      const int lmax = rup(std::max(b.Cin, b.C), 8);
-      hx = std::max(hx, hpad_floats(v, lmax));
-      hst = std::max(hst, hstage_floats(v, lmax));
-      wg = std::max(wg, conv3d_wgrad_ws_bytes(vp, p->KD, b.Cin, b.C));
-      wg = std::max(wg, conv3d_wgrad_ws_bytes(vp, p->KD, b.C, b.C));
-      wg = std::max(wg, conv3d_splitk_bytes(vp, p->KD, b.Cin, b.C));
-      wg = std::max(wg, conv3d_splitk_bytes(vp, p->KD, b.C, b.C));
+    if (hsh) {  // the boundary-row staging slab of the widest conv input at this level
+      hst = std::max(hst, hstage_floats(v, hrows_ld(std::max(b.Cin, b.C))));
       gd = std::max(gd, (size_t)(b.pr1 - (b.b2 + b.C)) + (size_t)(b.se1 - b.se0));
     }
     bcd = std::max(bcd, bcdz);
@@ -471,8 +463,6 @@ int build_plan(spff_plan* p) {
   }
   if (world > 1) p->part_d = p->alloc((size_t)B * 8 * f * 2 * sizeof(double));
   if (hsh) {
-    p->hxp = p->alloc(hx * sizeof(float));
-    p->hyp = p->alloc(hx * sizeof(float));
     p->hst = p->alloc(hst * sizeof(float));
     p->gdum = p->alloc(std::max<size_t>(gd, 1) * sizeof(float));
   }
@@ -535,52 +525,65 @@ int halo_src(spff_plan* p, const Src2& x, const Vol& v, hipStream_t st = nullptr
   if (x.p1 != x.p0) CK(halo(p, x.p1, v, x.ld1, st));
   return SPFF_OK;
 }
-// ---- height-sharded plans (hshard.hip): every 3x3x3 conv runs on a row-padded copy ----
-Vol conv_vol(const spff_plan* p, Vol v) {
-  if (p->hsh) v.H += 2;
-  return v;
-}
-// x row-padded into xp (pitch rup(cin, 8)); exch: rows 0 / H + 1 = the neighbours'
-// boundary rows through spff_coll.halo (zero at the global ends), else zero rows
-int hpad_src(spff_plan* p, const Src2& x, const Vol& v, int cin, float* xp, bool exch) {
-  const int ldp = rup(cin, 8);
-  float* stg = exch ? p->F(p->hst) : nullptr;
-  HIPCK(hpad(x, cin, xp, stg, v, ldp, p->st));
-  if (!exch) return SPFF_OK;
-  const int64_t S = (int64_t)v.B * v.D * v.W * ldp;
-  if (p->co.do_halo(stg + S, S, 2, p->st) != 0)
-    return fail(SPFF_ECOLL, "halo exchange failed");
-  HIPCK(hfill(xp, stg, v, ldp, p->co.rank == 0, p->co.rank == p->co.world - 1, p->st));
+// ---- height-sharded plans (hshard.hip): the convs read the neighbours' rows in place ----
+// x's boundary rows 0 and H - 1 -> the neighbours, theirs -> the staging slab's recv
+// slices; *xr = x reading them as its stencil rows -1 / H (zero at the global ends).
+// On stream st (the side stream when the exchange overlaps a conv's interior tiles).
+int hrows_exchange(spff_plan* p, const Src2& x, const Vol& v, int cin, Src2* xr,
+                   hipStream_t st) {
+  const int ldr = hrows_ld(cin);
+  float* stg = p->F(p->hst);
+  const int64_t S = (int64_t)v.B * v.D * v.W * ldr;
+  HIPCK(hrows_pack(x, cin, stg + S, v, ldr, st));
+  if (p->co.do_halo(stg + S, S, 2, st) != 0) return fail(SPFF_ECOLL, "row halo exchange failed");
+  *xr = x;
+  xr->rlo = p->co.rank > 0 ? stg : nullptr;
+  xr->rhi = p->co.rank < p->co.world - 1 ? stg + 3 * S : nullptr;
+  xr->ldr = ldr;
   return SPFF_OK;
 }
+// a height-sharded 3x3x3 conv: the row exchange on the side stream st2 beside the H tiles
+// that read no boundary row, then the first and last H tiles (conv3d_splits_height); else
+// exchange, then convolve.  The ranks at both global ends still exchange (their single
+// neighbour), so every rank runs the same collective sequence.
 int conv_h(spff_plan* p, int cls, double flops, double bytes, const Src2& x, const Dst2& y,
            const Vol& v, int Cin_w, int Cout_w, bool dgrad) {
-  const int cin = dgrad ? Cout_w : Cin_w, cout = dgrad ? Cin_w : Cout_w;
-  float* xp = p->F(p->hxp);
-  float* yp = p->F(p->hyp);
-  CK(hpad_src(p, x, v, cin, xp, true));
-  PROFB(p, cls, flops, bytes,
-        conv3d_run(src1(xp, rup(cin, 8)), p->F(p->wt), dst1(yp, cout), conv_vol(p, v), p->KD,
-                   Cin_w, Cout_w, dgrad, p->cfg.math, p->st, p->F(p->wg_ws), nullptr));
-  HIPCK(hunpad(yp, y, cout, v, p->st));
-  return SPFF_OK;
-}
-// weight gradient of a 3x3x3 conv (height-sharded: over the padded volume, dy with
-// zero rows 0 / H + 1, so only the local output rows contribute)
-int conv_wgrad(spff_plan* p, double flops, double bytes, const Src2& x, const float* dy, float* dw,
-               const Vol& v, int Cin, int Cout) {
-  if (!p->hsh) {
-    PROFB(p, 2, flops, bytes,
-          conv3d_wgrad(x, dy, Cout, dw, v, p->KD, Cin, Cout, p->cfg.math, p->F(p->wg_ws), p->st));
+  const int cin = dgrad ? Cout_w : Cin_w, KD = p->KD, math = p->cfg.math;
+  Src2 xr;
+  const bool ovl = conv3d_splits_height(v, KD, Cin_w, Cout_w, dgrad, math);
+  if (!ovl) {
+    CK(hrows_exchange(p, x, v, cin, &xr, p->st));
+    PROFB(p, cls, flops, bytes,
+          conv3d_run(xr, p->F(p->wt), y, v, KD, Cin_w, Cout_w, dgrad, math, p->st,
+                     p->F(p->wg_ws), nullptr));
     return SPFF_OK;
   }
-  float* xp = p->F(p->hxp);
-  float* dp = p->F(p->hyp);
-  CK(hpad_src(p, x, v, Cin, xp, true));
-  CK(hpad_src(p, src1(dy, Cout), v, Cout, dp, false));
+  if (!p->st2) {
+    HIPCK(hipStreamCreateWithFlags(&p->st2, hipStreamNonBlocking));
+    HIPCK(hipEventCreateWithFlags(&p->ev_in, hipEventDisableTiming));
+    HIPCK(hipEventCreateWithFlags(&p->ev_halo, hipEventDisableTiming));
+  }
+  HIPCK(hipEventRecord(p->ev_in, p->st));  // x is final (and the previous conv is done
+  HIPCK(hipStreamWaitEvent(p->st2, p->ev_in, 0));  //   reading the staging slab)
+  CK(hrows_exchange(p, x, v, cin, &xr, p->st2));
+  HIPCK(hipEventRecord(p->ev_halo, p->st2));
+  PROFB(p, cls, flops, bytes,
+        conv3d_run(xr, p->F(p->wt), y, v, KD, Cin_w, Cout_w, dgrad, math, p->st,
+                   p->F(p->wg_ws), nullptr, 3));
+  HIPCK(hipStreamWaitEvent(p->st, p->ev_halo, 0));
+  PROFB(p, cls, 0.0, 0.0,
+        conv3d_run(xr, p->F(p->wt), y, v, KD, Cin_w, Cout_w, dgrad, math, p->st,
+                   p->F(p->wg_ws), nullptr, 4));
+  return SPFF_OK;
+}
+// weight gradient of a 3x3x3 conv (height-sharded: x's stencil rows from the neighbours;
+// dy is read at the local rows only)
+int conv_wgrad(spff_plan* p, double flops, double bytes, const Src2& x, const float* dy, float* dw,
+               const Vol& v, int Cin, int Cout) {
+  Src2 xr = x;
+  if (p->hsh) CK(hrows_exchange(p, x, v, Cin, &xr, p->st));
   PROFB(p, 2, flops, bytes,
-        conv3d_wgrad(src1(xp, rup(Cin, 8)), dp, rup(Cout, 8), dw, conv_vol(p, v), p->KD, Cin, Cout,
-                     p->cfg.math, p->F(p->wg_ws), p->st));
+        conv3d_wgrad(xr, dy, Cout, dw, v, p->KD, Cin, Cout, p->cfg.math, p->F(p->wg_ws), p->st));
   return SPFF_OK;
 }
 

@@ -24,6 +24,14 @@ struct Src2 {
   const float* al = nullptr;
   const float* de = nullptr;
   int zlo = 0, zhi = 0;  // depth-sharded: the d = -1 / d = D halo slice is zero padding
+  // height-sharded: the neighbours' boundary rows h = -1 / h = H, [B][D][W][ldr] with the
+  // conv's input channels in order (both sources), read by the conv kernels in place of
+  // the zero padding (nullptr at a global end: zero).  Raw values: the input activation
+  // (al / de) applies to them as to the local rows.
+  const float* rlo = nullptr;
+  const float* rhi = nullptr;
+  int ldr = 0;
+  __host__ __device__ bool rows() const { return rlo != nullptr || rhi != nullptr; }
 };
 struct Dst2 {
   float* p0; float* p1; int ld0, ld1, split;
@@ -39,6 +47,24 @@ struct Vol {
   int dh = 0;
 };
 inline int64_t nvox(const Vol& v) { return (int64_t)v.B * v.D * v.H * v.W; }
+
+// address of channels [c, c + 4) of the conv input at (b, gd, gh, gw), or nullptr where
+// the stencil reads zero padding: outside the volume, except the depth halo slices of a
+// depth-sharded input (vol.dh, Src2::zlo / zhi) and the boundary rows of a height-sharded
+// one (Src2::rlo / rhi).  No input activation (the split-bf16 kernels apply al / de).
+__device__ __forceinline__ const float* src_at(const Src2& x, const Vol& vol, int b, int gd,
+                                               int gh, int gw, int c) {
+  const int D = vol.D, H = vol.H, W = vol.W;
+  if ((unsigned)(gd + vol.dh) >= (unsigned)(D + 2 * vol.dh) || (unsigned)gw >= (unsigned)W ||
+      (gd < 0 && x.zlo) || (gd >= D && x.zhi))
+    return nullptr;
+  if ((unsigned)gh >= (unsigned)H) {
+    const float* r = gh < 0 ? (gh == -1 ? x.rlo : nullptr) : (gh == H ? x.rhi : nullptr);
+    return r ? r + (((int64_t)b * D + gd) * W + gw) * x.ldr + c : nullptr;
+  }
+  const int64_t vox = (((int64_t)b * D + gd) * H + gh) * W + gw;
+  return c < x.split ? x.p0 + vox * x.ld0 + c : x.p1 + vox * x.ld1 + (c - x.split);
+}
 
 // ---------------------------------------------------------------- conv3d --
 // Weight repack: reference layout W[Cout][Cin][KD][3][3] ->
@@ -67,11 +93,14 @@ hipError_t conv3d_pack(const float* w, void* wpack, Vol vol, int KD, int Cin_w, 
 // slab_reduce passes of the unfused path.
 // dpart (depth-sharded halo overlap, when conv3d_splits_depth): 1 = only the interior
 // depth tiles, whose 3x3x3 stencil reads no halo slice; 2 = only the first and last
-// depth tiles; 0 = all.  1 and 2 together write exactly what 0 writes.
+// depth tiles; 0 = all.  1 and 2 together write exactly what 0 writes.  3 / 4: the same
+// for the H tiles of a height-sharded conv (conv3d_splits_height: interior tiles read no
+// boundary row; 3 and 4 together write what 0 writes).
 hipError_t conv3d_run(const Src2& x, const void* wpack, const Dst2& y, Vol vol, int KD,
                       int Cin_w, int Cout_w, bool dgrad, int math, hipStream_t s,
                       float* ws = nullptr, float* stats = nullptr, int dpart = 0);
 bool conv3d_splits_depth(Vol vol, int KD, int Cin_w, int Cout_w, bool dgrad, int math);
+bool conv3d_splits_height(Vol vol, int KD, int Cin_w, int Cout_w, bool dgrad, int math);
 bool conv3d_fuses_stats(Vol vol, int KD, int Cin, int Cout, int math);
 size_t conv3d_stats_bytes(Vol vol, int KD, int Cin, int Cout);
 hipError_t conv3d_in_stats_fin(const float* stats, Vol vol, int KD, int Cin, int Cout,
@@ -295,17 +324,15 @@ hipError_t gates_bwd_sh(const GateParams& gp, const GateSaved& sv, const float* 
 size_t gates_sh_scratch_bytes(Vol vol, int C, int D_glob);
 
 // ------------------------------------------------------- height sharding --
-// (hshard.hip) row-padded conv inputs of a height-sharded plan: xp = [B][D][H + 2][W][ldp]
-// with rows 1 .. H from x (Src2: two sources, source-0 activation), rows 0 / H + 1 zero;
-// stage (optional) = [recv_lo | send_lo | send_hi | recv_hi] slab of B D W ldp floats each:
-// hpad writes the send rows, the caller exchanges them (spff_coll.halo at d_local = 2),
-// hfill copies the received rows into rows 0 / H + 1 (zlo / zhi: global end, zero).
-size_t hpad_floats(Vol v, int ldp);
-size_t hstage_floats(Vol v, int ldp);
-hipError_t hpad(const Src2& x, int cin, float* xp, float* stage, Vol v, int ldp, hipStream_t s);
-hipError_t hfill(float* xp, const float* stage, Vol v, int ldp, int zlo, int zhi, hipStream_t s);
-// y (local rows) <- rows 1 .. H of a conv output over the padded volume (pitch C)
-hipError_t hunpad(const float* yp, const Dst2& y, int C, Vol v, hipStream_t s);
+// (hshard.hip) the boundary rows of a height-sharded plan's conv input, in place: a
+// staging slab [recv_lo | send_lo | send_hi | recv_hi] of B D W ldr floats each
+// (ldr = hrows_ld(cin)); hrows_pack writes rows 0 and H - 1 of x (both sources, raw)
+// into the send slices, the caller exchanges them (spff_coll.halo at d_local = 2), and
+// the conv reads recv_lo / recv_hi through Src2::rlo / rhi -- no padded copy of the
+// volume and no copy of the conv output.
+int hrows_ld(int cin);
+size_t hstage_floats(Vol v, int ldr);
+hipError_t hrows_pack(const Src2& x, int cin, float* send, Vol v, int ldr, hipStream_t s);
 
 // ------------------------------------------------------------------ misc --
 hipError_t ncdhw_to_ndhwc(const float* x, float* y, Vol vol, int C, int ldy, hipStream_t s);
