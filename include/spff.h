@@ -136,7 +136,9 @@ int spff_forward(spff_plan* plan, const float* x, const float* params, float* lo
  * entry written).  Input gradient is not produced (the hot path never needs it). */
 int spff_backward(spff_plan* plan, const float* dlogits, const float* params, float* dparams,
                   void* workspace, void* stream);
-/* device pointer + shape of a saved intermediate (debug / tests), e.g. "enc1.out" */
+/* device pointer + shape of a saved intermediate (debug / tests), e.g. "enc1.out"
+ * (fp32 [nvox][channels]); "pool1.idx" .. "pool3.idx" are the max-pools' argmax BYTES
+ * [nvox][channels] (k = 2 dh + dw of each 2 x 2 window, first max in scan order) */
 int spff_saved_tensor(const spff_plan* plan, void* workspace, const char* name,
                       const float** ptr, int64_t* nvox, int* channels);
 

@@ -79,6 +79,11 @@
 #ifndef SPFF_XPRIO
 #define SPFF_XPRIO 1
 #endif
+#ifndef SPFF_XSTORE
+// 1: the output tile goes through LDS (conflict-free [row][BN + 4] image in MFMA row order)
+// and leaves as 16-byte row stores, instead of one 4-byte store per accumulator element
+#define SPFF_XSTORE 1
+#endif
 
 namespace spff {
 
@@ -164,7 +169,11 @@ __host__ __device__ constexpr int xt_t2() {
 }
 template <int BN, int KD, int NS, int TD, int TH>
 constexpr size_t xt_lds_bytes() {
-  return (size_t)NS * (xt_npos<KD, TD, TH>() + xt_t2<KD>() * BN) * 16;
+  // operand images; the epilogue reuses the space for the output tile [TD TH 16][BN + 4]
+  // fp32 plus the fused statistics' [8 waves][BN] partials
+  const size_t ops = (size_t)NS * (xt_npos<KD, TD, TH>() + xt_t2<KD>() * BN) * 16;
+  const size_t out = SPFF_XSTORE ? (size_t)TD * TH * 16 * (BN + 4) * 4 + 8 * BN * 4 : 0;
+  return ops > out ? ops : out;
 }
 // tile depth of a BN-wide launch (host side: launches, fused-statistics layout)
 constexpr int xt_td(int BN) { return (BN == 32 && SPFF_X16 && SPFF_X32T) ? 4 : XT_D; }
@@ -543,8 +552,40 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
   }
 
 // ---- epilogue: C[i][j], row i = voxel (vrow mapping), col j = out channel ----
+  constexpr int OP = BN + 4;  // output image pitch: 4 rows apart = 16 banks apart
+  constexpr int NROW = TD * TH * TW;
+  const bool vec = SPFF_XSTORE && !part && X16 && (Cout & 3) == 0 && (y.split & 3) == 0 &&
+                   (y.ld0 & 3) == 0 && (y.ld1 & 3) == 0;
+  if (vec) {
+    // every wave is past its last operand read; the image is in MFMA row order (row block
+    // q = wave RB + rb, row r), so a lane's 4 rows x 16 lanes hit 64 distinct banks
+    __syncthreads();
+    float* ot = reinterpret_cast<float*>(lds4);
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+      for (int r = 0; r < NREG; ++r)
+#pragma unroll
+        for (int cb = 0; cb < CB; ++cb)
+          ot[((wave * RB + rb) * 16 + orow(r)) * OP + cb * NCOL + lcol] = acc[rb][cb][r];
+    __syncthreads();
+    constexpr int Q4 = BN / 4;
+    for (int i = tid; i < NROW * Q4; i += XT_THREADS) {
+      const int row = i / Q4, q = i % Q4;
+      int td, th, tw;
+      vrow(row >> 4, row & 15, td, th, tw);
+      const int gd = d0 + td, gh = h0 + th, gw = w0 + tw;
+      const int n = n0 + 4 * q;
+      if (gd >= D || gh >= H || gw >= W || n >= Cout) continue;
+      const int64_t vox = (((int64_t)b * D + gd) * H + gh) * W + gw;
+      const float4 v = *reinterpret_cast<const float4*>(ot + row * OP + 4 * q);
+      float* pp = n < y.split ? y.p0 + vox * y.ld0 + n : y.p1 + vox * y.ld1 + (n - y.split);
+      *reinterpret_cast<float4*>(pp) = v;
+    }
+  }
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb) {
+    if (vec) break;
 #pragma unroll
     for (int r = 0; r < NREG; ++r) {
       int td, th, tw;
@@ -573,7 +614,8 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
   // by k_in_stats_fin (Chan).  stats[(tile*npad + n)*2 + {0,1}], count[tile].
   if (stats) {
     __syncthreads();  // every wave is past its last LDS operand read
-    float* sred = reinterpret_cast<float*>(lds4);  // [NW][CB][NCOL]
+    // [NW][CB][NCOL], after the output image when the epilogue staged it
+    float* sred = reinterpret_cast<float*>(lds4) + (vec ? NROW * OP : 0);
     const int nd = min(D - d0, TD), nh = min(H - h0, TH), nwv = min(W - w0, TW);
     const float cnt = (float)(nd * nh * nwv);
     bool ok[RB][NREG];

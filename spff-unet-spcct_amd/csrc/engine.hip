@@ -1164,8 +1164,12 @@ int spff_saved_tensor(const spff_plan* p, void* ws, const char* name, const floa
     if (n == b.name + ".al2") return ret(b.al2, bv, b.C);
     if (n == b.name + ".de2") return ret(b.de2, bv, b.C);
   }
-  for (int l = 0; l < 3; ++l)
+  for (int l = 0; l < 3; ++l) {
     if (n == "pool" + std::to_string(l + 1)) return ret(p->pool[l], p->vol[l + 1], p->f << l);
+    // the max-pool's argmax bytes [V_low][C] (k = 2 dh + dw of the 2 x 2 window): uint8
+    if (n == "pool" + std::to_string(l + 1) + ".idx")
+      return ret(p->pidx[l], p->vol[l + 1], p->f << l);
+  }
   const char* upn[3] = {"up3", "up2", "up1"};
   for (int u = 0; u < 3; ++u)
     if (n == upn[u]) return ret(p->up[u].out, p->vol[p->up[u].lvl_low - 1], p->up[u].Cout);

@@ -435,7 +435,8 @@ class Plan:
                 for i, c in enumerate(self.PROF_CLASSES)}
 
     def saved(self, name: str) -> torch.Tensor:
-        """Copy of a saved intermediate as a channel-last [V, C] tensor (debug/tests)."""
+        """Copy of a saved intermediate as a channel-last [V, C] tensor (debug/tests):
+        fp32, or uint8 for the max-pool argmax bytes "poolN.idx"."""
         ws = self._ws
         if ws is None:
             raise SpffError("no forward has run")
@@ -446,6 +447,8 @@ class Plan:
                                       ctypes.byref(nv), ctypes.byref(ch)), "spff_saved_tensor")
         off = ptr.value - ws.data_ptr()
         n = nv.value * ch.value
+        if name.endswith(".idx"):
+            return ws[off:off + n].view(nv.value, ch.value).clone()
         return ws[off:off + 4 * n].view(torch.float32).view(nv.value, ch.value).clone()
 
 

@@ -173,16 +173,15 @@ def engine_branch_masks(core, xshape, st, cfg):
             if nd:
                 print(f"  {blk}.{tag}: {nd} knife-edge signs (engine affine vs fp64 IN)")
             masks[f"{blk}.{tag}"] = m
-    # max-pool windows: the engine's own first-max argmax over its pool inputs
+    # max-pool windows: the engine's own argmax bytes (k = 2 dh + dw, first max in scan
+    # order), as its backward routed them -- also valid for lean plans, whose block
+    # outputs live in backward scratch
     Dd = xshape[2]
-    for k, blk in enumerate(("enc1", "enc2", "enc3")):
-        Hh_, Ww = xshape[3] >> k, xshape[4] >> k
-        y = plan.saved(f"{blk}.out").double().cpu()
-        C = y.shape[1]
-        y = y.view(B, Dd, Hh_, Ww, C).permute(0, 4, 1, 2, 3)
-        v = y[..., :Hh_ // 2 * 2, :Ww // 2 * 2].reshape(B, C, Dd, Hh_ // 2, 2, Ww // 2, 2)
-        v = v.permute(0, 1, 2, 3, 5, 4, 6)
-        masks[f"pool{k + 1}"] = v.reshape(B, C, Dd, Hh_ // 2, Ww // 2, 4).argmax(-1).contiguous()
+    for k in range(3):
+        Hh_, Ww = xshape[3] >> (k + 1), xshape[4] >> (k + 1)
+        idx = plan.saved(f"pool{k + 1}.idx").to(torch.int64).cpu()
+        C = idx.shape[1]
+        masks[f"pool{k + 1}"] = idx.view(B, Dd, Hh_, Ww, C).permute(0, 4, 1, 2, 3).contiguous()
     return masks
 
 
