@@ -179,7 +179,10 @@ constexpr size_t xt_lds_bytes() {
 constexpr int xt_td(int BN) { return (BN == 32 && SPFF_X16 && SPFF_X32T) ? 4 : XT_D; }
 constexpr int xt_mb(int BN) { return (BN == 32 && SPFF_X16 && SPFF_X32T) ? 4 : 2; }
 // waves of a BN-wide workgroup (4-wave 32-wide tiles: SPFF_X32NW, 2-deep tiles only)
-constexpr int xt_nw(int BN) { return (BN == 32 && SPFF_X16 && !SPFF_X32T) ? SPFF_X32NW : 8; }
+// (16-wide tiles, Cout <= 16 -- the SwinUNETR's C = 12 convs: also 4 waves, 2 WGs / CU)
+constexpr int xt_nw(int BN) {
+  return (BN <= 32 && SPFF_X16 && !(BN == 32 && SPFF_X32T)) ? SPFF_X32NW : 8;
+}
 }  // namespace
 
 // 16x16x32 tap-quad schedule (X16): k = 4 lane groups x 8 channels, lane group g
@@ -816,7 +819,9 @@ XDims xdims(int KD, int Cin_w, int Cout_w, bool dgrad) {
   XDims d;
   d.K = dgrad ? Cout_w : Cin_w;
   d.N = dgrad ? Cin_w : Cout_w;
-  d.BN = d.N >= 64 ? 64 : 32;
+  // 16-wide tiles for narrow outputs (N <= 16, 3x3x3): the SwinUNETR's C = 12 convs
+  // ran their 12 columns in 32-wide tiles (62 % of the MFMA columns padding)
+  d.BN = d.N >= 64 ? 64 : (d.N <= 16 && KD == 3 && SPFF_X16) ? 16 : 32;
   d.nkc = cdiv(d.K, 8);
   d.npad = rup(d.N, d.BN);
   d.T = KD * 9;
@@ -917,6 +922,9 @@ static hipError_t run_x(const Src2& x, const uint4* wu, const Dst2& y, Vol vol, 
                                                 k.nsplit, k.kps, stats, dpart)
                : launch_fwd_x<64, 1, NS>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s, part,
                                                 k.nsplit, k.kps, stats, dpart);
+  if (d.BN == 16)
+    return launch_fwd_x<16, 3, NS>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s, part, k.nsplit,
+                                   k.kps, stats, dpart);
   return KD == 3 ? launch_fwd_x<32, 3, NS>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s,
                                                   part, k.nsplit, k.kps, stats, dpart)
                  : launch_fwd_x<32, 1, NS>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s,

@@ -683,7 +683,9 @@ Src2 act_src(const spff_plan* p, const Blk& b) {
   return s;
 }
 
-int fwd_block(spff_plan* p, Blk& b, const Src2& in) {
+// pool >= 0: encoder block b's output also feeds MaxPool3d((1,2,2)) into p->pool[pool]
+// (the output apply and the pool run as one pass where H and W are even)
+int fwd_block(spff_plan* p, Blk& b, const Src2& in, int pool = -1) {
   const Vol& v = p->vol[b.lvl];
   const int C = b.C, KD = p->KD;
   const int math = p->cfg.math;
@@ -731,14 +733,22 @@ int fwd_block(spff_plan* p, Blk& b, const Src2& in) {
       HIPCK(gates_fwd_sh(gp, p->F(b.Sa), sv, v, C, p->F(p->gscr), p->co, p->st));
     else
       HIPCK(gates_fwd(gp, p->F(b.Sa), sv, v, C, p->F(p->gscr), p->st));
-    PROFB(p, 5, 0.0, 8.0 * (double)nvox(v) * C,
-        act_apply(p->F(b.y2), p->F(b.out), p->F(b.al2), p->F(b.de2), p->F(b.P), p->F(b.Q), v,
-                    C, p->st));
-  } else {
-    PROFB(p, 5, 0.0, 8.0 * (double)nvox(v) * C,
-        act_apply(p->F(b.y2), p->F(b.out), p->F(b.al2), p->F(b.de2), nullptr, nullptr, v, C,
-                    p->st));
   }
+  const float* P = b.tail() ? p->F(b.P) : nullptr;
+  const float* Q = b.tail() ? p->F(b.Q) : nullptr;
+  if (pool >= 0 && !((v.H | v.W) & 1)) {
+    // read y2, write out + pooled + argmax bytes: 4C + 4C + C + C / 4 bytes per voxel
+    PROFB(p, 5, 0.0, 9.25 * (double)nvox(v) * C,
+          act_apply_pool(p->F(b.y2), p->F(b.out), p->F(b.al2), p->F(b.de2), P, Q,
+                         p->F(p->pool[pool]),
+                         reinterpret_cast<uint8_t*>(p->ws + p->pidx[pool]), v, C, p->st));
+    return SPFF_OK;
+  }
+  PROFB(p, 5, 0.0, 8.0 * (double)nvox(v) * C,
+        act_apply(p->F(b.y2), p->F(b.out), p->F(b.al2), p->F(b.de2), P, Q, v, C, p->st));
+  if (pool >= 0)
+    HIPCK(maxpool_fwd(p->F(b.out), p->F(p->pool[pool]),
+                      reinterpret_cast<uint8_t*>(p->ws + p->pidx[pool]), v, C, p->st));
   return SPFF_OK;
 }
 
@@ -927,15 +937,9 @@ int forward(spff_plan* p, const float* x, float* logits) {
   const spff_cfg& c = p->cfg;
   HIPCK(ncdhw_to_ndhwc(x, p->F(p->x_cl), p->vol[0], c.in_ch, p->ldx, p->st));
   Blk* B = p->blk;
-  CK(fwd_block(p, B[0], src1(p->F(p->x_cl), p->ldx)));
-  HIPCK(maxpool_fwd(p->F(B[0].out), p->F(p->pool[0]), reinterpret_cast<uint8_t*>(p->ws + p->pidx[0]),
-                    p->vol[0], f, p->st));
-  CK(fwd_block(p, B[1], src1(p->F(p->pool[0]), f)));
-  HIPCK(maxpool_fwd(p->F(B[1].out), p->F(p->pool[1]), reinterpret_cast<uint8_t*>(p->ws + p->pidx[1]),
-                    p->vol[1], 2 * f, p->st));
-  CK(fwd_block(p, B[2], src1(p->F(p->pool[1]), 2 * f)));
-  HIPCK(maxpool_fwd(p->F(B[2].out), p->F(p->pool[2]), reinterpret_cast<uint8_t*>(p->ws + p->pidx[2]),
-                    p->vol[2], 4 * f, p->st));
+  CK(fwd_block(p, B[0], src1(p->F(p->x_cl), p->ldx), 0));
+  CK(fwd_block(p, B[1], src1(p->F(p->pool[0]), f), 1));
+  CK(fwd_block(p, B[2], src1(p->F(p->pool[1]), 2 * f), 2));
   CK(fwd_block(p, B[3], src1(p->F(p->pool[2]), 4 * f)));
   const float* prev = p->F(B[3].out);
   for (int u = 0; u < 3; ++u) {

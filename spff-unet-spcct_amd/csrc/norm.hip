@@ -596,6 +596,69 @@ hipError_t act_apply(const float* y, float* out, const float* al, const float* d
   return hipGetLastError();
 }
 
+// An encoder block's output apply fused with the MaxPool3d((1,2,2)) that consumes it
+// (models.py:661-665): per 2 x 2 window and channel quad, the four out = lrelu(y2 al + de)
+// P + Q are written (the decoder's skip source) and their max and first-max index
+// (k = 2 dh + dw, scan order, NaN wins: k_maxpool_fwd's rule) -- the pool never re-reads
+// the block output.  H and W even (the caller falls back to act_apply + maxpool_fwd).
+// grid.y = b D + d, grid.x strides over the slab's pooled (ho, wo, c/4).
+__global__ __launch_bounds__(256) void k_act_apply_pool(
+    const float* __restrict__ y, float* __restrict__ out, const float* __restrict__ al,
+    const float* __restrict__ de, const float* __restrict__ P, const float* __restrict__ Q,
+    float* __restrict__ pooled, uint8_t* __restrict__ idx, Vol vol, int C, float neg) {
+  const int bd = blockIdx.y, b = bd / vol.D, d = bd % vol.D;
+  const int Ho = vol.H / 2, Wo = vol.W / 2, C4 = C >> 2;
+  const int n4 = Ho * Wo * C4;
+  const int i0 = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = (i0 % C4) * 4;
+  float pa[4], pd[4], pp[4], pq[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int bc = b * C + c + j;
+    pa[j] = al[bc];
+    pd[j] = de[bc];
+    pp[j] = P ? P[(int64_t)bc * vol.D + d] : 1.f;
+    pq[j] = P ? Q[(int64_t)bc * vol.D + d] : 0.f;
+  }
+  for (int i = i0; i < n4; i += gridDim.x * blockDim.x) {
+    const int q = i / C4, wo = q % Wo, ho = q / Wo;
+    const int64_t vin = ((int64_t)bd * vol.H + 2 * ho) * vol.W + 2 * wo;
+    float best[4];
+    uint8_t bi[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int64_t vv = vin + (k >> 1) * vol.W + (k & 1);
+      const float4 v = *reinterpret_cast<const float4*>(y + vv * C + c);
+      float r[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        r[j] = lrelu(r[j] * pa[j] + pd[j], neg) * pp[j] + pq[j];
+        if (k == 0) {
+          best[j] = r[j];
+        } else if (r[j] > best[j] || isnan(r[j])) {
+          best[j] = r[j];
+          bi[j] = (uint8_t)k;
+        }
+      }
+      *reinterpret_cast<float4*>(out + vv * C + c) = make_float4(r[0], r[1], r[2], r[3]);
+    }
+    const int64_t vo = ((int64_t)bd * Ho + ho) * Wo + wo;
+    *reinterpret_cast<float4*>(pooled + vo * C + c) = make_float4(best[0], best[1], best[2], best[3]);
+    *reinterpret_cast<uchar4*>(idx + vo * C + c) = make_uchar4(bi[0], bi[1], bi[2], bi[3]);
+  }
+}
+
+hipError_t act_apply_pool(const float* y, float* out, const float* al, const float* de,
+                          const float* P, const float* Q, float* pooled, uint8_t* idx, Vol vol,
+                          int C, hipStream_t s, float neg) {
+  if ((vol.H | vol.W) & 1 || C % 4) return hipErrorInvalidValue;
+  const int n4 = (vol.H / 2) * (vol.W / 2) * (C / 4);
+  const dim3 grid(std::min(cdiv(n4, ew_bs(C)), SPFF_EW_GX), vol.B * vol.D);
+  hipLaunchKernelGGL(k_act_apply_pool, grid, dim3(ew_bs(C)), 0, s, y, out, al, de, P, Q, pooled,
+                     idx, vol, C, neg);
+  return hipGetLastError();
+}
+
 __global__ __launch_bounds__(256) void k_in_bwd_apply(
     const float* __restrict__ y, const float* g, float* dy, const float* __restrict__ mean,
     const float* __restrict__ rstd, const float* __restrict__ al, const float* __restrict__ de,

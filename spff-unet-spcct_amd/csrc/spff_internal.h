@@ -219,6 +219,11 @@ hipError_t in_rstd(const float* sqsums, const float* gamma, const float* beta,
 hipError_t act_apply(const float* y, float* out, const float* al, const float* de,
                      const float* P, const float* Q, Vol vol, int C, hipStream_t s,
                      float neg = 0.01f);
+// act_apply of an encoder block output fused with the (1,2,2) max-pool that reads it:
+// out as act_apply, pooled [B][D][H/2][W/2][C] and its argmax bytes as maxpool_fwd (H, W even)
+hipError_t act_apply_pool(const float* y, float* out, const float* al, const float* de,
+                          const float* P, const float* Q, float* pooled, uint8_t* idx, Vol vol,
+                          int C, hipStream_t s, float neg = 0.01f);
 // IN backward finalize: from per-(b,c,d) [sum dr, sum dr*xhat] -> dgamma, dbeta (over b),
 // k1[b,c] = mean dr, k2[b,c] = mean dr*xhat
 // depth-sharded variants: fp64 partials over the local slab, summed across the
