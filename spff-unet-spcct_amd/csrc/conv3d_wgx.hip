@@ -32,6 +32,9 @@
 #ifndef SPFF_WX16
 #define SPFF_WX16 1  // 1: v_mfma_f32_16x16x32_bf16 wgrad (k_conv3d_wgrad_x16), 0: 32x32x16
 #endif
+#ifndef SPFF_WXUNROLL
+#define SPFF_WXUNROLL 4  // k-step (W-row pair) loop unroll of k_conv3d_wgrad_x16
+#endif
 
 namespace spff {
 
@@ -296,6 +299,8 @@ __global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x(
 }
 
 // ------------------------------------------------- 16x16x32 wgrad (X16) --
+// CO (16 or 32): the Cout block of a workgroup; 16 for Cout <= 16 (the SwinUNETR's C = 12
+// convs ran 12 of 32 columns)
 // Same tiles, staging and partial slabs as k_conv3d_wgrad_x; the MFMA is
 // v_mfma_f32_16x16x32_bf16: rows = 16 (tap, channel) -- one tap x 16 channels
 // (CI 16) or two taps x 8 (CI 8), so 27 x 16 = 432 rows are 27 blocks with no
@@ -310,7 +315,7 @@ __global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x(
 // distinct banks.
 // HR: height-sharded input (the stencil's rows h = -1 / h = H from Src2::rlo / rhi, as in
 // k_conv3d_fwd_x); a separate instantiation
-template <int KD, int CI, int NS, int NJMAX, bool HR>
+template <int KD, int CI, int NS, int NJMAX, bool HR, int CO>
 __global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x16(
     Src2 x, const float* __restrict__ dy, int lddy, float* __restrict__ part, Vol vol, int Cin,
     int kpad, int Cout, int npad, int tilesH, int tilesW, int ntiles, int tps, int nblk) {
@@ -320,20 +325,20 @@ __global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x16(
   constexpr int CQ = CI / 4;                              // float4 per halo position
   constexpr int PPOS = HH * HWD;                           // positions per depth plane
   constexpr int NP = (PPOS * CQ + 255) / 256;              // plane float4 per thread
-  constexpr int NY = WX_TV * (WX_CO / 4) / 256;            // dy float4 per thread (= 4)
-  constexpr int NCB = WX_CO / 16;                          // 16-wide col blocks (2)
+  constexpr int NY = WX_TV * (CO / 4) / 256;            // dy float4 per thread (= 4)
+  constexpr int NCB = CO / 16;                          // 16-wide col blocks (2)
   __shared__ __attribute__((aligned(16))) unsigned short Xs[NS * NPOS * CI];
-  __shared__ __attribute__((aligned(16))) unsigned short Ys[NS * WX_TV * WX_CO];
+  __shared__ __attribute__((aligned(16))) unsigned short Ys[NS * WX_TV * CO];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, q = (lane & 15) >> 2, pq = lane & 3;
-  const int nci = kpad / CI, ncb = nci * (npad / WX_CO);
+  const int nci = kpad / CI, ncb = nci * (npad / CO);
   const int rk = blockIdx.x >> 3;
   const int nsp8 = gridDim.x / ncb;
   const int cbk = SPFF_XCDMAP ? rk % ncb : (int)(blockIdx.x / nsp8);
   const int split = SPFF_XCDMAP ? (rk / ncb) * 8 + (blockIdx.x & 7) : (int)(blockIdx.x % nsp8);
   if (split * tps >= ntiles) return;  // padding block (uniform)
-  const int ci_base = (cbk % nci) * CI, co0 = (cbk / nci) * WX_CO;
+  const int ci_base = (cbk % nci) * CI, co0 = (cbk / nci) * CO;
   const int D = vol.D, H = vol.H, W = vol.W;
 
   // row blocks of this wave: wave, wave + 4, ...; nj of them (uniform per wave)
@@ -352,12 +357,12 @@ __global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x16(
     aoff[j] = ((kd * HH + kh + (g >> 1)) * HWD + kw + 4 * (g & 1) + q) * CI + ch0;
   }
   // B: voxel (W-row g >> 1, w 4(g & 1) + q), co 16 cb + 4 pq, chunk-swizzled
-  const int bsw = (g & 1) << 1;
+  const int bsw = CO == 32 ? (g & 1) << 1 : 0;  // (16-wide rows: 32 B, no swizzle)
   const int bv = (g >> 1) * WX_TW + 4 * (g & 1) + q;
   int boff[NCB];
 #pragma unroll
   for (int cb = 0; cb < NCB; ++cb)
-    boff[cb] = bv * WX_CO + (((2 * cb + (pq >> 1)) ^ bsw) << 3) + 4 * (pq & 1);
+    boff[cb] = bv * CO + (((2 * cb + (pq >> 1)) ^ bsw) << 3) + 4 * (pq & 1);
 
   f32x4 acc[NJMAX][NCB];
 #pragma unroll
@@ -447,7 +452,7 @@ __global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x16(
 #pragma unroll
     for (int k = 0; k < NY; ++k) {
       const int i = tid + 256 * k;
-      const int c4 = i % (WX_CO / 4), kv = i / (WX_CO / 4);
+      const int c4 = i % (CO / 4), kv = i / (CO / 4);
       const int gh = h0 + kv / WX_TW, gw = w0 + kv % WX_TW;
       const int c = co0 + 4 * c4;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -463,15 +468,15 @@ __global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x16(
 #pragma unroll
     for (int k = 0; k < NY; ++k) {
       const int i = tid + 256 * k;
-      const int c4 = i % (WX_CO / 4), kv = i / (WX_CO / 4);
+      const int c4 = i % (CO / 4), kv = i / (CO / 4);
       uint2 o[NS];
       const float4 yv = negate ? make_float4(-yreg[k].x, -yreg[k].y, -yreg[k].z, -yreg[k].w)
                                : yreg[k];
       split4<NS>(yv, o);
-      const int off = kv * WX_CO + (((c4 >> 1) ^ (((kv >> 2) & 1) << 1)) << 3) + 4 * (c4 & 1);
+      const int off = kv * CO + (((c4 >> 1) ^ (CO == 32 ? ((kv >> 2) & 1) << 1 : 0)) << 3) + 4 * (c4 & 1);
 #pragma unroll
       for (int p = 0; p < NS; ++p)
-        *reinterpret_cast<uint2*>(Ys + p * WX_TV * WX_CO + off) = o[p];
+        *reinterpret_cast<uint2*>(Ys + p * WX_TV * CO + off) = o[p];
     }
   };
 
@@ -485,15 +490,15 @@ __global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x16(
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
       ab[j] = aoff[j] + (aoff[j] >= (KD - rot) * PL ? (rot - KD) * PL : rot * PL);
-#pragma unroll 2
+#pragma unroll SPFF_WXUNROLL
     for (int ks = 0; ks < WX_TH / 2; ++ks) {
       bf16x8 bq[NCB][NS];
 #pragma unroll
       for (int cb = 0; cb < NCB; ++cb)
 #pragma unroll
         for (int p = 0; p < NS; ++p) {
-          const unsigned short* yb = Ys + p * WX_TV * WX_CO + 2 * ks * WX_TW * WX_CO + boff[cb];
-          bq[cb][p] = frag(tr_read(yb), tr_read(yb + 8 * WX_CO));
+          const unsigned short* yb = Ys + p * WX_TV * CO + 2 * ks * WX_TW * CO + boff[cb];
+          bq[cb][p] = frag(tr_read(yb), tr_read(yb + 8 * CO));
         }
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
@@ -627,17 +632,18 @@ WxTable make_table(int KD, int CI) {
 }
 
 struct WxPlan {
-  int ci, kpad, npad, tilesH, tilesW, ntiles, nsplit, tps;
+  int ci, co, kpad, npad, tilesH, tilesW, ntiles, nsplit, tps;
 };
 WxPlan wx_plan(Vol vol, int Cin, int Cout) {
   WxPlan p;
   p.ci = Cin <= 8 ? 8 : 16;
+  p.co = (Cout <= 16 && SPFF_WX16) ? 16 : WX_CO;
   p.kpad = rup(Cin, p.ci);
-  p.npad = rup(Cout, WX_CO);
+  p.npad = rup(Cout, p.co);
   p.tilesH = cdiv(vol.H, WX_TH);
   p.tilesW = cdiv(vol.W, WX_TW);
   p.ntiles = vol.B * vol.D * p.tilesH * p.tilesW;
-  const int nout = (p.kpad / p.ci) * (p.npad / WX_CO);
+  const int nout = (p.kpad / p.ci) * (p.npad / p.co);
   // two workgroups per CU: aim at 2 rounds of 512, >= 4 tiles per workgroup
   int nsplit = std::max(1, cdiv(1024, nout));
   nsplit = std::min(nsplit, std::max(1, p.ntiles / 4));
@@ -657,7 +663,7 @@ hipError_t conv3d_wgrad_x(const Src2& x, const float* dy, int lddy, float* dw, V
   if (lddy % 4) return hipErrorInvalidValue;
   WxPlan p = wx_plan(vol, Cin, Cout);
   const WxTable tb = make_table(KD, p.ci);
-  dim3 grid(8 * cdiv(p.nsplit, 8) * (p.kpad / p.ci) * (p.npad / WX_CO));
+  dim3 grid(8 * cdiv(p.nsplit, 8) * (p.kpad / p.ci) * (p.npad / p.co));
 #define SPFF_WX(KD_, CI_, NS_, NJ_)                                                            \
   hipLaunchKernelGGL((k_conv3d_wgrad_x<KD_, CI_, NS_, NJ_>), grid, dim3(256), 0, s, x, dy,     \
                      lddy, ws, vol, Cin, p.kpad, Cout, p.npad, p.tilesH, p.tilesW, p.ntiles,   \
@@ -667,16 +673,19 @@ hipError_t conv3d_wgrad_x(const Src2& x, const float* dy, int lddy, float* dw, V
     // 16-row blocks: nblk = ceil(T CI / 16); NJMAX = ceil(nblk / 4):
     // KD3/CI16 27 -> 7, KD3/CI8 14 -> 4, KD1/CI16 9 -> 3, KD1/CI8 5 -> 2
     const int nblk = cdiv(KD * 9 * p.ci, 16);
+#define SPFF_WX16C(KD_, CI_, NS_, NJ_, HR_, CO_)                                                \
+  hipLaunchKernelGGL((k_conv3d_wgrad_x16<KD_, CI_, NS_, NJ_, HR_, CO_>), grid, dim3(256), 0, s, \
+                     x, dy, lddy, ws, vol, Cin, p.kpad, Cout, p.npad, p.tilesH, p.tilesW,      \
+                     p.ntiles, p.tps, nblk)
 #define SPFF_WX16(KD_, CI_, NS_, NJ_)                                                          \
   do {                                                                                         \
-    if (x.rows())                                                                              \
-      hipLaunchKernelGGL((k_conv3d_wgrad_x16<KD_, CI_, NS_, NJ_, true>), grid, dim3(256), 0, s, \
-                         x, dy, lddy, ws, vol, Cin, p.kpad, Cout, p.npad, p.tilesH, p.tilesW,  \
-                         p.ntiles, p.tps, nblk);                                               \
-    else                                                                                       \
-      hipLaunchKernelGGL((k_conv3d_wgrad_x16<KD_, CI_, NS_, NJ_, false>), grid, dim3(256), 0,  \
-                         s, x, dy, lddy, ws, vol, Cin, p.kpad, Cout, p.npad, p.tilesH,         \
-                         p.tilesW, p.ntiles, p.tps, nblk);                                     \
+    if (p.co == 16) {                                                                          \
+      if (x.rows()) SPFF_WX16C(KD_, CI_, NS_, NJ_, true, 16);                                  \
+      else SPFF_WX16C(KD_, CI_, NS_, NJ_, false, 16);                                          \
+    } else {                                                                                   \
+      if (x.rows()) SPFF_WX16C(KD_, CI_, NS_, NJ_, true, 32);                                  \
+      else SPFF_WX16C(KD_, CI_, NS_, NJ_, false, 32);                                          \
+    }                                                                                          \
   } while (0)
     if (KD == 3) {
       if (p.ci == 16) { if (x3) SPFF_WX16(3, 16, 2, 7); else SPFF_WX16(3, 16, 3, 7); }
@@ -686,6 +695,7 @@ hipError_t conv3d_wgrad_x(const Src2& x, const float* dy, int lddy, float* dw, V
       else            { if (x3) SPFF_WX16(1, 8, 2, 2);  else SPFF_WX16(1, 8, 3, 2); }
     }
 #undef SPFF_WX16
+#undef SPFF_WX16C
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     return conv3d_wgrad_reduce(ws, dw, p.nsplit, KD * 9, p.kpad, p.npad, Cin, Cout, s);

@@ -495,13 +495,15 @@ __global__ __launch_bounds__(AM_THREADS, 2) void k_attn_fwd_m(const float* __res
   }
 }
 
-// backward A: dq and the bias-table gradient, per 16-query block
+// backward A: dq per 16-query block; dS [NP][NP] of the (window, head) to dsw for the
+// bias-table gradient (k_attn_dtable_m: per-table-entry sums in a fixed order -- LDS
+// float atomics into per-wave tables measured 2.3x this kernel's time)
 template <int HD>
-__global__ __launch_bounds__(AM_THREADS, 1) void k_attn_bwd_q_m(
+__global__ __launch_bounds__(AM_THREADS, 2) void k_attn_bwd_q_m(
     const float* __restrict__ qkv, const float* __restrict__ bqkv,
     const float* __restrict__ table, const float* __restrict__ O, const float* __restrict__ dO,
     const float* __restrict__ lse, AttnGeo g, float* __restrict__ dqkv,
-    float* __restrict__ tpart) {
+    float* __restrict__ dsw) {
   extern __shared__ uint4 sm4[];
   const int n = g.n, NP = np32(n), R = g.R(), C = g.C, h = blockIdx.y, w = g.w;
   const int64_t win = blockIdx.x;
@@ -509,16 +511,14 @@ __global__ __launch_bounds__(AM_THREADS, 1) void k_attn_bwd_q_m(
   unsigned short* Vp = Kp + 3 * NP * PLW;
   float* tab = reinterpret_cast<float*>(Vp + 3 * NP * PLW);
   int* k7 = reinterpret_cast<int*>(tab + R);
-  float* wtab = reinterpret_cast<float*>(k7 + NP);  // [AM_WAVES][R]
   stage_planes<HD>(Kp, g, win, qkv, 3 * C, C + h * HD, bqkv, 1.f);
   stage_planes<HD>(Vp, g, win, qkv, 3 * C, 2 * C + h * HD, bqkv, 1.f);
   for (int r = threadIdx.x; r < R; r += blockDim.x) tab[r] = table[(int64_t)r * g.nh + h];
   for (int t = threadIdx.x; t < NP; t += blockDim.x) k7[t] = t < n ? key7(t, w) : 0;
-  for (int r = threadIdx.x; r < AM_WAVES * R; r += blockDim.x) wtab[r] = 0.f;
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, kg = lane >> 4;
   const int off0 = (w - 1) * ((2 * w - 1) * (2 * w - 1) + (2 * w - 1) + 1);
-  float* mt = wtab + wave * R;
+  float* dsb = dsw + (win * g.nh + h) * (int64_t)NP * NP;
   for (int qb = wave; qb < NP / 16; qb += AM_WAVES) {
     const int i = qb * 16 + l16;
     const bool iv = i < n;
@@ -554,10 +554,11 @@ __global__ __launch_bounds__(AM_THREADS, 1) void k_attn_bwd_q_m(
           const bool ok = iv && j < n;
           const int ri = ok ? base - k7[j] : 0;
           const float p = ok ? expf(s[r] + tab[ri] - li) : 0.f;
-          const float ds = p * (dp[r] - di);
-          dsv[4 * sb + r] = ds;
-          if (ok) atomicAdd(mt + ri, ds);  // this wave's private table (ds_add_f32)
+          dsv[4 * sb + r] = p * (dp[r] - di);
         }
+        if (iv)  // dS[i][j0 + 4 kg .. + 3] (zero beyond n)
+          *reinterpret_cast<float4*>(dsb + (int64_t)i * NP + j0 + 4 * kg) =
+              make_float4(dsv[4 * sb], dsv[4 * sb + 1], dsv[4 * sb + 2], dsv[4 * sb + 3]);
       }
       bf16x8m df[3], kf[3];
       split8m(dsv, df);
@@ -568,10 +569,50 @@ __global__ __launch_bounds__(AM_THREADS, 1) void k_attn_bwd_q_m(
       *reinterpret_cast<float4*>(dqkv + row * 3 * C + h * HD + 4 * kg) =
           make_float4(dq[0] * g.scale, dq[1] * g.scale, dq[2] * g.scale, dq[3] * g.scale);
   }
+}
+
+// bias-table gradient of one (window, head) from its dS.  Entry r is the relative offset
+// (od, oh, ow) of the configured WW^3 window (ridx = key7(i) - key7(j) + off0, tokens
+// enumerated t = (cd WW + ch) WW + cw).  Tokens group into WW^2 rows A = (cd, ch) of WW
+// tokens; the WW x WW block of dS between rows A and B contributes its 2 WW - 1 diagonal
+// sums to the entries (od, oh) = A - B.  Pass 1: a thread per row pair (A, B) reads its
+// block (7 contiguous floats per dS row) and keeps the diagonal sums in LDS; pass 2: a
+// thread per entry adds its row pairs in (cd, ch) order.  Fixed order; dS is read once.
+template <int WW>
+__global__ __launch_bounds__(256) void k_attn_dtable_m(const float* __restrict__ dsw, AttnGeo g,
+                                                       float* __restrict__ tpart) {
+  constexpr int NA = WW * WW, W2 = 2 * WW - 1;
+  extern __shared__ float dsh[];  // [NA][NA][W2]
+  const int n = g.n, NP = np32(n), R = g.R(), h = blockIdx.y;
+  const int64_t win = blockIdx.x;
+  const float* dsb = dsw + (win * g.nh + h) * (int64_t)NP * NP;
+  for (int t = threadIdx.x; t < NA * NA; t += blockDim.x) {
+    const int A = t / NA, Bq = t % NA;
+    float d[W2];
+#pragma unroll
+    for (int e = 0; e < W2; ++e) d[e] = 0.f;
+#pragma unroll
+    for (int cw = 0; cw < WW; ++cw) {
+      const int i = A * WW + cw;
+      float v[WW];
+#pragma unroll
+      for (int c2 = 0; c2 < WW; ++c2) {
+        const int j = Bq * WW + c2;
+        v[c2] = (i < n && j < n) ? dsb[(int64_t)i * NP + j] : 0.f;
+      }
+#pragma unroll
+      for (int c2 = 0; c2 < WW; ++c2) d[cw - c2 + WW - 1] += v[c2];
+    }
+#pragma unroll
+    for (int e = 0; e < W2; ++e) dsh[t * W2 + e] = d[e];
+  }
   __syncthreads();
   for (int r = threadIdx.x; r < R; r += blockDim.x) {
+    const int od = r / (W2 * W2) - (WW - 1), oh = (r / W2) % W2 - (WW - 1), e = r % W2;
     float acc = 0.f;
-    for (int wv = 0; wv < AM_WAVES; ++wv) acc += wtab[wv * R + r];
+    for (int cd = max(0, od); cd < min(WW, WW + od); ++cd)
+      for (int ch = max(0, oh); ch < min(WW, WW + oh); ++ch)
+        acc += dsh[((cd * WW + ch) * NA + (cd - od) * WW + (ch - oh)) * W2 + e];
     tpart[(win * g.nh + h) * R + r] = acc;
   }
 }
@@ -698,20 +739,19 @@ size_t mfma_fwd_lds(const AttnGeo& g) {
   const size_t NP = (size_t)((g.n + 31) & ~31);
   return 2 * 3 * NP * PLW * 2 + (size_t)g.R() * 4 + NP * 4;
 }
-size_t mfma_bwdq_lds(const AttnGeo& g) {
-  return mfma_fwd_lds(g) + (size_t)AM_WAVES * g.R() * 4;
-}
+size_t mfma_bwdq_lds(const AttnGeo& g) { return mfma_fwd_lds(g); }
 size_t mfma_bwdkv_lds(const AttnGeo& g) {
   const size_t NP = (size_t)((g.n + 31) & ~31);
   return 2 * 3 * NP * PLW * 2 + 3 * NP * 4 + (size_t)g.R() * 4 + (size_t)AM_WAVES * 2 * g.hd * 4;
 }
-// the MFMA kernels: head dims 4 .. 16 in multiples of 4 (SPFF_ATTN_VALU=1: the VALU kernels)
+// the MFMA kernels: window 7 (the registry's), head dims 4 .. 16 in multiples of 4
+// (SPFF_ATTN_VALU=1: the VALU kernels)
 bool use_mfma_attn(const AttnGeo& g) {
   static const bool valu = [] {
     const char* e = getenv("SPFF_ATTN_VALU");
     return e && e[0] == '1';
   }();
-  return !valu && g.hd <= 16 && g.hd % 4 == 0 && mfma_bwdq_lds(g) <= 160 * 1024 &&
+  return !valu && g.w == 7 && g.hd <= 16 && g.hd % 4 == 0 && mfma_bwdq_lds(g) <= 160 * 1024 &&
          mfma_bwdkv_lds(g) <= 160 * 1024;
 }
 template <typename K>
@@ -730,7 +770,9 @@ static size_t bwd_lds(const AttnGeo& g) {
 }
 
 size_t swin_attn_ws_bytes(const AttnGeo& g) {
-  return (size_t)g.nwin() * g.nh * (g.R() + 2 * g.hd) * sizeof(float);
+  // tpart [nwin][nh][R], ppart [nwin][nh][2 hd], then the MFMA backward's dS [nwin][nh][NP][NP]
+  const size_t NP = (size_t)((g.n + 31) & ~31);
+  return (size_t)g.nwin() * g.nh * (g.R() + 2 * g.hd + NP * NP) * sizeof(float);
 }
 
 #define SPFF_ATTN_HD(X) X(4) X(8) X(12) X(16) X(24) X(32)
@@ -782,8 +824,14 @@ hipError_t swin_attn_bwd(const float* qkv, const float* bqkv, const float* table
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   float* tpart = ws;
   float* ppart = ws + (size_t)g.nwin() * g.nh * g.R();
+  float* dsw = ppart + (size_t)g.nwin() * g.nh * 2 * g.hd;
   if (use_mfma_attn(g)) {
     const size_t lq = mfma_bwdq_lds(g), lkv = mfma_bwdkv_lds(g);
+    const size_t dtl = (size_t)49 * 49 * 13 * sizeof(float);  // k_attn_dtable_m<7> row-pair sums
+    {
+      hipError_t e0 = set_lds(k_attn_dtable_m<7>, dtl);
+      if (e0 != hipSuccess) return e0;
+    }
     switch (g.hd) {
 #define SPFF_BM(HD_)                                                                             \
   case HD_: {                                                                                    \
@@ -791,7 +839,8 @@ hipError_t swin_attn_bwd(const float* qkv, const float* bqkv, const float* table
     if (e0 != hipSuccess) return e0;                                                             \
     if ((e0 = set_lds(k_attn_bwd_kv_m<HD_>, lkv)) != hipSuccess) return e0;                      \
     hipLaunchKernelGGL(k_attn_bwd_q_m<HD_>, grid, dim3(AM_THREADS), lq, s, qkv, bqkv, table, O,  \
-                       dO, lse, g, dqkv, tpart);                                                 \
+                       dO, lse, g, dqkv, dsw);                                                   \
+    hipLaunchKernelGGL(k_attn_dtable_m<7>, grid, dim3(256), dtl, s, dsw, g, tpart);               \
     hipLaunchKernelGGL(k_attn_bwd_kv_m<HD_>, grid, dim3(AM_THREADS), lkv, s, qkv, bqkv, table,   \
                        O, dO, lse, g, dqkv, ppart);                                              \
   } break;
