@@ -22,6 +22,7 @@
 // tile's MFMAs.  Output: the fp32 partial slabs of conv3d.hip's wgrad
 // ([split][tap][kpad][npad]), summed in fixed order by k_wgrad_reduce.
 #include "spff_internal.h"
+#include "bf16split.h"
 
 #include <type_traits>
 #include <vector>
@@ -61,22 +62,7 @@ __device__ __forceinline__ unsigned short bfbits(__bf16 v) {
 }
 template <int NS>
 __device__ __forceinline__ void split4(const float4& v, uint2 (&o)[NS]) {
-  float r[4] = {v.x, v.y, v.z, v.w};
-  unsigned short s[4][NS];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-#pragma unroll
-    for (int p = 0; p < NS; ++p) {
-      const __bf16 b = (__bf16)r[e];
-      s[e][p] = bfbits(b);
-      r[e] = r[e] - (float)b;
-    }
-  }
-#pragma unroll
-  for (int p = 0; p < NS; ++p) {
-    o[p].x = (unsigned)s[0][p] | ((unsigned)s[1][p] << 16);
-    o[p].y = (unsigned)s[2][p] | ((unsigned)s[3][p] << 16);
-  }
+  split4_pk<NS>(v, o);  // bf16split.h
 }
 
 typedef __attribute__((address_space(3))) i16x4 lds_i16x4;

@@ -38,6 +38,7 @@
 //    and weight slab (both fp32) are in flight during chunk c's MFMAs, and
 //    are split into bf16 planes on their way into LDS.
 #include "spff_internal.h"
+#include "bf16split.h"
 
 #include <cstdlib>
 #include <cstring>
@@ -395,15 +396,22 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
       }
       v = make_float4(r[0], r[1], r[2], r[3]);
     }
-    unsigned short s0[NS], s1[NS], s2[NS], s3[NS];
-    split_bf16<NS>(ok ? v.x : 0.f, s0);
-    split_bf16<NS>(ok ? v.y : 0.f, s1);
-    split_bf16<NS>(ok ? v.z : 0.f, s2);
-    split_bf16<NS>(ok ? v.w : 0.f, s3);
+    if constexpr (BN <= 32) {
+      // packed pair split (bf16split.h): -0.5 to -3 % on the 16/32-wide launches; the
+      // 64-wide kernel (255 VGPRs) measured +1 to +3 % with it and keeps the per-value form
+      if (!ok) v = make_float4(0.f, 0.f, 0.f, 0.f);
+      split4_pk<NS>(v, hs[k]);
+    } else {
+      unsigned short s0[NS], s1[NS], s2[NS], s3[NS];
+      split_bf16<NS>(ok ? v.x : 0.f, s0);
+      split_bf16<NS>(ok ? v.y : 0.f, s1);
+      split_bf16<NS>(ok ? v.z : 0.f, s2);
+      split_bf16<NS>(ok ? v.w : 0.f, s3);
 #pragma unroll
-    for (int p = 0; p < NS; ++p) {
-      hs[k][p].x = (unsigned)s0[p] | ((unsigned)s1[p] << 16);
-      hs[k][p].y = (unsigned)s2[p] | ((unsigned)s3[p] << 16);
+      for (int p = 0; p < NS; ++p) {
+        hs[k][p].x = (unsigned)s0[p] | ((unsigned)s1[p] << 16);
+        hs[k][p].y = (unsigned)s2[p] | ((unsigned)s3[p] << 16);
+      }
     }
   };
   auto stash = [&](int kc, bool first) {

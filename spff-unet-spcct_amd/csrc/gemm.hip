@@ -8,6 +8,7 @@
 // voxels, split over voxel ranges into fp32 partial slabs summed in a fixed
 // order -> deterministic) which also produces the bias column sums.
 #include "spff_internal.h"
+#include "bf16split.h"
 
 namespace spff {
 
@@ -328,23 +329,7 @@ typedef __bf16 bf16x8g __attribute__((ext_vector_type(8)));
 typedef short i16x4g __attribute__((ext_vector_type(4)));
 typedef short i16x8g __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) i16x4g lds_i16x4g;
-__device__ __forceinline__ void gsplit4(float4 v, uint2 (&o)[3]) {
-  float r[4] = {v.x, v.y, v.z, v.w};
-  unsigned short h[4][3];
-#pragma unroll
-  for (int e = 0; e < 4; ++e)
-#pragma unroll
-    for (int p = 0; p < 3; ++p) {
-      const __bf16 b = (__bf16)r[e];
-      h[e][p] = __builtin_bit_cast(unsigned short, b);
-      r[e] -= (float)b;
-    }
-#pragma unroll
-  for (int p = 0; p < 3; ++p) {
-    o[p].x = (unsigned)h[0][p] | ((unsigned)h[1][p] << 16);
-    o[p].y = (unsigned)h[2][p] | ((unsigned)h[3][p] << 16);
-  }
-}
+__device__ __forceinline__ void gsplit4(float4 v, uint2 (&o)[3]) { split4_pk<3>(v, o); }
 // 32-B column-unit swizzle of B row k (BN / 16 units per row, 128 / BN rows per 256 B)
 template <int BN>
 __device__ __forceinline__ int gx_bsw(int k) {

@@ -3,21 +3,37 @@
 #include "spff_internal.h"
 
 #include <algorithm>
+#include <cstdint>
 #include <math.h>
 
 namespace spff {
 
 static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 
-// x [B][C][D][H][W] (reference layout) -> y [B][D][H][W][ldy], channels C..ldy-1 = 0
+// x [B][C][D][H][W] (reference layout) -> y [B][D][H][W][ldy], channels C..ldy-1 = 0.
+// One thread per voxel; the channel row leaves as 16-byte stores (ldy % 4 == 0: every
+// engine input has ldy = 8), the C plane reads are coalesced across the wave.
+template <bool V4>
 __global__ void k_ncdhw_to_ndhwc(const float* __restrict__ x, float* __restrict__ y, int B,
                                  int64_t S, int C, int ldy) {
   const int64_t V = (int64_t)B * S;
   for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < V;
        v += (int64_t)gridDim.x * blockDim.x) {
     const int64_t b = v / S, sp = v % S;
+    const float* xi = x + b * C * S + sp;
     float* o = y + v * ldy;
-    for (int c = 0; c < ldy; ++c) o[c] = c < C ? x[(b * C + c) * S + sp] : 0.f;
+    if constexpr (V4) {
+      for (int c = 0; c < ldy; c += 4) {
+        float4 q;
+        q.x = c < C ? xi[(int64_t)c * S] : 0.f;
+        q.y = c + 1 < C ? xi[(int64_t)(c + 1) * S] : 0.f;
+        q.z = c + 2 < C ? xi[(int64_t)(c + 2) * S] : 0.f;
+        q.w = c + 3 < C ? xi[(int64_t)(c + 3) * S] : 0.f;
+        *reinterpret_cast<float4*>(o + c) = q;
+      }
+    } else {
+      for (int c = 0; c < ldy; ++c) o[c] = c < C ? xi[(int64_t)c * S] : 0.f;
+    }
   }
 }
 
@@ -25,7 +41,10 @@ hipError_t ncdhw_to_ndhwc(const float* x, float* y, Vol vol, int C, int ldy, hip
   const int64_t S = (int64_t)vol.D * vol.H * vol.W;
   const int64_t V = vol.B * S;
   int grid = (int)std::min<int64_t>((V + 255) / 256, 8192);
-  hipLaunchKernelGGL(k_ncdhw_to_ndhwc, dim3(grid), dim3(256), 0, s, x, y, vol.B, S, C, ldy);
+  if (ldy % 4 == 0 && reinterpret_cast<uintptr_t>(y) % 16 == 0)
+    hipLaunchKernelGGL(k_ncdhw_to_ndhwc<true>, dim3(grid), dim3(256), 0, s, x, y, vol.B, S, C, ldy);
+  else
+    hipLaunchKernelGGL(k_ncdhw_to_ndhwc<false>, dim3(grid), dim3(256), 0, s, x, y, vol.B, S, C, ldy);
   return hipGetLastError();
 }
 
@@ -430,8 +449,13 @@ hipError_t resize_d_rows_bwd(const float* dy, float* dx, int B, int K, int Din, 
   return hipGetLastError();
 }
 
+// x *= *scale.  The scale is the upstream gradient of a scalar loss, 1 whenever the loss is
+// the last op before backward(): then every workgroup returns after one scalar load (the
+// logits-sized pass, 2 x 218 MB at config 2, is skipped) -- a uniform branch on device data,
+// no host sync.
 __global__ void k_scale(float* x, int64_t n, const float* scale) {
   const float a = *scale;
+  if (a == 1.f) return;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x)
     x[i] *= a;
