@@ -142,7 +142,9 @@ int spff_backward(spff_plan* plan, const float* dlogits, const float* params, fl
 int spff_saved_tensor(const spff_plan* plan, void* workspace, const char* name,
                       const float** ptr, int64_t* nvox, int* channels);
 
-/* debug knobs (tests): key 0 = stop the backward after N decoder blocks (-1 off) */
+/* debug knobs (tests): key 0 = stop the backward after N decoder blocks (-1 off);
+ * key 1 = also store the block outputs the up-conv / head GEMMs apply on the fly
+ * (bott/dec*.out; otherwise spff_saved_tensor reports them as not stored) */
 int spff_debug_set(spff_plan* plan, int key, int value);
 
 /* optional HIP-event timing of the engine's kernels on the plan's stream (bench.py):

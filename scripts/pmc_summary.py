@@ -4,9 +4,9 @@
     python scripts/pmc_summary.py gpurun_out/kpmc/run_counter_collection.csv \
         [gpurun_out/kpmc2/run_counter_collection.csv ...]
 
-Derived (MI355X: 256 CUs x 4 SIMDs): clock = GRBM_GUI_ACTIVE / kernel time,
-MFMA share = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x active cycles), and the
-SQ wave-state split (SQ_* count quad-cycles)."""
+Derived (MI355X: 256 CUs x 4 SIMDs, 8 XCDs): clock = GRBM_GUI_ACTIVE / 8 / kernel time
+(rocprofv3 sums GRBM_GUI_ACTIVE over the 8 XCDs), MFMA share = SQ_VALU_MFMA_BUSY_CYCLES /
+(1024 SIMDs x GRBM_GUI_ACTIVE / 8), and the SQ wave-state split (SQ_* count quad-cycles)."""
 import collections
 import csv
 import sys
@@ -25,13 +25,13 @@ for k, c in acc.items():
     ns = sum(dur[k].values()) / max(1, len({p for p, _ in dur[k]}))  # per counter pass
     line = [f"{k}: {ns / 1e6:.3f} ms"]
     if c.get("GRBM_GUI_ACTIVE"):
-        line.append(f"clock {c['GRBM_GUI_ACTIVE'] / ns:.2f} GHz")
+        line.append(f"clock {c['GRBM_GUI_ACTIVE'] / 8 / ns:.2f} GHz")
         if c.get("SQ_VALU_MFMA_BUSY_CYCLES"):
-            line.append(f"MFMA busy {c['SQ_VALU_MFMA_BUSY_CYCLES'] / (1024 * c['GRBM_GUI_ACTIVE']):.3f}")
+            line.append(f"MFMA busy {c['SQ_VALU_MFMA_BUSY_CYCLES'] / (128 * c['GRBM_GUI_ACTIVE']):.3f}")
     w = c.get("SQ_WAVE_CYCLES")
     if w:
         for n in ("SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY",
-                  "SQ_WAIT_INST_LDS"):
+                  "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_LDS", "SQ_WAIT_INST_LDS"):
             if n in c:
                 line.append(f"{n[3:]} {c[n] / w:.3f}")
     if c.get("SQ_LDS_IDX_ACTIVE"):

@@ -13,6 +13,16 @@
 // out and the (b,c)/(b,c,d) statistics -- everything else is recomputed.
 #include "spff_internal.h"
 
+#ifndef SPFF_OUTFUSE
+// block outputs applied by the GEMMs that read them (ActRows) instead of a stored act_apply
+// pass: 1 = dec1's, read by the head (forward GEMM + streaming weight gradient); 2 = also the
+// bottleneck's and dec3 / dec2's, read by the up-convs; 0 = none.  Measured (round 3, one
+// box, profiles/r03/ab/outfuse_kstats.txt): the up-conv loaders pay 5 loads per A float4 and
+// the transform's VALU in kernels that are VALU-issue-bound already -- k_atb_x 0.64 -> 1.07,
+// the up-conv forward 0.47 -> 0.69 ms/step against 0.16 ms/step of act_apply saved; the
+// head's loaders +0.14 ms/step against dec1's 0.2 ms/step level-0 pass
+#define SPFF_OUTFUSE 1
+#endif
 #ifndef SPFF_RED_FUSE
 #define SPFF_RED_FUSE 1  // 0 (A/B diagnostics): separate tail and IN-backward reductions
 #endif
@@ -90,6 +100,8 @@ struct Blk {
   size_t Sa, t, bt, hid, s1, g1s, sg2, p, h, e, P, Q;
   size_t spec = 0;  // sharded plans: full-depth s1 spectrum [B][L][2] (fp64)
   bool fa = false;  // conv2 reads y1 through the IN affine (a1 never stored)
+  bool fout = false;  // out never stored: its GEMM consumers apply it to y2 (ActRows)
+  size_t PT = 0, QT = 0;  // fout + gates: P, Q as [B][D][C]
   bool tail() const { return efilm || fgate || post_se || post_spec; }
 };
 
@@ -142,6 +154,7 @@ struct spff_plan {
   size_t prof_n = 0;
   bool prof_on = false;
   int dbg_stop = -1;  // debug: stop backward after this many blocks (-1 = off)
+  bool keep_out = false;  // debug: store the fused block outputs too (saved views)
   // per call
   char* ws = nullptr;
   const float* prm = nullptr;
@@ -304,6 +317,9 @@ int build_plan(spff_plan* p) {
     b.post_se = i < 4 && c.use_se;
     b.post_spec = i < 4 && c.use_specse;
     b.fa = conv3d_fuses_act(c.math, b.C);
+    // the bottleneck and decoder outputs feed only the up-convs and the head (GEMMs)
+    b.fout = (SPFF_OUTFUSE >= 2 ? i >= 3 : SPFF_OUTFUSE == 1 && i == 6) && !p->lean &&
+             b.C % 4 == 0;
     conv_dims(b.c1, b.Cin, b.C);
     conv_dims(b.c2, b.C, b.C);
   }
@@ -371,6 +387,10 @@ int build_plan(spff_plan* p) {
       b.Sa = p->alloc(bcdz);
       b.P = p->alloc(bcdz);
       b.Q = p->alloc(bcdz);
+      if (b.fout) {
+        b.PT = p->alloc(bcdz);
+        b.QT = p->alloc(bcdz);
+      }
       b.s1 = p->alloc((size_t)B * D * 4);
       b.g1s = p->alloc((size_t)B * D * 4);
       b.sg2 = p->alloc((size_t)B * D * 4);
@@ -504,8 +524,24 @@ GateSaved gate_saved(const spff_plan* p, const Blk& b) {
   s.s1 = p->F(b.s1); s.g1 = p->F(b.g1s); s.sg2 = p->F(b.sg2);
   s.p = p->F(b.p); s.h = p->F(b.h); s.e = p->F(b.e);
   s.P = p->F(b.P); s.Q = p->F(b.Q);
+  s.PT = b.fout ? p->F(b.PT) : nullptr;
+  s.QT = b.fout ? p->F(b.QT) : nullptr;
   s.spec = p->co.on() ? p->D64(b.spec) : nullptr;
   return s;
+}
+
+// the rows of block b's output as its GEMM consumers apply them (b.fout)
+ActRows act_rows(const spff_plan* p, const Blk& b) {
+  const Vol& v = p->vol[b.lvl];
+  ActRows a;
+  a.y = p->F(b.y2);
+  a.al = p->F(b.al2);
+  a.de = p->F(b.de2);
+  a.PT = b.tail() ? p->F(b.PT) : nullptr;
+  a.QT = b.tail() ? p->F(b.QT) : nullptr;
+  a.D = v.D;
+  a.HW = v.H * v.W;
+  return a;
 }
 
 // one D-slice halo per side for a conv input of a depth-sharded plan (no-op otherwise)
@@ -736,6 +772,7 @@ int fwd_block(spff_plan* p, Blk& b, const Src2& in, int pool = -1) {
   }
   const float* P = b.tail() ? p->F(b.P) : nullptr;
   const float* Q = b.tail() ? p->F(b.Q) : nullptr;
+  if (b.fout && !p->keep_out) return SPFF_OK;  // applied by the up-conv / head GEMMs
   if (pool >= 0 && !((v.H | v.W) & 1)) {
     // read y2, write out + pooled + argmax bytes: 4C + 4C + C + C / 4 bytes per voxel
     PROFB(p, 5, 0.0, 9.25 * (double)nvox(v) * C,
@@ -754,13 +791,14 @@ int fwd_block(spff_plan* p, Blk& b, const Src2& in, int pool = -1) {
 
 Src2 src2(const float* a, const float* b, int C) { return Src2{a, b, C, C, C}; }
 
-// up-conv of `in` into U.out at the skip's resolution (through U.raw and the _cat
-// trilinear resize when the pooled extents were odd)
-int upconv_out(spff_plan* p, const UpL& U, const float* in) {
+// up-conv of block src's output into U.out at the skip's resolution (through U.raw and
+// the _cat trilinear resize when the pooled extents were odd)
+int upconv_out(spff_plan* p, const UpL& U, const Blk& src) {
   const Vol& low = p->vol[U.lvl_low];
+  const ActRows act = act_rows(p, src);
   PROF(p, 3, 2.0 * nvox(low) * U.Cin * 4.0 * U.Cout,
-       upconv_fwd(in, p->F(U.pk), p->P(U.b), p->F(U.rs ? U.raw : U.out), low, U.Cin, U.Cout,
-                  p->st, 4, p->cfg.math));
+       upconv_fwd(p->F(src.out), p->F(U.pk), p->P(U.b), p->F(U.rs ? U.raw : U.out), low, U.Cin,
+                  U.Cout, p->st, 4, p->cfg.math, src.fout ? &act : nullptr));
   if (U.rs) {
     const Vol& vh = p->vol[U.lvl_low - 1];
     Vol vr = low;
@@ -791,7 +829,7 @@ int lean_dec_input(spff_plan* p, int bi, Src2* in) {
   const Blk& prev = B[bi - 1];
   UpL& U = p->up[bi - 4];
   if (bi - 1 >= 4) CK(recompute_out(p, prev, p->F(prev.out)));
-  CK(upconv_out(p, U, p->F(prev.out)));
+  CK(upconv_out(p, U, prev));
   CK(recompute_out(p, skip, p->F(p->G_out)));
   *in = src2(p->F(U.out), p->F(p->G_out), d.C);
   return halo_src(p, *in, p->vol[d.lvl]);
@@ -941,22 +979,24 @@ int forward(spff_plan* p, const float* x, float* logits) {
   CK(fwd_block(p, B[1], src1(p->F(p->pool[0]), f), 1));
   CK(fwd_block(p, B[2], src1(p->F(p->pool[1]), 2 * f), 2));
   CK(fwd_block(p, B[3], src1(p->F(p->pool[2]), 4 * f)));
-  const float* prev = p->F(B[3].out);
+  const Blk* prev = &B[3];
   for (int u = 0; u < 3; ++u) {
     UpL& U = p->up[u];
     float* pk = p->F(U.pk);
     HIPCK(upconv_pack(p->P(U.w), pk, pk + upconv_pack_dgrad_offset(U.Cin, U.Cout), U.Cin, U.Cout,
                       p->st));
-    CK(upconv_out(p, U, prev));
+    CK(upconv_out(p, U, *prev));
     Blk& d = B[4 + u];
     const Blk& skip = B[2 - u];
     CK(fwd_block(p, d, src2(p->F(U.out), p->F(skip.out), U.Cout)));
-    prev = p->F(d.out);
+    prev = &d;
   }
   float* hp = p->F(p->head_pk);
   HIPCK(head_pack(p->P(p->out_w), hp, hp + head_pack_dgrad_offset(f, p->K), f, p->K, p->st));
+  const ActRows hact = act_rows(p, *prev);
   PROF(p, 3, 2.0 * nvox(p->vol[0]) * f * p->K,
-       head_fwd(prev, hp, p->P(p->out_b), logits, nvox(p->vol[0]), f, p->K, p->st, p->cfg.math));
+       head_fwd(p->F(prev->out), hp, p->P(p->out_b), logits, nvox(p->vol[0]), f, p->K, p->st,
+                p->cfg.math, prev->fout ? &hact : nullptr));
   return SPFF_OK;
 }
 
@@ -965,9 +1005,10 @@ int backward(spff_plan* p, const float* dl) {
   Blk* B = p->blk;
   const int64_t V0 = nvox(p->vol[0]);
   float* hp = p->F(p->head_pk);
+  const ActRows hact = act_rows(p, B[6]);
   PROF(p, 3, 2.0 * V0 * f * p->K,
        head_wgrad(p->F(B[6].out), dl, p->DP(p->out_w), p->DP(p->out_b), V0, f, p->K,
-                  p->F(p->wg_ws), p->st));
+                  p->F(p->wg_ws), p->st, B[6].fout ? &hact : nullptr));
   CK(grad_ready(p, p->out_w, p->out_b + p->K));
   PROF(p, 3, 2.0 * V0 * f * p->K,
        head_dgrad(dl, hp + head_pack_dgrad_offset(f, p->K), p->F(p->G_out), V0, f, p->K,
@@ -984,7 +1025,8 @@ int backward(spff_plan* p, const float* dl) {
     CK(bwd_block(p, d, p->F(p->G_out), &dx, src2(p->F(U.out), p->F(B[lvl].out), C), bi));
     CK(block_grads_ready(p, d));
     if (p->dbg_stop == k + 1) return SPFF_OK;
-    const float* upin = (ui == 0) ? p->F(B[3].out) : p->F(B[bi - 1].out);
+    const Blk& ub = (ui == 0) ? B[3] : B[bi - 1];  // the up-conv's input block
+    const ActRows uact = act_rows(p, ub);
     const Vol& low = p->vol[U.lvl_low];
     const float* gup = p->F(p->G_dx);
     if (U.rs) {  // back through the _cat resize to the up-conv's 2H x 2W grid
@@ -996,8 +1038,8 @@ int backward(spff_plan* p, const float* dl) {
       gup = p->F(U.raw);
     }
     PROF(p, 3, 2.0 * nvox(low) * U.Cin * 4.0 * U.Cout,
-         upconv_wgrad(upin, gup, C, p->DP(U.w), p->DP(U.b), low, U.Cin, U.Cout,
-                      p->F(p->wg_ws), p->st, 4, p->cfg.math));
+         upconv_wgrad(p->F(ub.out), gup, C, p->DP(U.w), p->DP(U.b), low, U.Cin, U.Cout,
+                      p->F(p->wg_ws), p->st, 4, p->cfg.math, ub.fout ? &uact : nullptr));
     CK(grad_ready(p, U.w, U.b + U.Cout));
     float* pk = p->F(U.pk);
     PROF(p, 3, 2.0 * nvox(low) * U.Cin * 4.0 * U.Cout,
@@ -1160,7 +1202,12 @@ int spff_saved_tensor(const spff_plan* p, void* ws, const char* name, const floa
       return ret(b.a1, v, b.C);
     }
     if (n == b.name + ".y2") return ret(b.y2, v, b.C);
-    if (n == b.name + ".out") return ret(b.out, v, b.C);
+    if (n == b.name + ".out") {
+      if (b.fout && !p->keep_out)
+        return fail(SPFF_EINVAL, "out is not stored: the up-conv / head GEMMs apply it as they "
+                                 "read y2 (spff_debug_set key 1 stores it too)");
+      return ret(b.out, v, b.C);
+    }
     // per-(b,c) normalisation of the IN that follows conv 1 / 2: r = y*al + de
     const Vol bv{v.B, 1, 1, 1};
     if (n == b.name + ".al1") return ret(b.al1, bv, b.C);
@@ -1183,6 +1230,7 @@ int spff_saved_tensor(const spff_plan* p, void* ws, const char* name, const floa
 int spff_debug_set(spff_plan* p, int key, int value) {
   if (!p) return fail(SPFF_EINVAL, "null plan");
   if (key == 0) p->dbg_stop = value;
+  if (key == 1) p->keep_out = value != 0;  // store the GEMM-applied block outputs too
   return SPFF_OK;
 }
 

@@ -231,6 +231,10 @@ __global__ __launch_bounds__(GT) void k_gates_fwd(GateParams gp, const float* __
     const float btv = efilm ? sv.bt[i] : 0.f;
     sv.P[(int64_t)b * C * D + i] = onept * G;
     sv.Q[(int64_t)b * C * D + i] = btv * G;
+    if (sv.PT) {  // [B][D][C] copies for the GEMM loaders (ActRows)
+      sv.PT[((int64_t)b * D + d) * C + c] = onept * G;
+      sv.QT[((int64_t)b * D + d) * C + c] = btv * G;
+    }
   }
 }
 
@@ -778,6 +782,10 @@ __global__ __launch_bounds__(GT) void k_gsh_fwd_c(GateParams gp, GateSaved sv, V
     const float btv = efilm ? sv.bt[i] : 0.f;
     sv.P[(int64_t)b * C * D + i] = onept * G;
     sv.Q[(int64_t)b * C * D + i] = btv * G;
+    if (sv.PT) {  // [B][D][C] copies for the GEMM loaders (ActRows)
+      sv.PT[((int64_t)b * D + d) * C + c] = onept * G;
+      sv.QT[((int64_t)b * D + d) * C + c] = btv * G;
+    }
   }
 }
 

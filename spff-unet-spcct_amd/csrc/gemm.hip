@@ -62,14 +62,39 @@ struct LoadRowsScalar {  // generic
     return v;
   }
 };
+// log2(v) for a power of two, else -1: the gather / scatter index math then shifts and
+// masks instead of dividing (every SPFF level and the 3DUNet's power-of-two extents; a
+// runtime division is ~20 VALU, and these GEMMs are VALU-issue-bound, PMC round 3)
+static inline int pow2_shift(int v) { return (v > 0 && !(v & (v - 1))) ? __builtin_ctz(v) : -1; }
+// q = n / d, r = n % d (sh = log2 d, or -1); sh is uniform, so this is a scalar branch
+__device__ __forceinline__ void udivmod_s(uint32_t n, uint32_t d, int sh, uint32_t& q, uint32_t& r) {
+  if (sh >= 0) {
+    q = n >> sh;
+    r = n & (d - 1);
+  } else {
+    q = n / d;
+    r = n - q * d;
+  }
+}
+// A[m][k] = a block output applied as it loads (ActRows, spff_internal.h): the pre-IN rows
+// y through lrelu(y al + de) P + Q -- k_act_apply's expression, so bitwise the stored out.
+// The row's (b, d) = m / HW = b D + d selects the per-(b, c) and per-(b, d, c) parameters
+// (float4 loads, L1/L2-resident); ld = C, a multiple of 4.
+struct LoadRowsAct {
+  const float* p; int ld; int kmax; int64_t M;
+  const float* al; const float* de; const float* PT; const float* QT;
+  int D, HW, dsh, hwsh; float neg;
+  __device__ int64_t prep(int64_t m) const { return m < M ? m : -1; }
+  __device__ float4 load4(int64_t h, int k) const;
+};
 // high-res voxel of low-res voxel m's sub-lattice ij = 0: nsub = 4 for the
 // (1,2,2) up-convs of SPFF (ij = kh*2 + kw, depth kept), nsub = 8 for the
 // 2x2x2 ones of the 3DUNet (ij = (kd*2 + kh)*2 + kw, depth doubled)
-__device__ inline int64_t up_high_base(uint32_t m, int D, int Hl, int Wl, int nsub) {
-  const uint32_t w = m % (uint32_t)Wl;
-  uint32_t t = m / (uint32_t)Wl;
-  const uint32_t h = t % (uint32_t)Hl;
-  t /= (uint32_t)Hl;  // t = b*D + d
+__device__ inline int64_t up_high_base(uint32_t m, int D, int Hl, int Wl, int nsub, int wsh = -1,
+                                       int hsh = -1) {
+  uint32_t t, w, h;
+  udivmod_s(m, (uint32_t)Wl, wsh, t, w);
+  udivmod_s(t, (uint32_t)Hl, hsh, t, h);  // t = b*D + d
   int64_t tt = t;
   if (nsub == 8) tt = (int64_t)(t / (uint32_t)D) * (2 * D) + 2 * (t % (uint32_t)D);
   return (tt * (2 * Hl) + 2 * h) * (int64_t)(2 * Wl) + 2 * w;
@@ -78,15 +103,47 @@ __device__ inline int64_t up_high_base(uint32_t m, int D, int Hl, int Wl, int ns
 __device__ inline int64_t up_sub_off(int ij, int Hl, int Wl) {
   return (int64_t)(ij >> 2) * (4 * (int64_t)Hl * Wl) + ((ij >> 1) & 1) * (2 * Wl) + (ij & 1);
 }
+__device__ float4 LoadRowsAct::load4(int64_t h, int k) const {
+  if (h < 0 || k >= kmax) return make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4 v = *reinterpret_cast<const float4*>(p + h * ld + k);
+  uint32_t bd, r, b, d;
+  udivmod_s((uint32_t)h, (uint32_t)HW, hwsh, bd, r);
+  udivmod_s(bd, (uint32_t)D, dsh, b, d);
+  const float4 a = *reinterpret_cast<const float4*>(al + (int64_t)b * ld + k);
+  const float4 e = *reinterpret_cast<const float4*>(de + (int64_t)b * ld + k);
+  float4 pp = make_float4(1.f, 1.f, 1.f, 1.f), qq = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (PT) {
+    pp = *reinterpret_cast<const float4*>(PT + (int64_t)bd * ld + k);
+    qq = *reinterpret_cast<const float4*>(QT + (int64_t)bd * ld + k);
+  }
+  auto f = [&](float y, float a_, float e_, float p_, float q_) {
+    const float t = y * a_ + e_;
+    return (t > 0.f ? t : neg * t) * p_ + q_;
+  };
+  return make_float4(f(v.x, a.x, e.x, pp.x, qq.x), f(v.y, a.y, e.y, pp.y, qq.y),
+                     f(v.z, a.z, e.z, pp.z, qq.z), f(v.w, a.w, e.w, pp.w, qq.w));
+}
+static LoadRowsAct act_loader(const ActRows& a, int C, int64_t M) {
+  return LoadRowsAct{a.y, C, C, M, a.al, a.de, a.PT, a.QT, a.D, a.HW, pow2_shift(a.D),
+                     pow2_shift(a.HW), a.neg};
+}
+static bool act_ok(const ActRows* a, int C) {
+  return a && a->y && a->al && a->de && C % 4 == 0 && a->D > 0 && a->HW > 0 &&
+         !((reinterpret_cast<uintptr_t>(a->y) | reinterpret_cast<uintptr_t>(a->al) |
+            reinterpret_cast<uintptr_t>(a->de) | reinterpret_cast<uintptr_t>(a->PT) |
+            reinterpret_cast<uintptr_t>(a->QT)) & 15);
+}
 struct LoadUpGather {  // A[m][k], k = ij*Cout + co -> dy[high(m,ij)*ld + co]
   const float* p; int ld; int Cout; int D, Hl, Wl; int64_t M; int nsub;
+  int csh = -1, wsh = -1, hsh = -1;  // pow2_shift of Cout, Wl, Hl (set by the launchers)
   __device__ int64_t prep(int64_t m) const {
-    return m < M ? up_high_base((uint32_t)m, D, Hl, Wl, nsub) : -1;
+    return m < M ? up_high_base((uint32_t)m, D, Hl, Wl, nsub, wsh, hsh) : -1;
   }
   __device__ float4 load4(int64_t h, int k) const {
     if (h < 0 || k >= nsub * Cout) return make_float4(0.f, 0.f, 0.f, 0.f);
-    const int ij = k / Cout, co = k - ij * Cout;
-    return *reinterpret_cast<const float4*>(p + (h + up_sub_off(ij, Hl, Wl)) * ld + co);
+    uint32_t ij, co;
+    udivmod_s((uint32_t)k, (uint32_t)Cout, csh, ij, co);
+    return *reinterpret_cast<const float4*>(p + (h + up_sub_off((int)ij, Hl, Wl)) * ld + co);
   }
 };
 struct StoreRows {  // C[m][n] -> p[m*ld + n] (+bias[n]), n < nmax
@@ -106,13 +163,15 @@ struct StoreRows {  // C[m][n] -> p[m*ld + n] (+bias[n]), n < nmax
 };
 struct StoreUp {  // C[m][n], n = ij*Cout + co -> y[high(m,ij)*Cout + co] + bias[co]
   float* p; int Cout; const float* bias; int D, Hl, Wl; int64_t M; int nsub;
+  int csh = -1, wsh = -1, hsh = -1;  // pow2_shift of Cout, Wl, Hl (set by the launchers)
   __device__ int64_t prep(int64_t m) const {
-    return m < M ? up_high_base((uint32_t)m, D, Hl, Wl, nsub) * Cout : -1;
+    return m < M ? up_high_base((uint32_t)m, D, Hl, Wl, nsub, wsh, hsh) * Cout : -1;
   }
   __device__ int64_t col(int n) const {
     if (n >= nsub * Cout) return -1;
-    const int ij = n / Cout;
-    return up_sub_off(ij, Hl, Wl) * Cout + (n - ij * Cout);
+    uint32_t ij, co;
+    udivmod_s((uint32_t)n, (uint32_t)Cout, csh, ij, co);
+    return up_sub_off((int)ij, Hl, Wl) * Cout + co;
   }
   __device__ float bias_of(int n) const { return n < nsub * Cout ? bias[n % Cout] : 0.f; }
   __device__ void put(int64_t idx, float v) const { p[idx] = v; }
@@ -757,12 +816,15 @@ __global__ __launch_bounds__(256, 2) void k_atb_x(XL X, YL Y, float* __restrict_
 struct UpGeo {
   int D, Hl, Wl, nsub, Cout;
 };
-template <int TM, int TN, bool UP>
+// ACT: X is a block output applied as it loads (ActRows): each lane keeps its column's
+// parameters for the (b, d) slab of its current voxel and reloads them when that changes
+template <int TM, int TN, bool UP, bool ACT = false>
 __global__ __launch_bounds__(256) void k_xty(const float* __restrict__ X, int ldx, int K1,
                                              const float* __restrict__ Y, int ldy, int N, UpGeo g,
                                              float* __restrict__ part, float* __restrict__ csum,
                                              int64_t M, int64_t rps, int k1pad, int npad,
-                                             const float* __restrict__ X2, int ldx2, int xsplit) {
+                                             const float* __restrict__ X2, int ldx2, int xsplit,
+                                             LoadRowsAct act = {}) {
   constexpr int NE = TM * TN * 16;
   __shared__ float red[4][NE][64];
   __shared__ float cred[4][2][TN][32];
@@ -796,12 +858,21 @@ __global__ __launch_bounds__(256) void k_xty(const float* __restrict__ X, int ld
   for (int t = 0; t < TN; ++t) cs[t] = 0.f;
   const int64_t npairs = (ve - vb + 1) / 2;
   constexpr int U = 4;  // voxel pairs per iteration, loads issued first
+  uint32_t cbd = 0xffffffffu;  // ACT: the (b, d) slab the cached parameters belong to
+  float ca[TM], ce[TM], cp[TM], cq[TM];
+#pragma unroll
+  for (int t = 0; t < TM; ++t) { ca[t] = 1.f; ce[t] = 0.f; cp[t] = 1.f; cq[t] = 0.f; }
   for (int64_t p0 = wave; p0 < npairs; p0 += 4 * U) {
     float xa[U][TM], yb[U][TN];
+    uint32_t vbd[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t v = vb + 2 * (p0 + 4 * u) + khalf;
       const bool vok = (p0 + 4 * u < npairs) && v < ve;
+      if constexpr (ACT) {
+        uint32_t r;
+        udivmod_s((uint32_t)(vok ? v : vb), (uint32_t)act.HW, act.hwsh, vbd[u], r);
+      }
       int64_t yr = 0;
       if (vok) yr = UP ? up_high_base((uint32_t)v, g.D, g.Hl, g.Wl, g.nsub) * ldy : v * ldy;
 #pragma unroll
@@ -817,6 +888,29 @@ __global__ __launch_bounds__(256) void k_xty(const float* __restrict__ X, int ld
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
+      if constexpr (ACT) {
+        if (vbd[u] != cbd) {  // (divergent only where a voxel pair straddles two slabs)
+          cbd = vbd[u];
+          uint32_t b, d;
+          udivmod_s(cbd, (uint32_t)act.D, act.dsh, b, d);
+#pragma unroll
+          for (int t = 0; t < TM; ++t) {
+            const int col = k10 + 32 * t + l32;
+            if (!kok[t]) continue;
+            ca[t] = act.al[(int64_t)b * act.ld + col];
+            ce[t] = act.de[(int64_t)b * act.ld + col];
+            cp[t] = act.PT ? act.PT[(int64_t)cbd * act.ld + col] : 1.f;
+            cq[t] = act.PT ? act.QT[(int64_t)cbd * act.ld + col] : 0.f;
+          }
+        }
+#pragma unroll
+        for (int t = 0; t < TM; ++t) {
+          // (a row past the split loads 0 and comes out non-zero here: its Y is 0, so its
+          //  products vanish; a padding column keeps ca, ce, cp, cq = 1, 0, 1, 0 -> 0)
+          const float tt = xa[u][t] * ca[t] + ce[t];
+          xa[u][t] = (tt > 0.f ? tt : act.neg * tt) * cp[t] + cq[t];
+        }
+      }
 #pragma unroll
       for (int t = 0; t < TN; ++t) cs[t] += yb[u][t];
 #pragma unroll
@@ -881,7 +975,7 @@ static size_t xty_ws_bytes(int64_t M, int K1, int N) {
 static hipError_t launch_xty(const float* X, int ldx, int K1, const float* Y, int ldy, int N,
                              const UpGeo* up, int64_t M, int Cout, int mode, float* dw, float* db,
                              float* ws, hipStream_t s, const float* X2 = nullptr, int ldx2 = 0,
-                             int xsplit = 1 << 30);
+                             int xsplit = 1 << 30, const ActRows* act = nullptr);
 
 // dW layouts: mode 0 = upconv W[Cin][Cout][1][2][2] from C[ci][ij*Cout+co]
 //             mode 2 = upconv W[Cin][Cout][2][2][2] from C[ci][ij*Cout+co]
@@ -937,8 +1031,10 @@ __global__ __launch_bounds__(256) void k_atb_reduce(const float* __restrict__ pa
 
 static hipError_t launch_xty(const float* X, int ldx, int K1, const float* Y, int ldy, int N,
                              const UpGeo* up, int64_t M, int Cout, int mode, float* dw, float* db,
-                             float* ws, hipStream_t s, const float* X2, int ldx2, int xsplit) {
+                             float* ws, hipStream_t s, const float* X2, int ldx2, int xsplit,
+                             const ActRows* act) {
   if (!X2) X2 = X;
+  if (act && (up || xsplit < K1)) return hipErrorInvalidValue;
   if (M >= (int64_t(1) << 31)) return hipErrorInvalidValue;
   const XtyPlan p = xty_plan(M, K1, N);
   float* part = ws;
@@ -953,6 +1049,16 @@ static hipError_t launch_xty(const float* X, int ldx, int K1, const float* Y, in
     else if (p.tm == 2) SPFF_XTY(2, 1, true);
     else if (p.tn == 2) SPFF_XTY(1, 2, true);
     else SPFF_XTY(1, 1, true);
+  } else if (act) {
+    const LoadRowsAct la = act_loader(*act, ldx, M);
+#define SPFF_XTYA(TM_, TN_)                                                                      \
+  hipLaunchKernelGGL((k_xty<TM_, TN_, false, true>), grid, dim3(256), 0, s, X, ldx, K1, Y, ldy, N, \
+                     g, part, csum, M, p.rps, p.k1pad, p.npad, X2, ldx2, xsplit, la)
+    if (p.tm == 2 && p.tn == 2) SPFF_XTYA(2, 2);
+    else if (p.tm == 2) SPFF_XTYA(2, 1);
+    else if (p.tn == 2) SPFF_XTYA(1, 2);
+    else SPFF_XTYA(1, 1);
+#undef SPFF_XTYA
   } else {
     if (p.tm == 2 && p.tn == 2) SPFF_XTY(2, 2, false);
     else if (p.tm == 2) SPFF_XTY(2, 1, false);
@@ -1045,17 +1151,23 @@ hipError_t upconv_pack(const float* w, float* wf, float* wd, int Cin, int Cout, 
 }
 
 hipError_t upconv_fwd(const float* x, const float* wf, const float* bias, float* y, Vol low,
-                      int Cin, int Cout, hipStream_t s, int ns, int math) {
+                      int Cin, int Cout, hipStream_t s, int ns, int math, const ActRows* act) {
   const int64_t M = nvox(low);
+  if (act && !act_ok(act, Cin)) return hipErrorInvalidValue;
+  StoreUp C{y, Cout, bias, low.D, low.H, low.W, M, ns, pow2_shift(Cout), pow2_shift(low.W),
+            pow2_shift(low.H)};
+  if (act)
+    return launch_gemm(act_loader(*act, Cin, M), wf, C, M, up_f_kpad(Cin), up_f_npad(Cout, ns),
+                       s, gemm_split(math));
   LoadRowsVec A{x, Cin, Cin, M};
-  StoreUp C{y, Cout, bias, low.D, low.H, low.W, M, ns};
   return launch_gemm(A, wf, C, M, up_f_kpad(Cin), up_f_npad(Cout, ns), s, gemm_split(math));
 }
 
 hipError_t upconv_dgrad(const float* dy, int lddy, const float* wd, float* dx, Vol low, int Cin,
                         int Cout, hipStream_t s, int ns, int math) {
   const int64_t M = nvox(low);
-  LoadUpGather A{dy, lddy, Cout, low.D, low.H, low.W, M, ns};
+  LoadUpGather A{dy, lddy, Cout, low.D, low.H, low.W, M, ns, pow2_shift(Cout),
+                 pow2_shift(low.W), pow2_shift(low.H)};
   StoreRows C{dx, Cin, Cin, nullptr, M};
   return launch_gemm(A, wd, C, M, up_d_kpad(Cout, ns), up_d_npad(Cin), s, gemm_split(math));
 }
@@ -1065,12 +1177,19 @@ size_t upconv_wgrad_ws_bytes(Vol low, int Cin, int Cout, int ns) {
 }
 
 hipError_t upconv_wgrad(const float* x, const float* dy, int lddy, float* dw, float* db, Vol low,
-                        int Cin, int Cout, float* ws, hipStream_t s, int ns, int math) {
+                        int Cin, int Cout, float* ws, hipStream_t s, int ns, int math,
+                        const ActRows* act) {
   // (the streaming k_xty measured 15 % slower here: the up-conv gather needs a
   //  per-voxel index division, and 64 x 64 LDS tiles reuse X and Y better)
   const int64_t M = nvox(low);
+  LoadUpGather Y{dy, lddy, Cout, low.D, low.H, low.W, M, ns, pow2_shift(Cout),
+                 pow2_shift(low.W), pow2_shift(low.H)};
+  if (act) {
+    if (!act_ok(act, Cin)) return hipErrorInvalidValue;
+    return launch_atb(act_loader(*act, Cin, M), Y, M, Cin, ns * Cout, Cout, ns == 8 ? 2 : 0, dw,
+                      db, ws, s, gemm_split(math));
+  }
   LoadRowsVec X{x, Cin, Cin, M};
-  LoadUpGather Y{dy, lddy, Cout, low.D, low.H, low.W, M, ns};
   return launch_atb(X, Y, M, Cin, ns * Cout, Cout, ns == 8 ? 2 : 0, dw, db, ws, s,
                     gemm_split(math));
 }
@@ -1099,9 +1218,14 @@ static inline int head_dk(int K) { return cdiv(K, G_BK) * G_BK; }
 static inline int head_dn(int Cin) { return cdiv(Cin, 32) * 32; }
 
 hipError_t head_fwd(const float* x, const float* wf, const float* b, float* y, int64_t V, int Cin,
-                    int K, hipStream_t s, int math) {
-  LoadRowsVec A{x, Cin, Cin, V};
+                    int K, hipStream_t s, int math, const ActRows* act) {
   StoreRows C{y, K, K, b, V};
+  if (act) {
+    if (!act_ok(act, Cin)) return hipErrorInvalidValue;
+    return launch_gemm(act_loader(*act, Cin, V), wf, C, V, head_fk(Cin), head_fn(K), s,
+                       gemm_split(math));
+  }
+  LoadRowsVec A{x, Cin, Cin, V};
   return launch_gemm(A, wf, C, V, head_fk(Cin), head_fn(K), s, gemm_split(math));
 }
 
@@ -1134,7 +1258,12 @@ hipError_t head_dgrad(const float* dy, const float* wd, float* dx, int64_t V, in
 size_t head_wgrad_ws_bytes(int64_t V, int Cin, int K) { return xty_ws_bytes(V, Cin, K); }
 
 hipError_t head_wgrad(const float* x, const float* dy, float* dw, float* db, int64_t V, int Cin,
-                      int K, float* ws, hipStream_t s) {
+                      int K, float* ws, hipStream_t s, const ActRows* act) {
+  if (act) {
+    if (!act_ok(act, Cin)) return hipErrorInvalidValue;
+    return launch_xty(act->y, Cin, Cin, dy, K, K, nullptr, V, K, 1, dw, db, ws, s, nullptr, 0,
+                      1 << 30, act);
+  }
   return launch_xty(x, Cin, Cin, dy, K, K, nullptr, V, K, 1, dw, db, ws, s);
 }
 

@@ -125,21 +125,36 @@ hipError_t conv3d_wgrad_reduce(const float* part, float* dw, int nsplit, int T, 
                                int npad, int Cin, int Cout, hipStream_t s);
 
 // ---------------------------------------------------------------- gemms --
+// A block output applied as a GEMM reads it (the decoders' and the bottleneck's outputs
+// feed only the up-convs and the head): row v = lrelu(y[v] al[b] + de[b], neg) P[b,d] + Q[b,d]
+// (k_act_apply's formula, bitwise), y [V][C] channel-last, al / de [B][C], PT / QT the
+// gate coefficients transposed to [B][D][C] (null: P = 1, Q = 0).  The row's (b, d) is
+// v / HW = b D + d.
+struct ActRows {
+  const float* y = nullptr;
+  const float* al = nullptr;
+  const float* de = nullptr;
+  const float* PT = nullptr;
+  const float* QT = nullptr;
+  int D = 1, HW = 1;
+  float neg = 0.01f;
+};
 // ConvTranspose3d(Cin->Cout, k=s=(1,2,2) [ns = 4] or 2x2x2 [ns = 8]) + bias,
 // low-res x [Vlow][Cin], high-res y [Vhigh][Cout] (H, W doubled; D too for
 // ns = 8).  Reference weight W[Cin][Cout][1 or 2][2][2].
 hipError_t upconv_pack(const float* w, float* wf, float* wd, int Cin, int Cout, hipStream_t s,
                        int ns = 4);
 // (math = SPFF_MATH_BF16X6: the split-bf16 MFMA GEMM; otherwise the fp32 MFMA one)
+// (act: x = the rows ActRows describes, applied as they load; the x argument is ignored)
 hipError_t upconv_fwd(const float* x, const float* wf, const float* bias, float* y,
                       Vol low, int Cin, int Cout, hipStream_t s, int ns = 4,
-                      int math = SPFF_MATH_F32);
+                      int math = SPFF_MATH_F32, const ActRows* act = nullptr);
 hipError_t upconv_dgrad(const float* dy, int lddy, const float* wd, float* dx, Vol low,
                         int Cin, int Cout, hipStream_t s, int ns = 4, int math = SPFF_MATH_F32);
 size_t upconv_wgrad_ws_bytes(Vol low, int Cin, int Cout, int ns = 4);
 hipError_t upconv_wgrad(const float* x, const float* dy, int lddy, float* dw, float* db,
                         Vol low, int Cin, int Cout, float* ws, hipStream_t s, int ns = 4,
-                        int math = SPFF_MATH_F32);
+                        int math = SPFF_MATH_F32, const ActRows* act = nullptr);
 size_t upconv_pack_floats(int Cin, int Cout, int ns = 4);
 size_t upconv_pack_dgrad_offset(int Cin, int Cout, int ns = 4);
 // 1x1x1 conv head: y[v][K] = x[v][:Cin] . W[K][Cin] + b  (wf/wd from head_pack)
@@ -147,12 +162,13 @@ hipError_t head_pack(const float* w, float* wf, float* wd, int Cin, int K, hipSt
 size_t head_pack_floats(int Cin, int K);
 size_t head_pack_dgrad_offset(int Cin, int K);
 hipError_t head_fwd(const float* x, const float* wf, const float* b, float* y, int64_t V,
-                    int Cin, int K, hipStream_t s, int math = SPFF_MATH_F32);
+                    int Cin, int K, hipStream_t s, int math = SPFF_MATH_F32,
+                    const ActRows* act = nullptr);
 hipError_t head_dgrad(const float* dy, const float* wd, float* dx, int64_t V, int Cin, int K,
                       hipStream_t s, int math = SPFF_MATH_F32);
 size_t head_wgrad_ws_bytes(int64_t V, int Cin, int K);
 hipError_t head_wgrad(const float* x, const float* dy, float* dw, float* db, int64_t V,
-                      int Cin, int K, float* ws, hipStream_t s);
+                      int Cin, int K, float* ws, hipStream_t s, const ActRows* act = nullptr);
 
 // nn.Linear / 1x1x1 Conv3d on channel-last rows (SwinUNETR path): W [N][K] packed by
 // head_pack(w, wf, wd, K, N) (wf = W^T for the forward, wd = W for dgrad).
@@ -302,6 +318,8 @@ struct GateSaved {
   float* s1; float* g1; float* sg2;   // [B][D]
   float* p; float* h; float* e;       // SE: p[B][C], h[B][Hse] (pre-ReLU), e[B][C]
   float* P; float* Q;                 // [B][C][D] apply coefficients
+  float* PT = nullptr;                // optional copies [B][D][C] (GEMM loaders, ActRows)
+  float* QT = nullptr;
   double* spec;                       // sharded plans: s1 spectrum [B][L][2] (global D)
 };
 int se_hidden(int C);

@@ -434,6 +434,11 @@ class Plan:
         return {c: (buf[4 * i], buf[4 * i + 1], int(buf[4 * i + 2]), buf[4 * i + 3])
                 for i, c in enumerate(self.PROF_CLASSES)}
 
+    def debug_set(self, key: int, value: int):
+        """spff_debug_set: key 0 = stop the backward after N decoder blocks, key 1 = store
+        the GEMM-applied block outputs too (saved("dec1.out") etc.)."""
+        check(lib().spff_debug_set(self._h, int(key), int(value)), "spff_debug_set")
+
     def saved(self, name: str) -> torch.Tensor:
         """Copy of a saved intermediate as a channel-last [V, C] tensor (debug/tests):
         fp32, or uint8 for the max-pool argmax bytes "poolN.idx"."""

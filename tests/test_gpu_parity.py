@@ -296,6 +296,10 @@ def test_stagewise_forward(name):
     core = load_core(d)
     core(x.to(DEV)).sum().backward()  # grad-mode forward -> training plan holds the stages
     plan = core._plan
+    # the bottleneck / decoder outputs are applied by their GEMM consumers and not stored:
+    # store them too for this view, and run the forward again
+    plan.debug_set(1, 1)
+    core(x.to(DEV)).sum().backward()
     order = ["enc1.y1", "enc1.a1", "enc1.y2", "enc1.out", "pool1", "enc2.out", "pool2", "enc3.out",
              "pool3", "bott.y1", "bott.out", "up3", "dec3.y1", "dec3.out", "up2", "dec2.out", "up1",
              "dec1.y1", "dec1.out"]
