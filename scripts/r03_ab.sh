@@ -15,6 +15,7 @@ fi
 OUT=gpurun_out/ab_kbench.log
 : > $OUT
 for lib in base "$@"; do
+  [ -n "${KV_SKIP:-}" ] && break
   echo "=== $lib" >> $OUT
   if [ "$lib" = base ]; then
     timeout -k 10 240 python scripts/kbench.py --math bf16x6 --iters 10 --ops ${KV_OPS:-fwd,dgrad,wgrad} >> $OUT 2>&1 || exit $?

@@ -154,6 +154,7 @@ struct spff_plan {
   size_t prof_n = 0;
   bool prof_on = false;
   int dbg_stop = -1;  // debug: stop backward after this many blocks (-1 = off)
+  bool efilm_ready = false;  // this forward's EFiLM coefficients are computed (all blocks)
   bool keep_out = false;  // debug: store the fused block outputs too (saved views)
   // per call
   char* ws = nullptr;
@@ -515,6 +516,7 @@ GateParams gate_params(const spff_plan* p, const Blk& b) {
   g.sw2 = b.post_se ? p->P(b.sw2) : nullptr;
   g.sb2 = b.post_se ? p->P(b.sb2) : nullptr;
   g.specse = b.post_spec ? 1 : 0;
+  g.efilm_ready = p->efilm_ready;
   return g;
 }
 
@@ -973,6 +975,18 @@ int block_grads_ready(spff_plan* p, const Blk& b) {
 int forward(spff_plan* p, const float* x, float* logits) {
   const int f = p->f;
   const spff_cfg& c = p->cfg;
+  {  // every block's EnergyFiLM coefficients in one launch (parameters only)
+    EfilmJobs jobs;
+    for (int i = 0; i < 7; ++i) {
+      const Blk& b = p->blk[i];
+      if (!b.efilm) continue;
+      jobs.j[jobs.n++] = EfilmJob{p->P(b.fw0), p->P(b.fb0), p->P(b.fw2), p->P(b.fb2),
+                                  p->F(b.t), p->F(b.bt), p->F(b.hid), b.C};
+    }
+    p->efilm_ready = false;
+    HIPCK(efilm_fwd_all(p->pe_dev + p->co.d_off, p->co.D_glob, jobs, c.depth, p->st));
+    p->efilm_ready = jobs.n > 0;
+  }
   HIPCK(ncdhw_to_ndhwc(x, p->F(p->x_cl), p->vol[0], c.in_ch, p->ldx, p->st));
   Blk* B = p->blk;
   CK(fwd_block(p, B[0], src1(p->F(p->x_cl), p->ldx), 0));

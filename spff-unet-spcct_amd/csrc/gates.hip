@@ -17,6 +17,8 @@
 #include "spff_internal.h"
 #include <math.h>
 
+#include <algorithm>
+
 namespace spff {
 
 static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
@@ -73,11 +75,15 @@ __device__ void rowsum(int NI, int NJ, Fn f, double* part, double scale, double*
 
 // ------------------------------------------------------------- EFiLM fwd --
 // hid[j][d] = fw0[j] . pe[:,d] + fb0[j]; gb[o][d] = fw2[o] . relu(hid[:,d]) + fb2[o]
-__global__ void k_efilm_fwd(const float* __restrict__ pe, const float* __restrict__ fw0,
-                            const float* __restrict__ fb0, const float* __restrict__ fw2,
-                            const float* __restrict__ fb2, float* __restrict__ t,
-                            float* __restrict__ bt, float* __restrict__ hid, int C, int D,
-                            int pitch) {
+// one workgroup = 32 of the 2C FiLM outputs of one block (the hidden layer recomputed per
+// workgroup: 32 x 16 x D MACs)
+__device__ __forceinline__ void efilm_fwd_body(const float* __restrict__ pe,
+                                               const float* __restrict__ fw0,
+                                               const float* __restrict__ fb0,
+                                               const float* __restrict__ fw2,
+                                               const float* __restrict__ fb2, float* __restrict__ t,
+                                               float* __restrict__ bt, float* __restrict__ hid,
+                                               int C, int D, int pitch, int wg) {
   extern __shared__ float hs[];  // [32][D] hidden, then pe [16][D] and fw0 [32][16] staged
   float* pes = hs + 32 * D;
   float* w0s = pes + 16 * D;
@@ -90,10 +96,10 @@ __global__ void k_efilm_fwd(const float* __restrict__ pe, const float* __restric
     for (int q = 0; q < 16; ++q) s += w0s[j * 16 + q] * pes[q * D + d];
     s += fb0[j];
     hs[i] = s;
-    if (blockIdx.x == 0) hid[i] = s;
+    if (wg == 0) hid[i] = s;
   }
   __syncthreads();
-  const int o0 = blockIdx.x * 32;
+  const int o0 = wg * 32;
   for (int i = threadIdx.x; i < 32 * D; i += blockDim.x) {
     const int o = o0 + i / D, d = i % D;
     if (o >= 2 * C) continue;
@@ -103,6 +109,36 @@ __global__ void k_efilm_fwd(const float* __restrict__ pe, const float* __restric
     if (o < C) t[o * D + d] = tanhf(s);
     else bt[(o - C) * D + d] = s;
   }
+}
+__global__ void k_efilm_fwd(const float* __restrict__ pe, const float* __restrict__ fw0,
+                            const float* __restrict__ fb0, const float* __restrict__ fw2,
+                            const float* __restrict__ fb2, float* __restrict__ t,
+                            float* __restrict__ bt, float* __restrict__ hid, int C, int D,
+                            int pitch) {
+  efilm_fwd_body(pe, fw0, fb0, fw2, fb2, t, bt, hid, C, D, pitch, blockIdx.x);
+}
+// all blocks' coefficients in one launch: grid.y = job (block), grid.x = 32-output groups
+__global__ void k_efilm_fwd_all(const float* __restrict__ pe, EfilmJobs jobs, int D, int pitch) {
+  const EfilmJob& J = jobs.j[blockIdx.y];
+  if ((int)blockIdx.x * 32 >= 2 * J.C) return;  // (uniform: the whole workgroup)
+  efilm_fwd_body(pe, J.fw0, J.fb0, J.fw2, J.fb2, J.t, J.bt, J.hid, J.C, D, pitch, blockIdx.x);
+}
+
+hipError_t efilm_fwd_all(const float* pe, int pe_pitch, const EfilmJobs& jobs, int D,
+                         hipStream_t s) {
+  if (jobs.n <= 0) return hipSuccess;
+  if (jobs.n > 8) return hipErrorInvalidValue;
+  const size_t shm = (48 * (size_t)D + 512) * sizeof(float);
+  if (shm > 64 * 1024) {
+    if (shm > GATE_LDS_MAX) return hipErrorInvalidValue;
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_efilm_fwd_all),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+    if (e != hipSuccess) return e;
+  }
+  int gx = 1;
+  for (int i = 0; i < jobs.n; ++i) gx = std::max(gx, cdiv(2 * jobs.j[i].C, 32));
+  hipLaunchKernelGGL(k_efilm_fwd_all, dim3(gx, jobs.n), dim3(256), shm, s, pe, jobs, D, pe_pitch);
+  return hipGetLastError();
 }
 
 static hipError_t efilm_fwd(const GateParams& gp, const GateSaved& sv, int C, int D,
@@ -243,7 +279,7 @@ hipError_t gates_fwd(const GateParams& gp, const float* Sa, GateSaved& sv, Vol v
   (void)scratch;
   const int D = vol.D, Hse = se_hidden(C);
   const int efilm = gp.fw0 != nullptr;
-  if (efilm) {
+  if (efilm && !gp.efilm_ready) {
     hipError_t e = efilm_fwd(gp, sv, C, D, s);
     if (e != hipSuccess) return e;
   }
@@ -795,7 +831,7 @@ hipError_t gates_fwd_sh(const GateParams& gp, const float* Sa, GateSaved& sv, Vo
   const int efilm = gp.fw0 != nullptr;
   if (C > 1024 || Hse > 64) return hipErrorInvalidValue;
   hipError_t e;
-  if (efilm) {
+  if (efilm && !gp.efilm_ready) {
     if ((e = efilm_fwd(gp, sv, C, D, s)) != hipSuccess) return e;
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }

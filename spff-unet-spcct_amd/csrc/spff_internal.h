@@ -312,6 +312,7 @@ struct GateParams {
   // SE (models.py:600-609)
   const float* sw0; const float* sb0; const float* sw2; const float* sb2;   // null if off
   int specse;
+  bool efilm_ready = false;  // t, bt, hid already computed (efilm_fwd_all at the forward start)
 };
 struct GateSaved {
   float* t; float* bt; float* hid;    // EFiLM: t=tanh(gamma)[C][D], beta[C][D], hid_pre[32][D]
@@ -323,6 +324,18 @@ struct GateSaved {
   double* spec;                       // sharded plans: s1 spectrum [B][L][2] (global D)
 };
 int se_hidden(int C);
+// EnergyFiLM coefficients of several blocks in one launch (they depend on the parameters
+// only): t = tanh(gamma), bt = beta [C][D] and the hidden pre-activations hid [32][D]
+struct EfilmJob {
+  const float* fw0; const float* fb0; const float* fw2; const float* fb2;
+  float* t; float* bt; float* hid; int C;
+};
+struct EfilmJobs {
+  EfilmJob j[8];
+  int n = 0;
+};
+hipError_t efilm_fwd_all(const float* pe, int pe_pitch, const EfilmJobs& jobs, int D,
+                         hipStream_t s);
 // forward gate algebra from Sa[b,c,d] = sum_hw lrelu(IN(y2))
 hipError_t gates_fwd(const GateParams& gp, const float* Sa, GateSaved& sv, Vol vol, int C,
                      float* scratch, hipStream_t s);
