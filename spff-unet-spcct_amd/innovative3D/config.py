@@ -15,7 +15,8 @@ engine implements.  Differences, all deliberate:
   the SPFF hot path (SURVEY §8);
 * the DICOM data module (``MultiDicomDataModule3D``) is the device-resident
   one of innovative3D/datasets.py (resize, ROI rasterisation and TrainGridAug as
-  HIP kernels); decoding DICOM itself needs pydicom, absent offline.
+  HIP kernels); DICOM files are decoded by pydicom when installed, else by the native
+  reader of innovative3D/dicom.py (uncompressed transfer syntaxes).
 """
 from __future__ import annotations
 

@@ -17,8 +17,8 @@ difference: the reference augments in 16 worker processes, each re-seeding
 ``random`` per worker, so its per-sample decisions are reproducible only with
 num_workers=0; that single-process order is the one kept here.
 
-DICOM decoding needs ``pydicom`` (absent offline): ``read_dicom_frames`` raises
-with a pointer to passing pre-decoded frames instead.
+DICOM decoding: ``read_dicom_frames`` uses pydicom when it is installed and otherwise the
+native reader of innovative3D/dicom.py (uncompressed transfer syntaxes).
 """
 from __future__ import annotations
 

@@ -218,12 +218,14 @@ def generate_cumulative_grid_sizes(num_images, num_grid_sizes=10, cumulative_per
 
 
 def read_dicom_frames(path):
-    """Decoded frames [n, h, w] of one DICOM file (pydicom, as helpers.py:190-191)."""
+    """Decoded frames [n, h, w] of one DICOM file: ``pydicom.dcmread(path).pixel_array`` as
+    helpers.py:190-191 when pydicom is installed, else the native reader (innovative3D/dicom.py:
+    uncompressed transfer syntaxes; a compressed one raises NotImplementedError)."""
     try:
-        import pydicom  # noqa: F401
-    except ImportError as e:  # pragma: no cover - pydicom is absent offline
-        raise ImportError("reading DICOM needs pydicom; pass frames_reader=callable(path) -> "
-                          "array [n, h, w] to create_image_and_labels_for_dataset instead") from e
+        import pydicom
+    except ImportError:
+        from .dicom import pixel_array
+        return pixel_array(path)
     return pydicom.dcmread(path).pixel_array
 
 
