@@ -40,12 +40,14 @@ BF16_MFMA_PEAK_TFLOPS = 256 * 4 * 1024 * 2.4e9 / 1e12
 # fp32-equivalent peak of each conv arithmetic: bf16x6 runs 6 bf16 MFMA products per
 # fp32 multiply-add, bf16x3 runs 3
 MATH_PEAK = {"f32": FP32_MFMA_PEAK_TFLOPS, "bf16x6": BF16_MFMA_PEAK_TFLOPS / 6,
-             "bf16x3": BF16_MFMA_PEAK_TFLOPS / 3}
+             "bf16x3": BF16_MFMA_PEAK_TFLOPS / 3, "f16x3": BF16_MFMA_PEAK_TFLOPS / 3}
 MATH_KERNEL = {"f32": "k_conv3d_fwd (fp32 MFMA 3x3x3 implicit GEMM, fwd+dgrad)",
                "bf16x6": "k_conv3d_fwd_x<.,.,3> (3-plane split-bf16 MFMA 3x3x3 implicit GEMM, "
                          "fwd+dgrad)",
                "bf16x3": "k_conv3d_fwd_x<.,.,2> (2-plane split-bf16 MFMA 3x3x3 implicit GEMM, "
-                         "fwd+dgrad)"}
+                         "fwd+dgrad)",
+               "f16x3": "k_conv3d_fwd_x<.,.,12> (2-plane scaled-fp16 MFMA 3x3x3 implicit GEMM, "
+                        "fwd+dgrad)"}
 HBM_PEAK_GBS = 8000.0
 
 
@@ -532,7 +534,7 @@ def main():
     ap.add_argument("--classes", type=int, default=13)
     ap.add_argument("--base", type=int, default=32)
     ap.add_argument("--cpu-baseline", choices=("auto", "skip"), default="auto")
-    ap.add_argument("--math", choices=("f32", "bf16x6", "bf16x3"), default="bf16x6",
+    ap.add_argument("--math", choices=("f32", "bf16x6", "bf16x3", "f16x3"), default="bf16x6",
                     help="conv arithmetic: bf16x6 = fp32 operands split exactly into 3 bf16 "
                          "planes, 6 products, fp32 accumulate (fp32 accuracy class; default)")
     ap.add_argument("--workload", choices=("patch128", "volume512", "registry", "unet3d", "swin"),

@@ -42,10 +42,15 @@ extern "C" {
  *   SPFF_MATH_BF16X6  fp32 operands split exactly into 3 bf16 planes, 6 cross
  *                     products on the bf16 MFMA, fp32 accumulate: dropped terms
  *                     < 2^-24 |xy| per product (fp32 accuracy class), ~2.7x the rate
- *   SPFF_MATH_BF16X3  2 planes, 3 products: ~2^-17 relative per product (opt-in) */
+ *   SPFF_MATH_BF16X3  2 planes, 3 products: ~2^-17 relative per product (opt-in)
+ *   SPFF_MATH_F16X3   each operand scaled by a power of two (max |x| 2^e < 2^14, from an
+ *                     on-device absmax) and split into 2 fp16 planes, 3 products on the
+ *                     fp16 MFMA: <= 2^-22 |x| per operand, dropped l*l <= 2^-22 |xy|,
+ *                     at the bf16x3 rate (the 1x1x1 / ConvTranspose GEMMs keep bf16x6) */
 #define SPFF_MATH_F32 0
 #define SPFF_MATH_BF16X6 1
 #define SPFF_MATH_BF16X3 2
+#define SPFF_MATH_F16X3 3
 
 typedef struct spff_cfg {
   int batch, in_ch, depth, height, width;  /* input [B][Cin][D][H][W] */

@@ -505,9 +505,10 @@ hipError_t conv3d_wgrad_reduce(const float* part, float* dw, int nsplit, int T, 
 }
 
 hipError_t conv3d_wgrad(const Src2& x, const float* dy, int lddy, float* dw, Vol vol, int KD,
-                        int Cin, int Cout, int math, float* ws, hipStream_t s) {
+                        int Cin, int Cout, int math, float* ws, hipStream_t s,
+                        const unsigned* xmax, const unsigned* ymax) {
   if (math != SPFF_MATH_F32 && debug_split_wgrad())
-    return conv3d_wgrad_x(x, dy, lddy, dw, vol, KD, Cin, Cout, math, ws, s);
+    return conv3d_wgrad_x(x, dy, lddy, dw, vol, KD, Cin, Cout, math, ws, s, xmax, ymax);
   if (lddy % 4) return hipErrorInvalidValue;
   WgradPlan p = wgrad_plan(vol, Cin, Cout);
   dim3 grid(p.nsplit, p.kpad / p.ci, p.npad / WG_CO);

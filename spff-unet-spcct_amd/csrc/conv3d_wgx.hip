@@ -61,7 +61,7 @@ __device__ __forceinline__ unsigned short bfbits(__bf16 v) {
   return __builtin_bit_cast(unsigned short, v);
 }
 template <int NS>
-__device__ __forceinline__ void split4(const float4& v, uint2 (&o)[NS]) {
+__device__ __forceinline__ void split4(const float4& v, uint2 (&o)[nplanes(NS)]) {
   split4_pk<NS>(v, o);  // bf16split.h
 }
 
@@ -304,7 +304,8 @@ __global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x(
 template <int KD, int CI, int NS, int NJMAX, bool HR, int CO>
 __global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x16(
     Src2 x, const float* __restrict__ dy, int lddy, float* __restrict__ part, Vol vol, int Cin,
-    int kpad, int Cout, int npad, int tilesH, int tilesW, int ntiles, int tps, int nblk) {
+    int kpad, int Cout, int npad, int tilesH, int tilesW, int ntiles, int tps, int nblk,
+    const unsigned* __restrict__ xmx, const unsigned* __restrict__ ymx) {
   constexpr int HD = KD, HH = WX_TH + 2, HWD = WX_TW + 2;
   constexpr int NPOS = HD * HH * HWD;
   constexpr int T = KD * 9;
@@ -313,8 +314,15 @@ __global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x16(
   constexpr int NP = (PPOS * CQ + 255) / 256;              // plane float4 per thread
   constexpr int NY = WX_TV * (CO / 4) / 256;            // dy float4 per thread (= 4)
   constexpr int NCB = CO / 16;                          // 16-wide col blocks (2)
-  __shared__ __attribute__((aligned(16))) unsigned short Xs[NS * NPOS * CI];
-  __shared__ __attribute__((aligned(16))) unsigned short Ys[NS * WX_TV * CO];
+  // operand planes; HF: two fp16 planes of the scaled operands (NS_F16, bf16split.h)
+  constexpr int NPL = nplanes(NS);
+  constexpr bool HF = NS == NS_F16;
+  __shared__ __attribute__((aligned(16))) unsigned short Xs[NPL * NPOS * CI];
+  __shared__ __attribute__((aligned(16))) unsigned short Ys[NPL * WX_TV * CO];
+  // HF: x scaled by 2^ex (*xmx: max |x|), dy by 2^ey (*ymx: max |dy|)
+  const int ex = HF ? f16_scale_exp(*xmx) : 0;
+  const int ey = HF ? f16_scale_exp(*ymx) : 0;
+  const float sx = exp2i(ex), sy = exp2i(ey);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, q = (lane & 15) >> 2, pq = lane & 3;
@@ -416,10 +424,12 @@ __global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x16(
     for (int k = 0; k < NP; ++k) {
       const int i = tid + 256 * k;
       if (i < PPOS * CQ) {
-        uint2 o[NS];
-        split4<NS>(r[k], o);
+        uint2 o[NPL];
+        float4 v = r[k];
+        if constexpr (HF) v = make_float4(v.x * sx, v.y * sx, v.z * sx, v.w * sx);
+        split4<NS>(v, o);
 #pragma unroll
-        for (int p = 0; p < NS; ++p)
+        for (int p = 0; p < NPL; ++p)
           *reinterpret_cast<uint2*>(dst + p * NPOS * CI + 4 * i) = o[p];
       }
     }
@@ -455,13 +465,13 @@ __global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x16(
     for (int k = 0; k < NY; ++k) {
       const int i = tid + 256 * k;
       const int c4 = i % (CO / 4), kv = i / (CO / 4);
-      uint2 o[NS];
-      const float4 yv = negate ? make_float4(-yreg[k].x, -yreg[k].y, -yreg[k].z, -yreg[k].w)
-                               : yreg[k];
+      uint2 o[NPL];
+      const float ys = HF ? (negate ? -sy : sy) : (negate ? -1.f : 1.f);
+      const float4 yv = make_float4(yreg[k].x * ys, yreg[k].y * ys, yreg[k].z * ys, yreg[k].w * ys);
       split4<NS>(yv, o);
       const int off = kv * CO + (((c4 >> 1) ^ (CO == 32 ? ((kv >> 2) & 1) << 1 : 0)) << 3) + 4 * (c4 & 1);
 #pragma unroll
-      for (int p = 0; p < NS; ++p)
+      for (int p = 0; p < NPL; ++p)
         *reinterpret_cast<uint2*>(Ys + p * WX_TV * CO + off) = o[p];
     }
   };
@@ -478,35 +488,35 @@ __global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x16(
       ab[j] = aoff[j] + (aoff[j] >= (KD - rot) * PL ? (rot - KD) * PL : rot * PL);
 #pragma unroll SPFF_WXUNROLL
     for (int ks = 0; ks < WX_TH / 2; ++ks) {
-      bf16x8 bq[NCB][NS];
+      bf16x8 bq[NCB][NPL];
 #pragma unroll
       for (int cb = 0; cb < NCB; ++cb)
 #pragma unroll
-        for (int p = 0; p < NS; ++p) {
+        for (int p = 0; p < NPL; ++p) {
           const unsigned short* yb = Ys + p * WX_TV * CO + 2 * ks * WX_TW * CO + boff[cb];
           bq[cb][p] = frag(tr_read(yb), tr_read(yb + 8 * CO));
         }
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
-        bf16x8 aq[NS];
+        bf16x8 aq[NPL];
 #pragma unroll
-        for (int p = 0; p < NS; ++p) {
+        for (int p = 0; p < NPL; ++p) {
           const unsigned short* xb = Xs + p * NPOS * CI + 2 * ks * HWD * CI + ab[j];
           aq[p] = frag(tr_read(xb), tr_read(xb + 8 * CI));
         }
 #pragma unroll
         for (int cb = 0; cb < NCB; ++cb) {
           f32x4 c = acc[j][cb];
-          if constexpr (NS == 3) {
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq[1], bq[cb][1], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq[0], bq[cb][2], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq[2], bq[cb][0], c, 0, 0, 0);
+          if constexpr (NPL == 3) {
+            c = mfma16x32<HF>(aq[1], bq[cb][1], c);
+            c = mfma16x32<HF>(aq[0], bq[cb][2], c);
+            c = mfma16x32<HF>(aq[2], bq[cb][0], c);
           }
-          if constexpr (NS >= 2) {
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq[0], bq[cb][1], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq[1], bq[cb][0], c, 0, 0, 0);
+          if constexpr (NPL >= 2) {
+            c = mfma16x32<HF>(aq[0], bq[cb][1], c);
+            c = mfma16x32<HF>(aq[1], bq[cb][0], c);
           }
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq[0], bq[cb][0], c, 0, 0, 0);
+          c = mfma16x32<HF>(aq[0], bq[cb][0], c);
           acc[j][cb] = c;
         }
       }
@@ -565,7 +575,7 @@ __global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x16(
 #pragma unroll
       for (int cb = 0; cb < NCB; ++cb)
         part[(((int64_t)split * T + t) * kpad + ci) * npad + co0 + 16 * cb + (lane & 15)] =
-            acc[j][cb][r];
+            HF ? ldexpf(acc[j][cb][r], -(ex + ey)) : acc[j][cb][r];
     }
   }
 }
@@ -639,13 +649,18 @@ WxPlan wx_plan(Vol vol, int Cin, int Cout) {
 }
 }  // namespace
 
-size_t conv3d_wgrad_x_ws_bytes(Vol vol, int KD, int Cin, int Cout) {
+// partial slabs, then (SPFF_MATH_F16X3) the two operand-scale slots [max |x|, max |dy|]
+static size_t wx_main_bytes(Vol vol, int KD, int Cin, int Cout) {
   WxPlan p = wx_plan(vol, Cin, Cout);
-  return (size_t)p.nsplit * KD * 9 * p.kpad * p.npad * sizeof(float);
+  return ((size_t)p.nsplit * KD * 9 * p.kpad * p.npad * sizeof(float) + 255) & ~(size_t)255;
+}
+size_t conv3d_wgrad_x_ws_bytes(Vol vol, int KD, int Cin, int Cout) {
+  return wx_main_bytes(vol, KD, Cin, Cout) + 256;
 }
 
 hipError_t conv3d_wgrad_x(const Src2& x, const float* dy, int lddy, float* dw, Vol vol, int KD,
-                          int Cin, int Cout, int math, float* ws, hipStream_t s) {
+                          int Cin, int Cout, int math, float* ws, hipStream_t s,
+                          const unsigned* xmax, const unsigned* ymax) {
   if (lddy % 4) return hipErrorInvalidValue;
   WxPlan p = wx_plan(vol, Cin, Cout);
   const WxTable tb = make_table(KD, p.ci);
@@ -655,6 +670,26 @@ hipError_t conv3d_wgrad_x(const Src2& x, const float* dy, int lddy, float* dw, V
                      lddy, ws, vol, Cin, p.kpad, Cout, p.npad, p.tilesH, p.tilesW, p.ntiles,   \
                      p.tps, tb)
   const bool x3 = math == SPFF_MATH_BF16X3;
+  const bool hf = math == SPFF_MATH_F16X3;
+  unsigned* sl = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(ws) +
+                                             wx_main_bytes(vol, KD, Cin, Cout));
+  if (hf) {  // operand maxima: the caller's precomputed slots, else computed here
+    if (!SPFF_WX16) return hipErrorInvalidValue;
+    if (!xmax || !ymax) {
+      hipError_t e = hipMemsetAsync(sl, 0, 2 * sizeof(unsigned), s);
+      if (e != hipSuccess) return e;
+    }
+    if (!xmax) {
+      hipError_t e = absmax_src(x, vol, Cin, true, sl, s);
+      if (e != hipSuccess) return e;
+      xmax = sl;
+    }
+    if (!ymax) {
+      hipError_t e = absmax_src(src1(dy, lddy), vol, Cout, false, sl + 1, s);
+      if (e != hipSuccess) return e;
+      ymax = sl + 1;
+    }
+  }
   if (SPFF_WX16) {
     // 16-row blocks: nblk = ceil(T CI / 16); NJMAX = ceil(nblk / 4):
     // KD3/CI16 27 -> 7, KD3/CI8 14 -> 4, KD1/CI16 9 -> 3, KD1/CI8 5 -> 2
@@ -662,7 +697,7 @@ hipError_t conv3d_wgrad_x(const Src2& x, const float* dy, int lddy, float* dw, V
 #define SPFF_WX16C(KD_, CI_, NS_, NJ_, HR_, CO_)                                                \
   hipLaunchKernelGGL((k_conv3d_wgrad_x16<KD_, CI_, NS_, NJ_, HR_, CO_>), grid, dim3(256), 0, s, \
                      x, dy, lddy, ws, vol, Cin, p.kpad, Cout, p.npad, p.tilesH, p.tilesW,      \
-                     p.ntiles, p.tps, nblk)
+                     p.ntiles, p.tps, nblk, xmax, ymax)
 #define SPFF_WX16(KD_, CI_, NS_, NJ_)                                                          \
   do {                                                                                         \
     if (p.co == 16) {                                                                          \
@@ -674,11 +709,25 @@ hipError_t conv3d_wgrad_x(const Src2& x, const float* dy, int lddy, float* dw, V
     }                                                                                          \
   } while (0)
     if (KD == 3) {
-      if (p.ci == 16) { if (x3) SPFF_WX16(3, 16, 2, 7); else SPFF_WX16(3, 16, 3, 7); }
-      else            { if (x3) SPFF_WX16(3, 8, 2, 4);  else SPFF_WX16(3, 8, 3, 4); }
+      if (p.ci == 16) {
+        if (hf) SPFF_WX16(3, 16, NS_F16, 7);
+        else if (x3) SPFF_WX16(3, 16, 2, 7);
+        else SPFF_WX16(3, 16, 3, 7);
+      } else {
+        if (hf) SPFF_WX16(3, 8, NS_F16, 4);
+        else if (x3) SPFF_WX16(3, 8, 2, 4);
+        else SPFF_WX16(3, 8, 3, 4);
+      }
     } else {
-      if (p.ci == 16) { if (x3) SPFF_WX16(1, 16, 2, 3); else SPFF_WX16(1, 16, 3, 3); }
-      else            { if (x3) SPFF_WX16(1, 8, 2, 2);  else SPFF_WX16(1, 8, 3, 2); }
+      if (p.ci == 16) {
+        if (hf) SPFF_WX16(1, 16, NS_F16, 3);
+        else if (x3) SPFF_WX16(1, 16, 2, 3);
+        else SPFF_WX16(1, 16, 3, 3);
+      } else {
+        if (hf) SPFF_WX16(1, 8, NS_F16, 2);
+        else if (x3) SPFF_WX16(1, 8, 2, 2);
+        else SPFF_WX16(1, 8, 3, 2);
+      }
     }
 #undef SPFF_WX16
 #undef SPFF_WX16C

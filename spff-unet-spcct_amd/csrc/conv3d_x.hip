@@ -119,8 +119,12 @@ __device__ __forceinline__ void split_bf16(float x, unsigned short (&o)[NS]) {
 // Odd chunks kc are stored NEGATED (sign-alternating accumulation, see below).
 template <int NS>
 __global__ void k_conv_pack_x(const float* __restrict__ w, uint4* __restrict__ wp, int Cout,
-                              int Cin, int T, int T2, int nkc, int npad, int BN, int dgrad) {
+                              int Cin, int T, int T2, int nkc, int npad, int BN, int dgrad,
+                              const unsigned* __restrict__ wmx) {
+  constexpr int NP = nplanes(NS);
   const int64_t total = (int64_t)(npad / BN) * nkc * T2 * BN;
+  // NS_F16: the weights scaled by 2^e (*wmx: max |w|), fp16 planes
+  const float sw = NS == NS_F16 ? exp2i(f16_scale_exp(*wmx)) : 1.f;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int co = (int)(i % BN);
@@ -128,7 +132,7 @@ __global__ void k_conv_pack_x(const float* __restrict__ w, uint4* __restrict__ w
     const int kc = (int)((i / ((int64_t)BN * T2)) % nkc);
     const int nb = (int)(i / ((int64_t)BN * T2 * nkc));
     const int n = nb * BN + co;
-    unsigned short s[8][NS];
+    unsigned short s[8][NP];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const int k = kc * 8 + e;
@@ -140,11 +144,19 @@ __global__ void k_conv_pack_x(const float* __restrict__ w, uint4* __restrict__ w
           if (k < Cout && n < Cin) v = w[((int64_t)k * Cin + n) * T + (T - 1 - tap)];
         }
       }
-      split_bf16<NS>((kc & 1) ? -v : v, s[e]);
+      v = (kc & 1) ? -v : v;
+      if constexpr (NS == NS_F16) {
+        unsigned pl[2];
+        split_pair_f16(v * sw, 0.f, pl);
+        s[e][0] = (unsigned short)pl[0];
+        s[e][1] = (unsigned short)pl[1];
+      } else {
+        split_bf16<NS>(v, s[e]);
+      }
     }
-    const int64_t base = (((int64_t)nb * nkc + kc) * NS) * T2 * BN + (int64_t)tap * BN + co;
+    const int64_t base = (((int64_t)nb * nkc + kc) * NP) * T2 * BN + (int64_t)tap * BN + co;
 #pragma unroll
-    for (int p = 0; p < NS; ++p) {
+    for (int p = 0; p < NP; ++p) {
       uint4 u;
       u.x = (unsigned)s[0][p] | ((unsigned)s[1][p] << 16);
       u.y = (unsigned)s[2][p] | ((unsigned)s[3][p] << 16);
@@ -172,7 +184,7 @@ template <int BN, int KD, int NS, int TD, int TH>
 constexpr size_t xt_lds_bytes() {
   // operand images; the epilogue reuses the space for the output tile [TD TH 16][BN + 4]
   // fp32 plus the fused statistics' [8 waves][BN] partials
-  const size_t ops = (size_t)NS * (xt_npos<KD, TD, TH>() + xt_t2<KD>() * BN) * 16;
+  const size_t ops = (size_t)nplanes(NS) * (xt_npos<KD, TD, TH>() + xt_t2<KD>() * BN) * 16;
   const size_t out = SPFF_XSTORE ? (size_t)TD * TH * 16 * (BN + 4) * 4 + 8 * BN * 4 : 0;
   return ops > out ? ops : out;
 }
@@ -238,8 +250,12 @@ template <int BN, int KD, int NS, int MB, int NW, bool X16, int TD, bool HR>
 __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
     Src2 x, const uint4* __restrict__ wp, Dst2 y, Vol vol, int Cin, int nkc, int Cout, int npad,
     int tilesD, int tilesH, int tilesW, float* __restrict__ part, int kps,
-    float* __restrict__ stats, int ntiles, int td0, int tds, int th0, int ths) {
+    float* __restrict__ stats, int ntiles, int td0, int tds, int th0, int ths,
+    const unsigned* __restrict__ wmx, const unsigned* __restrict__ xmx) {
   constexpr int XT_THREADS = NW * 64;
+  // planes per operand; HF: two fp16 planes of the scaled operands (NS_F16, bf16split.h)
+  constexpr int NP = nplanes(NS);
+  constexpr bool HF = NS == NS_F16;
   constexpr int TH = X16 ? 2 * NW * MB / TD : NW * MB, TW = XT_W;
   static_assert(X16 || TD == 2, "32x32x16 schedule: 2-deep tiles");
   constexpr int HH = TH + 2, HWD = TW + 2;
@@ -254,14 +270,18 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
   using AccT = typename std::conditional<X16, f32x4, f32x16>::type;
   constexpr int NHX = NPOS * 2;  // halo float4 per chunk (8 channels = 2 float4)
   constexpr int RH = (NHX + XT_THREADS - 1) / XT_THREADS;
-  constexpr int NWU = NS * T2 * BN;  // pre-split weight units (16 B) per chunk
+  constexpr int NWU = NP * T2 * BN;  // pre-split weight units (16 B) per chunk
   static_assert(NWU % 64 == 0, "weight image must be whole 1 KiB DMA pieces");
   static_assert(!X16 || TD * TH == NW * RB, "X16: one W-row per 16-row block");
   constexpr int SPJ = (RH + (NJ - NJ / 2) - 1) / (NJ - NJ / 2);  // halo float4 split per k-step
   constexpr int NPC = NWU / 64;
   extern __shared__ uint4 lds4[];
-  uint4* Xs = lds4;               // [NS][NPOS]
-  uint4* Ws = lds4 + NS * NPOS;   // [NS][T2][BN]
+  uint4* Xs = lds4;               // [NP][NPOS]
+  uint4* Ws = lds4 + NP * NPOS;   // [NP][T2][BN]
+  // HF: x is scaled by 2^ex (*xmx: max |x|), the packed weights by 2^ew (*wmx: max |w|)
+  const int ex = HF ? f16_scale_exp(*xmx) : 0;
+  const int ew = HF ? f16_scale_exp(*wmx) : 0;
+  const float sx = exp2i(ex);
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -334,7 +354,7 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
   // MFMAs, split into bf16 planes half-way through it (VALU beside the MFMAs),
   // stored to LDS right after the chunk boundary
   float4 hreg[RH];
-  uint2 hs[RH][NS];
+  uint2 hs[RH][NP];
   unsigned hvalid = 0;  // bit k: hreg[k] is in bounds (else it is zeroed at the split)
   int fkc = 0;          // chunk of the registers in flight
   auto fetch = [&](int kc) {
@@ -396,10 +416,11 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
       }
       v = make_float4(r[0], r[1], r[2], r[3]);
     }
-    if constexpr (BN <= 32) {
+    if constexpr (BN <= 32 || HF) {
       // packed pair split (bf16split.h): -0.5 to -3 % on the 16/32-wide launches; the
       // 64-wide kernel (255 VGPRs) measured +1 to +3 % with it and keeps the per-value form
       if (!ok) v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if constexpr (HF) v = make_float4(v.x * sx, v.y * sx, v.z * sx, v.w * sx);
       split4_pk<NS>(v, hs[k]);
     } else {
       unsigned short s0[NS], s1[NS], s2[NS], s3[NS];
@@ -421,7 +442,7 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
       const int i = tid + XT_THREADS * k;
       if (i < NHX) {
 #pragma unroll
-        for (int p = 0; p < NS; ++p)
+        for (int p = 0; p < NP; ++p)
           reinterpret_cast<uint2*>(Xs + p * NPOS + (i >> 1))[i & 1] = hs[k][p];
       }
     }
@@ -485,17 +506,17 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
         // row blocks in groups of RBH (the 4 x 16 x 16 tiles' 8 row blocks: two groups,
         // so only half of the A fragments are live at a time)
         constexpr int RBH = RB > 4 ? 4 : RB;
-        bf16x8 bm[CB][NS];
+        bf16x8 bm[CB][NP];
 #pragma unroll
-        for (int p = 0; p < NS; ++p)
+        for (int p = 0; p < NP; ++p)
 #pragma unroll
           for (int cb = 0; cb < CB; ++cb)
             bm[cb][p] = __builtin_bit_cast(bf16x8, Ws[(p * T2 + wtap) * BN + cb * 16 + l16]);
 #pragma unroll
         for (int rg = 0; rg < RB; rg += RBH) {
-        bf16x8 a[RBH][NS];
+        bf16x8 a[RBH][NP];
 #pragma unroll
-        for (int p = 0; p < NS; ++p)
+        for (int p = 0; p < NP; ++p)
 #pragma unroll
           for (int rh = 0; rh < RBH; ++rh)
             a[rh][p] = __builtin_bit_cast(bf16x8, Xs[p * NPOS + hpos[rg + rh] + toff]);
@@ -505,16 +526,16 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
           for (int cb = 0; cb < CB; ++cb) {
             const int rb = rg + rh;
             f32x4 c = acc[rb][cb];
-            if constexpr (NS == 3) {
-              c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rh][1], bm[cb][1], c, 0, 0, 0);
-              c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rh][0], bm[cb][2], c, 0, 0, 0);
-              c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rh][2], bm[cb][0], c, 0, 0, 0);
+            if constexpr (NP == 3) {
+              c = mfma16x32<HF>(a[rh][1], bm[cb][1], c);
+              c = mfma16x32<HF>(a[rh][0], bm[cb][2], c);
+              c = mfma16x32<HF>(a[rh][2], bm[cb][0], c);
             }
-            if constexpr (NS >= 2) {
-              c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rh][0], bm[cb][1], c, 0, 0, 0);
-              c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rh][1], bm[cb][0], c, 0, 0, 0);
+            if constexpr (NP >= 2) {
+              c = mfma16x32<HF>(a[rh][0], bm[cb][1], c);
+              c = mfma16x32<HF>(a[rh][1], bm[cb][0], c);
             }
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rh][0], bm[cb][0], c, 0, 0, 0);
+            c = mfma16x32<HF>(a[rh][0], bm[cb][0], c);
             acc[rb][cb] = c;
           }
         }
@@ -524,9 +545,9 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
         const int tp0 = 2 * j, tp1 = (2 * j + 1 < T) ? 2 * j + 1 : T - 1;
         const int toff = khalf ? toff_of(tp1) : toff_of(tp0);
         const int wtap = 2 * j + khalf;
-        bf16x8 a[RB][NS], bm[CB][NS];
+        bf16x8 a[RB][NP], bm[CB][NP];
 #pragma unroll
-        for (int p = 0; p < NS; ++p) {
+        for (int p = 0; p < NP; ++p) {
 #pragma unroll
           for (int rb = 0; rb < RB; ++rb)
             a[rb][p] = __builtin_bit_cast(bf16x8, Xs[p * NPOS + hpos[rb] + toff]);
@@ -539,16 +560,16 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
 #pragma unroll
           for (int cb = 0; cb < CB; ++cb) {
             f32x16 c = acc[rb][cb];
-            if constexpr (NS == 3) {
-              c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[rb][1], bm[cb][1], c, 0, 0, 0);
-              c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[rb][0], bm[cb][2], c, 0, 0, 0);
-              c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[rb][2], bm[cb][0], c, 0, 0, 0);
+            if constexpr (NP == 3) {
+              c = mfma32x16<HF>(a[rb][1], bm[cb][1], c);
+              c = mfma32x16<HF>(a[rb][0], bm[cb][2], c);
+              c = mfma32x16<HF>(a[rb][2], bm[cb][0], c);
             }
-            if constexpr (NS >= 2) {
-              c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[rb][0], bm[cb][1], c, 0, 0, 0);
-              c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[rb][1], bm[cb][0], c, 0, 0, 0);
+            if constexpr (NP >= 2) {
+              c = mfma32x16<HF>(a[rb][0], bm[cb][1], c);
+              c = mfma32x16<HF>(a[rb][1], bm[cb][0], c);
             }
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[rb][0], bm[cb][0], c, 0, 0, 0);
+            c = mfma32x16<HF>(a[rb][0], bm[cb][0], c);
             acc[rb][cb] = c;
           }
       }
@@ -560,6 +581,14 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
     for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
       for (int cb = 0; cb < CB; ++cb) acc[rb][cb] = -acc[rb][cb];
+  }
+  if constexpr (HF) {  // undo the operand scales (exact: a power of two)
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+      for (int cb = 0; cb < CB; ++cb)
+#pragma unroll
+        for (int r = 0; r < NREG; ++r) acc[rb][cb][r] = ldexpf(acc[rb][cb][r], -(ex + ew));
   }
 
 // ---- epilogue: C[i][j], row i = voxel (vrow mapping), col j = out channel ----
@@ -772,7 +801,7 @@ template <int BN, int KD, int NS, bool HR, int MB = xt_mb(BN), int NW = xt_nw(BN
           int TD = xt_td(BN)>
 static hipError_t launch_fwd_xh(const Src2& x, const uint4* wx, const Dst2& y, Vol vol, int K,
                                 int nkc, int N, int npad, hipStream_t s, float* part, int nsplit,
-                                int kps, float* stats, int dpart) {
+                                int kps, float* stats, int dpart, const unsigned* wmx, const unsigned* xmx) {
   constexpr int TH = SPFF_X16 ? 2 * NW * MB / TD : NW * MB;
   static_assert(NW == 8 || TD == XT_D, "xt_ntiles assumes 8 waves for other tile depths");
   constexpr size_t shm = xt_lds_bytes<BN, KD, NS, TD, TH>();
@@ -800,7 +829,7 @@ static hipError_t launch_fwd_xh(const Src2& x, const uint4* wx, const Dst2& y, V
   dim3 grid(8 * cdiv(ntiles, 8) * (npad / BN), 1, part ? nsplit : 1);
   hipLaunchKernelGGL(kern, grid, dim3(NW * 64), shm, s, x, wx, y, vol, K, nkc, N, npad, tilesD,
                      tilesH, tilesW, part, part ? kps : nkc, part ? nullptr : stats, ntiles, td0,
-                     tds, th0, ths);
+                     tds, th0, ths, wmx, xmx);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || !part) return e;
   const int64_t total = nvox(vol) * N;
@@ -810,13 +839,12 @@ static hipError_t launch_fwd_xh(const Src2& x, const uint4* wx, const Dst2& y, V
 }
 template <int BN, int KD, int NS>
 static hipError_t launch_fwd_x(const Src2& x, const uint4* wx, const Dst2& y, Vol vol, int K,
-                               int nkc, int N, int npad, hipStream_t s, float* part = nullptr,
-                               int nsplit = 1, int kps = 0, float* stats = nullptr,
-                               int dpart = 0) {
+                               int nkc, int N, int npad, hipStream_t s, float* part, int nsplit,
+                               int kps, float* stats, int dpart, const unsigned* wmx, const unsigned* xmx) {
   return x.rows() ? launch_fwd_xh<BN, KD, NS, true>(x, wx, y, vol, K, nkc, N, npad, s, part,
-                                                    nsplit, kps, stats, dpart)
+                                                    nsplit, kps, stats, dpart, wmx, xmx)
                   : launch_fwd_xh<BN, KD, NS, false>(x, wx, y, vol, K, nkc, N, npad, s, part,
-                                                     nsplit, kps, stats, dpart);
+                                                     nsplit, kps, stats, dpart, wmx, xmx);
 }
 
 namespace {
@@ -887,29 +915,145 @@ SplitK splitk_plan(Vol vol, const XDims& d) {
 }  // namespace
 
 // ----------------------------------------------------------- dispatcher --
-size_t conv3d_pack_bytes(int KD, int Cin, int Cout) {
+// ---- SPFF_MATH_F16X3 operand scales ----
+// The largest |element| of each operand, as float bits (a non-negative float orders like
+// its bits), by integer atomicMax -- order-independent, so deterministic -- into two
+// slots after the packed weight image: [0] max |w| (conv3d_pack zeroes both and fills
+// it), [1] max |x| (conv3d_run, over exactly what the launch reads).
+__device__ __forceinline__ float wave_max(float m) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  return m;
+}
+__device__ __forceinline__ void block_max_to(float m, unsigned* slot) {
+  __shared__ float wm[16];
+  m = wave_max(m);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) wm[wave] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) m = fmaxf(m, wm[w]);
+    if (m > 0.f) atomicMax(slot, __float_as_uint(m));
+  }
+}
+__global__ __launch_bounds__(256) void k_absmax_f32(const float* __restrict__ p, int64_t n,
+                                                    unsigned* __restrict__ slot) {
+  float m = 0.f;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    m = fmaxf(m, fabsf(p[i]));
+  block_max_to(m, slot);
+}
+// |elements| of channels [c, c + 4) of one voxel's row (4-aligned, one source), input
+// activation applied; channels >= C (row padding) ignored
+__device__ __forceinline__ float amax4(const float* row, const Src2& x, int b, int c, int C) {
+  const float4 v = *reinterpret_cast<const float4*>(row);
+  float r[4] = {v.x, v.y, v.z, v.w};
+  float m = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float t = r[j];
+    if (x.al) {
+      t = t * x.al[(int64_t)b * x.ld0 + c + j] + x.de[(int64_t)b * x.ld0 + c + j];
+      t = t > 0.f ? t : 0.01f * t;
+    }
+    m = c + j < C ? fmaxf(m, fabsf(t)) : m;
+  }
+  return m;
+}
+// max |x| over what a conv launch reads: depth planes [dlo, dhi) of [B][D][H][W] (the
+// halo slices of a depth-sharded input when included), and the height-sharded boundary
+// rows rlo / rhi ([B][D][W][ldr]) when withrows
+__global__ __launch_bounds__(256) void k_absmax_src(Src2 x, Vol vol, int C, int dlo, int dhi,
+                                                    int withrows, unsigned* __restrict__ slot) {
+  const int C4 = (C + 3) >> 2, H = vol.H, W = vol.W, nd = dhi - dlo;
+  const int64_t total = (int64_t)vol.B * nd * H * W * C4;
+  float m = 0.f;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int c = 4 * (int)(i % C4);
+    int64_t t = i / C4;
+    const int gw = (int)(t % W); t /= W;
+    const int gh = (int)(t % H); t /= H;
+    const int gd = dlo + (int)(t % nd);
+    const int b = (int)(t / nd);
+    const int64_t vox = (((int64_t)b * vol.D + gd) * H + gh) * W + gw;
+    const float* row = c < x.split ? x.p0 + vox * x.ld0 + c : x.p1 + vox * x.ld1 + (c - x.split);
+    m = fmaxf(m, amax4(row, x, b, c, C));
+  }
+  if (withrows) {
+    const int64_t nr = (int64_t)vol.B * vol.D * W * C4;
+    for (int side = 0; side < 2; ++side) {
+      const float* rp = side ? x.rhi : x.rlo;
+      if (!rp) continue;
+      for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < nr; i += (int64_t)gridDim.x * 256) {
+        const int c = 4 * (int)(i % C4);
+        const int64_t bdw = i / C4;
+        const int b = (int)(bdw / ((int64_t)vol.D * W));
+        m = fmaxf(m, amax4(rp + bdw * x.ldr + c, x, b, c, C));
+      }
+    }
+  }
+  block_max_to(m, slot);
+}
+static unsigned absmax_grid(int64_t n) {
+  return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 2047) / 2048, 1024));
+}
+hipError_t absmax_src(const Src2& x, Vol vol, int C, bool halo, unsigned* slot, hipStream_t s) {
+  if ((x.ld0 & 3) || (x.ld1 & 3) || (x.split & 3) || (x.rows() && (x.ldr & 3)))
+    return hipErrorInvalidValue;
+  const int dlo = halo && vol.dh && !x.zlo ? -vol.dh : 0;
+  const int dhi = vol.D + (halo && vol.dh && !x.zhi ? vol.dh : 0);
+  const int64_t n = (int64_t)vol.B * (dhi - dlo) * vol.H * vol.W * ((C + 3) / 4);
+  hipLaunchKernelGGL(k_absmax_src, dim3(absmax_grid(n)), dim3(256), 0, s, x, vol, C, dlo, dhi,
+                     halo && x.rows() ? 1 : 0, slot);
+  return hipGetLastError();
+}
+hipError_t absmax_f32(const float* p, int64_t n, unsigned* slot, hipStream_t s) {
+  hipLaunchKernelGGL(k_absmax_f32, dim3(absmax_grid(n)), dim3(256), 0, s, p, n, slot);
+  return hipGetLastError();
+}
+
+static size_t pack_main_bytes(int KD, int Cin, int Cout) {
   size_t f32 = 0, x = 0;
   for (int dg = 0; dg < 2; ++dg) {
     const XDims d = xdims(KD, Cin, Cout, dg != 0);
     f32 = std::max(f32, (size_t)d.T * rup(d.K, 8) * rup(d.N, conv3d_bn(d.N)) * sizeof(float));
     x = std::max(x, (size_t)d.T2 * d.nkc * d.npad * 16 * 3);  // 3 bf16 planes of 8 k
   }
-  return std::max(f32, x);
+  return (std::max(f32, x) + 255) & ~(size_t)255;
+}
+size_t conv3d_pack_bytes(int KD, int Cin, int Cout) {
+  return pack_main_bytes(KD, Cin, Cout) + 256;  // + the F16X3 scale slots
+}
+static unsigned* f16_slots(const void* wpack, int KD, int Cin_w, int Cout_w) {
+  return reinterpret_cast<unsigned*>(static_cast<char*>(const_cast<void*>(wpack)) +
+                                     pack_main_bytes(KD, Cin_w, Cout_w));
 }
 
 hipError_t conv3d_pack(const float* w, void* wpack, Vol vol, int KD, int Cin_w, int Cout_w,
-                       bool dgrad, int math, hipStream_t s) {
+                       bool dgrad, int math, hipStream_t s, const unsigned* wmax) {
   const XDims d = xdims(KD, Cin_w, Cout_w, dgrad);
   if (use_split(vol, math, dgrad)) {
     const int64_t total = (int64_t)d.nkc * d.T2 * d.npad;
     const int grid = (int)std::min<int64_t>((total + 255) / 256, 4096);
     uint4* wp = static_cast<uint4*>(wpack);
-    if (math == SPFF_MATH_BF16X3)
+    unsigned* sl = f16_slots(wpack, KD, Cin_w, Cout_w);
+    if (math == SPFF_MATH_F16X3) {
+      if (!wmax) {  // max |w| into the image's slot 0 (else the caller's precomputed slot)
+        hipError_t e = hipMemsetAsync(sl, 0, sizeof(unsigned), s);
+        if (e != hipSuccess) return e;
+        e = absmax_f32(w, (int64_t)Cout_w * Cin_w * d.T, sl, s);
+        if (e != hipSuccess) return e;
+        wmax = sl;
+      }
+      hipLaunchKernelGGL(k_conv_pack_x<NS_F16>, dim3(grid), dim3(256), 0, s, w, wp, Cout_w, Cin_w,
+                         d.T, d.T2, d.nkc, d.npad, d.BN, dgrad ? 1 : 0, wmax);
+    } else if (math == SPFF_MATH_BF16X3) {
       hipLaunchKernelGGL(k_conv_pack_x<2>, dim3(grid), dim3(256), 0, s, w, wp, Cout_w, Cin_w, d.T,
-                         d.T2, d.nkc, d.npad, d.BN, dgrad ? 1 : 0);
-    else
+                         d.T2, d.nkc, d.npad, d.BN, dgrad ? 1 : 0, (const unsigned*)nullptr);
+    } else {
       hipLaunchKernelGGL(k_conv_pack_x<3>, dim3(grid), dim3(256), 0, s, w, wp, Cout_w, Cin_w, d.T,
-                         d.T2, d.nkc, d.npad, d.BN, dgrad ? 1 : 0);
+                         d.T2, d.nkc, d.npad, d.BN, dgrad ? 1 : 0, (const unsigned*)nullptr);
+    }
     return hipGetLastError();
   }
   return conv_pack_weights(w, static_cast<float*>(wpack), Cout_w, Cin_w, KD, rup(d.K, 8),
@@ -918,7 +1062,8 @@ hipError_t conv3d_pack(const float* w, void* wpack, Vol vol, int KD, int Cin_w, 
 
 template <int NS>
 static hipError_t run_x(const Src2& x, const uint4* wu, const Dst2& y, Vol vol, int KD,
-                        const XDims& d, hipStream_t s, float* ws, float* stats, int dpart) {
+                        const XDims& d, hipStream_t s, float* ws, float* stats, int dpart,
+                        const unsigned* wmx, const unsigned* xmx) {
   // (32x32x16, MB = 4, 2 x 32 x 16 tiles for Cout <= 32: fits LDS but spills 91 VGPRs)
   // (32x32x16 schedule, NW = 4 waves, 2 x 8 x 16 tiles: measured 6 % slower; the 16x16x32
   // schedule takes NW = 4 for BN 32 by default, SPFF_X32NW)
@@ -927,16 +1072,16 @@ static hipError_t run_x(const Src2& x, const uint4* wu, const Dst2& y, Vol vol, 
   if (d.BN == 64)
     return KD == 3
                ? launch_fwd_x<64, 3, NS>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s, part,
-                                                k.nsplit, k.kps, stats, dpart)
+                                                k.nsplit, k.kps, stats, dpart, wmx, xmx)
                : launch_fwd_x<64, 1, NS>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s, part,
-                                                k.nsplit, k.kps, stats, dpart);
+                                                k.nsplit, k.kps, stats, dpart, wmx, xmx);
   if (d.BN == 16)
     return launch_fwd_x<16, 3, NS>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s, part, k.nsplit,
-                                   k.kps, stats, dpart);
+                                   k.kps, stats, dpart, wmx, xmx);
   return KD == 3 ? launch_fwd_x<32, 3, NS>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s,
-                                                  part, k.nsplit, k.kps, stats, dpart)
+                                                  part, k.nsplit, k.kps, stats, dpart, wmx, xmx)
                  : launch_fwd_x<32, 1, NS>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s,
-                                                  part, k.nsplit, k.kps, stats, dpart);
+                                                  part, k.nsplit, k.kps, stats, dpart, wmx, xmx);
 }
 
 
@@ -981,7 +1126,7 @@ hipError_t conv3d_in_stats_fin(const float* stats, Vol vol, int KD, int Cin, int
 
 hipError_t conv3d_run(const Src2& x, const void* wpack, const Dst2& y, Vol vol, int KD,
                       int Cin_w, int Cout_w, bool dgrad, int math, hipStream_t s, float* ws,
-                      float* stats, int dpart) {
+                      float* stats, int dpart, const unsigned* xmax, const unsigned* wmax) {
   const XDims d = xdims(KD, Cin_w, Cout_w, dgrad);
   if (stats && (dgrad || !conv3d_fuses_stats(vol, KD, Cin_w, Cout_w, math)))
     return hipErrorInvalidValue;
@@ -992,8 +1137,25 @@ hipError_t conv3d_run(const Src2& x, const void* wpack, const Dst2& y, Vol vol, 
     return hipErrorInvalidValue;
   if (use_split(vol, math, dgrad)) {
     const uint4* wu = static_cast<const uint4*>(wpack);
-    return math == SPFF_MATH_BF16X3 ? run_x<2>(x, wu, y, vol, KD, d, s, ws, stats, dpart)
-                                    : run_x<3>(x, wu, y, vol, KD, d, s, ws, stats, dpart);
+    if (math == SPFF_MATH_F16X3) {
+      unsigned* sl = f16_slots(wpack, KD, Cin_w, Cout_w);
+      if (!xmax) {
+        // max |x| over what this launch reads (interior depth / H tiles: no halo, no rows)
+        // into the image's slot 1; a boundary launch (dpart 2 / 4) after the interior one
+        // adds its halo to the same slot
+        if (dpart != 2 && dpart != 4) {
+          hipError_t e = hipMemsetAsync(sl + 1, 0, sizeof(unsigned), s);
+          if (e != hipSuccess) return e;
+        }
+        hipError_t e = absmax_src(x, vol, d.K, dpart != 1 && dpart != 3, sl + 1, s);
+        if (e != hipSuccess) return e;
+        xmax = sl + 1;
+      }
+      return run_x<NS_F16>(x, wu, y, vol, KD, d, s, ws, stats, dpart, wmax ? wmax : sl, xmax);
+    }
+    return math == SPFF_MATH_BF16X3
+               ? run_x<2>(x, wu, y, vol, KD, d, s, ws, stats, dpart, nullptr, nullptr)
+               : run_x<3>(x, wu, y, vol, KD, d, s, ws, stats, dpart, nullptr, nullptr);
   }
   return conv3d_fwd(x, static_cast<const float*>(wpack), y, vol, KD, d.K, rup(d.K, 8), d.N,
                     rup(d.N, conv3d_bn(d.N)), s);

@@ -133,6 +133,7 @@ struct spff_plan {
   size_t x_cl = 0, pool[3] = {0, 0, 0}, pidx[3] = {0, 0, 0};
   size_t red_ws = 0, red_out = 0, red_out4 = 0, gscr = 0, Abuf = 0, Bbuf = 0, kk1 = 0, kk2 = 0,
          wg_ws = 0, wt = 0, cst = 0;
+  size_t fsl = 0;  // SPFF_MATH_F16X3 operand maxima, 8 slots per block (f16_slot)
   size_t G_out = 0, G_dy2 = 0, G_da1 = 0, G_dx = 0, dskip[3] = {0, 0, 0};
   size_t part_d = 0;  // sharded plans: fp64 IN partials [B][C][2]
   // height-sharded plans (spff_cfg.shard_axis = SPFF_SHARD_HEIGHT, hshard.hip): the
@@ -269,7 +270,7 @@ int build_plan(spff_plan* p) {
   if (c.height < 8 || c.width < 8)
     return fail(SPFF_ESHAPE, "H and W must be >= 8 (three (1,2,2) pools)");
   if (c.in_ch > 64) return fail(SPFF_EINVAL, "in_ch > 64 not supported");
-  if (c.math < SPFF_MATH_F32 || c.math > SPFF_MATH_BF16X3)
+  if (c.math < SPFF_MATH_F32 || c.math > SPFF_MATH_F16X3)
     return fail(SPFF_EINVAL, "math must be one of SPFF_MATH_*");
   if (c.memory_mode < SPFF_MEM_AUTO || c.memory_mode > SPFF_MEM_LEAN)
     return fail(SPFF_EINVAL, "memory_mode must be one of SPFF_MEM_*");
@@ -450,6 +451,7 @@ int build_plan(spff_plan* p) {
   p->kk2 = p->alloc((size_t)B * 8 * f * sizeof(float));
   p->wg_ws = p->alloc(wg);
   p->wt = p->alloc(wt);
+  p->fsl = p->alloc(7 * 8 * sizeof(unsigned));
   p->cst = p->alloc(cst);
   // gradient scratch, sized for level 0 ([V0][f]); a level-l tensor of the path
   // (V0 / 4^l voxels x f 2^l channels) fills 1 / 2^l of a buffer.  Halo'd (level-0
@@ -617,11 +619,13 @@ int conv_h(spff_plan* p, int cls, double flops, double bytes, const Src2& x, con
 // weight gradient of a 3x3x3 conv (height-sharded: x's stencil rows from the neighbours;
 // dy is read at the local rows only)
 int conv_wgrad(spff_plan* p, double flops, double bytes, const Src2& x, const float* dy, float* dw,
-               const Vol& v, int Cin, int Cout) {
+               const Vol& v, int Cin, int Cout, const unsigned* xmax = nullptr,
+               const unsigned* ymax = nullptr) {
   Src2 xr = x;
   if (p->hsh) CK(hrows_exchange(p, x, v, Cin, &xr, p->st));
   PROFB(p, 2, flops, bytes,
-        conv3d_wgrad(xr, dy, Cout, dw, v, p->KD, Cin, Cout, p->cfg.math, p->F(p->wg_ws), p->st));
+        conv3d_wgrad(xr, dy, Cout, dw, v, p->KD, Cin, Cout, p->cfg.math, p->F(p->wg_ws), p->st,
+                     xmax, ymax));
   return SPFF_OK;
 }
 
@@ -631,8 +635,10 @@ int conv_wgrad(spff_plan* p, double flops, double bytes, const Src2& x, const fl
 // last depth tiles after it; otherwise exchange, then convolve.  cls / flops / bytes:
 // the PROFB record of the launch (the interior launch carries the FLOPs, the
 // boundary one adds its time to the same class).
+// (xmax / wmax: f16_slot operand maxima of an unsharded SPFF_MATH_F16X3 plan, else null)
 int conv_halo(spff_plan* p, int cls, double flops, double bytes, const Src2& x, const Dst2& y,
-              const Vol& v, int Cin_w, int Cout_w, bool dgrad, float* stats) {
+              const Vol& v, int Cin_w, int Cout_w, bool dgrad, float* stats,
+              const unsigned* xmax = nullptr, const unsigned* wmax = nullptr) {
   if (p->hsh) return conv_h(p, cls, flops, bytes, x, y, v, Cin_w, Cout_w, dgrad);
   const int KD = p->KD, math = p->cfg.math;
   const bool ovl = v.dh && !stats && conv3d_splits_depth(v, KD, Cin_w, Cout_w, dgrad, math);
@@ -640,7 +646,7 @@ int conv_halo(spff_plan* p, int cls, double flops, double bytes, const Src2& x, 
     CK(halo_src(p, x, v));
     PROFB(p, cls, flops, bytes,
           conv3d_run(x, p->F(p->wt), y, v, KD, Cin_w, Cout_w, dgrad, math, p->st, p->F(p->wg_ws),
-                     stats));
+                     stats, 0, xmax, wmax));
     return SPFF_OK;
   }
   if (!p->st2) {
@@ -721,19 +727,49 @@ Src2 act_src(const spff_plan* p, const Blk& b) {
   return s;
 }
 
+// SPFF_MATH_F16X3 on an unsharded plan: every conv operand's max |element| (float bits, the
+// fp16 planes' scale) is precomputed once per step and shared by the convs that read the
+// tensor, instead of one absmax pass per launch: per block, slot F16_W1 / F16_W2 max |w| and
+// F16_A1 a parameter bound on a1 = lrelu(IN(y1)) (act_bound), all in one batch at the
+// forward start; F16_IN one pass over the block input before its first conv; F16_DY2 /
+// F16_DA1 from in_bwd_apply as it writes them.  Sharded plans compute them per launch
+// (their convs also read halo slices / boundary rows that arrive later).
+enum { F16_IN = 0, F16_A1, F16_DY2, F16_DA1, F16_W1, F16_W2 };
+unsigned* f16_slot(const spff_plan* p, const Blk& b, int k) {
+  if (p->cfg.math != SPFF_MATH_F16X3 || p->co.on() || p->hsh) return nullptr;
+  return reinterpret_cast<unsigned*>(p->ws + p->fsl) + 8 * (int)(&b - p->blk) + k;
+}
+int f16_param_slots(spff_plan* p) {
+  if (!f16_slot(p, p->blk[0], 0)) return SPFF_OK;
+  HIPCK(hipMemsetAsync(p->ws + p->fsl, 0, 7 * 8 * sizeof(unsigned), p->st));
+  const int T = 9 * p->KD;
+  for (int i = 0; i < 7; ++i) {
+    const Blk& b = p->blk[i];
+    const Vol& v = p->vol[b.lvl];
+    HIPCK(absmax_f32(p->P(b.c1.w), (int64_t)b.C * b.Cin * T, f16_slot(p, b, F16_W1), p->st));
+    HIPCK(absmax_f32(p->P(b.c2.w), (int64_t)b.C * b.C * T, f16_slot(p, b, F16_W2), p->st));
+    HIPCK(act_bound(p->P(b.g1), p->P(b.b1), b.C, (double)v.D * v.H * v.W,
+                    f16_slot(p, b, F16_A1), p->st));
+  }
+  return SPFF_OK;
+}
+
 // pool >= 0: encoder block b's output also feeds MaxPool3d((1,2,2)) into p->pool[pool]
 // (the output apply and the pool run as one pass where H and W are even)
 int fwd_block(spff_plan* p, Blk& b, const Src2& in, int pool = -1) {
   const Vol& v = p->vol[b.lvl];
   const int C = b.C, KD = p->KD;
   const int math = p->cfg.math;
-  HIPCK(conv3d_pack(p->P(b.c1.w), p->F(p->wt), v, KD, b.Cin, C, false, math, p->st));
+  HIPCK(conv3d_pack(p->P(b.c1.w), p->F(p->wt), v, KD, b.Cin, C, false, math, p->st,
+                    f16_slot(p, b, F16_W1)));
   const double V = (double)nvox(v), T = 9.0 * KD;
+  if (unsigned* sl = f16_slot(p, b, F16_IN)) HIPCK(absmax_src(in, v, b.Cin, false, sl, p->st));
   // InstanceNorm statistics fused into the conv epilogue where the split kernel
   // runs unsharded without split-K; otherwise the two slab_reduce passes
   const bool fuse1 = !p->co.on() && conv3d_fuses_stats(v, KD, b.Cin, C, math);
   CK(conv_halo(p, 0, 2.0 * V * b.Cin * C * T, cbytes(V, b.Cin, C, T), in, dst1(p->F(b.y1), C), v,
-               b.Cin, C, false, fuse1 ? p->F(p->cst) : nullptr));
+               b.Cin, C, false, fuse1 ? p->F(p->cst) : nullptr, f16_slot(p, b, F16_IN),
+               f16_slot(p, b, F16_W1)));
   if (fuse1)
     HIPCK(conv3d_in_stats_fin(p->F(p->cst), v, KD, b.Cin, C, p->P(b.g1), p->P(b.b1),
                               p->F(b.mean1), p->F(b.rstd1), p->F(b.al1), p->F(b.de1), p->st));
@@ -743,11 +779,13 @@ int fwd_block(spff_plan* p, Blk& b, const Src2& in, int pool = -1) {
     PROFB(p, 5, 0.0, 8.0 * (double)nvox(v) * C,
           act_apply(p->F(b.y1), p->F(b.a1), p->F(b.al1), p->F(b.de1), nullptr, nullptr, v, C,
                     p->st));
-  HIPCK(conv3d_pack(p->P(b.c2.w), p->F(p->wt), v, KD, C, C, false, math, p->st));
+  HIPCK(conv3d_pack(p->P(b.c2.w), p->F(p->wt), v, KD, C, C, false, math, p->st,
+                    f16_slot(p, b, F16_W2)));
   const Src2 in2 = act_src(p, b);
   const bool fuse2 = !p->co.on() && conv3d_fuses_stats(v, KD, C, C, math);
   CK(conv_halo(p, 0, 2.0 * V * C * C * T, cbytes(V, C, C, T), in2, dst1(p->F(b.y2), C), v, C, C,
-               false, fuse2 ? p->F(p->cst) : nullptr));
+               false, fuse2 ? p->F(p->cst) : nullptr, f16_slot(p, b, F16_A1),
+               f16_slot(p, b, F16_W2)));
   if (fuse2)
     HIPCK(conv3d_in_stats_fin(p->F(p->cst), v, KD, C, C, p->P(b.g2), p->P(b.b2), p->F(b.mean2),
                               p->F(b.rstd2), p->F(b.al2), p->F(b.de2), p->st));
@@ -923,7 +961,8 @@ int bwd_block(spff_plan* p, Blk& b, const float* dout, const Dst2* dx, const Src
     CK(in_bwd(p, v, C, b.g2, b.b2));
     PROFB(p, 6, 0.0, 12.0 * (double)nvox(v) * C,
           in_bwd_apply(p->F(b.y2), dout, dy2, p->F(b.mean2), p->F(b.rstd2), p->F(b.al2),
-                       p->F(b.de2), p->P(b.g2), A, Bc, p->F(p->kk1), p->F(p->kk2), v, C, p->st));
+                       p->F(b.de2), p->P(b.g2), A, Bc, p->F(p->kk1), p->F(p->kk2), v, C, p->st,
+                       0.01f, f16_slot(p, b, F16_DY2)));
   }
   const double V = (double)nvox(v), T = 9.0 * KD;
   Src2 a1 = act_src(p, b);  // (fused: y1 and its halo as the forward left them)
@@ -933,11 +972,13 @@ int bwd_block(spff_plan* p, Blk& b, const float* dout, const Dst2* dx, const Src
     CK(halo(p, da1, v, C));
     a1 = src1(da1, C);
   }
-  CK(conv_wgrad(p, 2.0 * V * C * C * T, cbytes(V, C, C, T), a1, dy2, p->DP(b.c2.w), v, C, C));
+  CK(conv_wgrad(p, 2.0 * V * C * C * T, cbytes(V, C, C, T), a1, dy2, p->DP(b.c2.w), v, C, C,
+                f16_slot(p, b, F16_A1), f16_slot(p, b, F16_DY2)));
   const int math = p->cfg.math;
-  HIPCK(conv3d_pack(p->P(b.c2.w), p->F(p->wt), v, KD, C, C, true, math, p->st));
+  HIPCK(conv3d_pack(p->P(b.c2.w), p->F(p->wt), v, KD, C, C, true, math, p->st,
+                    f16_slot(p, b, F16_W2)));
   CK(conv_halo(p, 1, 2.0 * V * C * C * T, cbytes(V, C, C, T), src1(dy2, C), dst1(da1, C), v, C, C,
-               true, nullptr));
+               true, nullptr, f16_slot(p, b, F16_DY2), f16_slot(p, b, F16_W2)));
   {
     RedArgs a{};
     a.y = p->F(b.y1); a.g = da1; a.mean = p->F(b.mean1); a.rstd = p->F(b.rstd1);
@@ -948,15 +989,16 @@ int bwd_block(spff_plan* p, Blk& b, const float* dout, const Dst2* dx, const Src
     PROFB(p, 6, 0.0, 12.0 * (double)nvox(v) * C,
           in_bwd_apply(p->F(b.y1), da1, da1, p->F(b.mean1), p->F(b.rstd1), p->F(b.al1),
                        p->F(b.de1), p->P(b.g1), nullptr, nullptr, p->F(p->kk1), p->F(p->kk2), v,
-                       C, p->st));
+                       C, p->st, 0.01f, f16_slot(p, b, F16_DA1)));
   }
   if (p->lean && dec_bi >= 0) CK(lean_dec_input(p, dec_bi, &in));
   CK(conv_wgrad(p, 2.0 * V * b.Cin * C * T, cbytes(V, b.Cin, C, T), in, da1, p->DP(b.c1.w), v,
-                b.Cin, C));
+                b.Cin, C, f16_slot(p, b, F16_IN), f16_slot(p, b, F16_DA1)));
   if (dx) {
-    HIPCK(conv3d_pack(p->P(b.c1.w), p->F(p->wt), v, KD, b.Cin, C, true, math, p->st));
+    HIPCK(conv3d_pack(p->P(b.c1.w), p->F(p->wt), v, KD, b.Cin, C, true, math, p->st,
+                      f16_slot(p, b, F16_W1)));
     CK(conv_halo(p, 1, 2.0 * V * b.Cin * C * T, cbytes(V, b.Cin, C, T), src1(da1, C), *dx, v,
-                 b.Cin, C, true, nullptr));
+                 b.Cin, C, true, nullptr, f16_slot(p, b, F16_DA1), f16_slot(p, b, F16_W1)));
   }
   return SPFF_OK;
 }
@@ -987,6 +1029,7 @@ int forward(spff_plan* p, const float* x, float* logits) {
     HIPCK(efilm_fwd_all(p->pe_dev + p->co.d_off, p->co.D_glob, jobs, c.depth, p->st));
     p->efilm_ready = jobs.n > 0;
   }
+  CK(f16_param_slots(p));
   HIPCK(ncdhw_to_ndhwc(x, p->F(p->x_cl), p->vol[0], c.in_ch, p->ldx, p->st));
   Blk* B = p->blk;
   CK(fwd_block(p, B[0], src1(p->F(p->x_cl), p->ldx), 0));
@@ -1338,7 +1381,7 @@ int spff_conv3d_fwd_ex(const float* x, int ldx, const float* w, float* y, int B,
   if (!x || !w || !y || !ws) return fail(SPFF_EINVAL, "null argument");
   if (ldx % 4 || ldx < cin) return fail(SPFF_EINVAL, "ldx must be >= cin and a multiple of 4");
   if (cout % 4) return fail(SPFF_EINVAL, "cout must be a multiple of 4");
-  if (math < SPFF_MATH_F32 || math > SPFF_MATH_BF16X3) return fail(SPFF_EINVAL, "bad math");
+  if (math < SPFF_MATH_F32 || math > SPFF_MATH_F16X3) return fail(SPFF_EINVAL, "bad math");
   hipStream_t s = static_cast<hipStream_t>(stream);
   const Vol v{B, D, H, W};
   HIPCK(conv3d_pack(w, ws, v, ksd, cin, cout, false, math, s));
@@ -1355,7 +1398,7 @@ int spff_conv3d_dgrad_ex(const float* dy, const float* w, float* dx, int B, int 
                          int cin, int cout, int ksd, int math, void* ws, void* stream) {
   if (!dy || !w || !dx || !ws) return fail(SPFF_EINVAL, "null argument");
   if (cout % 4 || cin % 4) return fail(SPFF_EINVAL, "channels must be multiples of 4");
-  if (math < SPFF_MATH_F32 || math > SPFF_MATH_BF16X3) return fail(SPFF_EINVAL, "bad math");
+  if (math < SPFF_MATH_F32 || math > SPFF_MATH_F16X3) return fail(SPFF_EINVAL, "bad math");
   hipStream_t s = static_cast<hipStream_t>(stream);
   const Vol v{B, D, H, W};
   HIPCK(conv3d_pack(w, ws, v, ksd, cin, cout, true, math, s));
@@ -1373,7 +1416,7 @@ int spff_conv3d_wgrad_ex(const float* x, int ldx, const float* dy, float* dw, in
                          void* stream) {
   if (!x || !dy || !dw || !ws) return fail(SPFF_EINVAL, "null argument");
   if (ldx % 4 || ldx < cin || cout % 4) return fail(SPFF_EINVAL, "bad channel strides");
-  if (math < SPFF_MATH_F32 || math > SPFF_MATH_BF16X3) return fail(SPFF_EINVAL, "bad math");
+  if (math < SPFF_MATH_F32 || math > SPFF_MATH_F16X3) return fail(SPFF_EINVAL, "bad math");
   hipStream_t s = static_cast<hipStream_t>(stream);
   float* part = static_cast<float*>(ws) + conv_op_pack_floats(cin, cout, ksd) + 64;
   HIPCK(conv3d_wgrad(src1(x, ldx), dy, cout, dw, Vol{B, D, H, W}, ksd, cin, cout, math, part,

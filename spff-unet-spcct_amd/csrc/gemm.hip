@@ -33,7 +33,10 @@ static int num_cus() {
 #ifndef SPFF_GEMM_PERSIST
 #define SPFF_GEMM_PERSIST 1
 #endif
-static inline bool gemm_split(int math) { return SPFF_GEMM_SPLIT && math == SPFF_MATH_BF16X6; }
+// (SPFF_MATH_F16X3 is a conv arithmetic: the GEMMs take the bf16x6 split with it)
+static inline bool gemm_split(int math) {
+  return SPFF_GEMM_SPLIT && (math == SPFF_MATH_BF16X6 || math == SPFF_MATH_F16X3);
+}
 static inline int64_t cdiv64(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 // ------------------------------------------------------------- functors --

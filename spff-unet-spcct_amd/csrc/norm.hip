@@ -9,6 +9,9 @@
 // transform form), a = lrelu(r).
 #include "spff_internal.h"
 
+#include <algorithm>
+#include <cmath>
+
 #ifndef SPFF_RED_CH
 #define SPFF_RED_CH 16
 #endif
@@ -663,7 +666,8 @@ __global__ __launch_bounds__(256) void k_in_bwd_apply(
     const float* __restrict__ y, const float* g, float* dy, const float* __restrict__ mean,
     const float* __restrict__ rstd, const float* __restrict__ al, const float* __restrict__ de,
     const float* __restrict__ gamma, const float* __restrict__ A, const float* __restrict__ Bc,
-    const float* __restrict__ k1, const float* __restrict__ k2, Vol vol, int C, float neg) {
+    const float* __restrict__ k1, const float* __restrict__ k2, Vol vol, int C, float neg,
+    unsigned* __restrict__ amax) {
   const int bd = blockIdx.y, b = bd / vol.D, d = bd % vol.D;
   const int n4 = vol.H * vol.W * (C >> 2);
   const int64_t base = (int64_t)bd * vol.H * vol.W * C;
@@ -678,6 +682,7 @@ __global__ __launch_bounds__(256) void k_in_bwd_apply(
     pA[j] = A ? A[(int64_t)bc * vol.D + d] : 1.f;
     pB[j] = A ? Bc[(int64_t)bc * vol.D + d] : 0.f;
   }
+  float m = 0.f;
   for (int i = i0; i < n4; i += gridDim.x * blockDim.x) {
     const float4 yv = *reinterpret_cast<const float4*>(y + base + 4 * (int64_t)i);
     const float4 gv = *reinterpret_cast<const float4*>(g + base + 4 * (int64_t)i);
@@ -690,17 +695,58 @@ __global__ __launch_bounds__(256) void k_in_bwd_apply(
       const float dr = (gs[j] * pA[j] + pB[j]) * slope(r, neg);
       const float xh = (ys[j] - pmu[j]) * prs[j];
       o[j] = psc[j] * (dr - pk1[j] - xh * pk2[j]);
+      m = fmaxf(m, fabsf(o[j]));
     }
     *reinterpret_cast<float4*>(dy + base + 4 * (int64_t)i) = make_float4(o[0], o[1], o[2], o[3]);
   }
+  if (amax) {  // (uniform) block max -> one integer atomicMax of its float bits
+    __shared__ float wm[16];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (int w = 1; w < (int)((blockDim.x + 63) >> 6); ++w) m = fmaxf(m, wm[w]);
+      if (m > 0.f) atomicMax(amax, __float_as_uint(m));
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_act_bound(const float* __restrict__ gamma,
+                                                   const float* __restrict__ beta, int C,
+                                                   float sq, unsigned* __restrict__ slot) {
+  __shared__ float rg[256], rb[256];
+  float mg = 0.f, mb = 0.f;
+  for (int c = threadIdx.x; c < C; c += 256) {
+    mg = fmaxf(mg, fabsf(gamma[c]));
+    mb = fmaxf(mb, fabsf(beta[c]));
+  }
+  rg[threadIdx.x] = mg;
+  rb[threadIdx.x] = mb;
+  __syncthreads();
+  for (int st = 128; st > 0; st >>= 1) {
+    if ((int)threadIdx.x < st) {
+      rg[threadIdx.x] = fmaxf(rg[threadIdx.x], rg[threadIdx.x + st]);
+      rb[threadIdx.x] = fmaxf(rb[threadIdx.x], rb[threadIdx.x + st]);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *slot = __float_as_uint(2.f * (rg[0] * sq + rb[0]) + 1e-30f);
+}
+
+hipError_t act_bound(const float* gamma, const float* beta, int C, double N, unsigned* slot,
+                     hipStream_t s) {
+  const float sq = (float)std::sqrt(std::max(N - 1.0, 1.0));
+  hipLaunchKernelGGL(k_act_bound, dim3(1), dim3(256), 0, s, gamma, beta, C, sq, slot);
+  return hipGetLastError();
 }
 
 hipError_t in_bwd_apply(const float* y, const float* g, float* dy, const float* mean,
                         const float* rstd, const float* al, const float* de, const float* gamma,
                         const float* A, const float* Bc, const float* k1, const float* k2, Vol vol,
-                        int C, hipStream_t s, float neg) {
+                        int C, hipStream_t s, float neg, unsigned* amax) {
   hipLaunchKernelGGL(k_in_bwd_apply, ew_grid(vol, C), dim3(ew_bs(C)), 0, s, y, g, dy, mean, rstd, al,
-                     de, gamma, A, Bc, k1, k2, vol, C, neg);
+                     de, gamma, A, Bc, k1, k2, vol, C, neg, amax);
   return hipGetLastError();
 }
 

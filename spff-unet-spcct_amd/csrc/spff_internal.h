@@ -83,8 +83,9 @@ int conv3d_bn(int Cout);        // output-channel tile the fwd kernel uses
 // the chosen arithmetic (SPFF_MATH_*) runs on, then run it.  Volumes smaller
 // than one 16 x 16 H/W tile take the fp32 kernel whatever the math.
 size_t conv3d_pack_bytes(int KD, int Cin_w, int Cout_w);
+// (SPFF_MATH_F16X3: wmax = a precomputed max |w| slot, else computed into the image's tail)
 hipError_t conv3d_pack(const float* w, void* wpack, Vol vol, int KD, int Cin_w, int Cout_w,
-                       bool dgrad, int math, hipStream_t s);
+                       bool dgrad, int math, hipStream_t s, const unsigned* wmax = nullptr);
 // ws (optional, >= conv3d_splitk_bytes): scratch for split-K partial sums on
 // launches that would not fill the chip; null = no split
 // stats (optional, forward only, when conv3d_fuses_stats): the conv's epilogue also
@@ -98,7 +99,8 @@ hipError_t conv3d_pack(const float* w, void* wpack, Vol vol, int KD, int Cin_w, 
 // boundary row; 3 and 4 together write what 0 writes).
 hipError_t conv3d_run(const Src2& x, const void* wpack, const Dst2& y, Vol vol, int KD,
                       int Cin_w, int Cout_w, bool dgrad, int math, hipStream_t s,
-                      float* ws = nullptr, float* stats = nullptr, int dpart = 0);
+                      float* ws = nullptr, float* stats = nullptr, int dpart = 0,
+                      const unsigned* xmax = nullptr, const unsigned* wmax = nullptr);
 bool conv3d_splits_depth(Vol vol, int KD, int Cin_w, int Cout_w, bool dgrad, int math);
 bool conv3d_splits_height(Vol vol, int KD, int Cin_w, int Cout_w, bool dgrad, int math);
 bool conv3d_fuses_stats(Vol vol, int KD, int Cin, int Cout, int math);
@@ -111,15 +113,24 @@ size_t conv3d_splitk_bytes(Vol vol, int KD, int Cin_w, int Cout_w);
 // math = SPFF_MATH_F32: fp32 MFMA kernel (conv3d.hip); otherwise the split-bf16
 // kernel of conv3d_wgx.hip.  ws >= conv3d_wgrad_ws_bytes (covers both).
 size_t conv3d_wgrad_ws_bytes(Vol vol, int KD, int Cin, int Cout);
+// (SPFF_MATH_F16X3: xmax / ymax = precomputed max |x| / |dy| slots, else computed here)
 hipError_t conv3d_wgrad(const Src2& x, const float* dy, int lddy, float* dw, Vol vol, int KD,
-                        int Cin, int Cout, int math, float* ws, hipStream_t s);
+                        int Cin, int Cout, int math, float* ws, hipStream_t s,
+                        const unsigned* xmax = nullptr, const unsigned* ymax = nullptr);
 size_t conv3d_wgrad_x_ws_bytes(Vol vol, int KD, int Cin, int Cout);
 bool debug_split_wgrad();  // SPFF_DEBUG_SPLIT (conv3d_x.hip)
 // the split-bf16 fwd and wgrad kernels apply Src2::al / de to a C-channel conv input of
 // a C -> C conv (conv3d_x.hip: the 32-wide tiles, so C == 32)
 bool conv3d_fuses_act(int math, int C);
 hipError_t conv3d_wgrad_x(const Src2& x, const float* dy, int lddy, float* dw, Vol vol, int KD,
-                          int Cin, int Cout, int math, float* ws, hipStream_t s);
+                          int Cin, int Cout, int math, float* ws, hipStream_t s,
+                          const unsigned* xmax = nullptr, const unsigned* ymax = nullptr);
+// SPFF_MATH_F16X3 operand scales (conv3d_x.hip): atomicMax of the largest |element| (float
+// bits) into *slot, which the caller zeroed.  absmax_src covers what a conv reads of x:
+// C channels with the input activation applied, plus (halo) a depth-sharded input's halo
+// slices and a height-sharded one's boundary rows; channel strides must be multiples of 4.
+hipError_t absmax_src(const Src2& x, Vol vol, int C, bool halo, unsigned* slot, hipStream_t s);
+hipError_t absmax_f32(const float* p, int64_t n, unsigned* slot, hipStream_t s);
 // fixed-order sum of the [nsplit][T][kpad][npad] partial slabs into dw[Cout][Cin][T]
 hipError_t conv3d_wgrad_reduce(const float* part, float* dw, int nsplit, int T, int kpad,
                                int npad, int Cin, int Cout, hipStream_t s);
@@ -258,7 +269,15 @@ hipError_t in_bwd_stats(const float* sums, const float* gamma, float* dgamma, fl
 hipError_t in_bwd_apply(const float* y, const float* g, float* dy, const float* mean,
                         const float* rstd, const float* al, const float* de, const float* gamma,
                         const float* A, const float* Bc, const float* k1, const float* k2,
-                        Vol vol, int C, hipStream_t s, float neg = 0.01f);
+                        Vol vol, int C, hipStream_t s, float neg = 0.01f,
+                        unsigned* amax = nullptr);
+// (amax: also atomicMax the largest |dy| (float bits) into *amax -- an SPFF_MATH_F16X3 operand
+// scale for the convs that read dy; the caller zeroed it)
+// a bound on max |lrelu(IN(y))| from the parameters alone, into *slot (float bits): per
+// instance |xhat| <= sqrt(N - 1) (N = instance voxel count, population variance), so
+// |lrelu(gamma xhat + beta)| <= max_c |gamma_c| sqrt(N - 1) + max_c |beta_c| (x 2 for rounding)
+hipError_t act_bound(const float* gamma, const float* beta, int C, double N, unsigned* slot,
+                     hipStream_t s);
 // BatchNorm3d (train: batch statistics over (b,d,h,w) + running-stat update;
 // eval: running statistics).  Per-channel values replicated over b into [B][C].
 hipError_t bn_mean(const float* sums, float* mean, Vol vol, int C, hipStream_t s);

@@ -173,7 +173,7 @@ int build(spff_swin* p) {
   if (c.feature_size < 4 || c.feature_size % 4)
     return sfail(SPFF_EINVAL, "feature_size must be a positive multiple of 4");
   if (c.window < 1 || c.window > 7) return sfail(SPFF_EINVAL, "window must be 1..7");
-  if (c.math < SPFF_MATH_F32 || c.math > SPFF_MATH_BF16X3)
+  if (c.math < SPFF_MATH_F32 || c.math > SPFF_MATH_F16X3)
     return sfail(SPFF_EINVAL, "math must be one of SPFF_MATH_*");
   p->f = c.feature_size;
   p->K = c.num_classes;

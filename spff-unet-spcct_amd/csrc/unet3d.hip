@@ -137,7 +137,7 @@ int build(spff_unet3d* p) {
   if (c.base < 8 || (c.base & (c.base - 1)))
     return ufail(SPFF_EINVAL, "base must be a power of two >= 8");
   if (c.in_ch > 64) return ufail(SPFF_EINVAL, "in_ch > 64 not supported");
-  if (c.math < SPFF_MATH_F32 || c.math > SPFF_MATH_BF16X3)
+  if (c.math < SPFF_MATH_F32 || c.math > SPFF_MATH_F16X3)
     return ufail(SPFF_EINVAL, "math must be one of SPFF_MATH_*");
   if (c.target_depth < 0) return ufail(SPFF_EINVAL, "target_depth must be >= 0");
   p->Dt = c.target_depth > 0 ? c.target_depth : c.depth;

@@ -91,8 +91,9 @@ def default_memory() -> str:
 
 
 # conv arithmetic (include/spff.h SPFF_MATH_*)
-MATH_F32, MATH_BF16X6, MATH_BF16X3 = 0, 1, 2
-MATH_NAMES = {"f32": MATH_F32, "bf16x6": MATH_BF16X6, "bf16x3": MATH_BF16X3}
+MATH_F32, MATH_BF16X6, MATH_BF16X3, MATH_F16X3 = 0, 1, 2, 3
+MATH_NAMES = {"f32": MATH_F32, "bf16x6": MATH_BF16X6, "bf16x3": MATH_BF16X3,
+              "f16x3": MATH_F16X3}
 
 
 def default_math() -> str:

@@ -197,7 +197,7 @@ def config2_oracle():
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("mth", ["bf16x6", "f32"])
+@pytest.mark.parametrize("mth", ["bf16x6", "f32", "f16x3"])
 def test_config2_headline_matches_oracle(config2_oracle, mth):
     import innovative3D.helpers as Hh
     st, x, y, ref_logits, ref_loss = config2_oracle

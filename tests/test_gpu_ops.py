@@ -84,18 +84,19 @@ SPLIT_CASES = [
 ]
 
 
-@pytest.mark.parametrize("math_mode", ["bf16x6", "bf16x3"])
+@pytest.mark.parametrize("math_mode", ["bf16x6", "bf16x3", "f16x3"])
 @pytest.mark.parametrize("case", SPLIT_CASES)
-def test_conv3d_split_bf16(case, math_mode):
+def test_conv3d_split_bf16(case, math_mode, amp=(1.0, 1.0, 1.0)):
     """fwd / dgrad / wgrad on the bf16 matrix cores with the exact 3-plane (2-plane)
-    operand split, against an fp64 conv.  bf16x6 must be as accurate as the fp32
-    MFMA path (error within 4x of it); bf16x3 within 3e-5 of max|ref|."""
+    operand split, against an fp64 conv.  bf16x6 and f16x3 (scaled fp16 planes) must be
+    as accurate as the fp32 MFMA path (error within 4x of it); bf16x3 within 3e-5 of
+    max|ref|.  amp: magnitudes of x, w, dy (f16x3's operand scaling)."""
     B, D, H, W, cin, cout, ksd = case
     mth = E.MATH_NAMES[math_mode]
     g = torch.Generator().manual_seed(7)
-    x = torch.randn(B, cin, D, H, W, generator=g)
-    w = torch.randn(cout, cin, ksd, 3, 3, generator=g) / math.sqrt(cin * ksd * 9)
-    dy = torch.randn(B, cout, D, H, W, generator=g)
+    x = torch.randn(B, cin, D, H, W, generator=g) * amp[0]
+    w = torch.randn(cout, cin, ksd, 3, 3, generator=g) / math.sqrt(cin * ksd * 9) * amp[1]
+    dy = torch.randn(B, cout, D, H, W, generator=g) * amp[2]
     y64 = F.conv3d(x.double(), w.double(), None, padding=(ksd // 2, 1, 1))
     dx64 = torch.nn.grad.conv3d_input(x.shape, w.double(), dy.double(), padding=(ksd // 2, 1, 1))
     dw64 = torch.nn.grad.conv3d_weight(x.double(), w.shape, dy.double(), padding=(ksd // 2, 1, 1))
@@ -127,10 +128,19 @@ def test_conv3d_split_bf16(case, math_mode):
         e32 = float((out[E.MATH_F32][k] - ref).abs().max())
         ex = float((out[mth][k] - ref).abs().max())
         scale = float(ref.abs().max())
-        if math_mode == "bf16x6":
+        print(f"{math_mode} {case} amp={amp} op {k}: max err {ex / scale:.2e} of max|ref| "
+              f"(f32 path {e32 / scale:.2e})")
+        if math_mode in ("bf16x6", "f16x3"):
             assert ex <= 4 * e32 + 1e-7 * scale, (k, ex, e32)
         else:
             assert ex <= 3e-5 * scale, (k, ex, scale)
+
+
+@pytest.mark.parametrize("amp", [(1e-12, 1e6, 1e-9), (3e4, 1e-5, 2e5), (1e-30, 1e-3, 1e20)])
+def test_conv3d_f16x3_operand_scaling(amp):
+    """f16x3 scales each operand by a power of two from its on-device max |element|: far
+    outside fp16's range (1e-30 .. 1e20) it is as accurate as the fp32 MFMA path."""
+    test_conv3d_split_bf16((1, 4, 16, 16, 32, 32, 3), "f16x3", amp)
 
 
 @pytest.mark.parametrize("K,shape", [(13, (2, 5, 16, 16)), (9, (1, 16, 32, 32)), (2, (1, 3, 8, 8))])

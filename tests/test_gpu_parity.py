@@ -54,10 +54,11 @@ def near_tie_mask(ref_logits, tol):
     return (top2[:, 1] - top2[:, 0]) < tol
 
 
-@pytest.mark.parametrize("mth", ["f32", "bf16x6", "bf16x3"])
+@pytest.mark.parametrize("mth", ["f32", "bf16x6", "bf16x3", "f16x3"])
 @pytest.mark.parametrize("name", fixture_names())
 def test_network_matches_reference(name, mth):
-    """f32 and bf16x6 (the fp32-faithful split) are held to the same bar;
+    """f32, bf16x6 (the fp32-faithful split) and f16x3 (scaled fp16 planes) are held to
+    the same bar;
     bf16x3 (opt-in, ~2^-17 per product) to the same logits / argmax bar, loss
     within 1e-4 and gradients within max(5e-3, 64 x the fp32 oracle's error)."""
     d = load(name)
