@@ -534,9 +534,11 @@ def main():
     ap.add_argument("--classes", type=int, default=13)
     ap.add_argument("--base", type=int, default=32)
     ap.add_argument("--cpu-baseline", choices=("auto", "skip"), default="auto")
-    ap.add_argument("--math", choices=("f32", "bf16x6", "bf16x3", "f16x3"), default="bf16x6",
-                    help="conv arithmetic: bf16x6 = fp32 operands split exactly into 3 bf16 "
-                         "planes, 6 products, fp32 accumulate (fp32 accuracy class; default)")
+    ap.add_argument("--math", choices=("f32", "bf16x6", "bf16x3", "f16x3"), default="f16x3",
+                    help="conv arithmetic: f16x3 (default) = each operand scaled by a power of "
+                         "two from its max |element| and split into 2 fp16 planes, 3 products, "
+                         "fp32 accumulate (measured as close to fp64 as the f32 path); bf16x6 = "
+                         "3 exact bf16 planes, 6 products")
     ap.add_argument("--workload", choices=("patch128", "volume512", "registry", "unet3d", "swin"),
                     default="patch128",
                     help="patch128 = the headline (BASELINE configs[1]): batch data parallelism; "

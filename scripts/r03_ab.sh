@@ -1,33 +1,20 @@
 #!/bin/bash
-# GPU call: correctness of the touched kernels, then conv-kernel A/B of variant libraries
-# (scripts/build_variant.py) against the in-tree library on the same box.
-#   bash scripts/r03_ab.sh [TESTS] -- variantA.so variantB.so ...
+# One GPU call: quick f16x3 correctness (op-level + reference fixtures) of the in-tree
+# library, then an A/B of bench.py between it and each variant library given (alternating,
+# REPS times, one box).  Each GPU step under its own timeout; stops at the first failure.
 set -u
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-mkdir -p gpurun_out
-T=${AB_TESTS:-"tests/test_gpu_ops.py tests/test_gpu_parity.py"}
-if [ -n "$T" ]; then
-  timeout -k 10 600 python -u -m pytest $T -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/ab_tests.log 2>&1
-  t=$?; echo "tests rc=$t"; tail -2 gpurun_out/ab_tests.log
-  [ $t -le 1 ] || exit $t
-fi
-OUT=gpurun_out/ab_kbench.log
-: > $OUT
-for lib in base "$@"; do
-  [ -n "${KV_SKIP:-}" ] && break
-  echo "=== $lib" >> $OUT
-  if [ "$lib" = base ]; then
-    timeout -k 10 240 python scripts/kbench.py --math bf16x6 --iters 10 --ops ${KV_OPS:-fwd,dgrad,wgrad} >> $OUT 2>&1 || exit $?
-  else
-    SPFF_LIB=$lib timeout -k 10 240 python scripts/kbench.py --math bf16x6 --iters 10 --ops ${KV_OPS:-fwd,dgrad,wgrad} >> $OUT 2>&1 || exit $?
-  fi
-done
-for lib in base "$@"; do
-  if [ "$lib" = base ]; then
-    timeout -k 10 300 python bench.py --steps 10 --warmup 3 --cpu-baseline skip > gpurun_out/ab_bench_base.log 2>&1 || exit $?
-  else
-    SPFF_LIB=$lib timeout -k 10 300 python bench.py --steps 10 --warmup 3 --cpu-baseline skip > gpurun_out/ab_bench_$(basename $lib .so).log 2>&1 || exit $?
-  fi
+O=gpurun_out/ab
+rm -rf $O && mkdir -p $O
+PT="python -u -m pytest -x -v -s --timeout 300 --timeout-method thread -p no:cacheprovider"
+timeout -k 10 300 $PT tests/test_gpu_ops.py -m gpu -k "split or scaling" > $O/ops.log 2>&1 || { echo "ops rc=$?"; exit 1; }
+timeout -k 10 300 $PT tests/test_gpu_parity.py -m gpu -k "f16x3" > $O/parity.log 2>&1 || { echo "parity rc=$?"; exit 1; }
+for rep in $(seq 1 ${REPS:-2}); do
+  timeout -k 10 300 python bench.py --steps 20 --warmup 3 --cpu-baseline skip > $O/base_$rep.log 2>&1 || { echo "bench rc=$?"; exit 1; }
+  for lib in "$@"; do
+    n=$(basename "$lib" .so)
+    SPFF_LIB=$lib timeout -k 10 300 python bench.py --steps 20 --warmup 3 --cpu-baseline skip > $O/${n}_$rep.log 2>&1 || { echo "bench $n rc=$?"; exit 1; }
+  done
 done
 echo "[r03_ab] done"

@@ -74,6 +74,11 @@
 // (profiles/r02/ab_x32nw_branch_consistent.log; tests/test_gpu_sharded.py now judges that way)
 #define SPFF_X32NW 4
 #endif
+#ifndef SPFF_X64NW
+// waves per 64-wide f16x3 workgroup: 4 (a 2 x 8 x 16 tile in 80 KB of LDS -- two fp16 planes
+// leave room for two workgroups per CU, as the 32-wide tiles) or 8 (one 2 x 16 x 16 tile)
+#define SPFF_X64NW 4
+#endif
 #ifndef SPFF_XIGLP
 #define SPFF_XIGLP -1
 #endif
@@ -193,10 +198,17 @@ constexpr int xt_td(int BN) { return (BN == 32 && SPFF_X16 && SPFF_X32T) ? 4 : X
 constexpr int xt_mb(int BN) { return (BN == 32 && SPFF_X16 && SPFF_X32T) ? 4 : 2; }
 // waves of a BN-wide workgroup (4-wave 32-wide tiles: SPFF_X32NW, 2-deep tiles only)
 // (16-wide tiles, Cout <= 16 -- the SwinUNETR's C = 12 convs: also 4 waves, 2 WGs / CU)
-constexpr int xt_nw(int BN) {
-  return (BN <= 32 && SPFF_X16 && !(BN == 32 && SPFF_X32T)) ? SPFF_X32NW : 8;
+// (64-wide f16x3 tiles: SPFF_X64NW)
+constexpr int xt_nw(int BN, int NS) {
+  return (BN <= 32 && SPFF_X16 && !(BN == 32 && SPFF_X32T)) ? SPFF_X32NW
+         : (BN == 64 && NS == NS_F16 && SPFF_X16)             ? SPFF_X64NW
+                                                                : 8;
 }
 }  // namespace
+// template plane count of a math mode
+static int ns_of(int math) {
+  return math == SPFF_MATH_F16X3 ? NS_F16 : math == SPFF_MATH_BF16X3 ? 2 : 3;
+}
 
 // 16x16x32 tap-quad schedule (X16): k = 4 lane groups x 8 channels, lane group g
 // at its own tap.  A ds_read_b128 lane group mixes rows {0-3, 12-15} of k-group
@@ -797,7 +809,7 @@ __global__ void k_splitk_reduce(const float* __restrict__ part, int nsplit, int6
   }
 }
 
-template <int BN, int KD, int NS, bool HR, int MB = xt_mb(BN), int NW = xt_nw(BN),
+template <int BN, int KD, int NS, bool HR, int MB = xt_mb(BN), int NW = xt_nw(BN, NS),
           int TD = xt_td(BN)>
 static hipError_t launch_fwd_xh(const Src2& x, const uint4* wx, const Dst2& y, Vol vol, int K,
                                 int nkc, int N, int npad, hipStream_t s, float* part, int nsplit,
@@ -889,8 +901,8 @@ bool conv3d_fuses_act(int math, int C) {
   return math != SPFF_MATH_F32 && debug_split_dir() == 7 && C == 32;
 }
 // tiles of a BN-wide launch (the fused IN statistics are per (tile, out channel))
-static int64_t xt_ntiles(Vol vol, int BN) {
-  const int nw = xt_nw(BN);
+static int64_t xt_ntiles(Vol vol, int BN, int ns) {
+  const int nw = xt_nw(BN, ns);
   const int td = xt_td(BN), th = SPFF_X16 ? 2 * nw * xt_mb(BN) / td : nw * xt_mb(BN);
   return (int64_t)vol.B * cdiv(vol.D, td) * cdiv(vol.H, th) * cdiv(vol.W, XT_W);
 }
@@ -901,10 +913,10 @@ namespace {
 struct SplitK {
   int nsplit = 1, kps = 0;
 };
-SplitK splitk_plan(Vol vol, const XDims& d) {
+SplitK splitk_plan(Vol vol, const XDims& d, int nsp) {
   SplitK k;
   k.kps = d.nkc;
-  const int64_t wgs = xt_ntiles(vol, d.BN) * (d.npad / d.BN);
+  const int64_t wgs = xt_ntiles(vol, d.BN, nsp) * (d.npad / d.BN);
   if (wgs >= 256 || d.nkc < 4) return k;
   int ns = (int)std::min<int64_t>(d.nkc / 2, (512 + wgs - 1) / wgs);
   ns = std::max(1, ns);
@@ -1067,7 +1079,7 @@ static hipError_t run_x(const Src2& x, const uint4* wu, const Dst2& y, Vol vol, 
   // (32x32x16, MB = 4, 2 x 32 x 16 tiles for Cout <= 32: fits LDS but spills 91 VGPRs)
   // (32x32x16 schedule, NW = 4 waves, 2 x 8 x 16 tiles: measured 6 % slower; the 16x16x32
   // schedule takes NW = 4 for BN 32 by default, SPFF_X32NW)
-  SplitK k = ws ? splitk_plan(vol, d) : SplitK{1, d.nkc};
+  SplitK k = ws ? splitk_plan(vol, d, NS) : SplitK{1, d.nkc};
   float* part = k.nsplit > 1 ? ws : nullptr;
   if (d.BN == 64)
     return KD == 3
@@ -1089,36 +1101,40 @@ size_t conv3d_splitk_bytes(Vol vol, int KD, int Cin, int Cout) {
   size_t b = 0;
   for (int dg = 0; dg < 2; ++dg) {
     const XDims d = xdims(KD, Cin, Cout, dg != 0);
-    const SplitK k = splitk_plan(vol, d);
-    if (k.nsplit > 1) b = std::max(b, (size_t)k.nsplit * nvox(vol) * d.npad * sizeof(float));
+    for (int ns : {3, NS_F16}) {  // (the tile counts of every arithmetic)
+      const SplitK k = splitk_plan(vol, d, ns);
+      if (k.nsplit > 1) b = std::max(b, (size_t)k.nsplit * nvox(vol) * d.npad * sizeof(float));
+    }
   }
   return b;
 }
 
 bool conv3d_splits_depth(Vol vol, int KD, int Cin_w, int Cout_w, bool dgrad, int math) {
   const XDims d = xdims(KD, Cin_w, Cout_w, dgrad);
-  return KD == 3 && use_split(vol, math, dgrad) && splitk_plan(vol, d).nsplit == 1 &&
+  return KD == 3 && use_split(vol, math, dgrad) && splitk_plan(vol, d, ns_of(math)).nsplit == 1 &&
          cdiv(vol.D, xt_td(d.BN)) >= 3;
 }
 bool conv3d_splits_height(Vol vol, int KD, int Cin_w, int Cout_w, bool dgrad, int math) {
   const XDims d = xdims(KD, Cin_w, Cout_w, dgrad);
-  const int nw = xt_nw(d.BN);
+  const int nw = xt_nw(d.BN, ns_of(math));
   const int th = SPFF_X16 ? 2 * nw * xt_mb(d.BN) / xt_td(d.BN) : nw * xt_mb(d.BN);
-  return use_split(vol, math, dgrad) && splitk_plan(vol, d).nsplit == 1 && cdiv(vol.H, th) >= 3;
+  return use_split(vol, math, dgrad) && splitk_plan(vol, d, ns_of(math)).nsplit == 1 &&
+         cdiv(vol.H, th) >= 3;
 }
 size_t conv3d_stats_bytes(Vol vol, int KD, int Cin, int Cout) {
   const XDims d = xdims(KD, Cin, Cout, false);
-  return (size_t)xt_ntiles(vol, d.BN) * (2 * d.npad + 1) * sizeof(float);
+  const int64_t nt = std::max(xt_ntiles(vol, d.BN, 3), xt_ntiles(vol, d.BN, NS_F16));
+  return (size_t)nt * (2 * d.npad + 1) * sizeof(float);
 }
 bool conv3d_fuses_stats(Vol vol, int KD, int Cin, int Cout, int math) {
   const XDims d = xdims(KD, Cin, Cout, false);
-  return use_split(vol, math, false) && vol.dh == 0 && splitk_plan(vol, d).nsplit == 1;
+  return use_split(vol, math, false) && vol.dh == 0 && splitk_plan(vol, d, ns_of(math)).nsplit == 1;
 }
-hipError_t conv3d_in_stats_fin(const float* stats, Vol vol, int KD, int Cin, int Cout,
+hipError_t conv3d_in_stats_fin(const float* stats, Vol vol, int KD, int Cin, int Cout, int math,
                                const float* gamma, const float* beta, float* mean, float* rstd,
                                float* al, float* de, hipStream_t s) {
   const XDims d = xdims(KD, Cin, Cout, false);
-  const int64_t nt = xt_ntiles(vol, d.BN);
+  const int64_t nt = xt_ntiles(vol, d.BN, ns_of(math));
   hipLaunchKernelGGL(k_in_stats_fin, dim3(vol.B * Cout), dim3(256), 0, s, stats, (int)nt,
                      (int)(nt / vol.B), d.npad, Cout, gamma, beta, mean, rstd, al, de);
   return hipGetLastError();

@@ -771,7 +771,7 @@ int fwd_block(spff_plan* p, Blk& b, const Src2& in, int pool = -1) {
                b.Cin, C, false, fuse1 ? p->F(p->cst) : nullptr, f16_slot(p, b, F16_IN),
                f16_slot(p, b, F16_W1)));
   if (fuse1)
-    HIPCK(conv3d_in_stats_fin(p->F(p->cst), v, KD, b.Cin, C, p->P(b.g1), p->P(b.b1),
+    HIPCK(conv3d_in_stats_fin(p->F(p->cst), v, KD, b.Cin, C, math, p->P(b.g1), p->P(b.b1),
                               p->F(b.mean1), p->F(b.rstd1), p->F(b.al1), p->F(b.de1), p->st));
   else
     CK(in_stats(p, v, C, b.y1, b.mean1, b.rstd1, b.al1, b.de1, b.g1, b.b1));
@@ -787,7 +787,7 @@ int fwd_block(spff_plan* p, Blk& b, const Src2& in, int pool = -1) {
                false, fuse2 ? p->F(p->cst) : nullptr, f16_slot(p, b, F16_A1),
                f16_slot(p, b, F16_W2)));
   if (fuse2)
-    HIPCK(conv3d_in_stats_fin(p->F(p->cst), v, KD, C, C, p->P(b.g2), p->P(b.b2), p->F(b.mean2),
+    HIPCK(conv3d_in_stats_fin(p->F(p->cst), v, KD, C, C, math, p->P(b.g2), p->P(b.b2), p->F(b.mean2),
                               p->F(b.rstd2), p->F(b.al2), p->F(b.de2), p->st));
   else
     CK(in_stats(p, v, C, b.y2, b.mean2, b.rstd2, b.al2, b.de2, b.g2, b.b2));

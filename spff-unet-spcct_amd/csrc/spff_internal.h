@@ -105,7 +105,7 @@ bool conv3d_splits_depth(Vol vol, int KD, int Cin_w, int Cout_w, bool dgrad, int
 bool conv3d_splits_height(Vol vol, int KD, int Cin_w, int Cout_w, bool dgrad, int math);
 bool conv3d_fuses_stats(Vol vol, int KD, int Cin, int Cout, int math);
 size_t conv3d_stats_bytes(Vol vol, int KD, int Cin, int Cout);
-hipError_t conv3d_in_stats_fin(const float* stats, Vol vol, int KD, int Cin, int Cout,
+hipError_t conv3d_in_stats_fin(const float* stats, Vol vol, int KD, int Cin, int Cout, int math,
                                const float* gamma, const float* beta, float* mean, float* rstd,
                                float* al, float* de, hipStream_t s);
 size_t conv3d_splitk_bytes(Vol vol, int KD, int Cin_w, int Cout_w);

@@ -362,7 +362,7 @@ int conv_in(spff_swin* p, const Src2& in, int64_t w, const Vol& v, int Cin, int 
   SHIPCK(conv3d_run(in, p->F(p->wt), dst1(p->F(y), C), v, 3, Cin, C, false, math, p->st,
                     p->F(p->wg_ws), fuse ? p->F(p->cst) : nullptr));
   if (fuse) {
-    SHIPCK(conv3d_in_stats_fin(p->F(p->cst), v, 3, Cin, C, p->F(p->ones), p->F(p->zeros),
+    SHIPCK(conv3d_in_stats_fin(p->F(p->cst), v, 3, Cin, C, math, p->F(p->ones), p->F(p->zeros),
                                p->F(st4[0]), p->F(st4[1]), p->F(st4[2]), p->F(st4[3]), p->st));
     return SPFF_OK;
   }

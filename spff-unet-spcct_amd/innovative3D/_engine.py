@@ -97,8 +97,9 @@ MATH_NAMES = {"f32": MATH_F32, "bf16x6": MATH_BF16X6, "bf16x3": MATH_BF16X3,
 
 
 def default_math() -> str:
-    """Conv arithmetic for new plans: $SPFF_MATH, else "bf16x6" (fp32-faithful split)."""
-    m = os.environ.get("SPFF_MATH", "bf16x6")
+    """Conv arithmetic for new plans: $SPFF_MATH, else "f16x3" (scaled fp16 planes, measured
+    as close to fp64 as the fp32 MFMA path)."""
+    m = os.environ.get("SPFF_MATH", "f16x3")
     if m not in MATH_NAMES:
         raise SpffError(f"SPFF_MATH={m!r}: expected one of {sorted(MATH_NAMES)}")
     return m

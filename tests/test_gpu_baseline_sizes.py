@@ -3,7 +3,7 @@ Marked gpu; the CPU oracle runs on the host cores of the GPU box.
 
 * configs[1] (the headline): SPFF-UNet, batch 2 x 5 x 128^3, K = 13, base 32,
   weights from weightgen seed 0, inputs synthetic_batch(seed 0) -- bench.py's
-  rank-0 batch.  Engine (f32 and bf16x6) vs oracle/spff_oracle.py (fp32
+  rank-0 batch.  Engine (f32, bf16x6, f16x3) vs oracle/spff_oracle.py (fp32
   PyTorch-CPU restatement pinned to the reference's own outputs by
   tests/test_oracle_golden.py): logits within 1e-3 (north star), argmax
   identical except at near-ties (reference top-2 margin < 2 max|dlogit|;
@@ -197,7 +197,9 @@ def config2_oracle():
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("mth", ["bf16x6", "f32", "f16x3"])
+# (bf16x6, round 2's default: profiles/r02/gpu_baseline_sizes_parity.txt and
+#  profiles/r03/pytest_gpu_head.log hold its config-2 runs; dropped here for suite time)
+@pytest.mark.parametrize("mth", ["f16x3", "f32"])
 def test_config2_headline_matches_oracle(config2_oracle, mth):
     import innovative3D.helpers as Hh
     st, x, y, ref_logits, ref_loss = config2_oracle
@@ -247,7 +249,7 @@ def _sh_worker(rank, world, port, out):
     core, st = _spff_state(SH_SHAPE[2])
     core.load_state_dict({k: torch.from_numpy(v) for k, v in st.items()})
     core = core.to(DEV)
-    core.math = "bf16x6"
+    core.math = "f16x3"
     x, y = _sh_data()
     off, d = shard_bounds(SH_SHAPE[2], world, rank)
     step = DepthShardedSPFF(core, K13, 255)
@@ -292,7 +294,7 @@ def test_config4_sharded_512_matches_oracle(tmp_path):
         masks[k] = torch.from_numpy(cat) if cat.dtype == np.bool_ else torch.from_numpy(cat.astype(np.int64))
     ref_grads = _oracle_grads(st, x, y, masks)
     grads = {k: torch.from_numpy(parts[0]["g_" + k]) for k in ref_grads[0]}
-    _compare("config4 path: 1x5x16x512^2 depth-sharded world 2 (bf16x6)", lg,
+    _compare("config4 path: 1x5x16x512^2 depth-sharded world 2 (f16x3)", lg,
              float(parts[0]["loss"]), grads, ref_logits, ref_loss, ref_grads,
              scales=_mag_scales(st, ref_grads[0]))
 
@@ -320,7 +322,7 @@ def _hs_worker(rank, world, port, out):
     core, st = _spff_state(HS_SHAPE[2], in_ch=1)
     core.load_state_dict({k: torch.from_numpy(v) for k, v in st.items()})
     core = core.to(DEV)
-    core.math = "bf16x6"
+    core.math = "f16x3"
     x, y = _hs_data()
     off, h = height_bounds(HS_SHAPE[3], world, rank)
     step = HeightShardedSPFF(core, K13, 255)
@@ -366,7 +368,7 @@ def test_registry_height_sharded_512_matches_oracle(tmp_path):
         masks[k] = torch.from_numpy(cat) if cat.dtype == np.bool_ else torch.from_numpy(cat.astype(np.int64))
     ref_grads = _oracle_grads(st, x, y, masks)
     grads = {k: torch.from_numpy(parts[0]["g_" + k]) for k in ref_grads[0]}
-    _compare("registry 1x1x5x512^2 height-sharded world 2 (bf16x6)", lg,
+    _compare("registry 1x1x5x512^2 height-sharded world 2 (f16x3)", lg,
              float(parts[0]["loss"]), grads, ref_logits, ref_loss, ref_grads,
              scales=_mag_scales(st, ref_grads[0]))
 
@@ -387,7 +389,7 @@ def test_config5_swin_128_matches_oracle():
     sd = m.state_dict()
     sd.update({k: torch.from_numpy(v) for k, v in st.items()})
     m.load_state_dict(sd, strict=True)
-    m.math = "bf16x6"
+    m.math = "f16x3"
     m = m.to(DEV)
     logits = m(x.to(DEV))
     loss = M._SwinLoss.apply(logits, y.to(DEV), K13, 255, False, 0.5)
@@ -405,5 +407,5 @@ def test_config5_swin_128_matches_oracle():
         S.ACT_MASKS = None
     named = dict(m.named_parameters())
     grads = {k: named[k].grad for k in refs[0][2]}
-    _compare("config5 SwinUNETR 2x1x128^3 (bf16x6)", logits.detach().cpu(), float(loss), grads,
+    _compare("config5 SwinUNETR 2x1x128^3 (f16x3)", logits.detach().cpu(), float(loss), grads,
              refs[0][0], refs[0][1], (refs[0][2], refs[1][2]))

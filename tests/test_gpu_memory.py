@@ -40,7 +40,7 @@ def _run(core, x, y):
             {k: p.grad.cpu() for k, p in core.named_parameters(remove_duplicate=False)})
 
 
-@pytest.mark.parametrize("math_mode", ["f32", "bf16x6"])
+@pytest.mark.parametrize("math_mode", ["f32", "bf16x6", "f16x3"])
 def test_lean_equals_full_bitwise(math_mode):
     from innovative3D.synthetic import synthetic_batch
     x, y = synthetic_batch(*SHAPE, num_classes=K, ignore_frac=0.05, seed=3)

@@ -175,7 +175,8 @@ def _worker(rank, world, port, math_mode, out, depth):
 
 
 @pytest.mark.parametrize("world,math_mode,depth", [
-    (2, "f32", 8), (4, "f32", 8), (2, "bf16x6", 8), (4, "bf16x6", 8), (2, "bf16x6", 16)])
+    (2, "f32", 8), (4, "f32", 8), (2, "bf16x6", 8), (4, "bf16x6", 8), (2, "bf16x6", 16),
+    (2, "f16x3", 8)])
 def test_depth_sharded_engine_matches_unsharded(tmp_path, world, math_mode, depth):
     import innovative3D.helpers as Hh
     core = _model(math_mode, depth)
@@ -205,7 +206,7 @@ def test_depth_sharded_engine_matches_unsharded(tmp_path, world, math_mode, dept
 
 @pytest.mark.parametrize("world,math_mode,case,memory", [
     (2, "f32", "small", None), (4, "f32", "small", None), (2, "bf16x6", "small", None),
-    (4, "bf16x6", "small", None),
+    (4, "bf16x6", "small", None), (2, "f16x3", "small", None),
     # the lean saved-activation layout (recomputed block outputs / decoder inputs)
     (2, "bf16x6", "small", "lean")])
 def test_height_sharded_engine_matches_unsharded(tmp_path, world, math_mode, case, memory):

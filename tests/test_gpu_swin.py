@@ -42,7 +42,7 @@ def _engine_model(st, K, mth):
     return m.to(DEV)
 
 
-@pytest.mark.parametrize("mth", ["f32", "bf16x6"])
+@pytest.mark.parametrize("mth", ["f32", "bf16x6", "f16x3"])
 @pytest.mark.parametrize("shape", [(2, 32, 64, 32), (1, 64, 64, 64), (1, 32, 32, 64)])
 def test_swin_matches_oracle(shape, mth):
     B, D, H, W = shape

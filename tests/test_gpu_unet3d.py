@@ -91,7 +91,7 @@ def oracle_grads(d, hooks, dtype):
     return {k: v.grad.detach().double().numpy() for k, v in P.items()}
 
 
-@pytest.mark.parametrize("mth", ["f32", "bf16x6"])
+@pytest.mark.parametrize("mth", ["f32", "bf16x6", "f16x3"])
 @pytest.mark.parametrize("name", unet3d_fixture_names())
 def test_unet3d_matches_reference(name, mth):
     d = load(name)
