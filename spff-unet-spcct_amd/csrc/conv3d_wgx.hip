@@ -36,6 +36,12 @@
 #ifndef SPFF_WXUNROLL
 #define SPFF_WXUNROLL 4  // k-step (W-row pair) loop unroll of k_conv3d_wgrad_x16
 #endif
+#ifndef SPFF_WXUNROLL2
+// the same for two-plane operands (bf16x3, f16x3): unrolled 4 deep the compiler hoists the
+// fragment reads of later k-steps (fewer MFMAs per step) into 256 VGPRs + 11-23 spilled;
+// 2 deep: 218 VGPRs, no spill
+#define SPFF_WXUNROLL2 2
+#endif
 
 namespace spff {
 
@@ -486,7 +492,8 @@ __global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x16(
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
       ab[j] = aoff[j] + (aoff[j] >= (KD - rot) * PL ? (rot - KD) * PL : rot * PL);
-#pragma unroll SPFF_WXUNROLL
+    constexpr int KSU = NPL == 2 ? SPFF_WXUNROLL2 : SPFF_WXUNROLL;
+#pragma unroll KSU
     for (int ks = 0; ks < WX_TH / 2; ++ks) {
       bf16x8 bq[NCB][NPL];
 #pragma unroll
