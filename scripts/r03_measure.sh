@@ -16,7 +16,7 @@ run prof
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --cpu-baseline skip ${BENCH_ARGS:-} > $O/prof.log 2>&1 || { echo "prof rc=$?"; exit 1; }
 if [ "${M3_KBENCH:-1}" = 1 ]; then
   run kbench
-  timeout -k 10 300 python scripts/kbench.py --math bf16x6 --iters 10 > $O/kbench.log 2>&1 || { echo "kbench rc=$?"; exit 1; }
+  timeout -k 10 300 python scripts/kbench.py --math ${KB_MATH:-f16x3} --iters 10 > $O/kbench.log 2>&1 || { echo "kbench rc=$?"; exit 1; }
 fi
 if [ "${M3_PMC:-1}" = 1 ]; then
   run pmc

@@ -932,28 +932,12 @@ SplitK splitk_plan(Vol vol, const XDims& d, int nsp) {
 // its bits), by integer atomicMax -- order-independent, so deterministic -- into two
 // slots after the packed weight image: [0] max |w| (conv3d_pack zeroes both and fills
 // it), [1] max |x| (conv3d_run, over exactly what the launch reads).
-__device__ __forceinline__ float wave_max(float m) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-  return m;
-}
-__device__ __forceinline__ void block_max_to(float m, unsigned* slot) {
-  __shared__ float wm[16];
-  m = wave_max(m);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (lane == 0) wm[wave] = m;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) m = fmaxf(m, wm[w]);
-    if (m > 0.f) atomicMax(slot, __float_as_uint(m));
-  }
-}
 __global__ __launch_bounds__(256) void k_absmax_f32(const float* __restrict__ p, int64_t n,
                                                     unsigned* __restrict__ slot) {
   float m = 0.f;
   for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
     m = fmaxf(m, fabsf(p[i]));
-  block_max_to(m, slot);
+  block_amax(m, slot);
 }
 // |elements| of channels [c, c + 4) of one voxel's row (4-aligned, one source), input
 // activation applied; channels >= C (row padding) ignored
@@ -976,7 +960,8 @@ __device__ __forceinline__ float amax4(const float* row, const Src2& x, int b, i
 // halo slices of a depth-sharded input when included), and the height-sharded boundary
 // rows rlo / rhi ([B][D][W][ldr]) when withrows
 __global__ __launch_bounds__(256) void k_absmax_src(Src2 x, Vol vol, int C, int dlo, int dhi,
-                                                    int withrows, unsigned* __restrict__ slot) {
+                                                    int withrows, unsigned* __restrict__ slot,
+                                                    const unsigned* __restrict__ also) {
   const int C4 = (C + 3) >> 2, H = vol.H, W = vol.W, nd = dhi - dlo;
   const int64_t total = (int64_t)vol.B * nd * H * W * C4;
   float m = 0.f;
@@ -1004,19 +989,49 @@ __global__ __launch_bounds__(256) void k_absmax_src(Src2 x, Vol vol, int C, int 
       }
     }
   }
-  block_max_to(m, slot);
+  if (also && blockIdx.x == 0) m = fmaxf(m, __uint_as_float(*also));
+  block_amax(m, slot);
+}
+// a dense [n4] float4 array (one source, no padding channels, no activation, no halo):
+// pure streaming, 4 loads in flight per thread
+__global__ __launch_bounds__(256) void k_absmax_dense(const float4* __restrict__ p, int64_t n4,
+                                                      unsigned* __restrict__ slot,
+                                                      const unsigned* __restrict__ also) {
+  float m = 0.f;
+  const int64_t st = (int64_t)gridDim.x * 256;
+  int64_t i = blockIdx.x * 256 + threadIdx.x;
+  for (; i + 3 * st < n4; i += 4 * st) {
+    float4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = p[i + u * st];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      m = fmaxf(m, fmaxf(fmaxf(fabsf(v[u].x), fabsf(v[u].y)), fmaxf(fabsf(v[u].z), fabsf(v[u].w))));
+  }
+  for (; i < n4; i += st) {
+    const float4 v = p[i];
+    m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+  }
+  if (also && blockIdx.x == 0) m = fmaxf(m, __uint_as_float(*also));
+  block_amax(m, slot);
 }
 static unsigned absmax_grid(int64_t n) {
   return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 2047) / 2048, 1024));
 }
-hipError_t absmax_src(const Src2& x, Vol vol, int C, bool halo, unsigned* slot, hipStream_t s) {
+hipError_t absmax_src(const Src2& x, Vol vol, int C, bool halo, unsigned* slot, hipStream_t s,
+                      const unsigned* also) {
   if ((x.ld0 & 3) || (x.ld1 & 3) || (x.split & 3) || (x.rows() && (x.ldr & 3)))
     return hipErrorInvalidValue;
   const int dlo = halo && vol.dh && !x.zlo ? -vol.dh : 0;
   const int dhi = vol.D + (halo && vol.dh && !x.zhi ? vol.dh : 0);
   const int64_t n = (int64_t)vol.B * (dhi - dlo) * vol.H * vol.W * ((C + 3) / 4);
+  if (!x.al && dlo == 0 && dhi == vol.D && !(halo && x.rows()) && x.split >= C && x.ld0 == C) {
+    hipLaunchKernelGGL(k_absmax_dense, dim3(absmax_grid(n)), dim3(256), 0, s,
+                       reinterpret_cast<const float4*>(x.p0), n, slot, also);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(k_absmax_src, dim3(absmax_grid(n)), dim3(256), 0, s, x, vol, C, dlo, dhi,
-                     halo && x.rows() ? 1 : 0, slot);
+                     halo && x.rows() ? 1 : 0, slot, also);
   return hipGetLastError();
 }
 hipError_t absmax_f32(const float* p, int64_t n, unsigned* slot, hipStream_t s) {

@@ -731,13 +731,33 @@ Src2 act_src(const spff_plan* p, const Blk& b) {
 // fp16 planes' scale) is precomputed once per step and shared by the convs that read the
 // tensor, instead of one absmax pass per launch: per block, slot F16_W1 / F16_W2 max |w| and
 // F16_A1 a parameter bound on a1 = lrelu(IN(y1)) (act_bound), all in one batch at the
-// forward start; F16_IN one pass over the block input before its first conv; F16_DY2 /
+// forward start; F16_OUT from the block-output apply (act_apply[_pool]) as it writes out;
+// the block input: an encoder's is the previous block's pooled output, bounded by its
+// F16_OUT; a decoder's [up | skip] takes one pass over the up part (F16_IN) max-ed with the
+// skip encoder's F16_OUT; the first block's a pass over the network input; F16_DY2 /
 // F16_DA1 from in_bwd_apply as it writes them.  Sharded plans compute them per launch
 // (their convs also read halo slices / boundary rows that arrive later).
-enum { F16_IN = 0, F16_A1, F16_DY2, F16_DA1, F16_W1, F16_W2 };
+enum { F16_IN = 0, F16_A1, F16_DY2, F16_DA1, F16_W1, F16_W2, F16_OUT };
 unsigned* f16_slot(const spff_plan* p, const Blk& b, int k) {
   if (p->cfg.math != SPFF_MATH_F16X3 || p->co.on() || p->hsh) return nullptr;
   return reinterpret_cast<unsigned*>(p->ws + p->fsl) + 8 * (int)(&b - p->blk) + k;
+}
+// the slot bounding block b's first-conv input (see above; null: not f16x3 / sharded)
+const unsigned* f16_in_slot(const spff_plan* p, const Blk& b) {
+  const int bi = (int)(&b - p->blk);
+  if (bi >= 1 && bi <= 3) return f16_slot(p, p->blk[bi - 1], F16_OUT);
+  return f16_slot(p, b, F16_IN);
+}
+int f16_in_max(spff_plan* p, const Blk& b, const Src2& in, const Vol& v) {
+  unsigned* sl = f16_slot(p, b, F16_IN);
+  const int bi = (int)(&b - p->blk);
+  if (!sl || (bi >= 1 && bi <= 3)) return SPFF_OK;
+  if (bi >= 4)  // [up | skip]: the up part here, the skip encoder's max from its apply
+    HIPCK(absmax_src(src1(in.p0, in.ld0), v, in.split, false, sl, p->st,
+                     f16_slot(p, p->blk[6 - bi], F16_OUT)));
+  else
+    HIPCK(absmax_src(in, v, b.Cin, false, sl, p->st));
+  return SPFF_OK;
 }
 int f16_param_slots(spff_plan* p) {
   if (!f16_slot(p, p->blk[0], 0)) return SPFF_OK;
@@ -763,12 +783,12 @@ int fwd_block(spff_plan* p, Blk& b, const Src2& in, int pool = -1) {
   HIPCK(conv3d_pack(p->P(b.c1.w), p->F(p->wt), v, KD, b.Cin, C, false, math, p->st,
                     f16_slot(p, b, F16_W1)));
   const double V = (double)nvox(v), T = 9.0 * KD;
-  if (unsigned* sl = f16_slot(p, b, F16_IN)) HIPCK(absmax_src(in, v, b.Cin, false, sl, p->st));
+  CK(f16_in_max(p, b, in, v));
   // InstanceNorm statistics fused into the conv epilogue where the split kernel
   // runs unsharded without split-K; otherwise the two slab_reduce passes
   const bool fuse1 = !p->co.on() && conv3d_fuses_stats(v, KD, b.Cin, C, math);
   CK(conv_halo(p, 0, 2.0 * V * b.Cin * C * T, cbytes(V, b.Cin, C, T), in, dst1(p->F(b.y1), C), v,
-               b.Cin, C, false, fuse1 ? p->F(p->cst) : nullptr, f16_slot(p, b, F16_IN),
+               b.Cin, C, false, fuse1 ? p->F(p->cst) : nullptr, f16_in_slot(p, b),
                f16_slot(p, b, F16_W1)));
   if (fuse1)
     HIPCK(conv3d_in_stats_fin(p->F(p->cst), v, KD, b.Cin, C, math, p->P(b.g1), p->P(b.b1),
@@ -818,11 +838,13 @@ int fwd_block(spff_plan* p, Blk& b, const Src2& in, int pool = -1) {
     PROFB(p, 5, 0.0, 9.25 * (double)nvox(v) * C,
           act_apply_pool(p->F(b.y2), p->F(b.out), p->F(b.al2), p->F(b.de2), P, Q,
                          p->F(p->pool[pool]),
-                         reinterpret_cast<uint8_t*>(p->ws + p->pidx[pool]), v, C, p->st));
+                         reinterpret_cast<uint8_t*>(p->ws + p->pidx[pool]), v, C, p->st, 0.01f,
+                         f16_slot(p, b, F16_OUT)));
     return SPFF_OK;
   }
   PROFB(p, 5, 0.0, 8.0 * (double)nvox(v) * C,
-        act_apply(p->F(b.y2), p->F(b.out), p->F(b.al2), p->F(b.de2), P, Q, v, C, p->st));
+        act_apply(p->F(b.y2), p->F(b.out), p->F(b.al2), p->F(b.de2), P, Q, v, C, p->st, 0.01f,
+                  f16_slot(p, b, F16_OUT)));
   if (pool >= 0)
     HIPCK(maxpool_fwd(p->F(b.out), p->F(p->pool[pool]),
                       reinterpret_cast<uint8_t*>(p->ws + p->pidx[pool]), v, C, p->st));
@@ -993,7 +1015,7 @@ int bwd_block(spff_plan* p, Blk& b, const float* dout, const Dst2* dx, const Src
   }
   if (p->lean && dec_bi >= 0) CK(lean_dec_input(p, dec_bi, &in));
   CK(conv_wgrad(p, 2.0 * V * b.Cin * C * T, cbytes(V, b.Cin, C, T), in, da1, p->DP(b.c1.w), v,
-                b.Cin, C, f16_slot(p, b, F16_IN), f16_slot(p, b, F16_DA1)));
+                b.Cin, C, f16_in_slot(p, b), f16_slot(p, b, F16_DA1)));
   if (dx) {
     HIPCK(conv3d_pack(p->P(b.c1.w), p->F(p->wt), v, KD, b.Cin, C, true, math, p->st,
                       f16_slot(p, b, F16_W1)));

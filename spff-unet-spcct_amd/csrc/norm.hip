@@ -562,7 +562,7 @@ hipError_t bn_bwd_stats(const float* sums, float* dgamma, float* dbeta, float* k
 __global__ __launch_bounds__(256) void k_act_apply(const float* __restrict__ y, float* __restrict__ out,
                                                    const float* __restrict__ al, const float* __restrict__ de,
                                                    const float* __restrict__ P, const float* __restrict__ Q,
-                                                   Vol vol, int C, float neg) {
+                                                   Vol vol, int C, float neg, unsigned* __restrict__ amax) {
   const int bd = blockIdx.y, b = bd / vol.D, d = bd % vol.D;
   const int n4 = vol.H * vol.W * (C >> 2);
   const int64_t base = (int64_t)bd * vol.H * vol.W * C;
@@ -577,13 +577,18 @@ __global__ __launch_bounds__(256) void k_act_apply(const float* __restrict__ y, 
     pp[j] = P ? P[(int64_t)bc * vol.D + d] : 1.f;
     pq[j] = P ? Q[(int64_t)bc * vol.D + d] : 0.f;
   }
+  float m = 0.f;
   for (int i = i0; i < n4; i += gridDim.x * blockDim.x) {
     const float4 v = *reinterpret_cast<const float4*>(y + base + 4 * (int64_t)i);
     float r[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-    for (int j = 0; j < 4; ++j) r[j] = lrelu(r[j] * pa[j] + pd[j], neg) * pp[j] + pq[j];
+    for (int j = 0; j < 4; ++j) {
+      r[j] = lrelu(r[j] * pa[j] + pd[j], neg) * pp[j] + pq[j];
+      m = fmaxf(m, fabsf(r[j]));
+    }
     *reinterpret_cast<float4*>(out + base + 4 * (int64_t)i) = make_float4(r[0], r[1], r[2], r[3]);
   }
+  if (amax) block_amax(m, amax);
 }
 
 static dim3 ew_grid(Vol vol, int C) {
@@ -593,9 +598,9 @@ static dim3 ew_grid(Vol vol, int C) {
 }
 
 hipError_t act_apply(const float* y, float* out, const float* al, const float* de, const float* P,
-                     const float* Q, Vol vol, int C, hipStream_t s, float neg) {
+                     const float* Q, Vol vol, int C, hipStream_t s, float neg, unsigned* amax) {
   hipLaunchKernelGGL(k_act_apply, ew_grid(vol, C), dim3(ew_bs(C)), 0, s, y, out, al, de, P, Q, vol, C,
-                     neg);
+                     neg, amax);
   return hipGetLastError();
 }
 
@@ -608,7 +613,8 @@ hipError_t act_apply(const float* y, float* out, const float* al, const float* d
 __global__ __launch_bounds__(256) void k_act_apply_pool(
     const float* __restrict__ y, float* __restrict__ out, const float* __restrict__ al,
     const float* __restrict__ de, const float* __restrict__ P, const float* __restrict__ Q,
-    float* __restrict__ pooled, uint8_t* __restrict__ idx, Vol vol, int C, float neg) {
+    float* __restrict__ pooled, uint8_t* __restrict__ idx, Vol vol, int C, float neg,
+    unsigned* __restrict__ amax) {
   const int bd = blockIdx.y, b = bd / vol.D, d = bd % vol.D;
   const int Ho = vol.H / 2, Wo = vol.W / 2, C4 = C >> 2;
   const int n4 = Ho * Wo * C4;
@@ -623,6 +629,7 @@ __global__ __launch_bounds__(256) void k_act_apply_pool(
     pp[j] = P ? P[(int64_t)bc * vol.D + d] : 1.f;
     pq[j] = P ? Q[(int64_t)bc * vol.D + d] : 0.f;
   }
+  float m = 0.f;  // max |out| (>= max |pooled|: the pool selects elements of out)
   for (int i = i0; i < n4; i += gridDim.x * blockDim.x) {
     const int q = i / C4, wo = q % Wo, ho = q / Wo;
     const int64_t vin = ((int64_t)bd * vol.H + 2 * ho) * vol.W + 2 * wo;
@@ -636,6 +643,7 @@ __global__ __launch_bounds__(256) void k_act_apply_pool(
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         r[j] = lrelu(r[j] * pa[j] + pd[j], neg) * pp[j] + pq[j];
+        m = fmaxf(m, fabsf(r[j]));
         if (k == 0) {
           best[j] = r[j];
         } else if (r[j] > best[j] || isnan(r[j])) {
@@ -649,16 +657,17 @@ __global__ __launch_bounds__(256) void k_act_apply_pool(
     *reinterpret_cast<float4*>(pooled + vo * C + c) = make_float4(best[0], best[1], best[2], best[3]);
     *reinterpret_cast<uchar4*>(idx + vo * C + c) = make_uchar4(bi[0], bi[1], bi[2], bi[3]);
   }
+  if (amax) block_amax(m, amax);
 }
 
 hipError_t act_apply_pool(const float* y, float* out, const float* al, const float* de,
                           const float* P, const float* Q, float* pooled, uint8_t* idx, Vol vol,
-                          int C, hipStream_t s, float neg) {
+                          int C, hipStream_t s, float neg, unsigned* amax) {
   if ((vol.H | vol.W) & 1 || C % 4) return hipErrorInvalidValue;
   const int n4 = (vol.H / 2) * (vol.W / 2) * (C / 4);
   const dim3 grid(std::min(cdiv(n4, ew_bs(C)), SPFF_EW_GX), vol.B * vol.D);
   hipLaunchKernelGGL(k_act_apply_pool, grid, dim3(ew_bs(C)), 0, s, y, out, al, de, P, Q, pooled,
-                     idx, vol, C, neg);
+                     idx, vol, C, neg, amax);
   return hipGetLastError();
 }
 
@@ -699,17 +708,7 @@ __global__ __launch_bounds__(256) void k_in_bwd_apply(
     }
     *reinterpret_cast<float4*>(dy + base + 4 * (int64_t)i) = make_float4(o[0], o[1], o[2], o[3]);
   }
-  if (amax) {  // (uniform) block max -> one integer atomicMax of its float bits
-    __shared__ float wm[16];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-    if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      for (int w = 1; w < (int)((blockDim.x + 63) >> 6); ++w) m = fmaxf(m, wm[w]);
-      if (m > 0.f) atomicMax(amax, __float_as_uint(m));
-    }
-  }
+  if (amax) block_amax(m, amax);
 }
 
 __global__ __launch_bounds__(256) void k_act_bound(const float* __restrict__ gamma,

@@ -66,6 +66,21 @@ __device__ __forceinline__ const float* src_at(const Src2& x, const Vol& vol, in
   return c < x.split ? x.p0 + vox * x.ld0 + c : x.p1 + vox * x.ld1 + (c - x.split);
 }
 
+// SPFF_MATH_F16X3 operand maxima: the block's largest m (>= 0) into *slot as an integer
+// atomicMax of its float bits (non-negative floats order like their bits; order-independent,
+// so deterministic).  Every thread of the block must call it (it synchronises the block).
+__device__ __forceinline__ void block_amax(float m, unsigned* slot) {
+  __shared__ float wm[16];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < (int)((blockDim.x + 63) >> 6); ++w) m = fmaxf(m, wm[w]);
+    if (m > 0.f) atomicMax(slot, __float_as_uint(m));
+  }
+}
+
 // ---------------------------------------------------------------- conv3d --
 // Weight repack: reference layout W[Cout][Cin][KD][3][3] ->
 //   fwd:   Wt[tap][ci(pad cin_pad)][co(pad cout_pad)]
@@ -129,7 +144,9 @@ hipError_t conv3d_wgrad_x(const Src2& x, const float* dy, int lddy, float* dw, V
 // bits) into *slot, which the caller zeroed.  absmax_src covers what a conv reads of x:
 // C channels with the input activation applied, plus (halo) a depth-sharded input's halo
 // slices and a height-sharded one's boundary rows; channel strides must be multiples of 4.
-hipError_t absmax_src(const Src2& x, Vol vol, int C, bool halo, unsigned* slot, hipStream_t s);
+// (also: a slot whose value is max-ed into *slot too, after the caller's stream order)
+hipError_t absmax_src(const Src2& x, Vol vol, int C, bool halo, unsigned* slot, hipStream_t s,
+                      const unsigned* also = nullptr);
 hipError_t absmax_f32(const float* p, int64_t n, unsigned* slot, hipStream_t s);
 // fixed-order sum of the [nsplit][T][kpad][npad] partial slabs into dw[Cout][Cin][T]
 hipError_t conv3d_wgrad_reduce(const float* part, float* dw, int nsplit, int T, int kpad,
@@ -243,14 +260,15 @@ hipError_t in_rstd(const float* sqsums, const float* gamma, const float* beta,
                    const float* mean, float* rstd, float* al, float* de, Vol vol, int C,
                    hipStream_t s);
 // out = lrelu(y*al[b,c]+de[b,c]) * P[b,c,d] + Q[b,c,d]   (P/Q null -> identity)
+// (amax: also block_amax the largest |out| into *amax -- an f16x3 operand scale)
 hipError_t act_apply(const float* y, float* out, const float* al, const float* de,
                      const float* P, const float* Q, Vol vol, int C, hipStream_t s,
-                     float neg = 0.01f);
+                     float neg = 0.01f, unsigned* amax = nullptr);
 // act_apply of an encoder block output fused with the (1,2,2) max-pool that reads it:
 // out as act_apply, pooled [B][D][H/2][W/2][C] and its argmax bytes as maxpool_fwd (H, W even)
 hipError_t act_apply_pool(const float* y, float* out, const float* al, const float* de,
                           const float* P, const float* Q, float* pooled, uint8_t* idx, Vol vol,
-                          int C, hipStream_t s, float neg = 0.01f);
+                          int C, hipStream_t s, float neg = 0.01f, unsigned* amax = nullptr);
 // IN backward finalize: from per-(b,c,d) [sum dr, sum dr*xhat] -> dgamma, dbeta (over b),
 // k1[b,c] = mean dr, k2[b,c] = mean dr*xhat
 // depth-sharded variants: fp64 partials over the local slab, summed across the
