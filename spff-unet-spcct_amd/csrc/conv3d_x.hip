@@ -79,6 +79,11 @@
 // leave room for two workgroups per CU, as the 32-wide tiles) or 8 (one 2 x 16 x 16 tile)
 #define SPFF_X64NW 4
 #endif
+#ifndef SPFF_X32WG
+// workgroups per CU the 16/32-wide f16x3 kernels are compiled for (their 52 KB image
+// allows 3; 3 caps them at 168 VGPRs)
+#define SPFF_X32WG 3
+#endif
 #ifndef SPFF_XIGLP
 #define SPFF_XIGLP -1
 #endif
@@ -259,7 +264,7 @@ __device__ __forceinline__ int x16_w(int r) {
 // rows (Src2::rlo / rhi; zero where null) instead of zero padding (hshard.hip).  A
 // separate instantiation, so the unsharded kernels' register budget is unchanged.
 template <int BN, int KD, int NS, int MB, int NW, bool X16, int TD, bool HR>
-__global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
+__global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : (BN <= 32 && NS == NS_F16 ? SPFF_X32WG : 2)) void k_conv3d_fwd_x(
     Src2 x, const uint4* __restrict__ wp, Dst2 y, Vol vol, int Cin, int nkc, int Cout, int npad,
     int tilesD, int tilesH, int tilesW, float* __restrict__ part, int kps,
     float* __restrict__ stats, int ntiles, int td0, int tds, int th0, int ths,
@@ -369,9 +374,47 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void k_conv3d_fwd_x(
   uint2 hs[RH][NP];
   unsigned hvalid = 0;  // bit k: hreg[k] is in bounds (else it is zeroed at the split)
   int fkc = 0;          // chunk of the registers in flight
+  // PRE (16/32-wide tiles, no boundary rows): the chunk-invariant part of each halo float4's
+  // address -- its voxel and spatial validity -- computed once, not per chunk (the position
+  // decomposition and bounds are ~20 VALU per float4 beside MFMAs that now take half the
+  // cycles with two fp16 planes); the 64-wide kernel has no registers to spare
+  constexpr bool PRE = BN <= 32 && !HR;
+  int64_t pvox[PRE ? RH : 1];
+  unsigned pok = 0;
+  if constexpr (PRE) {
+#pragma unroll
+    for (int k = 0; k < RH; ++k) {
+      const int i = tid + XT_THREADS * k;
+      const int pos = (i < NHX ? i : 0) >> 1;
+      const int hw = pos % HWD, t2 = pos / HWD, hh = t2 % HH, hd = t2 / HH;
+      const int gd = d0 + hd - KD / 2, gh = h0 + hh - 1, gw = w0 + hw - 1;
+      const bool ok = i < NHX && (unsigned)(gd + vol.dh) < (unsigned)(D + 2 * vol.dh) &&
+                      (unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W &&
+                      !((gd < 0 && x.zlo) || (gd >= D && x.zhi));
+      pvox[k] = ok ? (((int64_t)b * D + gd) * H + gh) * W + gw : 0;
+      pok |= ok ? (1u << k) : 0u;
+    }
+  }
   auto fetch = [&](int kc) {
     hvalid = 0;
     fkc = kc;
+    if constexpr (PRE) {
+      // a thread's channel quad q = tid & 1 is the same for every k (XT_THREADS is even)
+      const int cq = kc * 8 + 4 * (tid & 1);
+      const bool cok = cq < Cin;
+#pragma unroll
+      for (int k = 0; k < RH; ++k) {
+        const bool ok = ((pok >> k) & 1u) && cok;
+        const int c = ok ? cq : 0;
+        const bool s0 = c < x.split;
+        const float* src = s0 ? x.p0 : x.p1;
+        const int64_t ld = s0 ? x.ld0 : x.ld1;
+        hreg[k] = *reinterpret_cast<const float4*>(src + (ok ? pvox[k] : 0) * ld +
+                                                   (s0 ? c : c - x.split));
+        hvalid |= ok ? (1u << k) : 0u;
+      }
+      return;
+    }
 #pragma unroll
     for (int k = 0; k < RH; ++k) {
       const int i = tid + XT_THREADS * k;
