@@ -79,6 +79,11 @@
 // leave room for two workgroups per CU, as the 32-wide tiles) or 8 (one 2 x 16 x 16 tile)
 #define SPFF_X64NW 4
 #endif
+#ifndef SPFF_X32D4
+// 32-wide f16x3 tiles 4 x 8 x 16 voxels (4 waves x 8 row blocks, 75 KB, two workgroups per
+// CU) instead of 2 x 8 x 16: 2.1 instead of 2.8 staged halo positions per output voxel
+#define SPFF_X32D4 1
+#endif
 #ifndef SPFF_X32WG
 // workgroups per CU the 16/32-wide f16x3 kernels are compiled for (their 52 KB image
 // allows 3; 3 caps them at 168 VGPRs)
@@ -199,8 +204,15 @@ constexpr size_t xt_lds_bytes() {
   return ops > out ? ops : out;
 }
 // tile depth of a BN-wide launch (host side: launches, fused-statistics layout)
-constexpr int xt_td(int BN) { return (BN == 32 && SPFF_X16 && SPFF_X32T) ? 4 : XT_D; }
-constexpr int xt_mb(int BN) { return (BN == 32 && SPFF_X16 && SPFF_X32T) ? 4 : 2; }
+constexpr bool xt_d4(int BN, int NS) {
+  return BN == 32 && NS == NS_F16 && SPFF_X16 && SPFF_X32D4 && !SPFF_X32T;
+}
+constexpr int xt_td(int BN, int NS) {
+  return ((BN == 32 && SPFF_X16 && SPFF_X32T) || xt_d4(BN, NS)) ? 4 : XT_D;
+}
+constexpr int xt_mb(int BN, int NS) {
+  return ((BN == 32 && SPFF_X16 && SPFF_X32T) || xt_d4(BN, NS)) ? 4 : 2;
+}
 // waves of a BN-wide workgroup (4-wave 32-wide tiles: SPFF_X32NW, 2-deep tiles only)
 // (16-wide tiles, Cout <= 16 -- the SwinUNETR's C = 12 convs: also 4 waves, 2 WGs / CU)
 // (64-wide f16x3 tiles: SPFF_X64NW)
@@ -264,7 +276,7 @@ __device__ __forceinline__ int x16_w(int r) {
 // rows (Src2::rlo / rhi; zero where null) instead of zero padding (hshard.hip).  A
 // separate instantiation, so the unsharded kernels' register budget is unchanged.
 template <int BN, int KD, int NS, int MB, int NW, bool X16, int TD, bool HR>
-__global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : (BN <= 32 && NS == NS_F16 ? SPFF_X32WG : 2)) void k_conv3d_fwd_x(
+__global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : (BN <= 32 && NS == NS_F16 && TD == 2 ? SPFF_X32WG : 2)) void k_conv3d_fwd_x(
     Src2 x, const uint4* __restrict__ wp, Dst2 y, Vol vol, int Cin, int nkc, int Cout, int npad,
     int tilesD, int tilesH, int tilesW, float* __restrict__ part, int kps,
     float* __restrict__ stats, int ntiles, int td0, int tds, int th0, int ths,
@@ -852,13 +864,13 @@ __global__ void k_splitk_reduce(const float* __restrict__ part, int nsplit, int6
   }
 }
 
-template <int BN, int KD, int NS, bool HR, int MB = xt_mb(BN), int NW = xt_nw(BN, NS),
-          int TD = xt_td(BN)>
+template <int BN, int KD, int NS, bool HR, int MB = xt_mb(BN, NS), int NW = xt_nw(BN, NS),
+          int TD = xt_td(BN, NS)>
 static hipError_t launch_fwd_xh(const Src2& x, const uint4* wx, const Dst2& y, Vol vol, int K,
                                 int nkc, int N, int npad, hipStream_t s, float* part, int nsplit,
                                 int kps, float* stats, int dpart, const unsigned* wmx, const unsigned* xmx) {
   constexpr int TH = SPFF_X16 ? 2 * NW * MB / TD : NW * MB;
-  static_assert(NW == 8 || TD == XT_D, "xt_ntiles assumes 8 waves for other tile depths");
+  static_assert(NW == 8 || TD == XT_D || xt_d4(BN, NS), "xt_ntiles: tile shape");
   constexpr size_t shm = xt_lds_bytes<BN, KD, NS, TD, TH>();
   static_assert(shm <= (NW == 8 ? 160 : 80) * 1024, "LDS budget");
   if (x.al && BN != 32) return hipErrorInvalidValue;  // fused activation: 32-wide tiles only
@@ -946,7 +958,7 @@ bool conv3d_fuses_act(int math, int C) {
 // tiles of a BN-wide launch (the fused IN statistics are per (tile, out channel))
 static int64_t xt_ntiles(Vol vol, int BN, int ns) {
   const int nw = xt_nw(BN, ns);
-  const int td = xt_td(BN), th = SPFF_X16 ? 2 * nw * xt_mb(BN) / td : nw * xt_mb(BN);
+  const int td = xt_td(BN, ns), th = SPFF_X16 ? 2 * nw * xt_mb(BN, ns) / td : nw * xt_mb(BN, ns);
   return (int64_t)vol.B * cdiv(vol.D, td) * cdiv(vol.H, th) * cdiv(vol.W, XT_W);
 }
 namespace {
@@ -1170,12 +1182,13 @@ size_t conv3d_splitk_bytes(Vol vol, int KD, int Cin, int Cout) {
 bool conv3d_splits_depth(Vol vol, int KD, int Cin_w, int Cout_w, bool dgrad, int math) {
   const XDims d = xdims(KD, Cin_w, Cout_w, dgrad);
   return KD == 3 && use_split(vol, math, dgrad) && splitk_plan(vol, d, ns_of(math)).nsplit == 1 &&
-         cdiv(vol.D, xt_td(d.BN)) >= 3;
+         cdiv(vol.D, xt_td(d.BN, ns_of(math))) >= 3;
 }
 bool conv3d_splits_height(Vol vol, int KD, int Cin_w, int Cout_w, bool dgrad, int math) {
   const XDims d = xdims(KD, Cin_w, Cout_w, dgrad);
   const int nw = xt_nw(d.BN, ns_of(math));
-  const int th = SPFF_X16 ? 2 * nw * xt_mb(d.BN) / xt_td(d.BN) : nw * xt_mb(d.BN);
+  const int ns = ns_of(math);
+  const int th = SPFF_X16 ? 2 * nw * xt_mb(d.BN, ns) / xt_td(d.BN, ns) : nw * xt_mb(d.BN, ns);
   return use_split(vol, math, dgrad) && splitk_plan(vol, d, ns_of(math)).nsplit == 1 &&
          cdiv(vol.H, th) >= 3;
 }
