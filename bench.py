@@ -682,11 +682,13 @@ def main():
     try:
         pm = json.loads(pathlib.Path(args.pmc).read_text())
         traffic_src["file"] = str(pathlib.Path(args.pmc).resolve().relative_to(ROOT))
-        if pm.get("workload_key") == wkey:
+        # the summary counts for THIS kernel build only: same workload key and the same
+        # library sources (a kernel change makes a committed measurement stale -> null)
+        same = pm.get("lib_sources_sha256") == build_record()["lib_sources_sha256"]
+        traffic_src["same_sources"] = same
+        if pm.get("workload_key") == wkey and same:
             traffic = pm.get("hbm_bytes_per_launch")
             traffic_src["matched"] = True
-            traffic_src["same_sources"] = (pm.get("lib_sources_sha256")
-                                           == build_record()["lib_sources_sha256"])
         else:
             traffic_src["pmc_workload_key"] = pm.get("workload_key")
     except Exception:
@@ -707,7 +709,7 @@ def main():
             "traffic_over_compulsory": (traffic / (cb / nl)) if (traffic and nl and cb) else None,
             "traffic_note": ("PMC HBM bytes per launch of this kernel (2 x FETCH_SIZE + WRITE_SIZE, "
                              "rocprofv3 --pmc passes of this same bench workload); null when the "
-                             "summary's workload key differs from this run's"),
+                             "summary's workload key or library sources differ from this run's"),
             "traffic_source": traffic_src,
             "per_class_ms_per_step": {k: v[0] / args.steps for k, v in prof.items()},
             "per_class_tflops": {k: (v[1] / (v[0] * 1e-3) / 1e12 if v[0] > 0 else None)
