@@ -36,6 +36,9 @@
 #ifndef SPFF_WXUNROLL
 #define SPFF_WXUNROLL 4  // k-step (W-row pair) loop unroll of k_conv3d_wgrad_x16
 #endif
+#ifndef SPFF_WXRING4
+#define SPFF_WXRING4 1  // f16x3 3x3x3 wgrad: 4-slot plane ring + double dy buffer (one barrier)
+#endif
 #ifndef SPFF_WXUNROLL2
 // the same for two-plane operands (bf16x3, f16x3): unrolled 4 deep the compiler hoists the
 // fragment reads of later k-steps (fewer MFMAs per step) into 256 VGPRs + 11-23 spilled;
@@ -323,8 +326,16 @@ __global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x16(
   // operand planes; HF: two fp16 planes of the scaled operands (NS_F16, bf16split.h)
   constexpr int NPL = nplanes(NS);
   constexpr bool HF = NS == NS_F16;
-  __shared__ __attribute__((aligned(16))) unsigned short Xs[NPL * NPOS * CI];
-  __shared__ __attribute__((aligned(16))) unsigned short Ys[NPL * WX_TV * CO];
+  // R4 (f16x3, 3x3x3, SPFF_WXRING4): a 4-slot plane ring and two dy buffers (78 KB, still two
+  // workgroups per CU), so the next tile's plane and dy go to slots the current tile does
+  // not read: one barrier per tile instead of the write-after-read pair
+  constexpr bool R4 = HF && KD == 3 && SPFF_WXRING4;
+  constexpr int NSL = R4 ? 4 : KD;           // plane slots of the halo ring
+  constexpr int NPOSA = NSL * PPOS;          // halo image positions per split plane
+  constexpr int YB = NPL * WX_TV * CO;       // one dy buffer (elements)
+  __shared__ __attribute__((aligned(16))) unsigned short Xs[NPL * NPOSA * CI];
+  __shared__ __attribute__((aligned(16))) unsigned short Ys[(R4 ? 2 : 1) * YB];
+  int ybuf = 0;  // dy buffer of the current tile (R4)
   // HF: x scaled by 2^ex (*xmx: max |x|), dy by 2^ey (*ymx: max |dy|)
   const int ex = HF ? f16_scale_exp(*xmx) : 0;
   const int ey = HF ? f16_scale_exp(*ymx) : 0;
@@ -425,7 +436,7 @@ __global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x16(
     }
   };
   auto store_plane = [&](int gd, const float4 (&r)[NP]) {
-    unsigned short* dst = Xs + ((gd + 3) % KD) * PPOS * CI;
+    unsigned short* dst = Xs + (R4 ? ((gd + 4) & 3) : ((gd + 3) % KD)) * PPOS * CI;
 #pragma unroll
     for (int k = 0; k < NP; ++k) {
       const int i = tid + 256 * k;
@@ -436,7 +447,7 @@ __global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x16(
         split4<NS>(v, o);
 #pragma unroll
         for (int p = 0; p < NPL; ++p)
-          *reinterpret_cast<uint2*>(dst + p * NPOS * CI + 4 * i) = o[p];
+          *reinterpret_cast<uint2*>(dst + p * NPOSA * CI + 4 * i) = o[p];
       }
     }
   };
@@ -465,7 +476,7 @@ __global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x16(
       yreg[k] = v;
     }
   };
-  auto stash = [&](int d0, bool negate) {
+  auto stash = [&](int d0, bool negate, int yb) {
     store_plane(d0 + KD / 2, hreg);
 #pragma unroll
     for (int k = 0; k < NY; ++k) {
@@ -478,7 +489,7 @@ __global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x16(
       const int off = kv * CO + (((c4 >> 1) ^ (CO == 32 ? ((kv >> 2) & 1) << 1 : 0)) << 3) + 4 * (c4 & 1);
 #pragma unroll
       for (int p = 0; p < NPL; ++p)
-        *reinterpret_cast<uint2*>(Ys + p * WX_TV * CO + off) = o[p];
+        *reinterpret_cast<uint2*>(Ys + yb * YB + p * WX_TV * CO + off) = o[p];
     }
   };
 
@@ -486,12 +497,20 @@ __global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x16(
     constexpr int NJ = decltype(NJc)::value;
     // aoff[j] addresses plane kd as slot kd; tap kd reads gd = d0 + kd - KD / 2, in slot
     // (kd + rot) % KD with rot = (d0 - KD / 2 + 3) % KD
+    // (R4: tap kd reads gd = d0 + kd - 1 in slot (gd + 4) & 3)
     constexpr int PL = PPOS * CI;
     const int rot = (d0 - KD / 2 + 3) % KD;
     int ab[NJ];
 #pragma unroll
-    for (int j = 0; j < NJ; ++j)
-      ab[j] = aoff[j] + (aoff[j] >= (KD - rot) * PL ? (rot - KD) * PL : rot * PL);
+    for (int j = 0; j < NJ; ++j) {
+      if constexpr (R4) {
+        const int kd = aoff[j] >= 2 * PL ? 2 : aoff[j] >= PL ? 1 : 0;
+        ab[j] = aoff[j] + (((d0 + kd + 3) & 3) - kd) * PL;
+      } else {
+        ab[j] = aoff[j] + (aoff[j] >= (KD - rot) * PL ? (rot - KD) * PL : rot * PL);
+      }
+    }
+    const unsigned short* Yc = Ys + (R4 ? ybuf * YB : 0);
     constexpr int KSU = NPL == 2 ? SPFF_WXUNROLL2 : SPFF_WXUNROLL;
 #pragma unroll KSU
     for (int ks = 0; ks < WX_TH / 2; ++ks) {
@@ -500,7 +519,7 @@ __global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x16(
       for (int cb = 0; cb < NCB; ++cb)
 #pragma unroll
         for (int p = 0; p < NPL; ++p) {
-          const unsigned short* yb = Ys + p * WX_TV * CO + 2 * ks * WX_TW * CO + boff[cb];
+          const unsigned short* yb = Yc + p * WX_TV * CO + 2 * ks * WX_TW * CO + boff[cb];
           bq[cb][p] = frag(tr_read(yb), tr_read(yb + 8 * CO));
         }
 #pragma unroll
@@ -508,7 +527,7 @@ __global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x16(
         bf16x8 aq[NPL];
 #pragma unroll
         for (int p = 0; p < NPL; ++p) {
-          const unsigned short* xb = Xs + p * NPOS * CI + 2 * ks * HWD * CI + ab[j];
+          const unsigned short* xb = Xs + p * NPOSA * CI + 2 * ks * HWD * CI + ab[j];
           aq[p] = frag(tr_read(xb), tr_read(xb + 8 * CI));
         }
 #pragma unroll
@@ -532,6 +551,48 @@ __global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x16(
 
   const int tbeg = split * tps;
   const int tend = min(ntiles, tbeg + tps);
+  // first tile of a column: its other planes d0 - KD / 2 .. d0 + KD / 2 - 1
+  auto stage_column = [&](int tile, int d0) {
+    const TileXY tx = tile_xy(tile);
+#pragma unroll
+    for (int hd = 0; hd < KD - 1; ++hd) {
+      float4 r[NP];
+      load_plane(tx, d0 + hd - KD / 2, r);
+      store_plane(d0 + hd - KD / 2, r);
+    }
+  };
+  if constexpr (R4) {
+    // tile t computes from ring slots and dy buffer (t - tbeg) & 1, while tile t + 1's
+    // plane / dy are fetched and stored to the slot / buffer it does not read; a new
+    // column's two extra planes overwrite slots the tile before may read: one more barrier
+    if (tbeg < tend) {
+      fetch(tbeg);
+      stage_column(tbeg, tbeg % D);
+      stash(tbeg % D, false, 0);
+    }
+    for (int tile = tbeg; tile < tend; ++tile) {
+      if (tile != tbeg) {
+#pragma unroll
+        for (int j = 0; j < NJMAX; ++j)
+#pragma unroll
+          for (int cb = 0; cb < NCB; ++cb) acc[j][cb] = -acc[j][cb];
+      }
+      __syncthreads();  // this tile's plane / dy visible; every wave is past tile - 1
+      const int d0 = tile % D;
+      ybuf = (tile - tbeg) & 1;
+      if (tile + 1 < tend) fetch(tile + 1);
+      if (nj == NJMAX) compute(std::integral_constant<int, NJMAX>{}, d0);
+      else if constexpr (NJMAX > 1) compute(std::integral_constant<int, NJMAX - 1>{}, d0);
+      if (tile + 1 < tend) {
+        const int d1 = (tile + 1) % D;
+        if (d1 == 0) {
+          __syncthreads();  // every wave is past this tile's reads of the ring
+          stage_column(tile + 1, d1);
+        }
+        stash(d1, ((tile + 1 - tbeg) & 1) != 0, ybuf ^ 1);
+      }
+    }
+  } else {
   if (tbeg < tend) fetch(tbeg);
   for (int tile = tbeg; tile < tend; ++tile) {
     // sign-alternating accumulation (conv3d_x.hip)
@@ -543,21 +604,13 @@ __global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x16(
     }
     __syncthreads();  // previous compute done reading LDS
     const int d0 = tile % D;
-    if (KD > 1 && (tile == tbeg || d0 == 0)) {
-      // first tile of a column: its other planes d0 - KD / 2 .. d0 + KD / 2 - 1
-      const TileXY tx = tile_xy(tile);
-#pragma unroll
-      for (int hd = 0; hd < KD - 1; ++hd) {
-        float4 r[NP];
-        load_plane(tx, d0 + hd - KD / 2, r);
-        store_plane(d0 + hd - KD / 2, r);
-      }
-    }
-    stash(d0, ((tile - tbeg) & 1) != 0);
+    if (KD > 1 && (tile == tbeg || d0 == 0)) stage_column(tile, d0);
+    stash(d0, ((tile - tbeg) & 1) != 0, 0);
     __syncthreads();
     if (tile + 1 < tend) fetch(tile + 1);
     if (nj == NJMAX) compute(std::integral_constant<int, NJMAX>{}, d0);
     else if constexpr (NJMAX > 1) compute(std::integral_constant<int, NJMAX - 1>{}, d0);
+  }
   }
 
   if (tend > tbeg && ((tend - 1 - tbeg) & 1)) {
