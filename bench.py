@@ -41,6 +41,16 @@ BF16_MFMA_PEAK_TFLOPS = 256 * 4 * 1024 * 2.4e9 / 1e12
 # fp32 multiply-add, bf16x3 runs 3
 MATH_PEAK = {"f32": FP32_MFMA_PEAK_TFLOPS, "bf16x6": BF16_MFMA_PEAK_TFLOPS / 6,
              "bf16x3": BF16_MFMA_PEAK_TFLOPS / 3, "f16x3": BF16_MFMA_PEAK_TFLOPS / 3}
+# what each conv arithmetic is, in one line, with where its accuracy is measured
+CONV_MATH_ACCURACY = {
+    "f32": "fp32 MFMA (an fp32 fma chain)",
+    "bf16x6": "fp32 operands split exactly into 3 bf16 planes, 6 products, fp32 accumulate",
+    "bf16x3": "2 bf16 planes, 3 products (~2^-17 per product; opt-in)",
+    "f16x3": ("each operand scaled by a power of two from its max |element| and split into 2 fp16 "
+              "planes (<= 2^-22 |x|), 3 products, fp32 accumulate; measured against fp64: below "
+              "the fp32 MFMA path's error in all 29 per-op cases and as close as it at config 2 "
+              "(logits 1.2e-5, gradients <= 4.5e-5 rel. L2; profiles/r03/f16x3/)"),
+}
 MATH_KERNEL = {"f32": "k_conv3d_fwd (fp32 MFMA 3x3x3 implicit GEMM, fwd+dgrad)",
                "bf16x6": "k_conv3d_fwd_x<.,.,3> (3-plane split-bf16 MFMA 3x3x3 implicit GEMM, "
                          "fwd+dgrad)",
@@ -767,6 +777,7 @@ def main():
         "scaling": "strong" if ((sharded and args.strong) or registry) else "weak",
         "vs_baseline": None,
         "dtype": "f32", "conv_math": args.math,
+        "conv_math_accuracy": CONV_MATH_ACCURACY.get(args.math),
         "data": "synthetic (x~N(0,1), labels U[0,K) with 1% ignore=255; weights from weightgen seed 0)",
         "config": cfg,
         "workload_key": wkey,
