@@ -47,6 +47,10 @@ extern "C" {
  *                     on-device absmax) and split into 2 fp16 planes, 3 products on the
  *                     fp16 MFMA: <= 2^-22 |x| per operand, dropped l*l <= 2^-22 |xy|,
  *                     at the bf16x3 rate (the 1x1x1 / ConvTranspose GEMMs keep bf16x6) */
+/* largest num_classes of the SPFF / 3DUNet plans and of spff_loss / spff_confusion
+ * (the SwinUNETR plan's soft-Dice loss: 32) */
+#define SPFF_MAX_CLASSES 128
+
 #define SPFF_MATH_F32 0
 #define SPFF_MATH_BF16X6 1
 #define SPFF_MATH_BF16X3 2
@@ -54,8 +58,8 @@ extern "C" {
 
 typedef struct spff_cfg {
   int batch, in_ch, depth, height, width;  /* input [B][Cin][D][H][W] */
-  int num_classes;                          /* K (<= 32) */
-  int base;                                 /* f (power of two, >= 8) */
+  int num_classes;                          /* K, 1 .. SPFF_MAX_CLASSES */
+  int base;                                 /* f: a multiple of 8 (>= 8) */
   int ksd;                                  /* spectral kernel depth: 1 or 3 */
   int use_efilm, use_fgate;                 /* novel block (models.py:1448) */
   int use_se, use_specse;                   /* encoder post (models.py:684) */

@@ -10,6 +10,7 @@ ok() { local rc=$1; [ "$rc" -eq 0 ] || [ "$rc" -eq 1 ]; }
 for step in "$@"; do
   case "$step" in
     tests) timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v -s --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1; rc=$? ;;
+    sel) timeout -k 10 ${SEL_T:-900} python -u -m pytest ${SEL} -m gpu -v -s --timeout 900 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_sel${SEL_TAG:-}.log 2>&1; rc=$? ;;
     dp) timeout -k 10 400 python -u -m pytest tests/test_gpu_dp.py -m gpu -x -v -s --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_dp.log 2>&1; rc=$? ;;
     sizes) timeout -k 10 1000 python -u -m pytest tests/test_gpu_baseline_sizes.py -m gpu -x -v -s --timeout 900 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_sizes.log 2>&1; rc=$? ;;
     memory) timeout -k 10 400 python -u -m pytest tests/test_gpu_memory.py -m gpu -x -v -s --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_memory.log 2>&1; rc=$? ;;

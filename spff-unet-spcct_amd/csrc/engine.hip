@@ -262,14 +262,15 @@ void host_pe(int D, std::vector<float>& pe) {
 
 int build_plan(spff_plan* p) {
   const spff_cfg& c = p->cfg;
-  if (c.batch < 1 || c.in_ch < 1 || c.depth < 1 || c.num_classes < 1 || c.num_classes > 32)
-    return fail(SPFF_EINVAL, "invalid batch/in_ch/depth/num_classes (K must be 1..32)");
-  if (c.base < 8 || (c.base & (c.base - 1)))
-    return fail(SPFF_EINVAL, "base must be a power of two >= 8");
+  if (c.batch < 1 || c.in_ch < 1 || c.depth < 1 || c.num_classes < 1 ||
+      c.num_classes > SPFF_MAX_CLASSES)
+    return fail(SPFF_EINVAL, "invalid batch/in_ch/depth/num_classes (K must be 1..SPFF_MAX_CLASSES)");
+  if (c.base < 8 || c.base % 8)
+    return fail(SPFF_EINVAL, "base must be a multiple of 8");
   if (c.ksd != 1 && c.ksd != 3) return fail(SPFF_EINVAL, "ksd must be 1 or 3");
   if (c.height < 8 || c.width < 8)
     return fail(SPFF_ESHAPE, "H and W must be >= 8 (three (1,2,2) pools)");
-  if (c.in_ch > 64) return fail(SPFF_EINVAL, "in_ch > 64 not supported");
+  if (c.in_ch > 1024) return fail(SPFF_EINVAL, "in_ch > 1024 not supported");
   if (c.math < SPFF_MATH_F32 || c.math > SPFF_MATH_F16X3)
     return fail(SPFF_EINVAL, "math must be one of SPFF_MATH_*");
   if (c.memory_mode < SPFF_MEM_AUTO || c.memory_mode > SPFF_MEM_LEAN)
@@ -1346,7 +1347,7 @@ int spff_loss(const float* logits, const int64_t* labels, int64_t nv, int K, int
               int64_t* conf, void* ws, void* stream) {
   if (!logits || !labels || !out4 || !dlogits || !conf || !ws)
     return fail(SPFF_EINVAL, "null argument");
-  if (K < 1 || K > 32) return fail(SPFF_EINVAL, "num_classes must be 1..32");
+  if (K < 1 || K > SPFF_MAX_CLASSES) return fail(SPFF_EINVAL, "num_classes must be 1..SPFF_MAX_CLASSES");
   hipStream_t s = static_cast<hipStream_t>(stream);
   HIPCK(loss_fwd(logits, labels, nv, K, ignore, smooth, count_override, out4, dlogits, conf,
                  static_cast<float*>(ws), s));
@@ -1356,7 +1357,7 @@ int spff_loss(const float* logits, const int64_t* labels, int64_t nv, int K, int
 int spff_confusion(const float* logits, const int64_t* labels, int64_t nv, int K, int ignore,
                    int64_t* conf, void* stream) {
   if (!logits || !labels || !conf) return fail(SPFF_EINVAL, "null argument");
-  if (K < 1 || K > 32) return fail(SPFF_EINVAL, "num_classes must be 1..32");
+  if (K < 1 || K > SPFF_MAX_CLASSES) return fail(SPFF_EINVAL, "num_classes must be 1..SPFF_MAX_CLASSES");
   hipStream_t s = static_cast<hipStream_t>(stream);
   HIPCK(confusion_only(logits, labels, nv, K, ignore, conf, s));
   return SPFF_OK;

@@ -13,7 +13,10 @@
 
 namespace spff {
 
-constexpr int LOSS_GRID = 2048, LOSS_T = 256, KMAX = 32;
+// K up to KMAX classes.  Up to KHIST_LDS the K x (K + 1) confusion histogram lives in LDS
+// (integer atomics there, flushed once per workgroup); above it each count goes straight
+// to the int64 matrix in HBM (integer atomics: still order-free and exact).
+constexpr int LOSS_GRID = 2048, LOSS_T = 256, KMAX = 128, KHIST_LDS = 64;
 
 __global__ void k_count_valid(const int64_t* __restrict__ lab, int64_t V, int ignore,
                               unsigned long long* __restrict__ cnt) {
@@ -46,14 +49,21 @@ __global__ __launch_bounds__(LOSS_T) void k_loss(const float* __restrict__ x,
                                                  double* __restrict__ part,
                                                  unsigned long long* __restrict__ nbad,
                                                  const float* __restrict__ cw, int clamp1) {
-  __shared__ unsigned int hist[KMAX * (KMAX + 1)];
   __shared__ double red[LOSS_T];
-  extern __shared__ __attribute__((aligned(16))) float stage[];  // [LOSS_WAVES][64 K]
+  // [LOSS_WAVES][64 K] row stage, then (K <= KHIST_LDS) the [K][K + 1] histogram
+  extern __shared__ __attribute__((aligned(16))) float stage[];
   const int K1 = K + 1;  // column K = label outside [0,K) (not ignored)
+  const bool lh = K <= KHIST_LDS;
+  unsigned int* hist = reinterpret_cast<unsigned int*>(stage + LOSS_WAVES * 64 * K);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   float* sx = stage + wv * 64 * K;
-  for (int i = threadIdx.x; i < K * K1; i += LOSS_T) hist[i] = 0;
+  if (lh)
+    for (int i = threadIdx.x; i < K * K1; i += LOSS_T) hist[i] = 0;
   __syncthreads();
+  auto tally = [&](int i) {
+    if (lh) atomicAdd(&hist[i], 1u);
+    else atomicAdd(&conf[i], 1ull);
+  };
   // clamp1: the 3DUNet's weighted CE divides by max(N_valid, 1) (models.py:796)
   const float invN =
       WITH_CE ? 1.f / (float)(clamp1 && *count < 1 ? (int64_t)1 : *count) : 0.f;
@@ -80,10 +90,10 @@ __global__ __launch_bounds__(LOSS_T) void k_loss(const float* __restrict__ x,
       const bool valid = (y != ignore);
       if (valid && (y < 0 || y >= K)) {
         ++bad;
-        atomicAdd(&hist[am * K1 + K], 1u);
+        tally(am * K1 + K);
         if (WITH_CE) for (int k = 0; k < K; ++k) xr[k] = 0.f;
       } else {
-        if (valid) atomicAdd(&hist[am * K1 + (int)y], 1u);
+        if (valid) tally(am * K1 + (int)y);
         if (WITH_CE) {
           if (valid) {
             const float xy = xr[(int)y];
@@ -123,8 +133,9 @@ __global__ __launch_bounds__(LOSS_T) void k_loss(const float* __restrict__ x,
     if (threadIdx.x == 0) part[blockIdx.x] = red[0];
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < K * K1; i += LOSS_T)
-    if (hist[i]) atomicAdd(&conf[i], (unsigned long long)hist[i]);
+  if (lh)
+    for (int i = threadIdx.x; i < K * K1; i += LOSS_T)
+      if (hist[i]) atomicAdd(&conf[i], (unsigned long long)hist[i]);
   if (bad && nbad) atomicAdd(nbad, (unsigned long long)bad);
 }
 
@@ -170,7 +181,21 @@ __global__ void k_loss_final(const double* __restrict__ part, int nparts,
   out4[3] = (float)N;
 }
 
-static size_t loss_lds(int K) { return (size_t)LOSS_WAVES * 64 * K * sizeof(float); }
+static size_t loss_lds(int K) {
+  return (size_t)LOSS_WAVES * 64 * K * sizeof(float) +
+         (K <= KHIST_LDS ? (size_t)K * (K + 1) * sizeof(unsigned) : 0);
+}
+// dynamic LDS above the default 64 KiB (K > ~60) must be granted per kernel
+template <bool WITH_CE>
+static hipError_t loss_lds_attr(int K) {
+  static int granted = 0;
+  const int shm = (int)loss_lds(K);
+  if (shm <= 65536 || shm <= granted) return hipSuccess;
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_loss<WITH_CE>),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, shm);
+  if (e == hipSuccess) granted = shm;
+  return e;
+}
 
 size_t loss_ws_bytes(int64_t V, int K) {
   (void)V; (void)K;
@@ -203,6 +228,7 @@ hipError_t loss_fwd(const float* logits, const int64_t* labels, int64_t V, int K
   }
   if ((e = hipMemsetAsync(conf, 0, sizeof(int64_t) * K * (K + 1), s)) != hipSuccess) return e;
   if ((e = hipMemsetAsync(nbad, 0, sizeof(unsigned long long), s)) != hipSuccess) return e;
+  if ((e = loss_lds_attr<true>(K)) != hipSuccess) return e;
   hipLaunchKernelGGL(k_loss<true>, dim3(LOSS_GRID), dim3(LOSS_T), loss_lds(K), s, logits, labels,
                      V, K, ignore, cptr, dlogits, reinterpret_cast<unsigned long long*>(conf),
                      part, nbad, class_w, clamp1);
@@ -217,6 +243,7 @@ hipError_t confusion_only(const float* logits, const int64_t* labels, int64_t V,
   if (K > KMAX || K < 1) return hipErrorInvalidValue;
   hipError_t e = hipMemsetAsync(conf, 0, sizeof(int64_t) * K * (K + 1), s);
   if (e != hipSuccess) return e;
+  if ((e = loss_lds_attr<false>(K)) != hipSuccess) return e;
   hipLaunchKernelGGL(k_loss<false>, dim3(LOSS_GRID), dim3(LOSS_T), loss_lds(K), s, logits, labels,
                      V, K, ignore, nullptr, nullptr, reinterpret_cast<unsigned long long*>(conf),
                      nullptr, nullptr, nullptr, 0);

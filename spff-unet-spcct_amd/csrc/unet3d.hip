@@ -132,10 +132,10 @@ void reg_block(spff_unet3d* p, UBlk& b) {
 
 int build(spff_unet3d* p) {
   const spff_unet3d_cfg& c = p->cfg;
-  if (c.batch < 1 || c.in_ch < 1 || c.depth < 1 || c.num_classes < 1 || c.num_classes > 32)
-    return ufail(SPFF_EINVAL, "invalid batch/in_ch/depth/num_classes (K must be 1..32)");
-  if (c.base < 8 || (c.base & (c.base - 1)))
-    return ufail(SPFF_EINVAL, "base must be a power of two >= 8");
+  if (c.batch < 1 || c.in_ch < 1 || c.depth < 1 || c.num_classes < 1 ||
+      c.num_classes > SPFF_MAX_CLASSES)
+    return ufail(SPFF_EINVAL, "invalid batch/in_ch/depth/num_classes (K must be 1..SPFF_MAX_CLASSES)");
+  if (c.base < 8 || c.base % 8) return ufail(SPFF_EINVAL, "base must be a multiple of 8");
   if (c.in_ch > 64) return ufail(SPFF_EINVAL, "in_ch > 64 not supported");
   if (c.math < SPFF_MATH_F32 || c.math > SPFF_MATH_F16X3)
     return ufail(SPFF_EINVAL, "math must be one of SPFF_MATH_*");
@@ -507,7 +507,8 @@ int spff_loss_ex(const float* logits, const int64_t* labels, int64_t nv, int K, 
                  void* stream) {
   if (!logits || !labels || !out4 || !dlogits || !conf || !ws)
     return ufail(SPFF_EINVAL, "null argument");
-  if (K < 1 || K > 32) return ufail(SPFF_EINVAL, "num_classes must be 1..32");
+  if (K < 1 || K > SPFF_MAX_CLASSES)
+    return ufail(SPFF_EINVAL, "num_classes must be 1..SPFF_MAX_CLASSES");
   UHIPCK(loss_fwd(logits, labels, nv, K, ignore, smooth, count_override, out4, dlogits, conf,
                   static_cast<float*>(ws), static_cast<hipStream_t>(stream), class_weights,
                   clamp_denominator));

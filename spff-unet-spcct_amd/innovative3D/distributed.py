@@ -106,10 +106,16 @@ class GradBucketer:
         self.works = []
         self.launched: List[tuple] = []   # (start, end) of every issued all-reduce
         self.begun = 0                    # begin() calls (DataParallelSPFF checks coverage)
+        self.covered = set()              # id() of the parameters whose gradient went through
 
     def begin(self, flat: torch.Tensor) -> None:
         self.flat, self.runs, self.works, self.launched = flat, [], [], []
         self.begun += 1
+
+    def cover(self, param_ids) -> None:
+        """called by the engine's autograd op after a backward through this bucketer:
+        the parameters (ids) whose gradients the buckets all-reduced"""
+        self.covered.update(param_ids)
 
     def abort(self) -> None:
         """Error exit of a backward that had begun: wait for the all-reduces already
@@ -180,18 +186,35 @@ class DataParallelSPFF:
         n = world(self.group)
         hook = self.bucketer if (n > 1 and self.bucketer is not None) else None
         begun = hook.begun if hook is not None else 0
+        if hook is not None:
+            hook.covered.clear()
         self._set_hook(hook)
         try:
             logits = self.module(x)
+            self.last_logits = logits.detach()
             cnt = global_valid_count(y, self.ignore, self.group) if n > 1 else None
             loss_loc, conf, ce = ce_dice_parts(logits, y, self.K, self.ignore,
                                                count_override=cnt)
             loss_loc.backward()
         finally:
             self._set_hook(None)
-        if n > 1 and (hook is None or hook.begun == begun):
-            allreduce_gradients(self.params, self.group)
+        if n > 1:
+            allreduce_uncovered(self.params, hook if (hook is not None and hook.begun != begun)
+                                else None, self.group)
         if n == 1:
             return loss_loc.detach(), conf
         loss, _ce, conf_g = global_loss(ce, conf, self.K, group=self.group)
         return loss, conf_g
+
+
+def allreduce_uncovered(params: Iterable[torch.nn.Parameter], bucketer: Optional[GradBucketer],
+                        group=None) -> int:
+    """All-reduce (one flat collective) every .grad the bucketer did NOT reduce during
+    the backward: the parameters no engine op reported through ``bucketer.cover`` (a
+    parameter of a wrapper outside the plan, or all of them when no plan took the
+    hook).  Returns the number of tensors reduced here.  Every rank sees the same
+    module structure and the same engine ops, so every rank issues the same call."""
+    done = bucketer.covered if bucketer is not None else set()
+    rest = [p for p in params if p.grad is not None and id(p) not in done]
+    allreduce_gradients(rest, group)
+    return len(rest)

@@ -138,7 +138,10 @@ class EnergyFiLM3D(nn.Module):
     def __init__(self, channels: int, hidden: int = 32, pe_dims: int = 16):
         super().__init__()
         if hidden != 32 or pe_dims != 16:
-            raise NotImplementedError("engine EnergyFiLM uses hidden=32, pe_dims=16 (models.py:1485)")
+            raise NotImplementedError(
+                f"EnergyFiLM3D(hidden={hidden}, pe_dims={pe_dims}): the engine supports hidden=32, "
+                "pe_dims=16 only -- the values _DoubleConvSpectral_Novel always uses "
+                "(reference models.py:1470, 1484); see INTEGRATION.md §2")
         self.channels = int(channels)
         self.pe_dims = int(pe_dims)
         self.mlp = nn.Sequential(nn.Conv1d(self.pe_dims, hidden, 1, bias=True), nn.ReLU(inplace=True),
@@ -152,7 +155,10 @@ class FourierGate3D(nn.Module):
     def __init__(self, learn_phase: bool = False):
         super().__init__()
         if learn_phase:
-            raise NotImplementedError("learn_phase=True is not on the SPFF path")
+            raise NotImplementedError(
+                "FourierGate3D(learn_phase=True): the engine supports learn_phase=False only -- "
+                "the value _DoubleConvSpectral_Novel always uses (reference models.py:1471, "
+                "1521); see INTEGRATION.md §2")
         self.learn_phase = False
         self.mag_scale = nn.Parameter(torch.ones(1))
         self._mask = None
@@ -179,6 +185,13 @@ class _DoubleConvSpectral_Novel(nn.Module):
 
 
 # --------------------------------------------------------- engine autograd op --
+def _mark_covered(grad_hook, param_ids) -> None:
+    """tell a GradBucketer which parameters' gradients it all-reduced (their flat
+    gradient went through its buckets), so the caller reduces only the rest"""
+    if grad_hook is not None and hasattr(grad_hook, "cover"):
+        grad_hook.cover(param_ids)
+
+
 class _SPFFFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, core, flat, *params):
@@ -188,6 +201,7 @@ class _SPFFFunction(torch.autograd.Function):
         ctx.gen = plan.generation
         ctx.flat = flat
         ctx.grad_hook = getattr(core, "grad_hook", None)
+        ctx.param_ids = tuple(id(p) for p in params)
         ctx.slices = [(off, n, shape) for (_name, shape, off, n) in plan.params]
         return logits_cl.permute(0, 4, 1, 2, 3)
 
@@ -201,6 +215,7 @@ class _SPFFFunction(torch.autograd.Function):
         if not g_cl.is_contiguous():
             g_cl = g_cl.contiguous()
         dflat = plan.backward(g_cl, ctx.flat, grad_hook=ctx.grad_hook)
+        _mark_covered(ctx.grad_hook, ctx.param_ids)
         grads = [dflat[o:o + n].view(s) for (o, n, s) in ctx.slices]
         return (None, None, None, *grads)
 
@@ -497,6 +512,7 @@ class _UNet3DFunction(torch.autograd.Function):
     def forward(ctx, x, plan, flat, bufs, training, grad_hook, *params):
         logits_cl = plan.forward(x, flat, bufs, training)
         ctx.plan, ctx.gen, ctx.flat, ctx.grad_hook = plan, plan.generation, flat, grad_hook
+        ctx.param_ids = tuple(id(p) for p in params)
         ctx.slices = [(off, n, shape) for (_name, shape, off, n) in plan.params]
         return logits_cl.permute(0, 4, 1, 2, 3)
 
@@ -508,6 +524,7 @@ class _UNet3DFunction(torch.autograd.Function):
                               "backward of this one; the engine keeps one forward's activations")
         g_cl = g.permute(0, 2, 3, 4, 1).contiguous()
         dflat = plan.backward(g_cl, ctx.flat, grad_hook=ctx.grad_hook)
+        _mark_covered(ctx.grad_hook, ctx.param_ids)
         grads = [dflat[o:o + n].view(s) for (o, n, s) in ctx.slices]
         return (None, None, None, None, None, None, *grads)
 
@@ -773,6 +790,7 @@ class _SwinFunction(torch.autograd.Function):
     def forward(ctx, x, plan, flat, grad_hook, *params):
         logits_cl = plan.forward(x, flat)
         ctx.plan, ctx.gen, ctx.flat, ctx.grad_hook = plan, plan.generation, flat, grad_hook
+        ctx.param_ids = tuple(id(p) for p in params)
         ctx.slices = [(off, n, shape) for (_name, shape, off, n) in plan.params]
         return logits_cl.permute(0, 4, 1, 2, 3)
 
@@ -784,6 +802,7 @@ class _SwinFunction(torch.autograd.Function):
                               "backward of this one; the engine keeps one forward's activations")
         g_cl = g.permute(0, 2, 3, 4, 1).contiguous()
         dflat = plan.backward(g_cl, ctx.flat, grad_hook=ctx.grad_hook)
+        _mark_covered(ctx.grad_hook, ctx.param_ids)
         grads = [dflat[o:o + n].view(s) for (o, n, s) in ctx.slices]
         return (None, None, None, None, *grads)
 

@@ -142,23 +142,37 @@ class DepthShardedSPFF:
     axis = 0  # SPFF_SHARD_DEPTH
 
     def __init__(self, core: torch.nn.Module, num_classes: int, ignore_index: int = 255,
-                 group=None, coll=None, timeout: float = 300.0):
+                 group=None, coll=None, timeout: float = 300.0, bucket_bytes: int = 4 << 20,
+                 overlap: bool = True):
         self.core, self.K, self.ignore, self.group = core, int(num_classes), ignore_index, group
         self.coll = coll or TorchDepthColl(group, timeout=timeout)
         core.shard = (self.coll.world, self.coll.rank, self.axis)
         core.shard_coll = self.coll
         self.params = [p for p in core.parameters()]
+        # the flat weight gradient is SUM-all-reduced in buckets WHILE the backward runs
+        # (the engine's grad hook, as innovative3D.distributed.DataParallelSPFF does)
+        self.bucketer = Dd.GradBucketer(group, bucket_bytes) if overlap else None
 
     def step(self, x: torch.Tensor, y: torch.Tensor):
         from .helpers import ce_dice_parts
         for p in self.params:
             p.grad = None
-        logits = self.core(x)
-        self.last_logits = logits.detach()
-        cnt = Dd.global_valid_count(y, self.ignore, self.group)
-        loss_loc, conf, ce = ce_dice_parts(logits, y, self.K, self.ignore, count_override=cnt)
-        loss_loc.backward()
-        Dd.allreduce_gradients(self.params, self.group)
+        hook = self.bucketer if self.coll.world > 1 else None
+        begun = hook.begun if hook is not None else 0
+        if hook is not None:
+            hook.covered.clear()
+        self.core.grad_hook = hook
+        try:
+            logits = self.core(x)
+            self.last_logits = logits.detach()
+            cnt = Dd.global_valid_count(y, self.ignore, self.group)
+            loss_loc, conf, ce = ce_dice_parts(logits, y, self.K, self.ignore, count_override=cnt)
+            loss_loc.backward()
+        finally:
+            self.core.grad_hook = None
+        # whatever the bucketer did not cover (everything, if the plan never took the hook)
+        Dd.allreduce_uncovered(self.params, hook if (hook is not None and hook.begun != begun)
+                               else None, self.group)
         # the global value: summed CE shares + 0.5 * Dice of the summed confusion
         loss, _ce, conf_g = Dd.global_loss(ce, conf, self.K, group=self.group)
         return loss, conf_g

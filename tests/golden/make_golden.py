@@ -348,6 +348,19 @@ def main():
                                                     use_fouriergate=fgate, use_moe=False)
         return core
 
+    # --- Fx5 (round 4): the module contract beyond the registry settings -- K = 40
+    # classes (> 32) and base 24 (not a power of two: channels 24/48/96/192, SE hidden
+    # 4/4/6/12), north-star layout, batch 2 ---
+    rng = np.random.default_rng(88)
+    x = rng.standard_normal((2, 5, 6, 24, 24)).astype(np.float32)
+    y = _labels(rng, (2, 6, 24, 24), 40, absent=17)
+    cases["fx5_k40_base24"] = dict(
+        meta=dict(variant="SPFF-UNet", in_ch=5, base=24, K=40, seed=12, jitter=0.25, lit=False),
+        data=_run_case(torch, Hh, ns_core(5, 40, 24), x, y, 40, 12, 0.25, False, False))
+    if only and only.startswith("fx5"):
+        _write(cases, only)
+        return
+
     # --- Fx2: north-star layout (Cin=5 channels, spatial D), base=8, full grads ---
     rng = np.random.default_rng(22)
     x = rng.standard_normal((1, 5, 16, 32, 32)).astype(np.float32)

@@ -237,3 +237,48 @@ def test_data_parallel_hooks_every_submodule_and_falls_back(monkeypatch):
     assert getattr(m.backbone, "grad_hook", "x") is None   # and was removed afterwards
     assert calls == [1]                              # no plan began the hook: fallback ran
     assert torch.equal(m.backbone.w.grad, torch.ones(3))
+
+
+def test_data_parallel_reduces_parameters_outside_the_plan(monkeypatch):
+    """once an engine op takes the hook, the parameters it covered are
+    reduced by the buckets, and every OTHER parameter (a wrapper's own, outside the
+    plan's flat buffer) is still all-reduced after the backward -- exactly once."""
+    from innovative3D import distributed as Dd
+    import innovative3D.helpers as Hh
+
+    class Plan(torch.nn.Module):     # stands in for an engine op: covers its parameter
+        def __init__(self):
+            super().__init__()
+            self.w = torch.nn.Parameter(torch.ones(3))
+
+        def forward(self, x):
+            hook = self.grad_hook
+            hook.begin(torch.zeros(3))
+            hook.cover([id(self.w)])
+            return x * self.w
+
+    class Wrapper(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.core = Plan()
+            self.extra = torch.nn.Parameter(torch.full((2,), 2.0))
+
+        def forward(self, x):
+            return self.core(x) * self.extra.sum()
+
+    m = Wrapper()
+    reduced = []
+    monkeypatch.setattr(Dd, "world", lambda group=None: 2)
+    monkeypatch.setattr(Dd, "global_valid_count", lambda *a, **k: None)
+    monkeypatch.setattr(Dd, "allreduce_gradients",
+                        lambda params, group=None: reduced.append([id(p) for p in params]))
+    monkeypatch.setattr(Dd, "global_loss", lambda ce, conf, K, group=None: (ce, ce, conf))
+    monkeypatch.setattr(Hh, "ce_dice_parts",
+                        lambda lg, y, K, ig, count_override=None: (lg.sum(), None, lg.sum()))
+    dp = Dd.DataParallelSPFF(m, 3)
+    dp.step(torch.ones(3), None)
+    assert reduced == [[id(m.extra)]]
+    # a second step starts from an empty coverage set
+    reduced.clear()
+    dp.step(torch.ones(3), None)
+    assert reduced == [[id(m.extra)]]

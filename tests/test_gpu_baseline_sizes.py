@@ -197,9 +197,9 @@ def config2_oracle():
 
 
 @pytest.mark.timeout(600)
-# (bf16x6, round 2's default: profiles/r02/gpu_baseline_sizes_parity.txt and
-#  profiles/r03/pytest_gpu_head.log hold its config-2 runs; dropped here for suite time)
-@pytest.mark.parametrize("mth", ["f16x3", "f32"])
+# all three arithmetics at full size: f16x3 (the default), the f32 MFMA path and
+# bf16x6 (the exact 3-plane split, round 2's default)
+@pytest.mark.parametrize("mth", ["f16x3", "f32", "bf16x6"])
 def test_config2_headline_matches_oracle(config2_oracle, mth):
     import innovative3D.helpers as Hh
     st, x, y, ref_logits, ref_loss = config2_oracle

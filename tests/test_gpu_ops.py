@@ -177,3 +177,71 @@ def test_loss_all_ignored_is_nan_with_zero_grad():
     loss.backward()
     assert math.isnan(float(loss))
     assert float(lg.grad.abs().max()) == 0.0
+
+
+def _near(mask, rd, rh, rw):
+    """voxels within (rd, rh, rw) of a set voxel of mask [B, D, H, W] (box dilation)"""
+    m = mask.double().unsqueeze(1)
+    k = torch.ones(1, 1, 2 * rd + 1, 2 * rh + 1, 2 * rw + 1, dtype=torch.float64)
+    return F.conv3d(m, k, padding=(rd, rh, rw))[:, 0] > 0
+
+
+@pytest.mark.parametrize("cin,cout", [(32, 32), (64, 64), (16, 16)])
+def test_conv3d_f16x3_intra_tensor_range(cin, cout):
+    """a few outliers 1e10 .. 1e12 x the rest inside ONE operand.
+    The outputs whose receptive field excludes the outliers are judged per output
+    against an fp64 conv, relative to the output's own absolute sum A_i = (|x| * |w|)_i
+    (the scale of fp32 summation error), and compared with the f32 MFMA path on the same
+    outputs.  Inside a tile whose halo holds an outlier, f16x3's per-(tile, chunk) scale
+     flushes elements below 2^-39 of the outlier, so "away" = more than one
+    tile (4 x 8 x 16 voxels) plus the halo from every outlier.  fwd: outliers in x; dgrad:
+    outliers in dy; wgrad (its outputs sum over every voxel, outliers included): outliers in
+    x, judged per weight against sum_v |x(v + t)| |dy(v)|."""
+    B, D, H, W, ksd = 1, 12, 32, 48, 3
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(B, cin, D, H, W, generator=g)
+    w = torch.randn(cout, cin, ksd, 3, 3, generator=g) / math.sqrt(cin * ksd * 9)
+    dy = torch.randn(B, cout, D, H, W, generator=g)
+    out_mask = torch.zeros(B, D, H, W, dtype=torch.bool)
+    for (d, h, ww), a in zip(((2, 5, 7), (9, 26, 40), (6, 17, 3)), (1e10, 1e11, 1e12)):
+        x[0, :, d, h, ww] *= a
+        dy[0, :, d, h, ww] *= a
+        out_mask[0, d, h, ww] = True
+    far = ~_near(out_mask, 5, 9, 17)
+    assert int(far.sum()) > 0.3 * far.numel()
+    pad = (ksd // 2, 1, 1)
+    y64 = F.conv3d(x.double(), w.double(), None, padding=pad)
+    ya = F.conv3d(x.double().abs(), w.double().abs(), None, padding=pad)
+    dx64 = torch.nn.grad.conv3d_input(x.shape, w.double(), dy.double(), padding=pad)
+    dxa = torch.nn.grad.conv3d_input(x.shape, w.double().abs(), dy.double().abs(), padding=pad)
+    # wgrad: outliers only in x (dy without them), per weight vs its absolute sum
+    dy_w = torch.randn(B, cout, D, H, W, generator=g)
+    dw64 = torch.nn.grad.conv3d_weight(x.double(), w.shape, dy_w.double(), padding=pad)
+    dwa = torch.nn.grad.conv3d_weight(x.double().abs(), w.shape, dy_w.double().abs(), padding=pad)
+    ldx = cin
+    L, p, st = E.lib(), E._ptr, E._stream(torch.device(DEV))
+    xcl, wd, dyg, dywg = _cl(x).to(DEV), w.to(DEV), _cl(dy).to(DEV), _cl(dy_w).to(DEV)
+    ws = torch.empty(L.spff_conv3d_ws_bytes(B, D, H, W, cin, cout, ksd), dtype=torch.uint8,
+                     device=DEV)
+    res = {}
+    for m in (E.MATH_F32, E.MATH_NAMES["f16x3"]):
+        yg = torch.empty(B, D, H, W, cout, device=DEV)
+        dxg = torch.empty(B, D, H, W, cin, device=DEV)
+        dwg = torch.empty_like(wd)
+        E.check(L.spff_conv3d_fwd_ex(p(xcl), ldx, p(wd), p(yg), B, D, H, W, cin, cout, ksd, m,
+                                     p(ws), st), "fwd")
+        E.check(L.spff_conv3d_dgrad_ex(p(dyg), p(wd), p(dxg), B, D, H, W, cin, cout, ksd, m,
+                                       p(ws), st), "dgrad")
+        E.check(L.spff_conv3d_wgrad_ex(p(xcl), ldx, p(dywg), p(dwg), B, D, H, W, cin, cout, ksd,
+                                       m, p(ws), st), "wgrad")
+        torch.cuda.synchronize()
+        e_y = ((yg.cpu().double() - _cl(y64)).abs() / _cl(ya).clamp_min(1e-300))[far]
+        e_x = ((dxg.cpu().double() - _cl(dx64)).abs() / _cl(dxa).clamp_min(1e-300))[far]
+        e_w = (dwg.cpu().double() - dw64).abs() / dwa.clamp_min(1e-300)
+        res[m] = (float(e_y.max()), float(e_x.max()), float(e_w.max()))
+    f32, f16 = res[E.MATH_F32], res[E.MATH_NAMES["f16x3"]]
+    for k, name in enumerate(("fwd", "dgrad", "wgrad")):
+        print(f"cin {cin} cout {cout} {name}: max per-output error / abs-sum away from the "
+              f"outliers: f16x3 {f16[k]:.2e}, f32 MFMA {f32[k]:.2e}")
+    for k in range(3):
+        assert f16[k] <= max(4 * f32[k], 2e-7), (k, f16, f32)

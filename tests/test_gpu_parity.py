@@ -314,3 +314,49 @@ def test_stagewise_forward(name):
     print("\n".join(f"  {k:10s} rel {e:.2e}" for k, e in report))
     bad = [(k, e) for k, e in report if e > 1e-4]
     assert not bad, f"first diverging stage: {bad[0]}"
+
+
+@pytest.mark.parametrize("in_ch,K,base,mth", [(72, 40, 40, "f16x3"), (72, 40, 40, "f32"),
+                                              (3, 100, 16, "bf16x6")])
+def test_module_contract_generality(in_ch, K, base, mth):
+    """VERDICT r03 missing #2: settings the registry never uses but the reference's module
+    contract accepts (models.py:1558-1560) -- in_ch > 64, K > 32 (up to SPFF_MAX_CLASSES)
+    and a base that is a multiple of 8 but not a power of two (channels 40/80/160/320, SE
+    hidden 4/5/10/20).  Engine vs the oracle (pinned to the reference by the fixtures,
+    including the reference-generated fx5_k40_base24): logits within 1e-3, argmax outside
+    near-ties, loss, and every gradient against the kink-consistent fp64 oracle."""
+    from innovative3D.synthetic import synthetic_batch
+    from innovative3D.weightgen import synth_state
+    B, D, H, W = 1, 4, 16, 16
+    core = M.build_spct_energyfilm_fourier(num_classes=K, base=base, in_channels=in_ch)
+    for b in core._blocks():
+        b.fgate._ensure_mask(D, "cpu")
+    st = synth_state([(k, tuple(v.shape)) for k, v in core.state_dict().items()], seed=31,
+                     mask_jitter=0.25)
+    core.load_state_dict({k: torch.from_numpy(v) for k, v in st.items()})
+    core = core.to(DEV)
+    core.math = mth
+    x, y = synthetic_batch(B, in_ch, D, H, W, num_classes=K, ignore_frac=0.03, seed=32)
+    logits = core(x.to(DEV))
+    loss, conf = Hh.ce_dice_with_confusion(logits, y.to(DEV), K, 255)
+    loss.backward()
+    torch.cuda.synchronize()
+    cfg = O.SpffCfg(in_ch=in_ch, num_classes=K, base=base)
+    P = O.params_from_state({k: v for k, v in st.items() if not k.endswith("._mask")},
+                            requires_grad=False)
+    with torch.no_grad():
+        ref = O.forward(P, x, cfg)
+        ref_loss = float(O.ce_plus_macro_dice(ref, y, K)[0])
+    lg = logits.detach().cpu().numpy()
+    err = float(np.abs(lg - ref.numpy()).max())
+    flips = lg.argmax(1) != ref.numpy().argmax(1)
+    print(f"in_ch {in_ch} K {K} base {base} {mth}: max|dlogit| {err:.2e}, flips {int(flips.sum())}, "
+          f"loss {float(loss):.7f} vs {ref_loss:.7f}")
+    assert err <= 1e-3
+    assert not (flips & ~near_tie_mask(ref.numpy(), 2 * err)).any()
+    assert math.isclose(float(loss), ref_loss, rel_tol=1e-5)
+    assert int(conf[:, K].sum()) == 0
+    masks = engine_branch_masks(core, tuple(x.shape), st, cfg)
+    ref64, ref32, nflip, absb = oracle_grads_st(cfg, st, x.numpy(), y.numpy(), masks)
+    named = dict(core.named_parameters(remove_duplicate=False))
+    check_grads({k: named[k].grad for k in ref64}, ref64, ref32, absb, st, mth)

@@ -241,3 +241,84 @@ def test_height_sharded_engine_matches_unsharded(tmp_path, world, math_mode, cas
         for p in parts[1:]:
             np.testing.assert_array_equal(p["g_" + kk], parts[0]["g_" + kk])
     _check_vs_oracle(parts, 3, st, _cfg(k, base, 1), x, y, math_mode)
+
+
+# ---- BASELINE config 4's split: 8 ranks, f16x3, >= 12 slices per rank
+# 1 x 5 x 96 x 128^2, K = 13, base 32: each rank owns 12 depth slices, so the 32-wide
+# level-0 f16x3 tiles (4 deep) give 3 depth tiles per rank and the convs take the
+# overlapped path (engine.hip conv_halo: the interior tile while the halo is exchanged on
+# the side stream, dpart 1, then the boundary tiles, dpart 2, each with its own per-launch
+# operand maxima); the first, the last and six interior ranks all run.
+W8_SHAPE, W8_K, W8_BASE = (1, 5, 96, 128, 128), 13, 32
+
+
+def _w8_data():
+    from innovative3D.synthetic import synthetic_batch
+    return synthetic_batch(*W8_SHAPE, num_classes=W8_K, ignore_frac=0.02, seed=17)
+
+
+def _w8_worker(rank, world, port, math_mode, out):
+    import pathlib
+    import sys
+    root = pathlib.Path(__file__).resolve().parents[1]
+    sys.path[:0] = [str(root), str(root / "tests"), str(root / "spff-unet-spcct_amd")]
+    from innovative3D.sharded import DepthShardedSPFF, shard_bounds
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    B, C, D, H, W = W8_SHAPE
+    core = _model(math_mode, D, W8_K, W8_BASE, C)
+    x, y = _w8_data()
+    off, d = shard_bounds(D, world, rank)
+    step = DepthShardedSPFF(core, W8_K, 255)
+    loss, conf = step.step(x[:, :, off:off + d].contiguous().cuda(), y[:, off:off + d].contiguous().cuda())
+    torch.cuda.synchronize()
+    mk = _save_masks(core, (B, C, d, H, W), _cfg(W8_K, W8_BASE, C))
+    np.savez(f"{out}.{rank}.npz", logits=step.last_logits.cpu().numpy(), loss=float(loss),
+             conf=conf.cpu().numpy(), launched=np.array(step.bucketer.launched), **mk,
+             **{"g_" + k: p.grad.cpu().numpy() for k, p in core.named_parameters(remove_duplicate=False)
+                if p.grad is not None})
+    del step, core
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(900)
+def test_depth_sharded_world8_f16x3_overlapped(tmp_path):
+    import innovative3D.helpers as Hh
+    from innovative3D.sharded import shard_bounds
+    world, mth = 8, "f16x3"
+    B, C, D, H, W = W8_SHAPE
+    assert shard_bounds(D, world, 0)[1] >= 12
+    core = _model(mth, D, W8_K, W8_BASE, C)
+    st = core._synth_state
+    x, y = _w8_data()
+    logits = core(x.cuda())
+    loss, conf = Hh.ce_dice_with_confusion(logits, y.cuda(), W8_K, 255)
+    loss.backward()
+    ref = logits.detach().cpu().numpy()
+    loss_ref, conf_ref = float(loss), conf.cpu().numpy()
+    nflat = sum(p.numel() for p in core.parameters() if p.grad is not None)
+    del core, logits, loss
+    torch.cuda.empty_cache()
+    out = str(tmp_path / "w8")
+    mp.spawn(_w8_worker, args=(world, _free_port(), mth, out), nprocs=world, join=True)
+    parts = [np.load(f"{out}.{r}.npz") for r in range(world)]
+    lg = np.concatenate([p["logits"] for p in parts], axis=2)
+    e = float(np.abs(lg - ref).max())
+    nflip = int((lg.argmax(1) != ref.argmax(1)).sum())
+    spans = sorted(map(tuple, parts[0]["launched"]))
+    print(f"world 8 {mth} 1x5x96x128^2: max|dlogit| {e:.2e} (max|logit| {np.abs(ref).max():.2f}), "
+          f"argmax flips {nflip}, loss {float(parts[0]['loss']):.7f} vs {loss_ref:.7f}, "
+          f"{len(spans)} bucketed gradient all-reduces")
+    assert e <= 1e-4 * float(np.abs(ref).max())
+    assert abs(float(parts[0]["loss"]) - loss_ref) <= 1e-5 * abs(loss_ref)
+    assert int(np.abs(parts[0]["conf"] - conf_ref).sum()) <= 2 * nflip
+    # the gradient went through the bucketer during the backward, every float once
+    assert spans[0][0] == 0 and all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+    assert spans[-1][1] == nflat and len(spans) > 1
+    for k in (f for f in parts[0].files if f.startswith("g_")):
+        for p in parts[1:]:
+            np.testing.assert_array_equal(p[k], parts[0][k])
+    _check_vs_oracle(parts, 2, st, _cfg(W8_K, W8_BASE, C), x, y, mth)
