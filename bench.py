@@ -567,6 +567,10 @@ def main():
     ap.add_argument("--memory", choices=("auto", "full", "lean"), default="auto",
                     help="saved-activation layout (include/spff.h SPFF_MEM_*)")
     ap.add_argument("--hw", type=int, default=512)
+    ap.add_argument("--one-gpu", action="store_true",
+                    help="functional dry run: every rank on cuda:0 with host-staged gloo "
+                         "collectives (e.g. 8 ranks of --workload volume512 --strong on a "
+                         "1-GPU box); the timings are not a scaling measurement")
     ap.add_argument("--coll-timeout", type=float, default=600.0,
                     help="seconds before a collective is declared failed (process group timeout)")
     ap.add_argument("--cpu-depth", type=int, default=0,
@@ -581,15 +585,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    device = torch.device("cuda", local)
+    device = torch.device("cuda", 0 if args.one_gpu else local)
     torch.cuda.set_device(device)
     if world > 1:
         # a dead or wedged peer fails the collective after this long instead of hanging the
         # job (SURVEY §5 failure detection; the reference sets NCCL_ASYNC_ERROR_HANDLING)
         os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
         import datetime
-        dist.init_process_group("nccl", device_id=device,
-                                timeout=datetime.timedelta(seconds=args.coll_timeout))
+        if args.one_gpu:  # RCCL refuses two ranks on one device: host-staged gloo
+            dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=args.coll_timeout))
+        else:
+            dist.init_process_group("nccl", device_id=device,
+                                    timeout=datetime.timedelta(seconds=args.coll_timeout))
 
     if args.workload == "unet3d":
         return bench_unet3d(args, world, rank, device)
@@ -653,6 +660,10 @@ def main():
     plan = core._plan
     plan.prof_enable(True)
     plan.prof_collect()
+    # the shard group's collective callbacks (halo exchanges, statistics all-reduces), timed
+    # with HIP events on the stream each one's work runs on
+    plan.coll_timing = world > 1 and (sharded or registry)
+    plan.coll_collect()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -666,6 +677,8 @@ def main():
     elapsed_local = elapsed
     prof = plan.prof_collect()
     plan.prof_enable(False)
+    coll = plan.coll_collect() if plan.coll_timing else {}
+    plan.coll_timing = False
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -788,6 +801,20 @@ def main():
     }
     if world > 1:
         out["ranks"] = rank_report(elapsed_local, args.steps, device)
+        bk = getattr(runner, "bucketer", None)
+        out["collectives"] = {
+            "per_step": {k: {"calls": v["calls"] / args.steps, "ms": v["ms"] / args.steps,
+                             "MB": v["bytes"] / args.steps / 1e6} for k, v in coll.items()},
+            # the bucketed gradient all-reduces of the last step (issued during its backward)
+            "grad_allreduce_buckets_last_step": len(bk.launched) if bk else None,
+            "grad_allreduce_MB": (sum(b - a for a, b in bk.launched) * 4 / 1e6) if bk else None,
+            "backend": dist.get_backend(),
+            "note": ("HIP events around each spff_coll callback's work on its stream (rank 0); "
+                     "halos on the side stream overlap the interior conv tiles, so their time "
+                     "is the exchange's own duration" + ("; --one-gpu: every rank shares one "
+                     "GPU through host-staged gloo, so these times are not a scaling "
+                     "measurement" if args.one_gpu else ""))}
+        out["f16_absmax_ms_per_step"] = prof["f16_absmax"][0] / args.steps
     if rank == 0 and world == 1 and args.cpu_baseline == "auto" and not (sharded or registry):
         out["cpu_baseline"] = cpu_baseline(st, K, args.base, x_cpu, y_cpu, args.cpu_depth,
                                            args.cpu_steps)

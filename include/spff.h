@@ -160,7 +160,9 @@ int spff_debug_set(spff_plan* plan, int key, int value);
  * classes 0 = conv3d fwd, 1 = conv3d dgrad (same kernel), 2 = conv3d wgrad,
  * 3 = ConvTranspose / 1x1 head GEMMs, and the HBM-bound passes 4 = per-(b,c,d)
  * slab reductions (IN statistics, gate sums; incl. the split combine),
- * 5 = IN/gate apply (act_apply), 6 = IN backward apply (in_bwd_apply).
+ * 5 = IN/gate apply (act_apply), 6 = IN backward apply (in_bwd_apply), 7 = the
+ * SPFF_MATH_F16X3 operand-max passes of the weight gradients' scales (the weights, the
+ * block inputs, the a1 bound; per launch in sharded plans).
  * collect() syncs on the recorded events and writes out[4*c + {0,1,2,3}] =
  * {total ms, algorithmic FLOPs, launches, algorithmic HBM bytes (operands read
  * once, result written once)}. */

@@ -14,9 +14,12 @@ HIPCC="${HIPCC:-/opt/rocm/bin/hipcc}"
 SAN="-Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-sanitize-recover=undefined -Xarch_host -fno-omit-frame-pointer"
 FLAGS="-O1 -g -std=c++17 -fPIC --offload-arch=gfx950 -I$ROOT/include -I$PKG/csrc -Wno-unused-result"
 pids=()
+# the newest header any translation unit may include (csrc/*.h, include/*.h): an object
+# older than it is rebuilt, so a header edit never leaves stale sanitizer objects
+newest_h="$(ls -t "$PKG"/csrc/*.h "$ROOT"/include/*.h | head -1)"
 for src in "$PKG"/csrc/*.hip; do
   obj="$OUT/$(basename "${src%.hip}").o"
-  if [ ! -f "$obj" ] || [ "$src" -nt "$obj" ] || [ "$PKG/csrc/spff_internal.h" -nt "$obj" ] || [ "$ROOT/include/spff.h" -nt "$obj" ]; then
+  if [ ! -f "$obj" ] || [ "$src" -nt "$obj" ] || [ "$newest_h" -nt "$obj" ]; then
     $HIPCC $FLAGS $SAN -c "$src" -o "$obj" &
     pids+=($!)
   fi

@@ -113,8 +113,9 @@ int main() {
   plan_case("ablation no efilm/fgate", cfg_of(1, 5, 8, 32, 32, 9, 8, 1, 0, 0, 0, 1, 0, 0, 1, 1));
   plan_case("ablation no se/specse", cfg_of(1, 5, 8, 32, 32, 9, 8, 1, 0, 0, 0, 1, 1, 1, 0, 0));
   reject("H < 8", cfg_of(1, 1, 5, 4, 64, 13));
-  reject("K > 32", cfg_of(1, 1, 5, 64, 64, 40));
-  reject("base 24", cfg_of(1, 1, 5, 64, 64, 13, 24));
+  plan_case("K 40 base 24 (fx5)", cfg_of(1, 5, 6, 24, 24, 40, 24));
+  reject("K > SPFF_MAX_CLASSES", cfg_of(1, 1, 5, 64, 64, SPFF_MAX_CLASSES + 1));
+  reject("base 20", cfg_of(1, 1, 5, 64, 64, 13, 20));
   reject("depth shard batch 2", cfg_of(2, 1, 8, 64, 64, 13, 32, 2, 0, SPFF_SHARD_DEPTH));
   reject("height shard 60 rows", cfg_of(1, 1, 5, 60, 512, 13, 32, 2, 0, SPFF_SHARD_HEIGHT));
   reject("bad shard axis", cfg_of(1, 1, 5, 64, 512, 13, 32, 2, 0, 2));

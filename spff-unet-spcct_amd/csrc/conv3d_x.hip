@@ -89,6 +89,17 @@
 // allows 3; 3 caps them at 168 VGPRs)
 #define SPFF_X32WG 3
 #endif
+#ifndef SPFF_XSCALE_LATE
+// f16x3 per-(tile, chunk) input scale: 1 = each wave publishes its max of the next chunk's
+// halo late in the current chunk and the halo is split after the chunk-boundary barrier;
+// 0 = a workgroup barrier in the middle of the chunk, the split beside the MFMAs
+#define SPFF_XSCALE_LATE 0
+#endif
+#ifndef SPFF_XSCALEJ
+// (SPFF_XSCALE_LATE 0) the k-step of the chunk at which the workgroup takes the next
+// chunk's max and starts splitting its halo; -1 = the middle (NJ / 2)
+#define SPFF_XSCALEJ -1
+#endif
 #ifndef SPFF_XIGLP
 #define SPFF_XIGLP -1
 #endif
@@ -280,7 +291,7 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : (BN <= 32 && NS == NS_F16 &&
     Src2 x, const uint4* __restrict__ wp, Dst2 y, Vol vol, int Cin, int nkc, int Cout, int npad,
     int tilesD, int tilesH, int tilesW, float* __restrict__ part, int kps,
     float* __restrict__ stats, int ntiles, int td0, int tds, int th0, int ths,
-    const unsigned* __restrict__ wmx, const unsigned* __restrict__ xmx) {
+    const unsigned* __restrict__ wmx) {
   constexpr int XT_THREADS = NW * 64;
   // planes per operand; HF: two fp16 planes of the scaled operands (NS_F16, bf16split.h)
   constexpr int NP = nplanes(NS);
@@ -302,15 +313,26 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : (BN <= 32 && NS == NS_F16 &&
   constexpr int NWU = NP * T2 * BN;  // pre-split weight units (16 B) per chunk
   static_assert(NWU % 64 == 0, "weight image must be whole 1 KiB DMA pieces");
   static_assert(!X16 || TD * TH == NW * RB, "X16: one W-row per 16-row block");
-  constexpr int SPJ = (RH + (NJ - NJ / 2) - 1) / (NJ - NJ / 2);  // halo float4 split per k-step
+  // the k-step from which the next chunk's halo is split (HF: after its block max), and the
+  // halo float4 split per k-step from there on
+  constexpr int J0 = (NS == NS_F16 && SPFF_XSCALEJ >= 0 && SPFF_XSCALEJ < NJ) ? SPFF_XSCALEJ : NJ / 2;
+  constexpr int SPJ = (RH + (NJ - J0) - 1) / (NJ - J0);
   constexpr int NPC = NWU / 64;
   extern __shared__ uint4 lds4[];
   uint4* Xs = lds4;               // [NP][NPOS]
   uint4* Ws = lds4 + NP * NPOS;   // [NP][T2][BN]
-  // HF: x is scaled by 2^ex (*xmx: max |x|), the packed weights by 2^ew (*wmx: max |w|)
-  const int ex = HF ? f16_scale_exp(*xmx) : 0;
+  // HF: the packed weights are scaled by 2^ew (*wmx: max |w| of the tensor); the input by a
+  // scale of its own per (tile, 8-channel chunk): 2^exc from the max |element| of exactly
+  // the halo chunk this workgroup stages (block max below), so an element is flushed to
+  // the fp16 subnormal floor only below 2^-39 of the largest element of its own tile's
+  // halo chunk -- not of the whole tensor (f16_scale_exp, bf16split.h).  The accumulator
+  // holds the products in units of 2^(exc + ew) and is rescaled (exact: a power of two)
+  // when the next chunk's exponent differs.
   const int ew = HF ? f16_scale_exp(*wmx) : 0;
-  const float sx = exp2i(ex);
+  int exc = 0;       // exponent of the chunk being accumulated
+  int exn = 0;       // exponent of the chunk in the registers (the next one)
+  float sx = 1.f;    // 2^exn: the scale the halo split applies
+  __shared__ unsigned smx[2][NW];  // per-wave max |x| bits of a chunk (parity slots)
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -391,7 +413,7 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : (BN <= 32 && NS == NS_F16 &&
   // decomposition and bounds are ~20 VALU per float4 beside MFMAs that now take half the
   // cycles with two fp16 planes); the 64-wide kernel has no registers to spare
   constexpr bool PRE = BN <= 32 && !HR;
-  int64_t pvox[PRE ? RH : 1];
+  int pvox[PRE ? RH : 1];  // (voxel indices < 2^31: launch_fwd_xh checks)
   unsigned pok = 0;
   if constexpr (PRE) {
 #pragma unroll
@@ -403,7 +425,7 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : (BN <= 32 && NS == NS_F16 &&
       const bool ok = i < NHX && (unsigned)(gd + vol.dh) < (unsigned)(D + 2 * vol.dh) &&
                       (unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W &&
                       !((gd < 0 && x.zlo) || (gd >= D && x.zhi));
-      pvox[k] = ok ? (((int64_t)b * D + gd) * H + gh) * W + gw : 0;
+      pvox[k] = ok ? ((b * D + gd) * H + gh) * W + gw : 0;
       pok |= ok ? (1u << k) : 0u;
     }
   }
@@ -421,7 +443,7 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : (BN <= 32 && NS == NS_F16 &&
         const bool s0 = c < x.split;
         const float* src = s0 ? x.p0 : x.p1;
         const int64_t ld = s0 ? x.ld0 : x.ld1;
-        hreg[k] = *reinterpret_cast<const float4*>(src + (ok ? pvox[k] : 0) * ld +
+        hreg[k] = *reinterpret_cast<const float4*>(src + (int64_t)(ok ? pvox[k] : 0) * ld +
                                                    (s0 ? c : c - x.split));
         hvalid |= ok ? (1u << k) : 0u;
       }
@@ -462,7 +484,57 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : (BN <= 32 && NS == NS_F16 &&
       hvalid |= ok ? (1u << k) : 0u;
     }
   };
+  // HF: the fused input activation (32-wide tiles) and the zero padding applied to the
+  // prefetched halo in place, and this thread's max |element| of it
+  auto prep_max = [&]() {
+    float m = 0.f;
+#pragma unroll
+    for (int k = 0; k < RH; ++k) {
+      const bool ok = (hvalid >> k) & 1u;
+      float4 v = hreg[k];
+      if constexpr (BN == 32) if (x.al) {
+        const float* ap = x.al + (int64_t)b * x.ld0 + fkc * 8;
+        const float* dp = x.de + (int64_t)b * x.ld0 + fkc * 8;
+        const bool hi = tid & 1;
+        float r[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float a = hi ? ap[4 + j] : ap[j], e = hi ? dp[4 + j] : dp[j];
+          const float t = r[j] * a + e;
+          r[j] = fmaxf(t, 0.01f * t);
+        }
+        v = make_float4(r[0], r[1], r[2], r[3]);
+      }
+      if (!ok) v = make_float4(0.f, 0.f, 0.f, 0.f);
+      hreg[k] = v;
+      m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    }
+    return m;
+  };
+  // HF: the workgroup's max over the chunk (every thread's prep_max) -> its scale exponent.
+  // Contains a workgroup barrier: call uniformly.
+  auto wave_max_store = [&](float m, int slot) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    if (lane == 0) smx[slot][wave] = __float_as_uint(m);
+  };
+  auto read_scale = [&](int slot) {
+    unsigned mb = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) mb = max(mb, smx[slot][w]);
+    return f16_scale_exp(__builtin_amdgcn_readfirstlane(mb));
+  };
+  auto block_scale = [&](float m, int slot) {
+    wave_max_store(m, slot);
+    __syncthreads();
+    return read_scale(slot);
+  };
   auto split_one = [&](int k) {
+    if constexpr (HF) {  // (prep_max has applied the activation and the padding)
+      const float4 v = hreg[k];
+      split4_pk<NS>(make_float4(v.x * sx, v.y * sx, v.z * sx, v.w * sx), hs[k]);
+      return;
+    }
     const bool ok = (hvalid >> k) & 1u;
     float4 v = hreg[k];
     // fused input activation (zero padding stays zero: applied to valid only).  Compiled
@@ -502,9 +574,19 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : (BN <= 32 && NS == NS_F16 &&
       }
     }
   };
-  auto stash = [&](int kc, bool first) {
+  // store halo float4 k's planes (hs[k]) into the LDS image
+  auto store_one = [&](int k) {
+    const int i = tid + XT_THREADS * k;
+    if (i < NHX) {
+#pragma unroll
+      for (int p = 0; p < NP; ++p)
+        reinterpret_cast<uint2*>(Xs + p * NPOS + (i >> 1))[i & 1] = hs[k][p];
+    }
+  };
+  auto stash = [&](int kc, bool first, bool halo = true) {
 #pragma unroll
     for (int k = 0; k < RH; ++k) {
+      if (!halo) break;
       if (SPFF_XDIAG == 4 && !first) break;
       const int i = tid + XT_THREADS * k;
       if (i < NHX) {
@@ -533,35 +615,77 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : (BN <= 32 && NS == NS_F16 &&
   const int kc0 = part ? blockIdx.z * kps : 0;
   const int kc1 = part ? min(nkc, kc0 + kps) : nkc;
   fetch(kc0);
+  if constexpr (HF) {
+    exc = exn = block_scale(prep_max(), kc0 & 1);
+    sx = exp2i(exn);
+  }
 #pragma unroll
   for (int k = 0; k < RH; ++k) split_one(k);
   // the second-dispatched half of the workgroup loses every issue arbitration
   // on its SIMD: one static priority bump (MI355X_MICROARCH "two waves per SIMD")
   if (SPFF_XPRIO && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
   for (int kc = kc0; kc < kc1; ++kc) {
+    constexpr bool LATE = HF && SPFF_XSCALE_LATE;
+    if (LATE && kc != kc0) {
+      // every wave is past chunk kc - 1's MFMAs and has published its max of chunk kc's
+      // halo: the chunk's scale (capped 2^64 above the current one, so the rescaled
+      // accumulator cannot overflow: |acc| < 2^40 in these units), then the split
+      __syncthreads();
+      exn = min(read_scale(kc & 1), exc + 64);
+      sx = exp2i(exn);
+#pragma unroll
+      for (int k = 0; k < RH; ++k) {
+        split_one(k);
+        store_one(k);
+      }
+    }
     if (kc != kc0) {
       // sign-alternating accumulation: odd chunks carry negated weights, so the
       // accumulator holds (-1)^kc x the partial sum; flip it at every chunk boundary
+      // (HF: and move it to the units of the next chunk's scale)
+      const int dsc = exn - exc;
+      if (HF && dsc != 0) {
 #pragma unroll
-      for (int rb = 0; rb < RB; ++rb)
+        for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
-        for (int cb = 0; cb < CB; ++cb) acc[rb][cb] = -acc[rb][cb];
-      __syncthreads();
+          for (int cb = 0; cb < CB; ++cb)
+#pragma unroll
+            for (int r = 0; r < NREG; ++r) acc[rb][cb][r] = -ldexpf(acc[rb][cb][r], dsc);
+      } else {
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+          for (int cb = 0; cb < CB; ++cb) acc[rb][cb] = -acc[rb][cb];
+      }
+      exc = exn;
+      if (!LATE) __syncthreads();
     }
-    if (SPFF_XDIAG != 1 || kc == kc0) stash(kc, kc == kc0);
+    if (SPFF_XDIAG != 1 || kc == kc0) stash(kc, kc == kc0, !(LATE && kc != kc0));
     __syncthreads();  // (vmcnt(0): the weight DMA has landed)
     if (kc + 1 < kc1) fetch(kc + 1);
 #pragma unroll
     for (int j = 0; j < (SPFF_XDIAG == 2 ? 0 : NJ); ++j) {
       if constexpr (SPFF_XIGLP >= 0) __builtin_amdgcn_iglp_opt(SPFF_XIGLP);
+      // HF: the next chunk's scale before its halo is split (uniform: kc + 1 < kc1).
+      // Capped at 2^64 above the current chunk's, so the rescaled accumulator cannot
+      // overflow (|acc| < 2^40 in these units)
+      if (HF && !LATE && j == J0 && kc + 1 < kc1) {
+        exn = min(block_scale(prep_max(), (kc + 1) & 1), exc + 64);
+        sx = exp2i(exn);
+      }
+      if (LATE && j == (NJ > 2 ? NJ - 2 : 0) && kc + 1 < kc1) {
+        __builtin_amdgcn_sched_barrier(0x10C);
+        wave_max_store(prep_max(), (kc + 1) & 1);
+        __builtin_amdgcn_sched_barrier(0x10C);
+      }
       // split one prefetched halo float4 per k-step from the middle of the
       // chunk on; the fences keep this VALU (and its vmcnt wait) in place
       // while MFMAs and LDS reads may still move across
-      if (j >= NJ / 2 && (j - NJ / 2) * SPJ < RH) {
+      if (!LATE && j >= J0 && (j - J0) * SPJ < RH) {
         __builtin_amdgcn_sched_barrier(0x10C);
 #pragma unroll
         for (int u = 0; u < SPJ; ++u)
-          if ((j - NJ / 2) * SPJ + u < RH) split_one((j - NJ / 2) * SPJ + u);
+          if ((j - J0) * SPJ + u < RH) split_one((j - J0) * SPJ + u);
         __builtin_amdgcn_sched_barrier(0x10C);
       }
       if constexpr (X16) {
@@ -655,7 +779,7 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : (BN <= 32 && NS == NS_F16 &&
 #pragma unroll
       for (int cb = 0; cb < CB; ++cb)
 #pragma unroll
-        for (int r = 0; r < NREG; ++r) acc[rb][cb][r] = ldexpf(acc[rb][cb][r], -(ex + ew));
+        for (int r = 0; r < NREG; ++r) acc[rb][cb][r] = ldexpf(acc[rb][cb][r], -(exc + ew));
   }
 
 // ---- epilogue: C[i][j], row i = voxel (vrow mapping), col j = out channel ----
@@ -868,12 +992,15 @@ template <int BN, int KD, int NS, bool HR, int MB = xt_mb(BN, NS), int NW = xt_n
           int TD = xt_td(BN, NS)>
 static hipError_t launch_fwd_xh(const Src2& x, const uint4* wx, const Dst2& y, Vol vol, int K,
                                 int nkc, int N, int npad, hipStream_t s, float* part, int nsplit,
-                                int kps, float* stats, int dpart, const unsigned* wmx, const unsigned* xmx) {
+                                int kps, float* stats, int dpart, const unsigned* wmx) {
   constexpr int TH = SPFF_X16 ? 2 * NW * MB / TD : NW * MB;
   static_assert(NW == 8 || TD == XT_D || xt_d4(BN, NS), "xt_ntiles: tile shape");
   constexpr size_t shm = xt_lds_bytes<BN, KD, NS, TD, TH>();
   static_assert(shm <= (NW == 8 ? 160 : 80) * 1024, "LDS budget");
   if (x.al && BN != 32) return hipErrorInvalidValue;  // fused activation: 32-wide tiles only
+  // the 16/32-wide kernels hold halo voxel indices in 32 bits (with the halo slices)
+  if (BN <= 32 && (int64_t)vol.B * (vol.D + 2 * vol.dh) * vol.H * vol.W >= (int64_t(1) << 31))
+    return hipErrorInvalidValue;
   auto kern = k_conv3d_fwd_x<BN, KD, NS, MB, NW, SPFF_X16 != 0, TD, HR>;
   static bool attr = false;
   if (!attr) {
@@ -896,7 +1023,7 @@ static hipError_t launch_fwd_xh(const Src2& x, const uint4* wx, const Dst2& y, V
   dim3 grid(8 * cdiv(ntiles, 8) * (npad / BN), 1, part ? nsplit : 1);
   hipLaunchKernelGGL(kern, grid, dim3(NW * 64), shm, s, x, wx, y, vol, K, nkc, N, npad, tilesD,
                      tilesH, tilesW, part, part ? kps : nkc, part ? nullptr : stats, ntiles, td0,
-                     tds, th0, ths, wmx, xmx);
+                     tds, th0, ths, wmx);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || !part) return e;
   const int64_t total = nvox(vol) * N;
@@ -907,11 +1034,11 @@ static hipError_t launch_fwd_xh(const Src2& x, const uint4* wx, const Dst2& y, V
 template <int BN, int KD, int NS>
 static hipError_t launch_fwd_x(const Src2& x, const uint4* wx, const Dst2& y, Vol vol, int K,
                                int nkc, int N, int npad, hipStream_t s, float* part, int nsplit,
-                               int kps, float* stats, int dpart, const unsigned* wmx, const unsigned* xmx) {
+                               int kps, float* stats, int dpart, const unsigned* wmx) {
   return x.rows() ? launch_fwd_xh<BN, KD, NS, true>(x, wx, y, vol, K, nkc, N, npad, s, part,
-                                                    nsplit, kps, stats, dpart, wmx, xmx)
+                                                    nsplit, kps, stats, dpart, wmx)
                   : launch_fwd_xh<BN, KD, NS, false>(x, wx, y, vol, K, nkc, N, npad, s, part,
-                                                     nsplit, kps, stats, dpart, wmx, xmx);
+                                                     nsplit, kps, stats, dpart, wmx);
 }
 
 namespace {
@@ -1145,7 +1272,7 @@ hipError_t conv3d_pack(const float* w, void* wpack, Vol vol, int KD, int Cin_w, 
 template <int NS>
 static hipError_t run_x(const Src2& x, const uint4* wu, const Dst2& y, Vol vol, int KD,
                         const XDims& d, hipStream_t s, float* ws, float* stats, int dpart,
-                        const unsigned* wmx, const unsigned* xmx) {
+                        const unsigned* wmx) {
   // (32x32x16, MB = 4, 2 x 32 x 16 tiles for Cout <= 32: fits LDS but spills 91 VGPRs)
   // (32x32x16 schedule, NW = 4 waves, 2 x 8 x 16 tiles: measured 6 % slower; the 16x16x32
   // schedule takes NW = 4 for BN 32 by default, SPFF_X32NW)
@@ -1154,16 +1281,16 @@ static hipError_t run_x(const Src2& x, const uint4* wu, const Dst2& y, Vol vol, 
   if (d.BN == 64)
     return KD == 3
                ? launch_fwd_x<64, 3, NS>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s, part,
-                                                k.nsplit, k.kps, stats, dpart, wmx, xmx)
+                                                k.nsplit, k.kps, stats, dpart, wmx)
                : launch_fwd_x<64, 1, NS>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s, part,
-                                                k.nsplit, k.kps, stats, dpart, wmx, xmx);
+                                                k.nsplit, k.kps, stats, dpart, wmx);
   if (d.BN == 16)
     return launch_fwd_x<16, 3, NS>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s, part, k.nsplit,
-                                   k.kps, stats, dpart, wmx, xmx);
+                                   k.kps, stats, dpart, wmx);
   return KD == 3 ? launch_fwd_x<32, 3, NS>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s,
-                                                  part, k.nsplit, k.kps, stats, dpart, wmx, xmx)
+                                                  part, k.nsplit, k.kps, stats, dpart, wmx)
                  : launch_fwd_x<32, 1, NS>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s,
-                                                  part, k.nsplit, k.kps, stats, dpart, wmx, xmx);
+                                                  part, k.nsplit, k.kps, stats, dpart, wmx);
 }
 
 
@@ -1213,7 +1340,7 @@ hipError_t conv3d_in_stats_fin(const float* stats, Vol vol, int KD, int Cin, int
 
 hipError_t conv3d_run(const Src2& x, const void* wpack, const Dst2& y, Vol vol, int KD,
                       int Cin_w, int Cout_w, bool dgrad, int math, hipStream_t s, float* ws,
-                      float* stats, int dpart, const unsigned* xmax, const unsigned* wmax) {
+                      float* stats, int dpart, const unsigned* wmax) {
   const XDims d = xdims(KD, Cin_w, Cout_w, dgrad);
   if (stats && (dgrad || !conv3d_fuses_stats(vol, KD, Cin_w, Cout_w, math)))
     return hipErrorInvalidValue;
@@ -1225,24 +1352,14 @@ hipError_t conv3d_run(const Src2& x, const void* wpack, const Dst2& y, Vol vol, 
   if (use_split(vol, math, dgrad)) {
     const uint4* wu = static_cast<const uint4*>(wpack);
     if (math == SPFF_MATH_F16X3) {
+      // the input's scale is taken per (tile, chunk) inside the kernel; the weights' from
+      // the caller's precomputed max |w| or the one conv3d_pack left in the image's slot 0
       unsigned* sl = f16_slots(wpack, KD, Cin_w, Cout_w);
-      if (!xmax) {
-        // max |x| over what this launch reads (interior depth / H tiles: no halo, no rows)
-        // into the image's slot 1; a boundary launch (dpart 2 / 4) after the interior one
-        // adds its halo to the same slot
-        if (dpart != 2 && dpart != 4) {
-          hipError_t e = hipMemsetAsync(sl + 1, 0, sizeof(unsigned), s);
-          if (e != hipSuccess) return e;
-        }
-        hipError_t e = absmax_src(x, vol, d.K, dpart != 1 && dpart != 3, sl + 1, s);
-        if (e != hipSuccess) return e;
-        xmax = sl + 1;
-      }
-      return run_x<NS_F16>(x, wu, y, vol, KD, d, s, ws, stats, dpart, wmax ? wmax : sl, xmax);
+      return run_x<NS_F16>(x, wu, y, vol, KD, d, s, ws, stats, dpart, wmax ? wmax : sl);
     }
     return math == SPFF_MATH_BF16X3
-               ? run_x<2>(x, wu, y, vol, KD, d, s, ws, stats, dpart, nullptr, nullptr)
-               : run_x<3>(x, wu, y, vol, KD, d, s, ws, stats, dpart, nullptr, nullptr);
+               ? run_x<2>(x, wu, y, vol, KD, d, s, ws, stats, dpart, nullptr)
+               : run_x<3>(x, wu, y, vol, KD, d, s, ws, stats, dpart, nullptr);
   }
   return conv3d_fwd(x, static_cast<const float*>(wpack), y, vol, KD, d.K, rup(d.K, 8), d.N,
                     rup(d.N, conv3d_bn(d.N)), s);

@@ -133,7 +133,8 @@ struct spff_plan {
   size_t x_cl = 0, pool[3] = {0, 0, 0}, pidx[3] = {0, 0, 0};
   size_t red_ws = 0, red_out = 0, red_out4 = 0, gscr = 0, Abuf = 0, Bbuf = 0, kk1 = 0, kk2 = 0,
          wg_ws = 0, wt = 0, cst = 0;
-  size_t fsl = 0;  // SPFF_MATH_F16X3 operand maxima, 8 slots per block (f16_slot)
+  size_t fsl = 0;  // SPFF_MATH_F16X3 operand maxima, 8 slots per block (f16_slot), then
+                   // two per-launch slots of the sharded plans' weight gradients
   size_t G_out = 0, G_dy2 = 0, G_da1 = 0, G_dx = 0, dskip[3] = {0, 0, 0};
   size_t part_d = 0;  // sharded plans: fp64 IN partials [B][C][2]
   // height-sharded plans (spff_cfg.shard_axis = SPFF_SHARD_HEIGHT, hshard.hip): the
@@ -196,6 +197,8 @@ struct spff_plan {
 static double cbytes(double V, int Cin, int Cout, int T) {
   return 4.0 * (V * Cin + V * Cout + (double)T * Cin * Cout);
 }
+
+constexpr int F16_SHARD_SLOTS = 7 * 8;
 
 static spff_plan::ProfRec* prof_slot(spff_plan* p, int cls, double flops, double bytes) {
   if (p->prof_n == p->prof.size()) {
@@ -452,7 +455,7 @@ int build_plan(spff_plan* p) {
   p->kk2 = p->alloc((size_t)B * 8 * f * sizeof(float));
   p->wg_ws = p->alloc(wg);
   p->wt = p->alloc(wt);
-  p->fsl = p->alloc(7 * 8 * sizeof(unsigned));
+  p->fsl = p->alloc((F16_SHARD_SLOTS + 2) * sizeof(unsigned));
   p->cst = p->alloc(cst);
   // gradient scratch, sized for level 0 ([V0][f]); a level-l tensor of the path
   // (V0 / 4^l voxels x f 2^l channels) fills 1 / 2^l of a buffer.  Halo'd (level-0
@@ -624,6 +627,17 @@ int conv_wgrad(spff_plan* p, double flops, double bytes, const Src2& x, const fl
                const unsigned* ymax = nullptr) {
   Src2 xr = x;
   if (p->hsh) CK(hrows_exchange(p, x, v, Cin, &xr, p->st));
+  if (p->cfg.math == SPFF_MATH_F16X3 && (!xmax || !ymax)) {
+    // sharded plans: the operand maxima of this launch (x with the halo slices / boundary
+    // rows it reads, dy), timed as class 7 like the unsharded plans' precomputed ones
+    unsigned* sl = reinterpret_cast<unsigned*>(p->ws + p->fsl) + F16_SHARD_SLOTS;
+    HIPCK(hipMemsetAsync(sl, 0, 2 * sizeof(unsigned), p->st));
+    PROFB(p, 7, 0.0, 4.0 * (double)nvox(v) * Cin, absmax_src(xr, v, Cin, true, sl, p->st));
+    PROFB(p, 7, 0.0, 4.0 * (double)nvox(v) * Cout,
+          absmax_src(src1(dy, Cout), v, Cout, false, sl + 1, p->st));
+    xmax = sl;
+    ymax = sl + 1;
+  }
   PROFB(p, 2, flops, bytes,
         conv3d_wgrad(xr, dy, Cout, dw, v, p->KD, Cin, Cout, p->cfg.math, p->F(p->wg_ws), p->st,
                      xmax, ymax));
@@ -636,10 +650,11 @@ int conv_wgrad(spff_plan* p, double flops, double bytes, const Src2& x, const fl
 // last depth tiles after it; otherwise exchange, then convolve.  cls / flops / bytes:
 // the PROFB record of the launch (the interior launch carries the FLOPs, the
 // boundary one adds its time to the same class).
-// (xmax / wmax: f16_slot operand maxima of an unsharded SPFF_MATH_F16X3 plan, else null)
+// (wmax: the f16_slot max |w| of an unsharded SPFF_MATH_F16X3 plan, else null; the input's
+// scale is per (tile, chunk), inside the conv kernel)
 int conv_halo(spff_plan* p, int cls, double flops, double bytes, const Src2& x, const Dst2& y,
               const Vol& v, int Cin_w, int Cout_w, bool dgrad, float* stats,
-              const unsigned* xmax = nullptr, const unsigned* wmax = nullptr) {
+              const unsigned* wmax = nullptr) {
   if (p->hsh) return conv_h(p, cls, flops, bytes, x, y, v, Cin_w, Cout_w, dgrad);
   const int KD = p->KD, math = p->cfg.math;
   const bool ovl = v.dh && !stats && conv3d_splits_depth(v, KD, Cin_w, Cout_w, dgrad, math);
@@ -647,7 +662,7 @@ int conv_halo(spff_plan* p, int cls, double flops, double bytes, const Src2& x, 
     CK(halo_src(p, x, v));
     PROFB(p, cls, flops, bytes,
           conv3d_run(x, p->F(p->wt), y, v, KD, Cin_w, Cout_w, dgrad, math, p->st, p->F(p->wg_ws),
-                     stats, 0, xmax, wmax));
+                     stats, 0, wmax));
     return SPFF_OK;
   }
   if (!p->st2) {
@@ -754,10 +769,11 @@ int f16_in_max(spff_plan* p, const Blk& b, const Src2& in, const Vol& v) {
   const int bi = (int)(&b - p->blk);
   if (!sl || (bi >= 1 && bi <= 3)) return SPFF_OK;
   if (bi >= 4)  // [up | skip]: the up part here, the skip encoder's max from its apply
-    HIPCK(absmax_src(src1(in.p0, in.ld0), v, in.split, false, sl, p->st,
+    PROFB(p, 7, 0.0, 4.0 * (double)nvox(v) * in.split,
+          absmax_src(src1(in.p0, in.ld0), v, in.split, false, sl, p->st,
                      f16_slot(p, p->blk[6 - bi], F16_OUT)));
   else
-    HIPCK(absmax_src(in, v, b.Cin, false, sl, p->st));
+    PROFB(p, 7, 0.0, 4.0 * (double)nvox(v) * b.Cin, absmax_src(in, v, b.Cin, false, sl, p->st));
   return SPFF_OK;
 }
 int f16_param_slots(spff_plan* p) {
@@ -767,9 +783,11 @@ int f16_param_slots(spff_plan* p) {
   for (int i = 0; i < 7; ++i) {
     const Blk& b = p->blk[i];
     const Vol& v = p->vol[b.lvl];
-    HIPCK(absmax_f32(p->P(b.c1.w), (int64_t)b.C * b.Cin * T, f16_slot(p, b, F16_W1), p->st));
-    HIPCK(absmax_f32(p->P(b.c2.w), (int64_t)b.C * b.C * T, f16_slot(p, b, F16_W2), p->st));
-    HIPCK(act_bound(p->P(b.g1), p->P(b.b1), b.C, (double)v.D * v.H * v.W,
+    PROFB(p, 7, 0.0, 4.0 * b.C * b.Cin * T,
+          absmax_f32(p->P(b.c1.w), (int64_t)b.C * b.Cin * T, f16_slot(p, b, F16_W1), p->st));
+    PROFB(p, 7, 0.0, 4.0 * b.C * b.C * T,
+          absmax_f32(p->P(b.c2.w), (int64_t)b.C * b.C * T, f16_slot(p, b, F16_W2), p->st));
+    PROFB(p, 7, 0.0, 8.0 * b.C, act_bound(p->P(b.g1), p->P(b.b1), b.C, (double)v.D * v.H * v.W,
                     f16_slot(p, b, F16_A1), p->st));
   }
   return SPFF_OK;
@@ -789,8 +807,7 @@ int fwd_block(spff_plan* p, Blk& b, const Src2& in, int pool = -1) {
   // runs unsharded without split-K; otherwise the two slab_reduce passes
   const bool fuse1 = !p->co.on() && conv3d_fuses_stats(v, KD, b.Cin, C, math);
   CK(conv_halo(p, 0, 2.0 * V * b.Cin * C * T, cbytes(V, b.Cin, C, T), in, dst1(p->F(b.y1), C), v,
-               b.Cin, C, false, fuse1 ? p->F(p->cst) : nullptr, f16_in_slot(p, b),
-               f16_slot(p, b, F16_W1)));
+               b.Cin, C, false, fuse1 ? p->F(p->cst) : nullptr, f16_slot(p, b, F16_W1)));
   if (fuse1)
     HIPCK(conv3d_in_stats_fin(p->F(p->cst), v, KD, b.Cin, C, math, p->P(b.g1), p->P(b.b1),
                               p->F(b.mean1), p->F(b.rstd1), p->F(b.al1), p->F(b.de1), p->st));
@@ -805,8 +822,7 @@ int fwd_block(spff_plan* p, Blk& b, const Src2& in, int pool = -1) {
   const Src2 in2 = act_src(p, b);
   const bool fuse2 = !p->co.on() && conv3d_fuses_stats(v, KD, C, C, math);
   CK(conv_halo(p, 0, 2.0 * V * C * C * T, cbytes(V, C, C, T), in2, dst1(p->F(b.y2), C), v, C, C,
-               false, fuse2 ? p->F(p->cst) : nullptr, f16_slot(p, b, F16_A1),
-               f16_slot(p, b, F16_W2)));
+               false, fuse2 ? p->F(p->cst) : nullptr, f16_slot(p, b, F16_W2)));
   if (fuse2)
     HIPCK(conv3d_in_stats_fin(p->F(p->cst), v, KD, C, C, math, p->P(b.g2), p->P(b.b2), p->F(b.mean2),
                               p->F(b.rstd2), p->F(b.al2), p->F(b.de2), p->st));
@@ -1001,7 +1017,7 @@ int bwd_block(spff_plan* p, Blk& b, const float* dout, const Dst2* dx, const Src
   HIPCK(conv3d_pack(p->P(b.c2.w), p->F(p->wt), v, KD, C, C, true, math, p->st,
                     f16_slot(p, b, F16_W2)));
   CK(conv_halo(p, 1, 2.0 * V * C * C * T, cbytes(V, C, C, T), src1(dy2, C), dst1(da1, C), v, C, C,
-               true, nullptr, f16_slot(p, b, F16_DY2), f16_slot(p, b, F16_W2)));
+               true, nullptr, f16_slot(p, b, F16_W2)));
   {
     RedArgs a{};
     a.y = p->F(b.y1); a.g = da1; a.mean = p->F(b.mean1); a.rstd = p->F(b.rstd1);
@@ -1021,7 +1037,7 @@ int bwd_block(spff_plan* p, Blk& b, const float* dout, const Dst2* dx, const Src
     HIPCK(conv3d_pack(p->P(b.c1.w), p->F(p->wt), v, KD, b.Cin, C, true, math, p->st,
                       f16_slot(p, b, F16_W1)));
     CK(conv_halo(p, 1, 2.0 * V * b.Cin * C * T, cbytes(V, b.Cin, C, T), src1(da1, C), *dx, v,
-                 b.Cin, C, true, nullptr, f16_slot(p, b, F16_DA1), f16_slot(p, b, F16_W1)));
+                 b.Cin, C, true, nullptr, f16_slot(p, b, F16_W1)));
   }
   return SPFF_OK;
 }

@@ -115,7 +115,7 @@ hipError_t conv3d_pack(const float* w, void* wpack, Vol vol, int KD, int Cin_w, 
 hipError_t conv3d_run(const Src2& x, const void* wpack, const Dst2& y, Vol vol, int KD,
                       int Cin_w, int Cout_w, bool dgrad, int math, hipStream_t s,
                       float* ws = nullptr, float* stats = nullptr, int dpart = 0,
-                      const unsigned* xmax = nullptr, const unsigned* wmax = nullptr);
+                      const unsigned* wmax = nullptr);
 bool conv3d_splits_depth(Vol vol, int KD, int Cin_w, int Cout_w, bool dgrad, int math);
 bool conv3d_splits_height(Vol vol, int KD, int Cin_w, int Cout_w, bool dgrad, int math);
 bool conv3d_fuses_stats(Vol vol, int KD, int Cin, int Cout, int math);

@@ -305,9 +305,24 @@ class Plan:
                 raise SpffError("collective buffer outside the plan workspace")
             return ws[off:off + n * esz].view(dtype)
 
+        def _timed(kind, nbytes, stream, dev, fn):
+            """fn(); with coll_timing on, bracketed by HIP events on the stream the engine
+            handed the callback (where the collective's work is issued)"""
+            if not self.coll_timing:
+                return fn()
+            st = (torch.cuda.ExternalStream(stream, device=dev) if stream
+                  else torch.cuda.current_stream(dev))
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(st)
+            fn()
+            b.record(st)
+            self._coll_ev.append((kind, nbytes, a, b))
+
         def _allreduce(ctx, buf, n, dt, stream):
             try:
-                impl.allreduce(view(buf, n, torch.float64 if dt == 1 else torch.float32))
+                t = view(buf, n, torch.float64 if dt == 1 else torch.float32)
+                _timed("allreduce", t.numel() * t.element_size(), stream, t.device,
+                       lambda: impl.allreduce(t))
                 return 0
             except Exception as e:  # noqa: BLE001 -- reported through the engine status
                 self.coll_error = e
@@ -317,22 +332,43 @@ class Plan:
             try:
                 slab = view(interior - 4 * sl, (d_local + 2) * sl, torch.float32)
                 cur = torch.cuda.current_stream(slab.device)
+                # 2 slices sent (and 2 received) per rank at most
+                nb = 2 * 4 * int(sl)
                 if stream and stream != cur.cuda_stream:
                     # the engine's side stream (halo exchange overlapping the interior
                     # depth tiles of the next convolution): issue the exchange there
                     with torch.cuda.stream(torch.cuda.ExternalStream(stream, device=slab.device)):
-                        impl.halo(slab, int(sl), int(d_local))
+                        _timed("halo", nb, stream, slab.device,
+                               lambda: impl.halo(slab, int(sl), int(d_local)))
                 else:
-                    impl.halo(slab, int(sl), int(d_local))
+                    _timed("halo", nb, stream, slab.device,
+                           lambda: impl.halo(slab, int(sl), int(d_local)))
                 return 0
             except Exception as e:  # noqa: BLE001
                 self.coll_error = e
                 return 1
+        self.coll_timing = getattr(self, "coll_timing", False)
+        self._coll_ev = []
         self._coll_fns = (ALLREDUCE_FN(_allreduce), HALO_FN(_halo))  # keep alive
         self._coll = spff_coll(None, self._coll_fns[0], self._coll_fns[1])
         self.coll_impl = impl
         self.coll_error = None
         check(lib().spff_plan_set_coll(self._h, ctypes.byref(self._coll)), "spff_plan_set_coll")
+
+    def coll_collect(self) -> Dict[str, Dict[str, float]]:
+        """{kind: {calls, ms, bytes}} of the shard-group collective callbacks since the
+        last collect (coll_timing on: HIP events around each callback's work on its
+        stream; a halo on the side stream overlaps the interior conv tiles, so its time
+        is the exchange's duration, not the step time it costs).  Syncs on the events."""
+        out: Dict[str, Dict[str, float]] = {}
+        for kind, nb, a, b in getattr(self, "_coll_ev", []):
+            b.synchronize()
+            r = out.setdefault(kind, {"calls": 0, "ms": 0.0, "bytes": 0.0})
+            r["calls"] += 1
+            r["ms"] += a.elapsed_time(b)
+            r["bytes"] += nb
+        self._coll_ev = []
+        return out
 
     def workspace(self, device) -> torch.Tensor:
         if self._ws is None or self._ws.device != device:
@@ -421,8 +457,8 @@ class Plan:
         return dflat
 
     PROF_CLASSES = ("conv_fwd", "conv_dgrad", "conv_wgrad", "gemm", "slab_reduce", "act_apply",
-                    "in_bwd_apply")
-    MEM_CLASSES = ("slab_reduce", "act_apply", "in_bwd_apply")
+                    "in_bwd_apply", "f16_absmax")
+    MEM_CLASSES = ("slab_reduce", "act_apply", "in_bwd_apply", "f16_absmax")
 
     def prof_enable(self, on: bool = True):
         check(lib().spff_prof_enable(self._h, int(bool(on))), "spff_prof_enable")

@@ -53,9 +53,13 @@ def test_plan_rejects_bad_shapes():
     # H, W not multiples of 8 take the _cat trilinear fallback (models.py:687-691)
     E.Plan(1, 1, 5, 60, 66, 13)
     with pytest.raises(E.SpffError):
-        E.Plan(1, 1, 5, 64, 64, 40)   # K > 32
+        E.Plan(1, 1, 5, 64, 64, 129)  # K > SPFF_MAX_CLASSES
     with pytest.raises(E.SpffError):
-        E.Plan(1, 1, 5, 64, 64, 13, base=24)
+        E.Plan(1, 1, 5, 64, 64, 13, base=20)  # base not a multiple of 8
+    # the module contract beyond the registry settings (fixture fx5_k40_base24)
+    p = E.Plan(1, 5, 6, 24, 24, 40, base=24)
+    assert p.nfloats > 0 and p.ws_bytes > 0
+    E.Plan(1, 72, 4, 16, 16, 128, base=40)
 
 
 def test_workspace_size_headline_config_fits_hbm():

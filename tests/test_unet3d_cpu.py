@@ -138,8 +138,13 @@ def test_unet3d_plan_rejects_bad_shapes():
         E.UNet3DPlan(batch=1, in_ch=1, depth=5, height=24, width=32, num_classes=13, base=32,
                      target_depth=16)
     with pytest.raises(E.SpffError):
-        E.UNet3DPlan(batch=1, in_ch=1, depth=5, height=32, width=32, num_classes=40, base=32,
-                     target_depth=16)
+        E.UNet3DPlan(batch=1, in_ch=1, depth=5, height=32, width=32, num_classes=129, base=32,
+                     target_depth=16)   # K > SPFF_MAX_CLASSES
+    with pytest.raises(E.SpffError):
+        E.UNet3DPlan(batch=1, in_ch=1, depth=5, height=32, width=32, num_classes=13, base=12,
+                     target_depth=16)   # base not a multiple of 8
+    E.UNet3DPlan(batch=1, in_ch=1, depth=5, height=32, width=32, num_classes=40, base=24,
+                 target_depth=16)
 
 
 def test_unet3d_runs_only_on_device():
