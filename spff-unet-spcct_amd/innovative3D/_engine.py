@@ -372,7 +372,7 @@ class Plan:
 
     def workspace(self, device) -> torch.Tensor:
         if self._ws is None or self._ws.device != device:
-            self._ws = torch.empty(self.ws_bytes, dtype=torch.uint8, device=device)
+            self._ws = _alloc_workspace(self, device)
         return self._ws
 
     def forward(self, x: torch.Tensor, flat: torch.Tensor, out: Optional[torch.Tensor] = None):
@@ -508,6 +508,38 @@ PLAN_CACHE = int(os.environ.get("SPFF_PLAN_CACHE", "3"))
 PLAN_CACHE_FRACTION = 0.4
 
 
+def _all_plans():
+    for slots in list(_OWNER_PLANS.values()):
+        for lru in slots.values():
+            yield from list(lru.values())
+    yield from list(_ANON_PLANS.values())
+
+
+def release_workspace(plan) -> None:
+    """Free a cached plan's workspace (the plan stays; the next forward allocates a new
+    one).  A backward still pending on that workspace's activations then fails loudly
+    (its plan generation no longer matches) instead of reading freed memory."""
+    if getattr(plan, "_ws", None) is not None:
+        plan._ws = None
+        plan.generation = getattr(plan, "generation", 0) + 1
+
+
+def _alloc_workspace(plan, device) -> torch.Tensor:
+    """The plan's workspace.  If the device is out of memory, the workspaces of every
+    OTHER cached plan (validation shapes, a partial last batch: see _owned_plan) are
+    released, torch's cache is emptied and the allocation retried once; a second
+    failure raises.  SPFF_PLAN_CACHE=1 keeps one plan per module and tag (round 2's
+    behaviour: the previous shape's workspace is freed before a new shape's is built)."""
+    try:
+        return torch.empty(plan.ws_bytes, dtype=torch.uint8, device=device)
+    except torch.OutOfMemoryError:
+        for q in _all_plans():
+            if q is not plan:
+                release_workspace(q)
+        torch.cuda.empty_cache()
+        return torch.empty(plan.ws_bytes, dtype=torch.uint8, device=device)
+
+
 def _device_bytes() -> int:
     try:
         if torch.cuda.is_available():
@@ -622,7 +654,7 @@ class UNet3DPlan:
 
     def workspace(self, device) -> torch.Tensor:
         if self._ws is None or self._ws.device != device:
-            self._ws = torch.empty(self.ws_bytes, dtype=torch.uint8, device=device)
+            self._ws = _alloc_workspace(self, device)
         return self._ws
 
     def forward(self, x: torch.Tensor, flat: torch.Tensor, bufs: torch.Tensor, training: bool,
@@ -729,7 +761,7 @@ class SwinPlan:
 
     def workspace(self, device) -> torch.Tensor:
         if self._ws is None or self._ws.device != device:
-            self._ws = torch.empty(self.ws_bytes, dtype=torch.uint8, device=device)
+            self._ws = _alloc_workspace(self, device)
         return self._ws
 
     def forward(self, x: torch.Tensor, flat: torch.Tensor,

@@ -209,7 +209,8 @@ class _SPFFFunction(torch.autograd.Function):
     def backward(ctx, g):
         plan = ctx.plan
         if plan.generation != ctx.gen:
-            raise E.SpffError("SPFF engine: another forward ran on this model before the backward "
+            raise E.SpffError("SPFF engine: another forward ran on this model (or its cached workspace "
+                              "was released for another plan's) before the backward "
                               "of this one; the engine keeps one forward's activations per model")
         g_cl = g.permute(0, 2, 3, 4, 1)
         if not g_cl.is_contiguous():

@@ -104,3 +104,26 @@ def test_height_sharded_plan_shapes():
         E.Plan(1, 1, 5, 64, 512, 13, shard_world=2, shard_rank=0, shard_axis=2)  # bad axis
     with pytest.raises(E.SpffError):  # depth sharding keeps batch 1
         E.Plan(2, 1, 8, 64, 64, 13, shard_world=2, shard_rank=0, shard_axis=0)
+
+
+def test_workspace_oom_releases_other_cached_plans(monkeypatch):
+    """a workspace allocation that runs out of device memory releases the
+    workspaces of the OTHER cached plans (their pending backward then fails loudly: the
+    generation moves), empties torch's cache and retries once."""
+    import types
+    other = types.SimpleNamespace(ws_bytes=8, _ws=torch.empty(8, dtype=torch.uint8), generation=3)
+    me = types.SimpleNamespace(ws_bytes=16, _ws=None, generation=0)
+    monkeypatch.setitem(E._ANON_PLANS, ("other",), other)
+    calls = []
+    real_empty = torch.empty
+
+    def fake_empty(*a, **k):
+        calls.append(1)
+        if len(calls) == 1:
+            raise torch.OutOfMemoryError("simulated")
+        return real_empty(*a, **{kk: v for kk, v in k.items() if kk != "device"})
+    monkeypatch.setattr(torch, "empty", fake_empty)
+    monkeypatch.setattr(torch.cuda, "empty_cache", lambda: None)
+    ws = E._alloc_workspace(me, "cpu")
+    assert ws.numel() == 16 and len(calls) == 2
+    assert other._ws is None and other.generation == 4
