@@ -14,10 +14,15 @@ the standard that path needs (PS3.5 data-element encoding, PS3.10 file format):
   (frames, rows, cols[, samples]) with the frame axis dropped for a single frame, planar
   configuration 1 reordered to interleaved samples.
 
-Encapsulated (compressed) pixel data -- JPEG, JPEG 2000, RLE ... -- needs a codec and
-raises ``NotImplementedError``.  Parity with pydicom is unpinned (pydicom is absent and no
-DICOM files are available offline); the tests check hand-assembled byte streams and
-round trips through an independent writer.
+* RLE Lossless (1.2.840.10008.1.2.5, PS3.5 Annex G): the encapsulated fragments (one per
+  frame, after the Basic Offset Table item) decoded as pydicom's built-in RLE handler does:
+  per frame up to 15 PackBits segments, one per sample and byte (most significant first).
+
+Other encapsulated (compressed) transfer syntaxes -- JPEG, JPEG-LS, JPEG 2000 -- need an
+image codec (pydicom itself decodes them only with a plugin such as pylibjpeg or GDCM
+installed) and raise ``NotImplementedError``.  Parity with pydicom is unpinned (pydicom is
+absent and no DICOM files are available offline); the tests check hand-assembled byte
+streams and round trips through an independent writer / RLE encoder.
 """
 from __future__ import annotations
 
@@ -31,6 +36,7 @@ IMPLICIT_LE = "1.2.840.10008.1.2"
 EXPLICIT_LE = "1.2.840.10008.1.2.1"
 DEFLATED_LE = "1.2.840.10008.1.2.1.99"
 EXPLICIT_BE = "1.2.840.10008.1.2.2"
+RLE_LOSSLESS = "1.2.840.10008.1.2.5"
 
 # explicit VRs with a 2-byte reserved field and a 4-byte length (PS3.5 7.1.2)
 _LONG_VRS = {b"OB", b"OD", b"OF", b"OL", b"OV", b"OW", b"SQ", b"UC", b"UN", b"UR", b"UT", b"SV",
@@ -101,9 +107,24 @@ def _skip_undefined(buf: bytes, pos: int, explicit: bool) -> int:
             pos = _skip_undefined(buf, v, explicit) if n == _UNDEFINED else v + n
 
 
+def _fragments(buf: bytes, pos: int, explicit: bool) -> Tuple[list, int]:
+    """Encapsulated pixel data (PS3.5 A.4): the items after the element header at pos, up to
+    the Sequence Delimitation Item -> ([Basic Offset Table, fragment, ...], end offset)."""
+    items = []
+    while True:
+        tag, _vr, n, v = _header(buf, pos, explicit)
+        if tag == _SEQ_END:
+            return items, v
+        if tag != _ITEM or n == _UNDEFINED or v + n > len(buf):
+            raise DicomError(f"malformed encapsulated pixel data item at byte {pos}")
+        items.append(buf[v:v + n])
+        pos = v + n
+
+
 def _parse(buf: bytes, pos: int, explicit: bool, stop_group: int = None,
            out: Dict = None) -> Tuple[Dict, int]:
-    """Top-level elements from pos: keeps _WANTED values (raw bytes) and (0002,0010)."""
+    """Top-level elements from pos: keeps _WANTED values (raw bytes) and (0002,0010);
+    encapsulated pixel data as the list of its items."""
     out = {} if out is None else out
     while pos < len(buf):
         if stop_group is not None:
@@ -113,8 +134,8 @@ def _parse(buf: bytes, pos: int, explicit: bool, stop_group: int = None,
         tag, vr, n, v = _header(buf, pos, explicit)
         if n == _UNDEFINED:
             if tag == (0x7FE0, 0x0010):
-                raise NotImplementedError(
-                    "encapsulated (compressed) pixel data: decoding it needs a codec")
+                out[tag], pos = _fragments(buf, v, explicit)
+                continue
             pos = _skip_undefined(buf, v, explicit)
             continue
         if v + n > len(buf):
@@ -147,18 +168,22 @@ def read_dataset(path_or_bytes) -> Dict[str, object]:
     if ts == DEFLATED_LE:
         buf, pos = zlib.decompress(buf[pos:], -15), 0
         explicit = True
-    elif ts in (IMPLICIT_LE, EXPLICIT_LE):
-        explicit = ts == EXPLICIT_LE
+    elif ts in (IMPLICIT_LE, EXPLICIT_LE, RLE_LOSSLESS):
+        explicit = ts != IMPLICIT_LE
     elif ts == EXPLICIT_BE:
         raise NotImplementedError("Explicit VR Big Endian (retired) is not supported")
     else:
         raise NotImplementedError(f"transfer syntax {ts}: compressed pixel data needs a codec")
     raw, _ = _parse(buf, pos, explicit)
     ds: Dict[str, object] = {"TransferSyntaxUID": ts}
-    for tag, (vr, val) in raw.items():
+    for tag, item in raw.items():
         key = _WANTED.get(tag)
         if key is None:
             continue
+        if key == "PixelData" and isinstance(item, list):
+            ds[key] = item  # encapsulated: [Basic Offset Table, fragment, ...]
+            continue
+        vr, val = item
         if key in _US:
             if len(val) < 2:
                 raise DicomError(f"{key}: empty value")
@@ -189,6 +214,14 @@ def pixel_array(path_or_bytes) -> np.ndarray:
     dt = np.dtype(("<i" if signed else "<u") + str(ba // 8))
     n = rows * cols * frames * spp
     data = ds["PixelData"]
+    if isinstance(data, list):  # encapsulated
+        if ds["TransferSyntaxUID"] != RLE_LOSSLESS:
+            raise NotImplementedError(f"encapsulated pixel data in transfer syntax "
+                                      f"{ds['TransferSyntaxUID']}: decoding it needs a codec")
+        data = _rle_frames(data[1:], frames, rows, cols, spp, ba // 8)
+        spp_planar = True
+    else:
+        spp_planar = int(ds.get("PlanarConfiguration", 0)) == 1
     if len(data) < n * dt.itemsize:
         raise DicomError(f"PixelData holds {len(data)} bytes, the image needs {n * dt.itemsize}")
     arr = np.frombuffer(data, dtype=dt, count=n).copy()
@@ -196,10 +229,58 @@ def pixel_array(path_or_bytes) -> np.ndarray:
         shift = ba - bs
         arr = ((arr << shift) >> shift).astype(dt)
     if spp > 1:
-        if int(ds.get("PlanarConfiguration", 0)) == 1:
+        if spp_planar:
             arr = arr.reshape(frames, spp, rows, cols).transpose(0, 2, 3, 1)
         else:
             arr = arr.reshape(frames, rows, cols, spp)
     else:
         arr = arr.reshape(frames, rows, cols)
     return np.ascontiguousarray(arr[0] if frames == 1 else arr)
+
+
+def _unpackbits(seg: bytes, n: int) -> bytes:
+    """One RLE segment (PS3.5 G.3.1, PackBits): header byte h < 128 copies the next h + 1
+    bytes, 129 .. 255 (-127 .. -1) repeats the next byte 257 - h times, 128 is a no-op;
+    the first n bytes of the output (a segment may carry one padding byte)."""
+    out = bytearray()
+    i, L = 0, len(seg)
+    while i < L and len(out) < n:
+        h = seg[i]
+        i += 1
+        if h < 128:
+            out += seg[i:i + h + 1]
+            i += h + 1
+        elif h > 128:
+            if i >= L:
+                break
+            out += bytes((seg[i],)) * (257 - h)
+            i += 1
+    if len(out) < n:
+        raise DicomError(f"RLE segment decodes to {len(out)} bytes, the frame needs {n}")
+    return bytes(out[:n])
+
+
+def _rle_frames(frags: list, frames: int, rows: int, cols: int, spp: int, nbytes: int) -> bytes:
+    """RLE Lossless frames (PS3.5 Annex G) -> little-endian native pixel bytes, samples
+    planar (sample-major within each frame): segment s * nbytes + k holds byte k (most
+    significant first) of sample s of every pixel."""
+    if len(frags) < frames:
+        raise DicomError(f"{len(frags)} RLE fragments for {frames} frames")
+    npix = rows * cols
+    out = bytearray()
+    for f in range(frames):
+        fr = frags[f]
+        if len(fr) < 64:
+            raise DicomError("RLE frame shorter than its 64-byte header")
+        nseg = struct.unpack_from("<I", fr, 0)[0]
+        offs = list(struct.unpack_from("<15I", fr, 4))[:nseg]
+        if nseg != spp * nbytes:
+            raise DicomError(f"RLE frame has {nseg} segments, expected {spp * nbytes}")
+        ends = offs[1:] + [len(fr)]
+        planes = np.empty((spp, npix, nbytes), dtype=np.uint8)
+        for sidx in range(nseg):
+            seg = _unpackbits(fr[offs[sidx]:ends[sidx]], npix)
+            s_, k = divmod(sidx, nbytes)
+            planes[s_, :, nbytes - 1 - k] = np.frombuffer(seg, dtype=np.uint8)
+        out += planes.tobytes()
+    return bytes(out)

@@ -157,11 +157,110 @@ def test_compressed_and_broken_inputs_fail_loudly():
     jpeg = write_dicom(np.zeros((2, 4, 4), np.uint8), "1.2.840.10008.1.2.4.50")
     with pytest.raises(NotImplementedError):
         D.pixel_array(jpeg)
+    # encapsulated pixel data in a JPEG transfer syntax: well-formed items, no codec
+    jpeg_encap = write_rle_dicom(np.zeros((1, 4, 4), np.uint8), ts="1.2.840.10008.1.2.4.70")
+    with pytest.raises(NotImplementedError):
+        D.pixel_array(jpeg_encap)
     encap = bytearray(write_dicom(np.zeros((1, 4, 4), np.uint8), with_sq=False))
     i = encap.index(struct.pack("<HH", 0x7FE0, 0x10))
-    encap[i + 8:i + 12] = struct.pack("<I", 0xFFFFFFFF)  # undefined length = encapsulated
-    with pytest.raises(NotImplementedError):
+    encap[i + 8:i + 12] = struct.pack("<I", 0xFFFFFFFF)  # undefined length, no items
+    with pytest.raises(D.DicomError):
         D.pixel_array(bytes(encap))
     good = write_dicom(np.zeros((2, 4, 4), np.uint16))
     with pytest.raises(D.DicomError):
         D.pixel_array(good[:-9])
+
+
+# ---- RLE Lossless (PS3.5 Annex G), encoded here independently of the reader ----
+def _packbits(data: bytes) -> bytes:
+    """PackBits as PS3.5 G.3.1 describes it: replicate runs of 3 .. 128 bytes as
+    (257 - n, byte), literal runs of 1 .. 128 bytes as (n - 1, bytes...)"""
+    out, i, n = bytearray(), 0, len(data)
+    while i < n:
+        j = i
+        while j + 1 < n and data[j + 1] == data[i] and j + 1 - i < 127:
+            j += 1
+        run = j - i + 1
+        if run >= 3:
+            out += bytes((257 - run, data[i]))
+            i = j + 1
+            continue
+        k = i
+        while k < n and k - i < 128:
+            if k + 2 < n and data[k] == data[k + 1] == data[k + 2]:
+                break
+            k += 1
+        out += bytes((k - i - 1,)) + data[i:k]
+        i = k
+    if len(out) % 2:
+        out += bytes((128,))  # a no-op pad byte keeps the segment even
+    return bytes(out)
+
+
+def _rle_frame(frame: np.ndarray) -> bytes:
+    """[R, C] or [R, C, S] -> one RLE frame: header + segments per sample, MSB first"""
+    f = frame if frame.ndim == 3 else frame[..., None]
+    nb = f.dtype.itemsize
+    segs = []
+    u = f.astype(f.dtype.newbyteorder("<")).view(np.uint8).reshape(f.shape[0] * f.shape[1],
+                                                                     f.shape[2], nb)
+    for smp in range(f.shape[2]):
+        for k in range(nb):
+            segs.append(_packbits(np.ascontiguousarray(u[:, smp, nb - 1 - k]).tobytes()))
+    offs, o = [], 64
+    for sg in segs:
+        offs.append(o)
+        o += len(sg)
+    head = struct.pack("<I", len(segs)) + struct.pack("<15I", *(offs + [0] * (15 - len(offs))))
+    return head + b"".join(segs)
+
+
+def write_rle_dicom(frames, ts=D.RLE_LOSSLESS, signed=None):
+    a = np.asarray(frames)
+    spp = a.shape[3] if a.ndim == 4 else 1
+    F, R, C = a.shape[:3]
+    ba = a.dtype.itemsize * 8
+    signed = a.dtype.kind == "i" if signed is None else signed
+    body = _sq_undefined(True)
+    body += _el(0x0028, 0x0002, "US", _us(spp))
+    body += _el(0x0028, 0x0004, "CS", "MONOCHROME2" if spp == 1 else "RGB")
+    if spp > 1:
+        body += _el(0x0028, 0x0006, "US", _us(1))  # RLE images are by plane (PS3.5 G.2)
+    body += _el(0x0028, 0x0008, "IS", str(F))
+    body += _el(0x0028, 0x0010, "US", _us(R))
+    body += _el(0x0028, 0x0011, "US", _us(C))
+    body += _el(0x0028, 0x0100, "US", _us(ba))
+    body += _el(0x0028, 0x0101, "US", _us(ba))
+    body += _el(0x0028, 0x0103, "US", _us(1 if signed else 0))
+    items = struct.pack("<HHI", 0xFFFE, 0xE000, 0)  # empty Basic Offset Table
+    for f in range(F):
+        fr = _rle_frame(a[f])
+        items += struct.pack("<HHI", 0xFFFE, 0xE000, len(fr)) + fr
+    body += struct.pack("<HH2sHI", 0x7FE0, 0x10, b"OB", 0, 0xFFFFFFFF) + items
+    body += struct.pack("<HHI", 0xFFFE, 0xE0DD, 0)
+    meta = _el(0x0002, 0x0010, "UI", ts)
+    meta = _el(0x0002, 0x0000, "UL", struct.pack("<I", len(meta))) + meta
+    return b"\x00" * 128 + b"DICM" + meta + body
+
+
+@pytest.mark.parametrize("dtype", [np.uint8, np.int8, np.uint16, np.int16, np.int32])
+def test_rle_lossless_round_trip(dtype):
+    rng = np.random.default_rng(3)
+    info = np.iinfo(dtype)
+    a = rng.integers(info.min, info.max, size=(3, 9, 14), dtype=dtype, endpoint=True)
+    a[:, 2:6, 3:11] = a[0, 0, 0]  # long replicate runs beside literal ones
+    got = D.pixel_array(write_rle_dicom(a))
+    assert got.dtype == np.dtype(dtype) and got.shape == a.shape
+    np.testing.assert_array_equal(got, a)
+    one = D.pixel_array(write_rle_dicom(a[:1]))
+    np.testing.assert_array_equal(one, a[0])  # one frame: (rows, cols)
+
+
+def test_rle_lossless_rgb_and_packbits_edge_cases():
+    a = np.zeros((2, 5, 40, 3), np.uint8)
+    a[0, :, :, 1] = 7                      # a 200-byte run: split into runs of <= 128
+    a[1] = np.arange(600, dtype=np.uint8).reshape(5, 40, 3)  # literal runs > 128
+    got = D.pixel_array(write_rle_dicom(a))
+    assert got.shape == a.shape
+    np.testing.assert_array_equal(got, a)
+    assert D._unpackbits(bytes((254, 9, 128, 1, 5, 6)), 5) == bytes((9, 9, 9, 5, 6))
