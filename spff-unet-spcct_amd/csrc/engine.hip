@@ -743,16 +743,17 @@ Src2 act_src(const spff_plan* p, const Blk& b) {
   return s;
 }
 
-// SPFF_MATH_F16X3 on an unsharded plan: every conv operand's max |element| (float bits, the
-// fp16 planes' scale) is precomputed once per step and shared by the convs that read the
-// tensor, instead of one absmax pass per launch: per block, slot F16_W1 / F16_W2 max |w| and
-// F16_A1 a parameter bound on a1 = lrelu(IN(y1)) (act_bound), all in one batch at the
-// forward start; F16_OUT from the block-output apply (act_apply[_pool]) as it writes out;
-// the block input: an encoder's is the previous block's pooled output, bounded by its
-// F16_OUT; a decoder's [up | skip] takes one pass over the up part (F16_IN) max-ed with the
-// skip encoder's F16_OUT; the first block's a pass over the network input; F16_DY2 /
-// F16_DA1 from in_bwd_apply as it writes them.  Sharded plans compute them per launch
-// (their convs also read halo slices / boundary rows that arrive later).
+// SPFF_MATH_F16X3 on an unsharded plan: the per-tensor operand maxima (float bits, the fp16
+// planes' scale) of the weights and of the weight gradients' operands (the fwd/dgrad
+// kernels scale their input per tile themselves), precomputed once per step and shared by
+// the launches that read the tensor: per block, slot F16_W1 / F16_W2 max |w| and F16_A1 a
+// parameter bound on a1 = lrelu(IN(y1)) (act_bound), all in one batch at the forward start;
+// F16_OUT from the block-output apply (act_apply[_pool]) as it writes out; the block input:
+// an encoder's is the previous block's pooled output, bounded by its F16_OUT; a decoder's
+// [up | skip] (F16_IN) from the up-conv GEMM as it stores the up part, max-ed with the skip
+// encoder's F16_OUT; the first block's a pass over the network input; F16_DY2 / F16_DA1
+// from in_bwd_apply as it writes them.  Sharded plans compute the weight gradients' per
+// launch (their operands also span halo slices / boundary rows that arrive later).
 enum { F16_IN = 0, F16_A1, F16_DY2, F16_DA1, F16_W1, F16_W2, F16_OUT };
 unsigned* f16_slot(const spff_plan* p, const Blk& b, int k) {
   if (p->cfg.math != SPFF_MATH_F16X3 || p->co.on() || p->hsh) return nullptr;
@@ -767,13 +768,10 @@ const unsigned* f16_in_slot(const spff_plan* p, const Blk& b) {
 int f16_in_max(spff_plan* p, const Blk& b, const Src2& in, const Vol& v) {
   unsigned* sl = f16_slot(p, b, F16_IN);
   const int bi = (int)(&b - p->blk);
-  if (!sl || (bi >= 1 && bi <= 3)) return SPFF_OK;
-  if (bi >= 4)  // [up | skip]: the up part here, the skip encoder's max from its apply
-    PROFB(p, 7, 0.0, 4.0 * (double)nvox(v) * in.split,
-          absmax_src(src1(in.p0, in.ld0), v, in.split, false, sl, p->st,
-                     f16_slot(p, p->blk[6 - bi], F16_OUT)));
-  else
-    PROFB(p, 7, 0.0, 4.0 * (double)nvox(v) * b.Cin, absmax_src(in, v, b.Cin, false, sl, p->st));
+  // encoders 2-4: the previous block's output max; decoders: the up-conv GEMM filled it as
+  // it stored [up | ...] (max-ed with the skip encoder's output max, upconv_out)
+  if (!sl || bi >= 1) return SPFF_OK;
+  PROFB(p, 7, 0.0, 4.0 * (double)nvox(v) * b.Cin, absmax_src(in, v, b.Cin, false, sl, p->st));
   return SPFF_OK;
 }
 int f16_param_slots(spff_plan* p) {
@@ -872,12 +870,15 @@ Src2 src2(const float* a, const float* b, int C) { return Src2{a, b, C, C, C}; }
 
 // up-conv of block src's output into U.out at the skip's resolution (through U.raw and
 // the _cat trilinear resize when the pooled extents were odd)
-int upconv_out(spff_plan* p, const UpL& U, const Blk& src) {
+// (amax / also: the decoder block input's f16x3 slot, filled by the GEMM as it stores the
+// up part and max-ed with the skip encoder's output max; null on the lean recompute)
+int upconv_out(spff_plan* p, const UpL& U, const Blk& src, unsigned* amax = nullptr,
+               const unsigned* also = nullptr) {
   const Vol& low = p->vol[U.lvl_low];
   const ActRows act = act_rows(p, src);
   PROF(p, 3, 2.0 * nvox(low) * U.Cin * 4.0 * U.Cout,
        upconv_fwd(p->F(src.out), p->F(U.pk), p->P(U.b), p->F(U.rs ? U.raw : U.out), low, U.Cin,
-                  U.Cout, p->st, 4, p->cfg.math, src.fout ? &act : nullptr));
+                  U.Cout, p->st, 4, p->cfg.math, src.fout ? &act : nullptr, amax, also));
   if (U.rs) {
     const Vol& vh = p->vol[U.lvl_low - 1];
     Vol vr = low;
@@ -1081,9 +1082,9 @@ int forward(spff_plan* p, const float* x, float* logits) {
     float* pk = p->F(U.pk);
     HIPCK(upconv_pack(p->P(U.w), pk, pk + upconv_pack_dgrad_offset(U.Cin, U.Cout), U.Cin, U.Cout,
                       p->st));
-    CK(upconv_out(p, U, *prev));
     Blk& d = B[4 + u];
     const Blk& skip = B[2 - u];
+    CK(upconv_out(p, U, *prev, f16_slot(p, d, F16_IN), f16_slot(p, skip, F16_OUT)));
     CK(fwd_block(p, d, src2(p->F(U.out), p->F(skip.out), U.Cout)));
     prev = &d;
   }

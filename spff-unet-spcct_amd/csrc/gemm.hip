@@ -10,6 +10,8 @@
 #include "spff_internal.h"
 #include "bf16split.h"
 
+#include <type_traits>
+
 namespace spff {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -167,6 +169,11 @@ struct StoreRows {  // C[m][n] -> p[m*ld + n] (+bias[n]), n < nmax
 struct StoreUp {  // C[m][n], n = ij*Cout + co -> y[high(m,ij)*Cout + co] + bias[co]
   float* p; int Cout; const float* bias; int D, Hl, Wl; int64_t M; int nsub;
   int csh = -1, wsh = -1, hsh = -1;  // pow2_shift of Cout, Wl, Hl (set by the launchers)
+  // SPFF_MATH_F16X3: max |y| (float bits) of everything stored, into *amax (with *also
+  // max-ed in) -- the decoder block input's operand scale, instead of a re-reading pass
+  unsigned* amax = nullptr;
+  const unsigned* also = nullptr;
+  static constexpr bool kAmax = true;
   __device__ int64_t prep(int64_t m) const {
     return m < M ? up_high_base((uint32_t)m, D, Hl, Wl, nsub, wsh, hsh) * Cout : -1;
   }
@@ -393,6 +400,12 @@ typedef short i16x8g __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) i16x4g lds_i16x4g;
 __device__ __forceinline__ void gsplit4(float4 v, uint2 (&o)[3]) { split4_pk<3>(v, o); }
 // 32-B column-unit swizzle of B row k (BN / 16 units per row, 128 / BN rows per 256 B)
+// store functors that track the max |element| they store (StoreUp::kAmax)
+template <class T, class = void>
+struct cs_amax : std::false_type {};
+template <class T>
+struct cs_amax<T, std::void_t<decltype(T::kAmax)>> : std::integral_constant<bool, T::kAmax> {};
+
 template <int BN>
 __device__ __forceinline__ int gx_bsw(int k) {
   constexpr int L = BN == 128 ? 0 : BN == 64 ? 1 : 2;
@@ -472,6 +485,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x(AL A, const float* __restrict
   const int kr0 = 8 * g + q, kr1 = kr0 + 4;
   fetch(0);
   bool first = true;
+  float amx = 0.f;  // (cs_amax: the largest |value| this thread stored)
   for (;;) {
   const int64_t m0 = tl * G_BM;
   const int64_t tn = tl + gridDim.x;
@@ -542,9 +556,13 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x(AL A, const float* __restrict
       const float4 bq = C.bias4(n);
 #pragma unroll
       for (int rb = 0; rb < 2; ++rb)
-        if (rh[rb] >= 0 && c0 >= 0)
-          C.put4(rh[rb] + c0, make_float4(sg * acc[rb][cb][0] + bq.x, sg * acc[rb][cb][1] + bq.y,
-                                          sg * acc[rb][cb][2] + bq.z, sg * acc[rb][cb][3] + bq.w));
+        if (rh[rb] >= 0 && c0 >= 0) {
+          const float4 v = make_float4(sg * acc[rb][cb][0] + bq.x, sg * acc[rb][cb][1] + bq.y,
+                                       sg * acc[rb][cb][2] + bq.z, sg * acc[rb][cb][3] + bq.w);
+          C.put4(rh[rb] + c0, v);
+          if constexpr (cs_amax<CS>::value)
+            amx = fmaxf(amx, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+        }
     }
   } else {
     // lane: rows 16 rb + 4 g + (0..3), column n0 + 16 cb + l16
@@ -563,7 +581,11 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x(AL A, const float* __restrict
         if (rh < 0) continue;
 #pragma unroll
         for (int cb = 0; cb < CB; ++cb)
-          if (cc[cb] >= 0) C.put(rh + cc[cb], sg * acc[rb][cb][r] + bv[cb]);
+          if (cc[cb] >= 0) {
+            const float v = sg * acc[rb][cb][r] + bv[cb];
+            C.put(rh + cc[cb], v);
+            if constexpr (cs_amax<CS>::value) amx = fmaxf(amx, fabsf(v));
+          }
       }
   }
 #pragma unroll
@@ -572,6 +594,12 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x(AL A, const float* __restrict
     for (int cb = 0; cb < CB; ++cb) acc[rb][cb] = f32x4g{0.f, 0.f, 0.f, 0.f};
   if (tn >= ntl) break;
   tl = tn;
+  }
+  if constexpr (cs_amax<CS>::value) {
+    if (C.amax) {  // (uniform: every thread of the workgroup reaches this)
+      if (blockIdx.x == 0 && blockIdx.y == 0 && C.also) amx = fmaxf(amx, __uint_as_float(*C.also));
+      block_amax(amx, C.amax);
+    }
   }
 }
 
@@ -1154,11 +1182,13 @@ hipError_t upconv_pack(const float* w, float* wf, float* wd, int Cin, int Cout, 
 }
 
 hipError_t upconv_fwd(const float* x, const float* wf, const float* bias, float* y, Vol low,
-                      int Cin, int Cout, hipStream_t s, int ns, int math, const ActRows* act) {
+                      int Cin, int Cout, hipStream_t s, int ns, int math, const ActRows* act,
+                      unsigned* amax, const unsigned* also) {
   const int64_t M = nvox(low);
   if (act && !act_ok(act, Cin)) return hipErrorInvalidValue;
+  if (amax && !gemm_split(math)) return hipErrorInvalidValue;  // (the split GEMM tracks it)
   StoreUp C{y, Cout, bias, low.D, low.H, low.W, M, ns, pow2_shift(Cout), pow2_shift(low.W),
-            pow2_shift(low.H)};
+            pow2_shift(low.H), amax, also};
   if (act)
     return launch_gemm(act_loader(*act, Cin, M), wf, C, M, up_f_kpad(Cin), up_f_npad(Cout, ns),
                        s, gemm_split(math));

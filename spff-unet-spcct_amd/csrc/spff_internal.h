@@ -174,9 +174,11 @@ hipError_t upconv_pack(const float* w, float* wf, float* wd, int Cin, int Cout, 
                        int ns = 4);
 // (math = SPFF_MATH_BF16X6: the split-bf16 MFMA GEMM; otherwise the fp32 MFMA one)
 // (act: x = the rows ActRows describes, applied as they load; the x argument is ignored)
+// (amax: also the largest |y| into *amax, max-ed with *also -- an f16x3 operand scale)
 hipError_t upconv_fwd(const float* x, const float* wf, const float* bias, float* y,
                       Vol low, int Cin, int Cout, hipStream_t s, int ns = 4,
-                      int math = SPFF_MATH_F32, const ActRows* act = nullptr);
+                      int math = SPFF_MATH_F32, const ActRows* act = nullptr,
+                      unsigned* amax = nullptr, const unsigned* also = nullptr);
 hipError_t upconv_dgrad(const float* dy, int lddy, const float* wd, float* dx, Vol low,
                         int Cin, int Cout, hipStream_t s, int ns = 4, int math = SPFF_MATH_F32);
 size_t upconv_wgrad_ws_bytes(Vol low, int Cin, int Cout, int ns = 4);
