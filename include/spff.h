@@ -81,7 +81,11 @@ typedef struct spff_cfg {
    * of height shard_world * height; height and width multiples of 8 (the three (1,2,2)
    * pools stay rank-local), any batch.  Same collectives table. */
   int shard_axis;
-  int reserved[3];                          /* zero */
+  /* the novel block's EnergyFiLM3D(hidden, pe_dims) and FourierGate3D(learn_phase)
+   * (models.py:1484-1489, 1521-1541), the same in every block; 0 = the reference's
+   * defaults (32, 16, off: what _DoubleConvSpectral_Novel builds).  hidden 1..64,
+   * pe_dims 2..32 ((hidden + pe_dims) * depth * 4 B of LDS <= 160 KiB) */
+  int efilm_hidden, efilm_pe_dims, fgate_learn_phase;
 } spff_cfg;
 
 #define SPFF_SHARD_DEPTH 0

@@ -97,19 +97,20 @@ def energy_film(P, pre, x, sh: Shard):
     return x * (1 + g[..., None, None]) + b[..., None, None]
 
 
-def fourier_gate(P, pre, x, sh: Shard):
+def fourier_gate(P, pre, x, sh: Shard, learn_phase: bool = False):
     if sh.axis == 3:   # s1 = mean over (c, h, w): partial sums over the local rows
         B, C, Fd, H, W = x.shape
         s_full = all_reduce(x.sum(dim=(1, 3, 4))) / (C * H * sh.world * W)
         Sf = torch.fft.rfft(s_full, dim=1)
         M = (P[pre + ".freq_mask"] * P[pre + ".mag_scale"]).reshape(1, -1)
-        w = torch.fft.irfft(Sf * M, n=Fd, dim=1)
+        w = torch.fft.irfft(Sf * (M + 1j * 0.01) if learn_phase else Sf * M, n=Fd, dim=1)
         return x * torch.sigmoid(w)[:, None, :, None, None]
     s = x.mean(dim=(1, 3, 4))                              # [B, D_loc]
     s_full = torch.cat(all_gather(s.contiguous()), dim=1)   # [B, D]
     Sf = torch.fft.rfft(s_full, dim=1)
     M = (P[pre + ".freq_mask"] * P[pre + ".mag_scale"]).reshape(1, -1)
-    w = torch.fft.irfft(Sf * M, n=sh.D, dim=1)[:, sh.off:sh.off + sh.D_loc]
+    Sf = Sf * (M + 1j * 0.01) if learn_phase else Sf * M
+    w = torch.fft.irfft(Sf, n=sh.D, dim=1)[:, sh.off:sh.off + sh.D_loc]
     return x * torch.sigmoid(w)[:, None, :, None, None]
 
 
@@ -138,7 +139,7 @@ def novel_block(P, pre, x, cfg, sh: Shard):
     if cfg.novel and cfg.efilm:
         x = energy_film(P, pre + ".efilm", x, sh)
     if cfg.novel and cfg.fgate:
-        x = fourier_gate(P, pre + ".fgate", x, sh)
+        x = fourier_gate(P, pre + ".fgate", x, sh, cfg.learn_phase)
     return x
 
 

@@ -114,6 +114,18 @@ int main() {
   plan_case("ablation no se/specse", cfg_of(1, 5, 8, 32, 32, 9, 8, 1, 0, 0, 0, 1, 1, 1, 0, 0));
   reject("H < 8", cfg_of(1, 1, 5, 4, 64, 13));
   plan_case("K 40 base 24 (fx5)", cfg_of(1, 5, 6, 24, 24, 40, 24));
+  {
+    spff_cfg g = cfg_of(1, 5, 8, 16, 16, 9, 8);
+    g.efilm_hidden = 24;
+    g.efilm_pe_dims = 11;
+    g.fgate_learn_phase = 1;
+    plan_case("gates hidden 24 pe_dims 11 learn_phase (fx6)", g);
+    g.efilm_hidden = 65;
+    reject("efilm hidden 65", g);
+    g.efilm_hidden = 24;
+    g.efilm_pe_dims = 1;
+    reject("efilm pe_dims 1", g);
+  }
   reject("K > SPFF_MAX_CLASSES", cfg_of(1, 1, 5, 64, 64, SPFF_MAX_CLASSES + 1));
   reject("base 20", cfg_of(1, 1, 5, 64, 64, 13, 20));
   reject("depth shard batch 2", cfg_of(2, 1, 8, 64, 64, 13, 32, 2, 0, SPFF_SHARD_DEPTH));

@@ -122,6 +122,7 @@ struct spff_plan {
   spff_cfg cfg;
   Vol vol[4];
   int f, KD, ldx, K;
+  int efh = 32, efp = 16, fphase = 0;  // EnergyFiLM3D(hidden, pe_dims), learn_phase
   bool lean = false;  // SPFF_MEM_LEAN layout: a1 / out / up-conv outputs live in the
                       // gradient scratch and are recomputed in the backward
   std::vector<PEnt> params;
@@ -226,9 +227,9 @@ void reg_block(spff_plan* p, Blk& b) {
   b.g2 = p->reg(b.name + "." + bb + ".1.weight", {C});
   b.b2 = p->reg(b.name + "." + bb + ".1.bias", {C});
   if (b.efilm) {
-    b.fw0 = p->reg(b.name + ".efilm.mlp.0.weight", {32, 16, 1});
-    b.fb0 = p->reg(b.name + ".efilm.mlp.0.bias", {32});
-    b.fw2 = p->reg(b.name + ".efilm.mlp.2.weight", {2 * C, 32, 1});
+    b.fw0 = p->reg(b.name + ".efilm.mlp.0.weight", {p->efh, p->efp, 1});
+    b.fb0 = p->reg(b.name + ".efilm.mlp.0.bias", {p->efh});
+    b.fw2 = p->reg(b.name + ".efilm.mlp.2.weight", {2 * C, p->efh, 1});
     b.fb2 = p->reg(b.name + ".efilm.mlp.2.bias", {2 * C});
   }
   if (b.fgate) {
@@ -249,16 +250,18 @@ void conv_dims(ConvL& c, int Cin, int Cout) {
 
 size_t conv_pack_bytes(const ConvL& c, int KD) { return conv3d_pack_bytes(KD, c.Cin, c.Cout); }
 
-void host_pe(int D, std::vector<float>& pe) {
-  // models.py:1495-1503 in fp32: denom = exp(i * (-ln(1e4)/8)), pe = [sin(pos*denom); cos(...)]
-  pe.assign(16 * (size_t)D, 0.f);
-  const float cst = (float)(-std::log(10000.0) / 8.0);
-  for (int i = 0; i < 8; ++i) {
+void host_pe(int D, int P, std::vector<float>& pe) {
+  // models.py:1495-1503 in fp32: h = max(1, P / 2) frequencies, denom = exp(i * (-ln(1e4)/h)),
+  // pe = [sin(pos*denom); cos(pos*denom)] (2 h rows), and a zero row when that is < P (odd P)
+  const int h = std::max(1, P / 2);
+  pe.assign((size_t)P * D, 0.f);
+  const float cst = (float)(-std::log(10000.0) / (double)h);
+  for (int i = 0; i < h; ++i) {
     const float denom = std::exp((float)i * cst);
     for (int d = 0; d < D; ++d) {
       const float arg = (float)d * denom;
-      pe[(size_t)i * D + d] = std::sin(arg);
-      pe[(size_t)(8 + i) * D + d] = std::cos(arg);
+      if (i < P) pe[(size_t)i * D + d] = std::sin(arg);
+      if (h + i < P) pe[(size_t)(h + i) * D + d] = std::cos(arg);
     }
   }
 }
@@ -278,6 +281,13 @@ int build_plan(spff_plan* p) {
     return fail(SPFF_EINVAL, "math must be one of SPFF_MATH_*");
   if (c.memory_mode < SPFF_MEM_AUTO || c.memory_mode > SPFF_MEM_LEAN)
     return fail(SPFF_EINVAL, "memory_mode must be one of SPFF_MEM_*");
+  p->efh = c.efilm_hidden > 0 ? c.efilm_hidden : 32;
+  p->efp = c.efilm_pe_dims > 0 ? c.efilm_pe_dims : 16;
+  p->fphase = c.fgate_learn_phase != 0;
+  // (pe_dims 1 would give the reference a 2-row code for a 1-channel Conv1d: it raises)
+  if (c.efilm_hidden < 0 || c.efilm_pe_dims < 0 || p->efh > EFH_MAX || p->efp < 2 ||
+      p->efp > EFP_MAX)
+    return fail(SPFF_EINVAL, "efilm_hidden must be 1..64 and efilm_pe_dims 2..32 (0: 32, 16)");
   p->lean = c.memory_mode == SPFF_MEM_LEAN ||
             (c.memory_mode == SPFF_MEM_AUTO &&
              (int64_t)c.batch * c.depth * c.height * c.width >= (int64_t(1) << 26));
@@ -405,7 +415,7 @@ int build_plan(spff_plan* p) {
       b.h = p->alloc((size_t)B * se_hidden(b.C) * 4);
       b.t = p->alloc((size_t)b.C * D * 4);
       b.bt = p->alloc((size_t)b.C * D * 4);
-      b.hid = p->alloc((size_t)32 * D * 4);
+      b.hid = p->alloc((size_t)p->efh * D * 4);
       if (world > 1 && !hsh)
         b.spec = p->alloc((size_t)B * (p->co.D_glob / 2 + 1) * 2 * sizeof(double));
     }
@@ -494,7 +504,9 @@ int build_plan(spff_plan* p) {
     p->gdum = p->alloc(std::max<size_t>(gd, 1) * sizeof(float));
   }
 
-  host_pe(p->co.D_glob, p->pe_host);  // global depths; a slab reads columns d_off + d  // uploaded on the first forward (plan creation needs no GPU)
+  if (c.use_efilm && efilm_fwd_lds(p->efh, p->efp, c.depth) > 160 * 1024)
+    return fail(SPFF_EINVAL, "(efilm_hidden + efilm_pe_dims) x depth x 4 B exceeds 160 KiB of LDS");
+  host_pe(p->co.D_glob, p->efp, p->pe_host);  // global depths; a slab reads columns d_off + d  // uploaded on the first forward (plan creation needs no GPU)
   return SPFF_OK;
 }
 
@@ -511,6 +523,9 @@ GateParams gate_params(const spff_plan* p, const Blk& b) {
   g.pe = p->pe_dev;
   g.pe_pitch = p->co.D_glob;
   g.d_off = p->co.d_off;
+  g.efh = p->efh;
+  g.efp = p->efp;
+  g.fphase = p->fphase;
   g.fw0 = b.efilm ? p->P(b.fw0) : nullptr;
   g.fb0 = b.efilm ? p->P(b.fb0) : nullptr;
   g.fw2 = b.efilm ? p->P(b.fw2) : nullptr;
@@ -1059,6 +1074,8 @@ int forward(spff_plan* p, const float* x, float* logits) {
   const spff_cfg& c = p->cfg;
   {  // every block's EnergyFiLM coefficients in one launch (parameters only)
     EfilmJobs jobs;
+    jobs.H = p->efh;
+    jobs.P = p->efp;
     for (int i = 0; i < 7; ++i) {
       const Blk& b = p->blk[i];
       if (!b.efilm) continue;

@@ -27,6 +27,25 @@ __device__ __forceinline__ double ck_coef(int k, int D) {
   return (k == 0 || (D % 2 == 0 && k == D / 2)) ? 1.0 : 2.0;
 }
 
+// FourierGate3D(learn_phase=True) multiplies the spectrum by M_k + 0.01 i (models.py:1538-1539).
+// irfft keeps only the real part of the DC and Nyquist bins, so the extra term of w[d] is
+//   (1/D) sum_k c'_k Re(0.01 i S_k e^{i theta}) = -(0.01/D) sum_k c'_k (Sre sin + Sim cos),
+// theta = 2 pi k d / D, c'_k = c_k except 0 at DC / Nyquist: a real circulant H with
+// H[d, d'] = -(1/D) sum_k c'_k sin(2 pi k (d - d') / D), independent of M (so the mask and
+// mag_scale gradients are unchanged).  Its transpose on the backward (T = the dw spectrum,
+// Tre = sum dw cos, Tim = sum dw sin): -(0.01/D) sum_k c'_k (Tim cos - Tre sin).
+__device__ __forceinline__ double phase_c(int k, int D) {
+  return (k == 0 || (D % 2 == 0 && k == D / 2)) ? 0.0 : 2.0;
+}
+__device__ __forceinline__ double phase_term(int on, int k, int D, double Sre, double Sim,
+                                             double c, double sn) {
+  return on ? -0.01 * phase_c(k, D) * (Sre * sn + Sim * c) : 0.0;
+}
+__device__ __forceinline__ double phase_term_t(int on, int k, int D, double Tre, double Tim,
+                                               double c, double sn) {
+  return on ? -0.01 * phase_c(k, D) * (Tim * c - Tre * sn) : 0.0;
+}
+
 int se_hidden(int C) { return C / 16 > 4 ? C / 16 : 4; }
 
 constexpr int GT = 1024;  // threads per gate workgroup
@@ -75,25 +94,26 @@ __device__ void rowsum(int NI, int NJ, Fn f, double* part, double scale, double*
 
 // ------------------------------------------------------------- EFiLM fwd --
 // hid[j][d] = fw0[j] . pe[:,d] + fb0[j]; gb[o][d] = fw2[o] . relu(hid[:,d]) + fb2[o]
+// (H hidden units, P code rows: EnergyFiLM3D(hidden, pe_dims), 32 and 16 by default)
 // one workgroup = 32 of the 2C FiLM outputs of one block (the hidden layer recomputed per
-// workgroup: 32 x 16 x D MACs)
+// workgroup: H x P x D MACs)
 __device__ __forceinline__ void efilm_fwd_body(const float* __restrict__ pe,
                                                const float* __restrict__ fw0,
                                                const float* __restrict__ fb0,
                                                const float* __restrict__ fw2,
                                                const float* __restrict__ fb2, float* __restrict__ t,
                                                float* __restrict__ bt, float* __restrict__ hid,
-                                               int C, int D, int pitch, int wg) {
-  extern __shared__ float hs[];  // [32][D] hidden, then pe [16][D] and fw0 [32][16] staged
-  float* pes = hs + 32 * D;
-  float* w0s = pes + 16 * D;
-  for (int i = threadIdx.x; i < 16 * D; i += blockDim.x) pes[i] = pe[(i / D) * pitch + i % D];
-  for (int i = threadIdx.x; i < 32 * 16; i += blockDim.x) w0s[i] = fw0[i];
+                                               int C, int D, int pitch, int wg, int H, int P) {
+  extern __shared__ float hs[];  // [H][D] hidden, then pe [P][D] and fw0 [H][P] staged
+  float* pes = hs + H * D;
+  float* w0s = pes + P * D;
+  for (int i = threadIdx.x; i < P * D; i += blockDim.x) pes[i] = pe[(i / D) * pitch + i % D];
+  for (int i = threadIdx.x; i < H * P; i += blockDim.x) w0s[i] = fw0[i];
   __syncthreads();
-  for (int i = threadIdx.x; i < 32 * D; i += blockDim.x) {
+  for (int i = threadIdx.x; i < H * D; i += blockDim.x) {
     const int j = i / D, d = i % D;
     float s = 0.f;
-    for (int q = 0; q < 16; ++q) s += w0s[j * 16 + q] * pes[q * D + d];
+    for (int q = 0; q < P; ++q) s += w0s[j * P + q] * pes[q * D + d];
     s += fb0[j];
     hs[i] = s;
     if (wg == 0) hid[i] = s;
@@ -104,7 +124,7 @@ __device__ __forceinline__ void efilm_fwd_body(const float* __restrict__ pe,
     const int o = o0 + i / D, d = i % D;
     if (o >= 2 * C) continue;
     float s = 0.f;
-    for (int j = 0; j < 32; ++j) s += fw2[o * 32 + j] * fmaxf(hs[j * D + d], 0.f);
+    for (int j = 0; j < H; ++j) s += fw2[o * H + j] * fmaxf(hs[j * D + d], 0.f);
     s += fb2[o];
     if (o < C) t[o * D + d] = tanhf(s);
     else bt[(o - C) * D + d] = s;
@@ -114,21 +134,27 @@ __global__ void k_efilm_fwd(const float* __restrict__ pe, const float* __restric
                             const float* __restrict__ fb0, const float* __restrict__ fw2,
                             const float* __restrict__ fb2, float* __restrict__ t,
                             float* __restrict__ bt, float* __restrict__ hid, int C, int D,
-                            int pitch) {
-  efilm_fwd_body(pe, fw0, fb0, fw2, fb2, t, bt, hid, C, D, pitch, blockIdx.x);
+                            int pitch, int H, int P) {
+  efilm_fwd_body(pe, fw0, fb0, fw2, fb2, t, bt, hid, C, D, pitch, blockIdx.x, H, P);
 }
 // all blocks' coefficients in one launch: grid.y = job (block), grid.x = 32-output groups
 __global__ void k_efilm_fwd_all(const float* __restrict__ pe, EfilmJobs jobs, int D, int pitch) {
   const EfilmJob& J = jobs.j[blockIdx.y];
   if ((int)blockIdx.x * 32 >= 2 * J.C) return;  // (uniform: the whole workgroup)
-  efilm_fwd_body(pe, J.fw0, J.fb0, J.fw2, J.fb2, J.t, J.bt, J.hid, J.C, D, pitch, blockIdx.x);
+  efilm_fwd_body(pe, J.fw0, J.fb0, J.fw2, J.fb2, J.t, J.bt, J.hid, J.C, D, pitch, blockIdx.x,
+                 jobs.H, jobs.P);
+}
+
+size_t efilm_fwd_lds(int H, int P, int D) {
+  return ((size_t)(H + P) * D + (size_t)H * P) * sizeof(float);
 }
 
 hipError_t efilm_fwd_all(const float* pe, int pe_pitch, const EfilmJobs& jobs, int D,
                          hipStream_t s) {
   if (jobs.n <= 0) return hipSuccess;
-  if (jobs.n > 8) return hipErrorInvalidValue;
-  const size_t shm = (48 * (size_t)D + 512) * sizeof(float);
+  if (jobs.n > 8 || jobs.H < 1 || jobs.H > EFH_MAX || jobs.P < 1 || jobs.P > EFP_MAX)
+    return hipErrorInvalidValue;
+  const size_t shm = efilm_fwd_lds(jobs.H, jobs.P, D);
   if (shm > 64 * 1024) {
     if (shm > GATE_LDS_MAX) return hipErrorInvalidValue;
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_efilm_fwd_all),
@@ -143,7 +169,7 @@ hipError_t efilm_fwd_all(const float* pe, int pe_pitch, const EfilmJobs& jobs, i
 
 static hipError_t efilm_fwd(const GateParams& gp, const GateSaved& sv, int C, int D,
                             hipStream_t s) {
-  const size_t shm = (48 * (size_t)D + 512) * sizeof(float);
+  const size_t shm = efilm_fwd_lds(gp.efh, gp.efp, D);
   if (shm > 64 * 1024) {
     if (shm > GATE_LDS_MAX) return hipErrorInvalidValue;
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_efilm_fwd),
@@ -151,7 +177,8 @@ static hipError_t efilm_fwd(const GateParams& gp, const GateSaved& sv, int C, in
     if (e != hipSuccess) return e;
   }
   hipLaunchKernelGGL(k_efilm_fwd, dim3(cdiv(2 * C, 32)), dim3(256), shm, s, gp.pe + gp.d_off,
-                     gp.fw0, gp.fb0, gp.fw2, gp.fb2, sv.t, sv.bt, sv.hid, C, D, gp.pe_pitch);
+                     gp.fw0, gp.fb0, gp.fw2, gp.fb2, sv.t, sv.bt, sv.hid, C, D, gp.pe_pitch,
+                     gp.efh, gp.efp);
   return hipGetLastError();
 }
 
@@ -221,7 +248,8 @@ __global__ __launch_bounds__(GT) void k_gates_fwd(GateParams gp, const float* __
     rowsum(D, L, [&](int d, int k) {
       const int q = (k * d) % D;
       const double Mk = (double)(gp.mask[k] * gp.mag[0]);
-      return ck_coef(k, D) * Mk * (m.Sre[k] * m.twc[q] - m.Sim[k] * m.tws[q]);
+      return ck_coef(k, D) * Mk * (m.Sre[k] * m.twc[q] - m.Sim[k] * m.tws[q]) +
+             phase_term(gp.fphase, k, D, m.Sre[k], m.Sim[k], m.twc[q], m.tws[q]);
     }, m.part, 1.0 / D, m.tmp);
     for (int d = threadIdx.x; d < D; d += blockDim.x) m.g1[d] = sigm((float)m.tmp[d]);
   } else {
@@ -299,7 +327,7 @@ hipError_t gates_fwd(const GateParams& gp, const float* Sa, GateSaved& sv, Vol v
 
 // ------------------------------------------------------------- gates bwd --
 // scratch layout (floats): dt[B][C][D], dbt[B][C][D], sw2p[B][C][Hse], sb2p[B][C],
-// sw0p[B][Hse][C], sb0p[B][Hse], dMr[B][L], dgb[2C][D], dh[32][D]
+// sw0p[B][Hse][C], sb0p[B][Hse], dMr[B][L], dgb[2C][D], dh[EFiLM hidden][D]
 struct GScr {
   float *dt, *dbt, *sw2p, *sb2p, *sw0p, *sb0p, *dMr, *dgb, *dh;
 };
@@ -320,7 +348,7 @@ static GScr gscr(float* base, int B, int C, int D, int Hse) {
 size_t gates_scratch_bytes(Vol vol, int C) {
   const int B = vol.B, D = vol.D, Hse = se_hidden(C), L = D / 2 + 1;
   size_t n = 2 * (size_t)B * C * D + (size_t)B * C * Hse + (size_t)B * C + (size_t)B * Hse * C +
-             (size_t)B * Hse + (size_t)B * L + 2 * (size_t)C * D + 32 * (size_t)D;
+             (size_t)B * Hse + (size_t)B * L + 2 * (size_t)C * D + EFH_MAX * (size_t)D;
   return n * sizeof(float) + 256;
 }
 
@@ -463,7 +491,8 @@ __global__ __launch_bounds__(GT) void k_gates_bwd(GateParams gp, GateSaved sv,
     rowsum(D, L, [&](int d, int k) {
       const int q = (k * d) % D;
       const double Mk = (double)(gp.mask[k] * gp.mag[0]);
-      return ck_coef(k, D) * Mk * (m.twc[q] * m.Tre[k] + m.tws[q] * m.Tim[k]);
+      return ck_coef(k, D) * Mk * (m.twc[q] * m.Tre[k] + m.tws[q] * m.Tim[k]) +
+             phase_term_t(gp.fphase, k, D, m.Tre[k], m.Tim[k], m.twc[q], m.tws[q]);
     }, m.part, 1.0 / D, m.tmp);
     for (int d = threadIdx.x; d < D; d += blockDim.x) m.ds1[d] = (float)m.tmp[d];
   }
@@ -554,23 +583,24 @@ __global__ __launch_bounds__(256) void k_efilm_bwd2(GateParams gp, GateGrads gg,
                                                     const float* __restrict__ hid, int C, int D) {
   const int lane = threadIdx.x & 63;
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (i >= 2 * C * 33 + 32 * D) return;
+  const int H = gp.efh, H1 = H + 1;
+  if (i >= 2 * C * H1 + H * D) return;
   float s = 0.f;
-  if (i < 2 * C * 33) {
-    const int o = i / 33, j = i % 33;
-    if (j < 32) {
+  if (i < 2 * C * H1) {
+    const int o = i / H1, j = i % H1;
+    if (j < H) {
       for (int d = lane; d < D; d += 64) s += gs.dgb[o * D + d] * fmaxf(hid[j * D + d], 0.f);
       s = gate_wave_sum(s);
-      if (lane == 0) gg.fw2[o * 32 + j] = s;
+      if (lane == 0) gg.fw2[o * H + j] = s;
     } else {
       for (int d = lane; d < D; d += 64) s += gs.dgb[o * D + d];
       s = gate_wave_sum(s);
       if (lane == 0) gg.fb2[o] = s;
     }
   } else {
-    const int k = i - 2 * C * 33;
+    const int k = i - 2 * C * H1;
     const int j = k / D, d = k % D;
-    for (int o = lane; o < 2 * C; o += 64) s += gp.fw2[o * 32 + j] * gs.dgb[o * D + d];
+    for (int o = lane; o < 2 * C; o += 64) s += gp.fw2[o * H + j] * gs.dgb[o * D + d];
     s = gate_wave_sum(s);
     if (lane == 0) gs.dh[k] = hid[k] > 0.f ? s : 0.f;
   }
@@ -579,14 +609,15 @@ __global__ __launch_bounds__(256) void k_efilm_bwd3(GateParams gp, GateGrads gg,
                                                     int D) {
   const int lane = threadIdx.x & 63;
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (i >= 32 * 17) return;
-  const int j = i / 17, q = i % 17;
+  const int P = gp.efp, P1 = P + 1;
+  if (i >= gp.efh * P1) return;
+  const int j = i / P1, q = i % P1;
   float s = 0.f;
-  if (q < 16) {
+  if (q < P) {
     const float* pe = gp.pe + q * gp.pe_pitch + gp.d_off;
     for (int d = lane; d < D; d += 64) s += gs.dh[j * D + d] * pe[d];
     s = gate_wave_sum(s);
-    if (lane == 0) gg.fw0[j * 16 + q] = s;
+    if (lane == 0) gg.fw0[j * P + q] = s;
   } else {
     for (int d = lane; d < D; d += 64) s += gs.dh[j * D + d];
     s = gate_wave_sum(s);
@@ -608,10 +639,13 @@ static hipError_t gates_bwd_tail(const GateParams& gp, const GateSaved& sv, Gate
     hipLaunchKernelGGL(k_efilm_bwd1, dim3(std::min(cdiv(2 * C * D, 256), 1024)), dim3(256), 0, s,
                        g, sv.t, B, C, D);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_efilm_bwd2, dim3(cdiv(2 * C * 33 + 32 * D, 4)), dim3(256), 0, s, gp,
-                       gg, g, sv.hid, C, D);
+    if (gp.efh < 1 || gp.efh > EFH_MAX || gp.efp < 1 || gp.efp > EFP_MAX)
+      return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_efilm_bwd2, dim3(cdiv(2 * C * (gp.efh + 1) + gp.efh * D, 4)), dim3(256),
+                       0, s, gp, gg, g, sv.hid, C, D);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_efilm_bwd3, dim3(cdiv(32 * 17, 4)), dim3(256), 0, s, gp, gg, g, D);
+    hipLaunchKernelGGL(k_efilm_bwd3, dim3(cdiv(gp.efh * (gp.efp + 1), 4)), dim3(256), 0, s, gp, gg,
+                       g, D);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   return hipSuccess;
@@ -763,7 +797,8 @@ __global__ __launch_bounds__(GT) void k_gsh_fwd_b(GateParams gp, const float* __
     rowsum(D, L, [&](int d, int k) {
       const int q = (k * (d_off + d)) % Dg;
       const double Mk = (double)(gp.mask[k] * gp.mag[0]);
-      return ck_coef(k, Dg) * Mk * (m.Sre[k] * m.twc[q] - m.Sim[k] * m.tws[q]);
+      return ck_coef(k, Dg) * Mk * (m.Sre[k] * m.twc[q] - m.Sim[k] * m.tws[q]) +
+             phase_term(gp.fphase, k, Dg, m.Sre[k], m.Sim[k], m.twc[q], m.tws[q]);
     }, m.part, 1.0 / Dg, m.tmp);
     for (int d = threadIdx.x; d < D; d += blockDim.x) m.g1[d] = sigm((float)m.tmp[d]);
   } else {
@@ -1005,7 +1040,8 @@ __global__ __launch_bounds__(GT) void k_gsh_bwd_c(GateParams gp, GateSaved sv,
     rowsum(D, L, [&](int d, int k) {
       const int q = (k * (d_off + d)) % Dg;
       const double Mk = (double)(gp.mask[k] * gp.mag[0]);
-      return ck_coef(k, Dg) * Mk * (m.twc[q] * m.Tre[k] + m.tws[q] * m.Tim[k]);
+      return ck_coef(k, Dg) * Mk * (m.twc[q] * m.Tre[k] + m.tws[q] * m.Tim[k]) +
+             phase_term_t(gp.fphase, k, Dg, m.Tre[k], m.Tim[k], m.twc[q], m.tws[q]);
     }, m.part, 1.0 / Dg, m.tmp);
     for (int d = threadIdx.x; d < D; d += blockDim.x) m.ds1[d] = (float)m.tmp[d];
     __syncthreads();

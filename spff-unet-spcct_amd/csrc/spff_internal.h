@@ -341,9 +341,13 @@ struct Coll {
   }
 };
 
+// EnergyFiLM hidden width / positional-code rows the scratch layouts are sized for
+constexpr int EFH_MAX = 64, EFP_MAX = 32;
 struct GateParams {
-  const float* pe;   // sinusoidal code [16][pe_pitch] (models.py:1495-1503), column d_off + d
+  const float* pe;   // sinusoidal code [efp][pe_pitch] (models.py:1495-1503), column d_off + d
   int pe_pitch, d_off;
+  int efh = 32, efp = 16;  // EnergyFiLM3D hidden, pe_dims
+  int fphase = 0;          // FourierGate3D(learn_phase=True): M_k + 0.01 i (models.py:1538-1539)
   // EnergyFiLM (models.py:1479-1512)
   const float* fw0; const float* fb0; const float* fw2; const float* fb2;  // null if off
   // FourierGate (models.py:1515-1544)
@@ -354,7 +358,7 @@ struct GateParams {
   bool efilm_ready = false;  // t, bt, hid already computed (efilm_fwd_all at the forward start)
 };
 struct GateSaved {
-  float* t; float* bt; float* hid;    // EFiLM: t=tanh(gamma)[C][D], beta[C][D], hid_pre[32][D]
+  float* t; float* bt; float* hid;    // EFiLM: t=tanh(gamma)[C][D], beta[C][D], hid_pre[H][D]
   float* s1; float* g1; float* sg2;   // [B][D]
   float* p; float* h; float* e;       // SE: p[B][C], h[B][Hse] (pre-ReLU), e[B][C]
   float* P; float* Q;                 // [B][C][D] apply coefficients
@@ -372,7 +376,10 @@ struct EfilmJob {
 struct EfilmJobs {
   EfilmJob j[8];
   int n = 0;
+  int H = 32, P = 16;  // hidden, pe_dims (every block alike)
 };
+// LDS bytes of the EFiLM coefficient kernels (H hidden, P code rows, D depths)
+size_t efilm_fwd_lds(int H, int P, int D);
 hipError_t efilm_fwd_all(const float* pe, int pe_pitch, const EfilmJobs& jobs, int D,
                          hipStream_t s);
 // forward gate algebra from Sa[b,c,d] = sum_hw lrelu(IN(y2))

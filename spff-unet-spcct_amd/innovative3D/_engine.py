@@ -39,7 +39,9 @@ class spff_cfg(ctypes.Structure):
         ("base", ctypes.c_int), ("ksd", ctypes.c_int), ("use_efilm", ctypes.c_int),
         ("use_fgate", ctypes.c_int), ("use_se", ctypes.c_int), ("use_specse", ctypes.c_int),
         ("math", ctypes.c_int), ("shard_world", ctypes.c_int), ("shard_rank", ctypes.c_int),
-        ("memory_mode", ctypes.c_int), ("shard_axis", ctypes.c_int), ("reserved", ctypes.c_int * 3),
+        ("memory_mode", ctypes.c_int), ("shard_axis", ctypes.c_int),
+        ("efilm_hidden", ctypes.c_int), ("efilm_pe_dims", ctypes.c_int),
+        ("fgate_learn_phase", ctypes.c_int),
     ]
 
 
@@ -235,7 +237,8 @@ class Plan:
 
     def __init__(self, batch, in_ch, depth, height, width, num_classes, base=32, ksd=3,
                  efilm=True, fgate=True, se=True, specse=True, device=None, math=None,
-                 shard_world=1, shard_rank=0, memory=None, shard_axis=0):
+                 shard_world=1, shard_rank=0, memory=None, shard_axis=0, efilm_hidden=32,
+                 efilm_pe_dims=16, fgate_learn_phase=False):
         math = default_math() if math is None else math
         if math not in MATH_NAMES:
             raise SpffError(f"math={math!r}: expected one of {sorted(MATH_NAMES)}")
@@ -259,9 +262,13 @@ class Plan:
         cfg.num_classes, cfg.base, cfg.ksd = num_classes, base, ksd
         cfg.use_efilm, cfg.use_fgate, cfg.use_se, cfg.use_specse = (int(bool(efilm)), int(bool(fgate)),
                                                                     int(bool(se)), int(bool(specse)))
+        # EnergyFiLM3D(hidden, pe_dims) / FourierGate3D(learn_phase) of the blocks
+        cfg.efilm_hidden, cfg.efilm_pe_dims = int(efilm_hidden), int(efilm_pe_dims)
+        cfg.fgate_learn_phase = int(bool(fgate_learn_phase))
         self.cfg = cfg
         self.key = (batch, in_ch, depth, height, width, num_classes, base, ksd, bool(efilm),
-                    bool(fgate), bool(se), bool(specse), math, self.shard, memory)
+                    bool(fgate), bool(se), bool(specse), math, self.shard, memory,
+                    int(efilm_hidden), int(efilm_pe_dims), bool(fgate_learn_phase))
         L = lib()
         h = ctypes.c_void_p()
         check(L.spff_plan_create(ctypes.byref(cfg), ctypes.byref(h)), "spff_plan_create")
@@ -594,7 +601,8 @@ def get_plan(owner=None, tag: str = "", **kw) -> Plan:
            kw.get("base", 32), kw.get("ksd", 3), bool(kw.get("efilm", True)),
            bool(kw.get("fgate", True)), bool(kw.get("se", True)), bool(kw.get("specse", True)),
            kw.get("math") or default_math(), shard_key(kw.get("shard", (1, 0))),
-           kw.get("memory") or default_memory())
+           kw.get("memory") or default_memory(), int(kw.get("efilm_hidden", 32)),
+           int(kw.get("efilm_pe_dims", 16)), bool(kw.get("fgate_learn_phase", False)))
 
     def make():
         kk = dict(kw)

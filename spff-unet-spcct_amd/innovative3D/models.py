@@ -135,14 +135,19 @@ class _DoubleConvSpectral(nn.Module):
 
 
 class EnergyFiLM3D(nn.Module):
+    """models.py:1479-1512 (parameter container; the engine computes it).  hidden 1..64,
+    pe_dims 2..32 (include/spff.h spff_cfg.efilm_hidden / efilm_pe_dims), the same in every
+    block of a network."""
+
     def __init__(self, channels: int, hidden: int = 32, pe_dims: int = 16):
         super().__init__()
-        if hidden != 32 or pe_dims != 16:
+        if not (1 <= int(hidden) <= 64 and 2 <= int(pe_dims) <= 32):
             raise NotImplementedError(
-                f"EnergyFiLM3D(hidden={hidden}, pe_dims={pe_dims}): the engine supports hidden=32, "
-                "pe_dims=16 only -- the values _DoubleConvSpectral_Novel always uses "
-                "(reference models.py:1470, 1484); see INTEGRATION.md §2")
+                f"EnergyFiLM3D(hidden={hidden}, pe_dims={pe_dims}): the engine supports hidden "
+                "1..64 and pe_dims 2..32 (reference models.py:1484; pe_dims 1 makes the "
+                "reference's own Conv1d raise); see INTEGRATION.md §2")
         self.channels = int(channels)
+        self.hidden = int(hidden)
         self.pe_dims = int(pe_dims)
         self.mlp = nn.Sequential(nn.Conv1d(self.pe_dims, hidden, 1, bias=True), nn.ReLU(inplace=True),
                                  nn.Conv1d(hidden, 2 * self.channels, 1, bias=True))
@@ -150,16 +155,13 @@ class EnergyFiLM3D(nn.Module):
 
 class FourierGate3D(nn.Module):
     """Same lazy mask semantics as the reference (models.py:1527-1535):
-    ``_mask``/``freq_mask`` (one tensor, two names) appear at the first forward."""
+    ``_mask``/``freq_mask`` (one tensor, two names) appear at the first forward.
+    learn_phase=True multiplies the spectrum by (M + 0.01 i) (models.py:1538-1539), on the
+    engine as an extra real circulant term (gates.hip phase_term)."""
 
     def __init__(self, learn_phase: bool = False):
         super().__init__()
-        if learn_phase:
-            raise NotImplementedError(
-                "FourierGate3D(learn_phase=True): the engine supports learn_phase=False only -- "
-                "the value _DoubleConvSpectral_Novel always uses (reference models.py:1471, "
-                "1521); see INTEGRATION.md §2")
-        self.learn_phase = False
+        self.learn_phase = bool(learn_phase)
         self.mag_scale = nn.Parameter(torch.ones(1))
         self._mask = None
 
@@ -275,6 +277,20 @@ class UNet3D_SpectralCore(nn.Module):
             raise NotImplementedError("mixed block kinds; upgrade_spct_with_novel_blocks upgrades all")
         return next(iter(kinds))
 
+    def _gate_settings(self) -> dict:
+        """EnergyFiLM3D(hidden, pe_dims) / FourierGate3D(learn_phase) of the blocks (one
+        setting for the whole network: include/spff.h spff_cfg)"""
+        ef = {(b.efilm.hidden, b.efilm.pe_dims) for b in self._blocks()
+              if isinstance(getattr(b, "efilm", None), EnergyFiLM3D)}
+        ph = {b.fgate.learn_phase for b in self._blocks()
+              if isinstance(getattr(b, "fgate", None), FourierGate3D)}
+        if len(ef) > 1 or len(ph) > 1:
+            raise NotImplementedError("EnergyFiLM3D(hidden, pe_dims) / FourierGate3D(learn_phase) "
+                                      "must be the same in every block on the engine")
+        h, pdim = next(iter(ef)) if ef else (32, 16)
+        return {"efilm_hidden": h, "efilm_pe_dims": pdim,
+                "fgate_learn_phase": bool(next(iter(ph))) if ph else False}
+
     def _engine_plan(self, x: torch.Tensor, tag: str):
         B, C, D, H, W = x.shape
         if C != self.in_channels:
@@ -292,7 +308,7 @@ class UNet3D_SpectralCore(nn.Module):
                           efilm=efilm, fgate=fgate, se=self.use_se, specse=self.use_specse,
                           device=x.device, math=getattr(self, "math", None), shard=shard,
                           memory=getattr(self, "memory", None),
-                          owner=self, tag=tag)
+                          owner=self, tag=tag, **self._gate_settings())
         if shard[0] > 1:
             coll = getattr(self, "shard_coll", None)
             if coll is None:

@@ -37,8 +37,26 @@ def load(name):
 
 def cfg_of(meta):
     from oracle.spff_oracle import SpffCfg
-    kw = {k: meta[k] for k in ("efilm", "fgate", "se", "specse") if k in meta}
+    kw = {k: meta[k] for k in ("efilm", "fgate", "se", "specse", "efilm_hidden", "efilm_pe_dims",
+                               "learn_phase") if k in meta}
     return SpffCfg(in_ch=meta["in_ch"], num_classes=meta["K"], base=meta["base"], ksd=3, **kw)
+
+
+def build_core(meta):
+    """The engine-backed module tree of a non-Lightning fixture, built the way the
+    fixture's generator built the reference's (make_golden.py ns_core / with_gates)."""
+    import innovative3D.models as M
+    fl = {k: meta.get(k, True) for k in ("efilm", "fgate", "se", "specse")}
+    core = M.UNet3D_SpectralCore(in_channels=meta["in_ch"], num_classes=meta["K"], base=meta["base"],
+                                 ksd=3, use_se=fl["se"], use_specse=fl["specse"])
+    if fl["efilm"] or fl["fgate"]:
+        core = M.upgrade_spct_with_novel_blocks(core, use_efilm=fl["efilm"], use_fouriergate=fl["fgate"])
+    g = (meta.get("efilm_hidden", 32), meta.get("efilm_pe_dims", 16), meta.get("learn_phase", False))
+    if g != (32, 16, False):
+        for b in core._blocks():
+            b.efilm = M.EnergyFiLM3D(b.efilm.channels, hidden=g[0], pe_dims=g[1])
+            b.fgate = M.FourierGate3D(learn_phase=g[2])
+    return core
 
 
 def state_of(d):

@@ -361,6 +361,40 @@ def main():
         _write(cases, only)
         return
 
+    def with_gates(core, hidden, pe_dims, learn_phase):
+        """EnergyFiLM3D(hidden, pe_dims) / FourierGate3D(learn_phase) in every block
+        (models.py:1484, 1521; upgrade_spct_with_novel_blocks builds the defaults)."""
+        for mod in core.modules():
+            if isinstance(mod, M._DoubleConvSpectral_Novel):
+                mod.efilm = M.EnergyFiLM3D(mod.efilm.channels, hidden=hidden, pe_dims=pe_dims)
+                mod.fgate = M.FourierGate3D(learn_phase=learn_phase)
+        return core
+
+    # --- Fx6 (round 4): non-default EnergyFiLM3D(hidden 24, pe_dims 11: odd, so the
+    # positional code carries its zero row) and FourierGate3D(learn_phase=True), even D
+    # (Nyquist bin), jittered masks, full grads ---
+    rng = np.random.default_rng(99)
+    x = rng.standard_normal((1, 5, 8, 16, 16)).astype(np.float32)
+    y = _labels(rng, (1, 8, 16, 16), 9, absent=6)
+    cases["fx6_gates_h24_pe11_phase"] = dict(
+        meta=dict(variant="SPFF-UNet", in_ch=5, base=8, K=9, seed=13, jitter=0.25, lit=False,
+                  efilm_hidden=24, efilm_pe_dims=11, learn_phase=True),
+        data=_run_case(torch, Hh, with_gates(ns_core(5, 9, 8), 24, 11, True), x, y, 9, 13,
+                       0.25, True, False))
+    # --- Fx6b: hidden 1, pe_dims 2 (the smallest the reference's Conv1d takes), odd D=7,
+    # learn_phase, batch 2 ---
+    rng = np.random.default_rng(100)
+    x = rng.standard_normal((2, 1, 7, 16, 16)).astype(np.float32)
+    y = _labels(rng, (2, 7, 16, 16), 5, absent=1)
+    cases["fx6b_gates_h1_pe2_phase"] = dict(
+        meta=dict(variant="SPFF-UNet", in_ch=1, base=8, K=5, seed=14, jitter=0.25, lit=False,
+                  efilm_hidden=1, efilm_pe_dims=2, learn_phase=True),
+        data=_run_case(torch, Hh, with_gates(ns_core(1, 5, 8), 1, 2, True), x, y, 5, 14,
+                       0.25, True, False))
+    if only and only.startswith("fx6"):
+        _write(cases, only)
+        return
+
     # --- Fx2: north-star layout (Cin=5 channels, spatial D), base=8, full grads ---
     rng = np.random.default_rng(22)
     x = rng.standard_normal((1, 5, 16, 32, 32)).astype(np.float32)

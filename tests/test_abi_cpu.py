@@ -35,7 +35,8 @@ def test_plan_layout_matches_reference_state_dict():
         x = d["x"]
         B, Cin, D, H, W = x.shape
         plan = E.Plan(B, Cin, D, H, W, cfg.num_classes, base=cfg.base, ksd=3, efilm=cfg.efilm,
-                      fgate=cfg.fgate, se=cfg.se, specse=cfg.specse)
+                      fgate=cfg.fgate, se=cfg.se, specse=cfg.specse, efilm_hidden=cfg.efilm_hidden,
+                      efilm_pe_dims=cfg.efilm_pe_dims, fgate_learn_phase=cfg.learn_phase)
         prefix = "model." if m.get("lit") else ""
         ref = {k[len(prefix):]: tuple(v) for k, v in d["state_shapes"].items()}
         ref_order = [k for k in ref if not k.endswith("._mask")]

@@ -20,6 +20,7 @@ import torch
 import torch.nn.functional as F
 
 from _golden import cfg_of, fixture_names, load, state_of
+from _golden import build_core as _build_core
 from oracle import spff_oracle as O
 import innovative3D.models as M
 import innovative3D.helpers as Hh
@@ -29,12 +30,7 @@ DEV = "cuda"
 
 
 def build_core(meta):
-    fl = {k: meta.get(k, True) for k in ("efilm", "fgate", "se", "specse")}
-    core = M.UNet3D_SpectralCore(in_channels=meta["in_ch"], num_classes=meta["K"], base=meta["base"],
-                                 ksd=3, use_se=fl["se"], use_specse=fl["specse"])
-    if fl["efilm"] or fl["fgate"]:
-        core = M.upgrade_spct_with_novel_blocks(core, use_efilm=fl["efilm"], use_fouriergate=fl["fgate"])
-    return core
+    return _build_core(meta)
 
 
 def load_core(d):
@@ -269,7 +265,7 @@ def _oracle_stages(P, x, cfg):
         if cfg.novel and cfg.efilm:
             z = O.energy_film(P, name + ".efilm", z)
         if cfg.novel and cfg.fgate:
-            z = O.fourier_gate(P, name + ".fgate", z)
+            z = O.fourier_gate(P, name + ".fgate", z, cfg.learn_phase)
         S[name + ".y1"], S[name + ".a1"], S[name + ".y2"] = y1, a1, y2
         return z
 

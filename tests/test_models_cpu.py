@@ -7,6 +7,7 @@ import pytest
 import torch
 
 from _golden import cfg_of, fixture_names, load
+from _golden import build_core as _build_core
 from oracle import spff_oracle as O
 import innovative3D.config as C
 import innovative3D.models as M
@@ -15,12 +16,7 @@ from innovative3D import _engine as E
 
 
 def _core_for(meta):
-    fl = {k: meta.get(k, True) for k in ("efilm", "fgate", "se", "specse")}
-    core = M.UNet3D_SpectralCore(in_channels=meta["in_ch"], num_classes=meta["K"], base=meta["base"],
-                                 ksd=3, use_se=fl["se"], use_specse=fl["specse"])
-    if fl["efilm"] or fl["fgate"]:
-        core = M.upgrade_spct_with_novel_blocks(core, use_efilm=fl["efilm"], use_fouriergate=fl["fgate"])
-    return core
+    return _build_core(meta)
 
 
 @pytest.mark.parametrize("name", fixture_names())
@@ -108,3 +104,23 @@ def test_metric_algebra_ignore_none_with_255_labels():
         tn = int((~pc & ~lc).sum())
         spec = (tn + 1e-6) / (tn + fp + 1e-6)
         assert math.isclose(met[2][c], spec, rel_tol=1e-12)
+
+
+def test_gate_settings_mirror():
+    """EnergyFiLM3D(hidden, pe_dims) / FourierGate3D(learn_phase): accepted in the engine's
+    range, one setting per network (include/spff.h spff_cfg.efilm_hidden ...)."""
+    core = _core_for({"in_ch": 1, "K": 5, "base": 8})
+    assert core._gate_settings() == {"efilm_hidden": 32, "efilm_pe_dims": 16,
+                                     "fgate_learn_phase": False}
+    for b in core._blocks():
+        b.efilm = M.EnergyFiLM3D(b.efilm.channels, hidden=7, pe_dims=5)
+        b.fgate = M.FourierGate3D(learn_phase=True)
+    assert core._gate_settings() == {"efilm_hidden": 7, "efilm_pe_dims": 5,
+                                     "fgate_learn_phase": True}
+    assert tuple(core.enc1.efilm.mlp[0].weight.shape) == (7, 5, 1)
+    core.enc2.fgate = M.FourierGate3D(learn_phase=False)
+    with pytest.raises(NotImplementedError, match="same in every block"):
+        core._gate_settings()
+    for bad in ({"hidden": 65}, {"pe_dims": 1}, {"pe_dims": 33}, {"hidden": 0}):
+        with pytest.raises(NotImplementedError, match="supports hidden"):
+            M.EnergyFiLM3D(8, **bad)
