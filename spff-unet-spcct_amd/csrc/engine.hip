@@ -168,6 +168,8 @@ struct spff_plan {
   // interior depth tiles of the next convolution (conv_halo)
   hipStream_t st2 = nullptr;
   hipEvent_t ev_in = nullptr, ev_halo = nullptr;
+  // the conv input whose halo exchange halo_begin already put on st2 (ev_halo marks it)
+  const float* halo_early = nullptr;
 
   float* F(size_t off) const { return reinterpret_cast<float*>(ws + off); }
   const float* P(int64_t off) const { return off < 0 ? nullptr : prm + off; }
@@ -601,6 +603,14 @@ int hrows_exchange(spff_plan* p, const Src2& x, const Vol& v, int cin, Src2* xr,
   xr->ldr = ldr;
   return SPFF_OK;
 }
+// the side stream st2 and its events (created at the first overlapped exchange)
+int side_stream(spff_plan* p) {
+  if (p->st2) return SPFF_OK;
+  HIPCK(hipStreamCreateWithFlags(&p->st2, hipStreamNonBlocking));
+  HIPCK(hipEventCreateWithFlags(&p->ev_in, hipEventDisableTiming));
+  HIPCK(hipEventCreateWithFlags(&p->ev_halo, hipEventDisableTiming));
+  return SPFF_OK;
+}
 // a height-sharded 3x3x3 conv: the row exchange on the side stream st2 beside the H tiles
 // that read no boundary row, then the first and last H tiles (conv3d_splits_height); else
 // exchange, then convolve.  The ranks at both global ends still exchange (their single
@@ -617,11 +627,7 @@ int conv_h(spff_plan* p, int cls, double flops, double bytes, const Src2& x, con
                      p->F(p->wg_ws), nullptr));
     return SPFF_OK;
   }
-  if (!p->st2) {
-    HIPCK(hipStreamCreateWithFlags(&p->st2, hipStreamNonBlocking));
-    HIPCK(hipEventCreateWithFlags(&p->ev_in, hipEventDisableTiming));
-    HIPCK(hipEventCreateWithFlags(&p->ev_halo, hipEventDisableTiming));
-  }
+  CK(side_stream(p));
   HIPCK(hipEventRecord(p->ev_in, p->st));  // x is final (and the previous conv is done
   HIPCK(hipStreamWaitEvent(p->st2, p->ev_in, 0));  //   reading the staging slab)
   CK(hrows_exchange(p, x, v, cin, &xr, p->st2));
@@ -659,6 +665,21 @@ int conv_wgrad(spff_plan* p, double flops, double bytes, const Src2& x, const fl
   return SPFF_OK;
 }
 
+// depth-sharded plans: start the halo exchange of the next dgrad's input on st2 as soon
+// as that input is final, so that it runs beside the weight gradient enqueued before the
+// dgrad (which reads the same tensor at the local slices only), not just beside the
+// dgrad's interior tiles; conv_halo then only waits for ev_halo.
+int halo_begin(spff_plan* p, const float* x, const Vol& v, int C) {
+  if (p->hsh || !v.dh) return SPFF_OK;
+  CK(side_stream(p));
+  HIPCK(hipEventRecord(p->ev_in, p->st));
+  HIPCK(hipStreamWaitEvent(p->st2, p->ev_in, 0));
+  CK(halo(p, x, v, C, p->st2));
+  HIPCK(hipEventRecord(p->ev_halo, p->st2));
+  p->halo_early = x;
+  return SPFF_OK;
+}
+
 // halo exchange of x + the 3x3x3 convolution reading it.  Depth-sharded plans whose
 // conv can split its depth tiles run the exchange on the side stream st2 while the
 // interior depth tiles (which read no halo slice) compute on st, then the first and
@@ -673,22 +694,25 @@ int conv_halo(spff_plan* p, int cls, double flops, double bytes, const Src2& x, 
   if (p->hsh) return conv_h(p, cls, flops, bytes, x, y, v, Cin_w, Cout_w, dgrad);
   const int KD = p->KD, math = p->cfg.math;
   const bool ovl = v.dh && !stats && conv3d_splits_depth(v, KD, Cin_w, Cout_w, dgrad, math);
+  const bool early = p->halo_early && p->halo_early == x.p0 && x.p1 == x.p0;
+  p->halo_early = nullptr;
   if (!ovl) {
-    CK(halo_src(p, x, v));
+    if (early)
+      HIPCK(hipStreamWaitEvent(p->st, p->ev_halo, 0));
+    else
+      CK(halo_src(p, x, v));
     PROFB(p, cls, flops, bytes,
           conv3d_run(x, p->F(p->wt), y, v, KD, Cin_w, Cout_w, dgrad, math, p->st, p->F(p->wg_ws),
                      stats, 0, wmax));
     return SPFF_OK;
   }
-  if (!p->st2) {
-    HIPCK(hipStreamCreateWithFlags(&p->st2, hipStreamNonBlocking));
-    HIPCK(hipEventCreateWithFlags(&p->ev_in, hipEventDisableTiming));
-    HIPCK(hipEventCreateWithFlags(&p->ev_halo, hipEventDisableTiming));
+  if (!early) {
+    CK(side_stream(p));
+    HIPCK(hipEventRecord(p->ev_in, p->st));  // x is final
+    HIPCK(hipStreamWaitEvent(p->st2, p->ev_in, 0));
+    CK(halo_src(p, x, v, p->st2));
+    HIPCK(hipEventRecord(p->ev_halo, p->st2));
   }
-  HIPCK(hipEventRecord(p->ev_in, p->st));  // x is final
-  HIPCK(hipStreamWaitEvent(p->st2, p->ev_in, 0));
-  CK(halo_src(p, x, v, p->st2));
-  HIPCK(hipEventRecord(p->ev_halo, p->st2));
   PROFB(p, cls, flops, bytes,
         conv3d_run(x, p->F(p->wt), y, v, KD, Cin_w, Cout_w, dgrad, math, p->st, p->F(p->wg_ws),
                    nullptr, 1));
@@ -1027,6 +1051,7 @@ int bwd_block(spff_plan* p, Blk& b, const float* dout, const Dst2* dx, const Src
     CK(halo(p, da1, v, C));
     a1 = src1(da1, C);
   }
+  CK(halo_begin(p, dy2, v, C));  // dgrad input: its exchange beside the weight gradient
   CK(conv_wgrad(p, 2.0 * V * C * C * T, cbytes(V, C, C, T), a1, dy2, p->DP(b.c2.w), v, C, C,
                 f16_slot(p, b, F16_A1), f16_slot(p, b, F16_DY2)));
   const int math = p->cfg.math;
@@ -1047,6 +1072,7 @@ int bwd_block(spff_plan* p, Blk& b, const float* dout, const Dst2* dx, const Src
                        C, p->st, 0.01f, f16_slot(p, b, F16_DA1)));
   }
   if (p->lean && dec_bi >= 0) CK(lean_dec_input(p, dec_bi, &in));
+  if (dx) CK(halo_begin(p, da1, v, C));
   CK(conv_wgrad(p, 2.0 * V * b.Cin * C * T, cbytes(V, b.Cin, C, T), in, da1, p->DP(b.c1.w), v,
                 b.Cin, C, f16_in_slot(p, b), f16_slot(p, b, F16_DA1)));
   if (dx) {
