@@ -1,15 +1,15 @@
 #!/bin/bash
 # One GPU call: default bench line, rocprofv3 kernel stats of the same command, per-layer
 # conv kernel rates, and the two PMC traffic passes (FETCH_SIZE / WRITE_SIZE) keyed to
-# the bench workload (scripts/pmc_traffic.py).  Each GPU step under its own timeout;
+# the bench workload (scripts/pmc_traffic.py), into gpurun_out/m$ROUND (default 4).  Each GPU step under its own timeout;
 # the call stops at the first failing step.
 set -u
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-O=gpurun_out/m3
+O=gpurun_out/m${ROUND:-4}
 rm -rf $O && mkdir -p $O
-run() { echo "[r03_measure] $1"; }
+run() { echo "[measure] $1"; }
 run bench
 timeout -k 10 400 python bench.py ${BENCH_ARGS:-} > $O/bench.log 2>&1 || { echo "bench rc=$?"; exit 1; }
 run prof
@@ -24,4 +24,4 @@ if [ "${M3_PMC:-1}" = 1 ]; then
   timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/pmc_write -o run -- python3 bench.py --steps 1 --warmup 1 --cpu-baseline skip ${BENCH_ARGS:-} > $O/pmc_write.log 2>&1 || { echo "pmc write rc=$?"; exit 1; }
   python scripts/pmc_traffic.py $O/pmc_fetch/run_counter_collection.csv $O/pmc_write/run_counter_collection.csv $O/pmc_conv.json $O/pmc_hbm_per_kernel.csv --bench-log $O/pmc_fetch.log > $O/pmc_traffic.log 2>&1 || { echo "pmc_traffic rc=$?"; exit 1; }
 fi
-echo "[r03_measure] done"
+echo "[measure] done"
