@@ -332,11 +332,7 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : (BN <= 32 && NS == NS_F16 &&
   int exc = 0;       // exponent of the chunk being accumulated
   int exn = 0;       // exponent of the chunk in the registers (the next one)
   float sx = 1.f;    // 2^exn: the scale the halo split applies
-  // SPFF_XSCALE_LATE: per-wave max |x| bits of a chunk (parity slots); else one 64-bit word
-  // max-ed by every lane: (chunk index + 1) << 32 | max |x| bits, so a chunk's values
-  // dominate every earlier chunk's and the word never needs clearing
-  __shared__ unsigned smx[2][SPFF_XSCALE_LATE ? NW : 1];
-  __shared__ unsigned long long smx64;
+  __shared__ unsigned smx[2][NW];  // per-wave max |x| bits of a chunk (parity slots)
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -525,21 +521,13 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : (BN <= 32 && NS == NS_F16 &&
   auto read_scale = [&](int slot) {
     unsigned mb = 0;
 #pragma unroll
-    for (int w = 0; w < (SPFF_XSCALE_LATE ? NW : 1); ++w) mb = max(mb, smx[slot][w]);
+    for (int w = 0; w < NW; ++w) mb = max(mb, smx[slot][w]);
     return f16_scale_exp(__builtin_amdgcn_readfirstlane(mb));
   };
-  // every lane adds its max with one LDS atomic (the slot was zeroed beforehand; no
-  // cross-lane reduction, no return value) -> workgroup barrier -> the chunk's exponent
-  auto block_scale = [&](float m, int c) {
-    if constexpr (SPFF_XSCALE_LATE) {
-      wave_max_store(m, c & 1);
-      __syncthreads();
-      return read_scale(c & 1);
-    } else {
-      atomicMax(&smx64, ((unsigned long long)(c + 1) << 32) | __float_as_uint(m));
-      __syncthreads();
-      return f16_scale_exp(__builtin_amdgcn_readfirstlane((unsigned)smx64));
-    }
+  auto block_scale = [&](float m, int slot) {
+    wave_max_store(m, slot);
+    __syncthreads();
+    return read_scale(slot);
   };
   auto split_one = [&](int k) {
     if constexpr (HF) {  // (prep_max has applied the activation and the padding)
@@ -626,13 +614,9 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : (BN <= 32 && NS == NS_F16 &&
   // writes fp32 partial sums that k_splitk_reduce adds in a fixed order
   const int kc0 = part ? blockIdx.z * kps : 0;
   const int kc1 = part ? min(nkc, kc0 + kps) : nkc;
-  if (HF && !SPFF_XSCALE_LATE) {  // (chunk indices start at kc0 >= 0: epoch 1 and up)
-    if (tid == 0) smx64 = 0ull;
-    __syncthreads();
-  }
   fetch(kc0);
   if constexpr (HF) {
-    exc = exn = block_scale(prep_max(), kc0);
+    exc = exn = block_scale(prep_max(), kc0 & 1);
     sx = exp2i(exn);
   }
 #pragma unroll
@@ -686,10 +670,8 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : (BN <= 32 && NS == NS_F16 &&
       // Capped at 2^64 above the current chunk's, so the rescaled accumulator cannot
       // overflow (|acc| < 2^40 in these units)
       if (HF && !LATE && j == J0 && kc + 1 < kc1) {
-        __builtin_amdgcn_sched_barrier(0);
-        exn = min(block_scale(prep_max(), kc + 1), exc + 64);
+        exn = min(block_scale(prep_max(), (kc + 1) & 1), exc + 64);
         sx = exp2i(exn);
-        __builtin_amdgcn_sched_barrier(0);
       }
       if (LATE && j == (NJ > 2 ? NJ - 2 : 0) && kc + 1 < kc1) {
         __builtin_amdgcn_sched_barrier(0x10C);
