@@ -310,7 +310,10 @@ __global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x(
 // distinct banks.
 // HR: height-sharded input (the stencil's rows h = -1 / h = H from Src2::rlo / rhi, as in
 // k_conv3d_fwd_x); a separate instantiation
-template <int KD, int CI, int NS, int NJMAX, bool HR, int CO>
+// ACT: x is y1 read through the fused input activation (x.al / x.de: lrelu(IN(y1)), the
+// 32-channel convs of conv3d_fuses_act) -- a separate instantiation, so the plain kernels
+// carry neither its per-tile coefficient loads nor its validity bookkeeping
+template <int KD, int CI, int NS, int NJMAX, bool HR, int CO, bool ACT>
 __global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x16(
     Src2 x, const float* __restrict__ dy, int lddy, float* __restrict__ part, Vol vol, int Cin,
     int kpad, int Cout, int npad, int tilesH, int tilesW, int ntiles, int tps, int nblk,
@@ -402,7 +405,11 @@ __global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x16(
     r.w0 = twi * WX_TW;
     return r;
   };
-  auto load_plane = [&](const TileXY& tx, int gd, float4 (&r)[NP]) {
+  // (the fused input activation is applied at the store, not here: applied to each load as
+  // it arrived, it made the prefetch wait for every load in turn before the MFMAs)
+  unsigned hm = 0;  // bit k: hreg[k] is a valid (not padding) position
+  auto load_plane = [&](const TileXY& tx, int gd, float4 (&r)[NP], unsigned& m) {
+    m = 0;
 #pragma unroll
     for (int k = 0; k < NP; ++k) {
       const int i = tid + 256 * k;
@@ -424,18 +431,13 @@ __global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x16(
               p = (gh < 0 ? x.rlo : x.rhi) + (((int64_t)b * D + gd) * W + gw) * x.ldr + c;
           }
           v = *reinterpret_cast<const float4*>(p);
-          if (x.al) {
-            v.x = v.x * xal.x + xde.x; v.x = v.x > 0.f ? v.x : 0.01f * v.x;
-            v.y = v.y * xal.y + xde.y; v.y = v.y > 0.f ? v.y : 0.01f * v.y;
-            v.z = v.z * xal.z + xde.z; v.z = v.z > 0.f ? v.z : 0.01f * v.z;
-            v.w = v.w * xal.w + xde.w; v.w = v.w > 0.f ? v.w : 0.01f * v.w;
-          }
+          m |= 1u << k;
         }
       }
       r[k] = v;
     }
   };
-  auto store_plane = [&](int gd, const float4 (&r)[NP]) {
+  auto store_plane = [&](int gd, const float4 (&r)[NP], unsigned m) {
     unsigned short* dst = Xs + (R4 ? ((gd + 4) & 3) : ((gd + 3) % KD)) * PPOS * CI;
 #pragma unroll
     for (int k = 0; k < NP; ++k) {
@@ -443,6 +445,12 @@ __global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x16(
       if (i < PPOS * CQ) {
         uint2 o[NPL];
         float4 v = r[k];
+        if (ACT && ((m >> k) & 1u)) {  // lrelu(IN(y)) of valid positions (padding stays 0)
+          v.x = v.x * xal.x + xde.x; v.x = v.x > 0.f ? v.x : 0.01f * v.x;
+          v.y = v.y * xal.y + xde.y; v.y = v.y > 0.f ? v.y : 0.01f * v.y;
+          v.z = v.z * xal.z + xde.z; v.z = v.z > 0.f ? v.z : 0.01f * v.z;
+          v.w = v.w * xal.w + xde.w; v.w = v.w > 0.f ? v.w : 0.01f * v.w;
+        }
         if constexpr (HF) v = make_float4(v.x * sx, v.y * sx, v.z * sx, v.w * sx);
         split4<NS>(v, o);
 #pragma unroll
@@ -453,14 +461,16 @@ __global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x16(
   };
   auto fetch = [&](int tile) {
     const TileXY tx = tile_xy(tile);
-    if (x.al) {
+    if constexpr (ACT) {
+      // the fused activation's coefficients of this tile's batch and this thread's 4
+      // channels, loaded unconditionally from a clamped channel, so no branch merge waits
+      // for them here -- store_plane does
       const int c = ci_base + 4 * (tid % CQ);
-      if (c < Cin) {
-        xal = *reinterpret_cast<const float4*>(x.al + (int64_t)tx.b * x.ld0 + c);
-        xde = *reinterpret_cast<const float4*>(x.de + (int64_t)tx.b * x.ld0 + c);
-      }
+      const int64_t o = (int64_t)tx.b * x.ld0 + (c < Cin ? c : 0);
+      xal = *reinterpret_cast<const float4*>(x.al + o);
+      xde = *reinterpret_cast<const float4*>(x.de + o);
     }
-    load_plane(tx, tx.d0 + KD / 2, hreg);
+    load_plane(tx, tx.d0 + KD / 2, hreg, hm);
     const int b = tx.b, d0 = tx.d0, h0 = tx.h0, w0 = tx.w0;
 #pragma unroll
     for (int k = 0; k < NY; ++k) {
@@ -477,7 +487,7 @@ __global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x16(
     }
   };
   auto stash = [&](int d0, bool negate, int yb) {
-    store_plane(d0 + KD / 2, hreg);
+    store_plane(d0 + KD / 2, hreg, hm);
 #pragma unroll
     for (int k = 0; k < NY; ++k) {
       const int i = tid + 256 * k;
@@ -557,8 +567,9 @@ __global__ __launch_bounds__(256, 2) void k_conv3d_wgrad_x16(
 #pragma unroll
     for (int hd = 0; hd < KD - 1; ++hd) {
       float4 r[NP];
-      load_plane(tx, d0 + hd - KD / 2, r);
-      store_plane(d0 + hd - KD / 2, r);
+      unsigned m;
+      load_plane(tx, d0 + hd - KD / 2, r, m);
+      store_plane(d0 + hd - KD / 2, r, m);
     }
   };
   if constexpr (R4) {
@@ -754,18 +765,23 @@ hipError_t conv3d_wgrad_x(const Src2& x, const float* dy, int lddy, float* dw, V
     // 16-row blocks: nblk = ceil(T CI / 16); NJMAX = ceil(nblk / 4):
     // KD3/CI16 27 -> 7, KD3/CI8 14 -> 4, KD1/CI16 9 -> 3, KD1/CI8 5 -> 2
     const int nblk = cdiv(KD * 9 * p.ci, 16);
-#define SPFF_WX16C(KD_, CI_, NS_, NJ_, HR_, CO_)                                                \
-  hipLaunchKernelGGL((k_conv3d_wgrad_x16<KD_, CI_, NS_, NJ_, HR_, CO_>), grid, dim3(256), 0, s, \
-                     x, dy, lddy, ws, vol, Cin, p.kpad, Cout, p.npad, p.tilesH, p.tilesW,      \
+    // (the fused input activation only on 32-wide output tiles: conv3d_fuses_act's C = 32)
+    if (x.al && p.co != 32) return hipErrorInvalidValue;
+#define SPFF_WX16C(KD_, CI_, NS_, NJ_, HR_, CO_, ACT_)                                            \
+  hipLaunchKernelGGL((k_conv3d_wgrad_x16<KD_, CI_, NS_, NJ_, HR_, CO_, ACT_>), grid, dim3(256),  \
+                     0, s, x, dy, lddy, ws, vol, Cin, p.kpad, Cout, p.npad, p.tilesH, p.tilesW, \
                      p.ntiles, p.tps, nblk, xmax, ymax)
 #define SPFF_WX16(KD_, CI_, NS_, NJ_)                                                          \
   do {                                                                                         \
     if (p.co == 16) {                                                                          \
-      if (x.rows()) SPFF_WX16C(KD_, CI_, NS_, NJ_, true, 16);                                  \
-      else SPFF_WX16C(KD_, CI_, NS_, NJ_, false, 16);                                          \
+      if (x.rows()) SPFF_WX16C(KD_, CI_, NS_, NJ_, true, 16, false);                           \
+      else SPFF_WX16C(KD_, CI_, NS_, NJ_, false, 16, false);                                   \
+    } else if (x.al) {                                                                         \
+      if (x.rows()) SPFF_WX16C(KD_, CI_, NS_, NJ_, true, 32, true);                            \
+      else SPFF_WX16C(KD_, CI_, NS_, NJ_, false, 32, true);                                    \
     } else {                                                                                   \
-      if (x.rows()) SPFF_WX16C(KD_, CI_, NS_, NJ_, true, 32);                                  \
-      else SPFF_WX16C(KD_, CI_, NS_, NJ_, false, 32);                                          \
+      if (x.rows()) SPFF_WX16C(KD_, CI_, NS_, NJ_, true, 32, false);                           \
+      else SPFF_WX16C(KD_, CI_, NS_, NJ_, false, 32, false);                                   \
     }                                                                                          \
   } while (0)
     if (KD == 3) {

@@ -136,6 +136,46 @@ __device__ __forceinline__ void split_bf16(float x, unsigned short (&o)[NS]) {
   }
 }
 
+// 16x16x32 tap-quad schedule (X16): k = 4 lane groups x 8 channels, lane group g
+// at its own tap.  A ds_read_b128 lane group mixes rows {0-3, 12-15} of k-group
+// 0 (2) with rows 4-11 of k-group 1 (3): with the rows of a block mapped to the
+// W-row's voxels as rows 4-11 -> even w, the rest -> odd w, every such group
+// covers 16 distinct 16-byte bank quads as long as the two taps' halo offsets
+// differ by an EVEN number of positions, i.e. have the same kw parity (offset
+// = (kd HH + kh) HWD + kw with even HH, HWD).  Pairs are therefore formed within
+// the even-kw and within the odd-kw taps; a leftover tap pairs with the zero
+// padding row (weight index T), which reads its partner's position.
+template <int KD>
+struct XQuads {
+  int nq = 0;
+  signed char tap[32] = {};  // weight row per slot (T = the zero padding row)
+  signed char src[32] = {};  // tap whose halo offset the slot reads
+};
+template <int KD>
+__host__ __device__ constexpr XQuads<KD> x_quads() {
+  XQuads<KD> q{};
+  constexpr int T = KD * 9;
+  int ev[27] = {}, od[27] = {}, ne = 0, no = 0;
+  for (int t = 0; t < T; ++t) {
+    if ((t % 3) % 2 == 0) ev[ne++] = t;
+    else od[no++] = t;
+  }
+  int pa[32] = {}, pb[32] = {}, np = 0;
+  for (int i = 0; i + 1 < ne; i += 2) { pa[np] = ev[i]; pb[np] = ev[i + 1]; ++np; }
+  for (int i = 0; i + 1 < no; i += 2) { pa[np] = od[i]; pb[np] = od[i + 1]; ++np; }
+  if (ne % 2) { pa[np] = ev[ne - 1]; pb[np] = -1; ++np; }
+  if (no % 2) { pa[np] = od[no - 1]; pb[np] = -1; ++np; }
+  if (np % 2) { pa[np] = -2; pb[np] = -2; ++np; }  // (pad, pad)
+  q.nq = np / 2;
+  for (int i = 0; i < np; ++i) {
+    const int a = pa[i], b = pb[i];
+    q.tap[2 * i] = (signed char)(a >= 0 ? a : T);
+    q.src[2 * i] = (signed char)(a >= 0 ? a : 0);
+    q.tap[2 * i + 1] = (signed char)(b >= 0 ? b : T);
+    q.src[2 * i + 1] = (signed char)(b >= 0 ? b : (a >= 0 ? a : 0));
+  }
+  return q;
+}
 // ------------------------------------------------------------ weight pack --
 // The weights are split into their NS bf16 planes once per launch, here, in the
 // exact LDS image the conv kernel reads, so its weight staging is a plain
@@ -238,46 +278,6 @@ static int ns_of(int math) {
   return math == SPFF_MATH_F16X3 ? NS_F16 : math == SPFF_MATH_BF16X3 ? 2 : 3;
 }
 
-// 16x16x32 tap-quad schedule (X16): k = 4 lane groups x 8 channels, lane group g
-// at its own tap.  A ds_read_b128 lane group mixes rows {0-3, 12-15} of k-group
-// 0 (2) with rows 4-11 of k-group 1 (3): with the rows of a block mapped to the
-// W-row's voxels as rows 4-11 -> even w, the rest -> odd w, every such group
-// covers 16 distinct 16-byte bank quads as long as the two taps' halo offsets
-// differ by an EVEN number of positions, i.e. have the same kw parity (offset
-// = (kd HH + kh) HWD + kw with even HH, HWD).  Pairs are therefore formed within
-// the even-kw and within the odd-kw taps; a leftover tap pairs with the zero
-// padding row (weight index T), which reads its partner's position.
-template <int KD>
-struct XQuads {
-  int nq = 0;
-  signed char tap[32] = {};  // weight row per slot (T = the zero padding row)
-  signed char src[32] = {};  // tap whose halo offset the slot reads
-};
-template <int KD>
-__host__ __device__ constexpr XQuads<KD> x_quads() {
-  XQuads<KD> q{};
-  constexpr int T = KD * 9;
-  int ev[27] = {}, od[27] = {}, ne = 0, no = 0;
-  for (int t = 0; t < T; ++t) {
-    if ((t % 3) % 2 == 0) ev[ne++] = t;
-    else od[no++] = t;
-  }
-  int pa[32] = {}, pb[32] = {}, np = 0;
-  for (int i = 0; i + 1 < ne; i += 2) { pa[np] = ev[i]; pb[np] = ev[i + 1]; ++np; }
-  for (int i = 0; i + 1 < no; i += 2) { pa[np] = od[i]; pb[np] = od[i + 1]; ++np; }
-  if (ne % 2) { pa[np] = ev[ne - 1]; pb[np] = -1; ++np; }
-  if (no % 2) { pa[np] = od[no - 1]; pb[np] = -1; ++np; }
-  if (np % 2) { pa[np] = -2; pb[np] = -2; ++np; }  // (pad, pad)
-  q.nq = np / 2;
-  for (int i = 0; i < np; ++i) {
-    const int a = pa[i], b = pb[i];
-    q.tap[2 * i] = (signed char)(a >= 0 ? a : T);
-    q.src[2 * i] = (signed char)(a >= 0 ? a : 0);
-    q.tap[2 * i + 1] = (signed char)(b >= 0 ? b : T);
-    q.src[2 * i + 1] = (signed char)(b >= 0 ? b : (a >= 0 ? a : 0));
-  }
-  return q;
-}
 // MFMA row r (0..15) of a 16-row block -> w within the W-row (see x_quads)
 __device__ __forceinline__ int x16_w(int r) {
   return (r >= 4 && r < 12) ? 2 * (r - 4) : (r < 4 ? 2 * r + 1 : 2 * r - 15);
@@ -429,13 +429,16 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : (BN <= 32 && NS == NS_F16 &&
       pok |= ok ? (1u << k) : 0u;
     }
   }
-  auto fetch = [&](int kc) {
+  // live = false: a dummy fetch (every quad invalid, loads from clamped addresses) after the
+  // last chunk, so that the fetch is unconditional: a conditional one left the registers'
+  // old and new values to merge, and the compiler waited for the first loads at the merge
+  auto fetch = [&](int kc, bool live = true) {
     hvalid = 0;
     fkc = kc;
     if constexpr (PRE) {
       // a thread's channel quad q = tid & 1 is the same for every k (XT_THREADS is even)
       const int cq = kc * 8 + 4 * (tid & 1);
-      const bool cok = cq < Cin;
+      const bool cok = live && cq < Cin;
 #pragma unroll
       for (int k = 0; k < RH; ++k) {
         const bool ok = ((pok >> k) & 1u) && cok;
@@ -463,8 +466,8 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : (BN <= 32 && NS == NS_F16 &&
         hrow = (gh < 0 && x.rlo) || (gh >= H && x.rhi);
         hin = hin || hrow;
       }
-      const bool ok = i < NHX && (unsigned)(gd + vol.dh) < (unsigned)(D + 2 * vol.dh) && hin &&
-                      (unsigned)gw < (unsigned)W &&
+      const bool ok = live && i < NHX && (unsigned)(gd + vol.dh) < (unsigned)(D + 2 * vol.dh) &&
+                      hin && (unsigned)gw < (unsigned)W &&
                       kc * 8 + 4 * q < Cin && !((gd < 0 && x.zlo) || (gd >= D && x.zhi));
       const int64_t vox = ok ? (((int64_t)b * D + gd) * H + gh) * W + gw : 0;
       // two-source select on the operands (v_cndmask), not on two address
@@ -486,21 +489,35 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : (BN <= 32 && NS == NS_F16 &&
   };
   // HF: the fused input activation (32-wide tiles) and the zero padding applied to the
   // prefetched halo in place, and this thread's max |element| of it
+  // the chunk's 8 (al, de) pairs of the fused input activation, loaded once per chunk from
+  // uniform addresses (scalar loads) and selected per lane: a thread's 4 channels are the
+  // lower or upper half (XT_THREADS is even: q = tid & 1 for all k).  Loaded per halo float4
+  // they became 9 dependent vector-memory round trips, each behind a vmcnt(0)
+  auto act_coef = [&](float (&a)[4], float (&e)[4]) {
+    const int64_t o = __builtin_amdgcn_readfirstlane((int)((int64_t)b * x.ld0 + fkc * 8));
+    const float* ap = x.al + o;
+    const float* dp = x.de + o;
+    const bool hi = tid & 1;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float alo = ap[j], ahi = ap[4 + j], elo = dp[j], ehi = dp[4 + j];
+      a[j] = hi ? ahi : alo;
+      e[j] = hi ? ehi : elo;
+    }
+  };
   auto prep_max = [&]() {
     float m = 0.f;
+    float ca[4] = {1.f, 1.f, 1.f, 1.f}, ce[4] = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (BN == 32) if (x.al) act_coef(ca, ce);
 #pragma unroll
     for (int k = 0; k < RH; ++k) {
       const bool ok = (hvalid >> k) & 1u;
       float4 v = hreg[k];
       if constexpr (BN == 32) if (x.al) {
-        const float* ap = x.al + (int64_t)b * x.ld0 + fkc * 8;
-        const float* dp = x.de + (int64_t)b * x.ld0 + fkc * 8;
-        const bool hi = tid & 1;
         float r[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const float a = hi ? ap[4 + j] : ap[j], e = hi ? dp[4 + j] : dp[j];
-          const float t = r[j] * a + e;
+          const float t = r[j] * ca[j] + ce[j];
           r[j] = fmaxf(t, 0.01f * t);
         }
         v = make_float4(r[0], r[1], r[2], r[3]);
@@ -662,7 +679,7 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : (BN <= 32 && NS == NS_F16 &&
     }
     if (SPFF_XDIAG != 1 || kc == kc0) stash(kc, kc == kc0, !(LATE && kc != kc0));
     __syncthreads();  // (vmcnt(0): the weight DMA has landed)
-    if (kc + 1 < kc1) fetch(kc + 1);
+    fetch(kc + 1 < kc1 ? kc + 1 : kc, kc + 1 < kc1);
 #pragma unroll
     for (int j = 0; j < (SPFF_XDIAG == 2 ? 0 : NJ); ++j) {
       if constexpr (SPFF_XIGLP >= 0) __builtin_amdgcn_iglp_opt(SPFF_XIGLP);
@@ -690,10 +707,19 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : (BN <= 32 && NS == NS_F16 &&
       }
       if constexpr (X16) {
         // lane group kg takes slot 4j + kg of the quad schedule
-        const int s01 = kg & 1;
-        const int sa = 4 * j + (kg & 2);
-        const int toff = s01 ? toff_of(QT.src[sa + 1]) : toff_of(QT.src[sa]);
-        const int wtap = s01 ? QT.tap[sa + 1] : QT.tap[sa];
+        // (the four slots' table entries are indexed by the unrolled j only and selected per
+        // lane group: a lane-varying index into the constexpr tables made the compiler load
+        // them from memory at every k-step, each load followed by a vmcnt(0) that drained the
+        // prefetched halo / weight DMA still in flight)
+        const bool g1 = kg & 1, g2 = kg & 2;
+        auto sel4 = [&](int c0, int c1, int c2, int c3) {
+          const int lo = g1 ? c1 : c0, hi = g1 ? c3 : c2;
+          return g2 ? hi : lo;
+        };
+        const int toff = sel4(toff_of(QT.src[4 * j]), toff_of(QT.src[4 * j + 1]),
+                              toff_of(QT.src[4 * j + 2]), toff_of(QT.src[4 * j + 3]));
+        const int wtap =
+            sel4(QT.tap[4 * j], QT.tap[4 * j + 1], QT.tap[4 * j + 2], QT.tap[4 * j + 3]);
         // row blocks in groups of RBH (the 4 x 16 x 16 tiles' 8 row blocks: two groups,
         // so only half of the A fragments are live at a time)
         constexpr int RBH = RB > 4 ? 4 : RB;

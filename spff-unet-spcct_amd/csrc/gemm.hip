@@ -45,14 +45,41 @@ static inline int64_t cdiv64(int64_t a, int64_t b) { return (a + b - 1) / b; }
 // Row-handle interface: prep(m) does the per-row index work once (-1 = row out
 // of range); load4(h, k) / put(h + col(n), n, v) are then a few adds.  Index
 // math is 32-bit (the launchers check M < 2^31); only byte offsets are 64-bit.
+// raw4(h, k, ok): the loaders with kRaw load UNCONDITIONALLY from a clamped address and
+// report whether the quad is in range; the kernels zero the out-of-range quads when they
+// stage them (ld4 / the validity masks below).  A conditional load (zero or the load,
+// merged in a branch) made the compiler wait for the load at the merge -- inside the
+// register prefetch, which then ran synchronously before the MFMAs it was meant to overlap.
 struct LoadRowsVec {  // A[m][k] = p[m*ld + k]; ld, kmax multiples of 4
   const float* p; int ld; int kmax; int64_t M;
+  static constexpr bool kRaw = true;
   __device__ int64_t prep(int64_t m) const { return m < M ? m * ld : -1; }
   __device__ float4 load4(int64_t h, int k) const {
     if (h < 0 || k >= kmax) return make_float4(0.f, 0.f, 0.f, 0.f);
     return *reinterpret_cast<const float4*>(p + h + k);
   }
+  __device__ float4 raw4(int64_t h, int k, bool& ok) const {
+    ok = h >= 0 && k < kmax;
+    return *reinterpret_cast<const float4*>(p + (ok ? h + k : 0));
+  }
 };
+template <class L, class = void>
+struct has_raw : std::false_type {};
+template <class L>
+struct has_raw<L, std::void_t<decltype(L::kRaw)>> : std::true_type {};
+// a quad for staging: raw (validity in ok) where the loader has raw4, else load4 (ok = true)
+template <class L>
+__device__ __forceinline__ float4 ld4(const L& A, int64_t h, int k, bool& ok) {
+  if constexpr (has_raw<L>::value) {
+    return A.raw4(h, k, ok);
+  } else {
+    ok = true;
+    return A.load4(h, k);
+  }
+}
+__device__ __forceinline__ float4 zero_unless(const float4& v, bool ok) {
+  return ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+}
 struct LoadRowsScalar {  // generic
   const float* p; int ld; int kmax; int64_t M;
   __device__ int64_t prep(int64_t m) const { return m < M ? m * ld : -1; }
@@ -150,6 +177,14 @@ struct LoadUpGather {  // A[m][k], k = ij*Cout + co -> dy[high(m,ij)*ld + co]
     udivmod_s((uint32_t)k, (uint32_t)Cout, csh, ij, co);
     return *reinterpret_cast<const float4*>(p + (h + up_sub_off((int)ij, Hl, Wl)) * ld + co);
   }
+  static constexpr bool kRaw = true;
+  __device__ float4 raw4(int64_t h, int k, bool& ok) const {
+    ok = h >= 0 && k < nsub * Cout;
+    uint32_t ij, co;
+    udivmod_s((uint32_t)(ok ? k : 0), (uint32_t)Cout, csh, ij, co);
+    return *reinterpret_cast<const float4*>(p + ((ok ? h : 0) + up_sub_off((int)ij, Hl, Wl)) * ld +
+                                            co);
+  }
 };
 struct StoreRows {  // C[m][n] -> p[m*ld + n] (+bias[n]), n < nmax
   float* p; int ld; int nmax; const float* bias; int64_t M;
@@ -201,6 +236,14 @@ struct LoadRows2 {  // A[m][k] from a two-source channel view (torch.cat([p0, p1
   __device__ float4 load4(int64_t m, int k) const {
     if (m < 0 || k >= kmax) return make_float4(0.f, 0.f, 0.f, 0.f);
     const float* q = k < x.split ? x.p0 + m * x.ld0 + k : x.p1 + m * x.ld1 + (k - x.split);
+    return *reinterpret_cast<const float4*>(q);
+  }
+  static constexpr bool kRaw = true;
+  __device__ float4 raw4(int64_t m, int k, bool& ok) const {
+    ok = m >= 0 && k < kmax;
+    const int64_t mm = ok ? m : 0;
+    const int kk = ok ? k : 0;
+    const float* q = kk < x.split ? x.p0 + mm * x.ld0 + kk : x.p1 + mm * x.ld1 + (kk - x.split);
     return *reinterpret_cast<const float4*>(q);
   }
 };
@@ -435,6 +478,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x(AL A, const float* __restrict
 #pragma unroll
     for (int cb = 0; cb < CB; ++cb) acc[rb][cb] = f32x4g{0.f, 0.f, 0.f, 0.f};
   float4 ra[4], rb[NRB];
+  unsigned am = 0;  // bit j: ra[j] is in range (else zeroed at the stash)
   int64_t ah[4];
   auto prep_rows = [&](int64_t t) {
 #pragma unroll
@@ -442,8 +486,13 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x(AL A, const float* __restrict
   };
   prep_rows(tl);
   auto fetch = [&](int k0) {
+    am = 0;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) ra[j] = A.load4(ah[j], k0 + 4 * aq);
+    for (int j = 0; j < 4; ++j) {
+      bool ok;
+      ra[j] = ld4(A, ah[j], k0 + 4 * aq, ok);
+      am |= ok ? 1u << j : 0u;
+    }
 #pragma unroll
     for (int j = 0; j < NRB; ++j) {
       const int i = tid + 256 * j, r = i / (BN / 4), c4 = i % (BN / 4);
@@ -455,7 +504,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x(AL A, const float* __restrict
     for (int j = 0; j < 4; ++j) {
       const int m = arow + 32 * j;
       uint2 o[3];
-      gsplit4(ra[j], o);
+      gsplit4(zero_unless(ra[j], (am >> j) & 1u), o);
       const int off = m * G_BK + 8 * ((aq >> 1) ^ ((m & 8) >> 2)) + 4 * (aq & 1);
 #pragma unroll
       for (int p = 0; p < 3; ++p) *reinterpret_cast<uint2*>(As + p * APL + off) = o[p];
@@ -500,10 +549,12 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x(AL A, const float* __restrict
     first = false;
     stash(kc & 1);
     __syncthreads();
-    {  // one fetch site: the next chunk of this tile, or the first of the next tile
+    {  // one fetch site: the next chunk of this tile, or the first of the next tile (after
+       // the last tile: a dummy re-fetch of this tile's first chunk, never staged -- the
+       // fetch is unconditional, so no merge of old and new registers waits for the loads)
       const bool last = kc + 1 == nkc;
       if (last && tn < ntl) prep_rows(tn);
-      if (!last || tn < ntl) fetch(last ? 0 : (kc + 1) * G_BK);
+      fetch(last ? 0 : (kc + 1) * G_BK);
     }
     bf16x8g a[2][3];
 #pragma unroll
@@ -734,14 +785,20 @@ __global__ __launch_bounds__(256, 2) void k_atb_x(XL X, YL Y, float* __restrict_
   float4 cs = make_float4(0.f, 0.f, 0.f, 0.f);  // columns n0 + 4 (tid & 15) .. + 3
   const int sq = tid & 15, sr = tid >> 4;      // staging: col quad, row (+ 16 j)
   float4 xr[4], yr[4];
+  unsigned xm = 0, ym = 0;  // validity bits of xr / yr (zeroed at the stash)
   const int64_t mb = (int64_t)split * rps, me = min(M, mb + rps);
   auto fetch = [&](int64_t m0) {
+    xm = ym = 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int64_t m = m0 + sr + 16 * j;
       const bool ok = m < me;
-      xr[j] = ok ? X.load4(X.prep(m), k10 + 4 * sq) : make_float4(0.f, 0.f, 0.f, 0.f);
-      yr[j] = ok ? Y.load4(Y.prep(m), n0 + 4 * sq) : make_float4(0.f, 0.f, 0.f, 0.f);
+      const int64_t mm = ok ? m : mb;  // (a row of this split: prep in range)
+      bool ox, oy;
+      xr[j] = ld4(X, X.prep(mm), k10 + 4 * sq, ox);
+      yr[j] = ld4(Y, Y.prep(mm), n0 + 4 * sq, oy);
+      xm |= (ok && ox) ? 1u << j : 0u;
+      ym |= (ok && oy) ? 1u << j : 0u;
     }
   };
   auto stash = [&](bool neg) {
@@ -750,10 +807,10 @@ __global__ __launch_bounds__(256, 2) void k_atb_x(XL X, YL Y, float* __restrict_
       const int m = sr + 16 * j;
       const int off = m * 64 + 16 * ((sq >> 2) ^ gx_bsw<64>(m)) + 4 * (sq & 3);
       uint2 o[3];
-      gsplit4(xr[j], o);
+      gsplit4(zero_unless(xr[j], (xm >> j) & 1u), o);
 #pragma unroll
       for (int p = 0; p < 3; ++p) *reinterpret_cast<uint2*>(Xs + p * PL + off) = o[p];
-      float4 y = yr[j];
+      float4 y = zero_unless(yr[j], (ym >> j) & 1u);
       if (do_cs) { cs.x += y.x; cs.y += y.y; cs.z += y.z; cs.w += y.w; }
       if (neg) y = make_float4(-y.x, -y.y, -y.z, -y.w);
       gsplit4(y, o);
@@ -784,7 +841,7 @@ __global__ __launch_bounds__(256, 2) void k_atb_x(XL X, YL Y, float* __restrict_
     }
     stash(kc & 1);
     __syncthreads();
-    if (m0 + T_BM < me) fetch(m0 + T_BM);
+    fetch(m0 + T_BM);  // (unconditional: past the split's rows every quad is masked)
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       bf16x8g a[2][3], b[2][3];
