@@ -458,27 +458,28 @@ __global__ __launch_bounds__(GT) void k_gates_bwd(GateParams gp, GateSaved sv,
   }
   __syncthreads();
   // ---- spectral SE: v = u * sg2[d] ----
-  if (gp.specse) {
+  // T[d] = sum_c (e[c] R1(c,d) + c0[c] Z(c,d)) serves both gates: the spectral SE's
+  // gradient, and the FourierGate's sum_c (a R1 + bb Z) with a = e[c] sg2[d],
+  // bb = c0[c] sg2[d] + ds2[d] / (C HW), which is sg2[d] T[d] + ds2[d] s1[d] because
+  // sum_c Z(c,d) = C HW s1[d] (the forward's mean over (c, hw)) -- one pass over the
+  // [C][D] inputs instead of two
+  if (gp.specse || gp.mask) {
     rowsum(D, C, [&](int d, int c) {
       return (double)m.e[c] * R1(c, d) + (double)m.c0[c] * Zf(c, d);
     }, m.part, 1.0, m.tmp);
-    for (int d = threadIdx.x; d < D; d += blockDim.x)
-      m.ds2[d] = m.sg2[d] * (1.f - m.sg2[d]) * m.g1[d] * (float)m.tmp[d];
-  } else {
-    for (int d = threadIdx.x; d < D; d += blockDim.x) m.ds2[d] = 0.f;
   }
+  for (int d = threadIdx.x; d < D; d += blockDim.x)
+    m.ds2[d] = gp.specse ? m.sg2[d] * (1.f - m.sg2[d]) * m.g1[d] * (float)m.tmp[d] : 0.f;
   __syncthreads();
   const float invCHW = 1.f / ((float)C * (float)HW);
   // du = dout*a + bb, a = e[c]*sg2[d], bb = c0[c]*sg2[d] + ds2[d]/(C*HW)
   // ---- FourierGate: u = z * g1[d] ----
   if (gp.mask) {
-    rowsum(D, C, [&](int d, int c) {
-      const float a = m.e[c] * m.sg2[d];
-      const float bb = m.c0[c] * m.sg2[d] + m.ds2[d] * invCHW;
-      return (double)a * R1(c, d) + (double)bb * Zf(c, d);
-    }, m.part, 1.0, m.tmp);
-    for (int d = threadIdx.x; d < D; d += blockDim.x)
-      m.dw[d] = (float)m.tmp[d] * m.g1[d] * (1.f - m.g1[d]);
+    const float* s1f = sv.s1 + b * D;
+    for (int d = threadIdx.x; d < D; d += blockDim.x) {
+      const double t = (double)m.sg2[d] * m.tmp[d] + (double)m.ds2[d] * s1f[d];
+      m.dw[d] = (float)t * m.g1[d] * (1.f - m.g1[d]);
+    }
     __syncthreads();
     const float* s1 = sv.s1 + b * D;
     rowsum(L, D, [&](int k, int d) { return (double)s1[d] * m.twc[(k * d) % D]; }, m.part, 1.0, m.Sre);

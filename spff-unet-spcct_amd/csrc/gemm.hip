@@ -118,6 +118,9 @@ struct LoadRowsAct {
   int D, HW, dsh, hwsh; float neg;
   __device__ int64_t prep(int64_t m) const { return m < M ? m : -1; }
   __device__ float4 load4(int64_t h, int k) const;
+  // (no branches: every quad of every row of a fetch can be in flight at once)
+  static constexpr bool kRaw = true;
+  __device__ float4 raw4(int64_t h, int k, bool& ok) const;
 };
 // high-res voxel of low-res voxel m's sub-lattice ij = 0: nsub = 4 for the
 // (1,2,2) up-convs of SPFF (ij = kh*2 + kw, depth kept), nsub = 8 for the
@@ -148,6 +151,32 @@ __device__ float4 LoadRowsAct::load4(int64_t h, int k) const {
     pp = *reinterpret_cast<const float4*>(PT + (int64_t)bd * ld + k);
     qq = *reinterpret_cast<const float4*>(QT + (int64_t)bd * ld + k);
   }
+  auto f = [&](float y, float a_, float e_, float p_, float q_) {
+    const float t = y * a_ + e_;
+    return (t > 0.f ? t : neg * t) * p_ + q_;
+  };
+  return make_float4(f(v.x, a.x, e.x, pp.x, qq.x), f(v.y, a.y, e.y, pp.y, qq.y),
+                     f(v.z, a.z, e.z, pp.z, qq.z), f(v.w, a.w, e.w, pp.w, qq.w));
+}
+__device__ float4 LoadRowsAct::raw4(int64_t h, int k, bool& ok) const {
+  ok = h >= 0 && k < kmax;
+  const int64_t hh = ok ? h : 0;
+  const int kk = ok ? k : 0;
+  const float4 v = *reinterpret_cast<const float4*>(p + hh * ld + kk);
+  uint32_t bd, r, b, d;
+  udivmod_s((uint32_t)hh, (uint32_t)HW, hwsh, bd, r);
+  udivmod_s(bd, (uint32_t)D, dsh, b, d);
+  const float4 a = *reinterpret_cast<const float4*>(al + (int64_t)b * ld + kk);
+  const float4 e = *reinterpret_cast<const float4*>(de + (int64_t)b * ld + kk);
+  const float* pt = PT ? PT : al;  // (without PT: loaded, then replaced by 1 / 0 below)
+  const float* qt = PT ? QT : de;
+  const int64_t po = PT ? (int64_t)bd * ld + kk : (int64_t)b * ld + kk;
+  const float4 pl = *reinterpret_cast<const float4*>(pt + po);
+  const float4 ql = *reinterpret_cast<const float4*>(qt + po);
+  // (blended, not branched: a branch would merge loaded and constant values and wait there)
+  const float ps = PT ? 1.f : 0.f, pn = 1.f - ps;
+  const float4 pp = make_float4(pl.x * ps + pn, pl.y * ps + pn, pl.z * ps + pn, pl.w * ps + pn);
+  const float4 qq = make_float4(ql.x * ps, ql.y * ps, ql.z * ps, ql.w * ps);
   auto f = [&](float y, float a_, float e_, float p_, float q_) {
     const float t = y * a_ + e_;
     return (t > 0.f ? t : neg * t) * p_ + q_;
