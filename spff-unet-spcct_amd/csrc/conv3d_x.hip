@@ -40,6 +40,7 @@
 #include "spff_internal.h"
 #include "bf16split.h"
 
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <type_traits>
@@ -184,15 +185,12 @@ __host__ __device__ constexpr XQuads<KD> x_quads() {
 // dgrad: k = co, n = ci with the tap flipped.  Taps >= T and padded k/n are zero.
 // Odd chunks kc are stored NEGATED (sign-alternating accumulation, see below).
 template <int NS>
-__global__ void k_conv_pack_x(const float* __restrict__ w, uint4* __restrict__ wp, int Cout,
-                              int Cin, int T, int T2, int nkc, int npad, int BN, int dgrad,
-                              const unsigned* __restrict__ wmx) {
+__device__ __forceinline__ void pack_units(const float* __restrict__ w, uint4* __restrict__ wp,
+                                           int Cout, int Cin, int T, int T2, int nkc, int npad,
+                                           int BN, int dgrad, float sw, int64_t i0, int64_t step) {
   constexpr int NP = nplanes(NS);
   const int64_t total = (int64_t)(npad / BN) * nkc * T2 * BN;
-  // NS_F16: the weights scaled by 2^e (*wmx: max |w|), fp16 planes
-  const float sw = NS == NS_F16 ? exp2i(f16_scale_exp(*wmx)) : 1.f;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t i = i0; i < total; i += step) {
     const int co = (int)(i % BN);
     const int tap = (int)((i / BN) % T2);
     const int kc = (int)((i / ((int64_t)BN * T2)) % nkc);
@@ -231,6 +229,26 @@ __global__ void k_conv_pack_x(const float* __restrict__ w, uint4* __restrict__ w
       wp[base + (int64_t)p * T2 * BN] = u;
     }
   }
+}
+template <int NS>
+__global__ void k_conv_pack_x(const float* __restrict__ w, uint4* __restrict__ wp, int Cout,
+                              int Cin, int T, int T2, int nkc, int npad, int BN, int dgrad,
+                              const unsigned* __restrict__ wmx) {
+  // NS_F16: the weights scaled by 2^e (*wmx: max |w|), fp16 planes
+  const float sw = NS == NS_F16 ? exp2i(f16_scale_exp(*wmx)) : 1.f;
+  pack_units<NS>(w, wp, Cout, Cin, T, T2, nkc, npad, BN, dgrad, sw,
+                 blockIdx.x * (int64_t)blockDim.x + threadIdx.x, (int64_t)gridDim.x * blockDim.x);
+}
+// Every conv image of a plan in one launch (conv3d_pack_many): the job table travels as
+// the kernel argument; job j owns blocks [blk0, blk0 + nblk).
+template <int NS>
+__global__ __launch_bounds__(256) void k_conv_pack_many(PackJobs J) {
+  int j = 0;
+  while (j + 1 < J.n && (int)blockIdx.x >= J.j[j + 1].blk0) ++j;
+  const PackJob& q = J.j[j];
+  const float sw = NS == NS_F16 ? exp2i(f16_scale_exp(*q.wmx)) : 1.f;
+  pack_units<NS>(q.w, q.wp, q.Cout, q.Cin, q.T, q.T2, q.nkc, q.npad, q.BN, q.dgrad, sw,
+                 (int64_t)((int)blockIdx.x - q.blk0) * 256 + threadIdx.x, (int64_t)q.nblk * 256);
 }
 
 // ------------------------------------------------------------ fwd / dgrad --
@@ -1293,6 +1311,98 @@ hipError_t conv3d_pack(const float* w, void* wpack, Vol vol, int KD, int Cin_w, 
   }
   return conv_pack_weights(w, static_cast<float*>(wpack), Cout_w, Cin_w, KD, rup(d.K, 8),
                            rup(d.N, conv3d_bn(d.N)), dgrad, s);
+}
+
+// ------------------------------------------------- batched weight preparation --
+// job j of the table owns blocks [blk0, blk0 + nblk); kinds: 0 max |a| over n elements
+// (integer atomicMax into the zeroed slot, like k_absmax_f32), 1 act_bound's parameter
+// bound 2 (max|gamma| sq + max|beta|) + 1e-30 (k_act_bound's value; max is exact in any order)
+__global__ __launch_bounds__(256) void k_prep_many(PrepJobs J) {
+  int j = 0;
+  while (j + 1 < J.n && (int)blockIdx.x >= J.j[j + 1].blk0) ++j;
+  const PrepJob& q = J.j[j];
+  if (q.kind == 0) {
+    float m = 0.f;
+    const int64_t st = (int64_t)q.nblk * 256;
+    for (int64_t i = (int64_t)((int)blockIdx.x - q.blk0) * 256 + threadIdx.x; i < q.n; i += st)
+      m = fmaxf(m, fabsf(q.a[i]));
+    block_amax(m, q.slot);
+    return;
+  }
+  __shared__ float wg[4], wb[4];
+  float mg = 0.f, mb = 0.f;
+  for (int c = threadIdx.x; c < (int)q.n; c += 256) {
+    mg = fmaxf(mg, fabsf(q.a[c]));
+    mb = fmaxf(mb, fabsf(q.b[c]));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    mg = fmaxf(mg, __shfl_xor(mg, o));
+    mb = fmaxf(mb, __shfl_xor(mb, o));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    wg[threadIdx.x >> 6] = mg;
+    wb[threadIdx.x >> 6] = mb;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    mg = fmaxf(fmaxf(wg[0], wg[1]), fmaxf(wg[2], wg[3]));
+    mb = fmaxf(fmaxf(wb[0], wb[1]), fmaxf(wb[2], wb[3]));
+    *q.slot = __float_as_uint(2.f * (mg * q.sq + mb) + 1e-30f);
+  }
+}
+// (SPFF_PACK_BATCH=0, diagnostics / A/B only: one max + one pack launch per conv again)
+bool conv3d_packs_batched(int math) {
+  static const bool off = [] {
+    const char* e = getenv("SPFF_PACK_BATCH");
+    return e && e[0] == '0';
+  }();
+  return !off && use_split(Vol{}, math, false) && use_split(Vol{}, math, true);
+}
+bool prep_absmax(PrepJobs* J, const float* p, int64_t n, unsigned* slot) {
+  if (J->n == 32 || n <= 0) return false;
+  const int nb = (int)std::min<int64_t>(64, std::max<int64_t>(1, (n + 8191) / 8192));
+  J->j[J->n++] = PrepJob{p, nullptr, slot, n, 0.f, 0, J->nblk, nb};
+  J->nblk += nb;
+  return true;
+}
+bool prep_act_bound(PrepJobs* J, const float* gamma, const float* beta, int C, double N,
+                    unsigned* slot) {
+  if (J->n == 32 || C <= 0) return false;
+  const float sq = (float)std::sqrt(std::max(N - 1.0, 1.0));
+  J->j[J->n++] = PrepJob{gamma, beta, slot, C, sq, 1, J->nblk, 1};
+  J->nblk += 1;
+  return true;
+}
+hipError_t prep_run(const PrepJobs& J, hipStream_t s) {
+  if (J.n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_prep_many, dim3(J.nblk), dim3(256), 0, s, J);
+  return hipGetLastError();
+}
+bool conv3d_pack_job(PackJobs* J, const float* w, void* wpack, int KD, int Cin_w, int Cout_w,
+                     bool dgrad, const unsigned* wmax) {
+  if (J->n == 40) return false;
+  const XDims d = xdims(KD, Cin_w, Cout_w, dgrad);
+  const int64_t total = (int64_t)d.nkc * d.T2 * d.npad;
+  const int nb = (int)std::min<int64_t>(64, (total + 255) / 256);
+  J->j[J->n++] = PackJob{w, static_cast<uint4*>(wpack), wmax, Cout_w, Cin_w, d.T, d.T2, d.nkc,
+                         d.npad, d.BN, dgrad ? 1 : 0, J->nblk, nb};
+  J->nblk += nb;
+  return true;
+}
+hipError_t conv3d_pack_many(const PackJobs& J, int math, hipStream_t s) {
+  if (!conv3d_packs_batched(math)) return hipErrorInvalidValue;
+  if (J.n == 0) return hipSuccess;
+  if (math == SPFF_MATH_F16X3) {
+    for (int i = 0; i < J.n; ++i)
+      if (!J.j[i].wmx) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_conv_pack_many<NS_F16>, dim3(J.nblk), dim3(256), 0, s, J);
+  } else if (math == SPFF_MATH_BF16X3) {
+    hipLaunchKernelGGL(k_conv_pack_many<2>, dim3(J.nblk), dim3(256), 0, s, J);
+  } else {
+    hipLaunchKernelGGL(k_conv_pack_many<3>, dim3(J.nblk), dim3(256), 0, s, J);
+  }
+  return hipGetLastError();
 }
 
 template <int NS>

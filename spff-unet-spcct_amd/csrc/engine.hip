@@ -101,6 +101,7 @@ struct Blk {
   size_t spec = 0;  // sharded plans: full-depth s1 spectrum [B][L][2] (fp64)
   bool fa = false;  // conv2 reads y1 through the IN affine (a1 never stored)
   bool fout = false;  // out never stored: its GEMM consumers apply it to y2 (ActRows)
+  size_t pk[4] = {0, 0, 0, 0};  // batched conv images: c1 fwd, c2 fwd, c2 dgrad, c1 dgrad
   size_t PT = 0, QT = 0;  // fout + gates: P, Q as [B][D][C]
   bool tail() const { return efilm || fgate || post_se || post_spec; }
 };
@@ -134,6 +135,8 @@ struct spff_plan {
   size_t x_cl = 0, pool[3] = {0, 0, 0}, pidx[3] = {0, 0, 0};
   size_t red_ws = 0, red_out = 0, red_out4 = 0, gscr = 0, Abuf = 0, Bbuf = 0, kk1 = 0, kk2 = 0,
          wg_ws = 0, wt = 0, cst = 0;
+  bool pkb = false;  // conv images packed in one batch at the forward start (b.pk)
+  size_t wcur = 0;   // the image the next conv3d_run reads (b.pk[k] or the scratch wt)
   size_t fsl = 0;  // SPFF_MATH_F16X3 operand maxima, 8 slots per block (f16_slot), then
                    // two per-launch slots of the sharded plans' weight gradients
   size_t G_out = 0, G_dy2 = 0, G_da1 = 0, G_dx = 0, dskip[3] = {0, 0, 0};
@@ -466,7 +469,18 @@ int build_plan(spff_plan* p) {
   p->kk1 = p->alloc((size_t)B * 8 * f * sizeof(float));
   p->kk2 = p->alloc((size_t)B * 8 * f * sizeof(float));
   p->wg_ws = p->alloc(wg);
-  p->wt = p->alloc(wt);
+  p->pkb = conv3d_packs_batched(p->cfg.math);
+  if (p->pkb) {
+    for (int i = 0; i < 7; ++i) {
+      Blk& b = p->blk[i];
+      b.pk[0] = p->alloc(conv_pack_bytes(b.c1, p->KD));
+      b.pk[1] = p->alloc(conv_pack_bytes(b.c2, p->KD));
+      b.pk[2] = p->alloc(conv_pack_bytes(b.c2, p->KD));
+      if (i > 0) b.pk[3] = p->alloc(conv_pack_bytes(b.c1, p->KD));  // enc1's input: no dx
+    }
+  } else {
+    p->wt = p->alloc(wt);
+  }
   p->fsl = p->alloc((F16_SHARD_SLOTS + 2) * sizeof(unsigned));
   p->cst = p->alloc(cst);
   // gradient scratch, sized for level 0 ([V0][f]); a level-l tensor of the path
@@ -616,15 +630,15 @@ int side_stream(spff_plan* p) {
 // exchange, then convolve.  The ranks at both global ends still exchange (their single
 // neighbour), so every rank runs the same collective sequence.
 int conv_h(spff_plan* p, int cls, double flops, double bytes, const Src2& x, const Dst2& y,
-           const Vol& v, int Cin_w, int Cout_w, bool dgrad) {
+           const Vol& v, int Cin_w, int Cout_w, bool dgrad, const unsigned* wmax) {
   const int cin = dgrad ? Cout_w : Cin_w, KD = p->KD, math = p->cfg.math;
   Src2 xr;
   const bool ovl = conv3d_splits_height(v, KD, Cin_w, Cout_w, dgrad, math);
   if (!ovl) {
     CK(hrows_exchange(p, x, v, cin, &xr, p->st));
     PROFB(p, cls, flops, bytes,
-          conv3d_run(xr, p->F(p->wt), y, v, KD, Cin_w, Cout_w, dgrad, math, p->st,
-                     p->F(p->wg_ws), nullptr));
+          conv3d_run(xr, p->F(p->wcur), y, v, KD, Cin_w, Cout_w, dgrad, math, p->st,
+                     p->F(p->wg_ws), nullptr, 0, wmax));
     return SPFF_OK;
   }
   CK(side_stream(p));
@@ -633,12 +647,12 @@ int conv_h(spff_plan* p, int cls, double flops, double bytes, const Src2& x, con
   CK(hrows_exchange(p, x, v, cin, &xr, p->st2));
   HIPCK(hipEventRecord(p->ev_halo, p->st2));
   PROFB(p, cls, flops, bytes,
-        conv3d_run(xr, p->F(p->wt), y, v, KD, Cin_w, Cout_w, dgrad, math, p->st,
-                   p->F(p->wg_ws), nullptr, 3));
+        conv3d_run(xr, p->F(p->wcur), y, v, KD, Cin_w, Cout_w, dgrad, math, p->st,
+                   p->F(p->wg_ws), nullptr, 3, wmax));
   HIPCK(hipStreamWaitEvent(p->st, p->ev_halo, 0));
   PROFB(p, cls, 0.0, 0.0,
-        conv3d_run(xr, p->F(p->wt), y, v, KD, Cin_w, Cout_w, dgrad, math, p->st,
-                   p->F(p->wg_ws), nullptr, 4));
+        conv3d_run(xr, p->F(p->wcur), y, v, KD, Cin_w, Cout_w, dgrad, math, p->st,
+                   p->F(p->wg_ws), nullptr, 4, wmax));
   return SPFF_OK;
 }
 // weight gradient of a 3x3x3 conv (height-sharded: x's stencil rows from the neighbours;
@@ -691,7 +705,7 @@ int halo_begin(spff_plan* p, const float* x, const Vol& v, int C) {
 int conv_halo(spff_plan* p, int cls, double flops, double bytes, const Src2& x, const Dst2& y,
               const Vol& v, int Cin_w, int Cout_w, bool dgrad, float* stats,
               const unsigned* wmax = nullptr) {
-  if (p->hsh) return conv_h(p, cls, flops, bytes, x, y, v, Cin_w, Cout_w, dgrad);
+  if (p->hsh) return conv_h(p, cls, flops, bytes, x, y, v, Cin_w, Cout_w, dgrad, wmax);
   const int KD = p->KD, math = p->cfg.math;
   const bool ovl = v.dh && !stats && conv3d_splits_depth(v, KD, Cin_w, Cout_w, dgrad, math);
   const bool early = p->halo_early && p->halo_early == x.p0 && x.p1 == x.p0;
@@ -702,7 +716,7 @@ int conv_halo(spff_plan* p, int cls, double flops, double bytes, const Src2& x, 
     else
       CK(halo_src(p, x, v));
     PROFB(p, cls, flops, bytes,
-          conv3d_run(x, p->F(p->wt), y, v, KD, Cin_w, Cout_w, dgrad, math, p->st, p->F(p->wg_ws),
+          conv3d_run(x, p->F(p->wcur), y, v, KD, Cin_w, Cout_w, dgrad, math, p->st, p->F(p->wg_ws),
                      stats, 0, wmax));
     return SPFF_OK;
   }
@@ -714,12 +728,12 @@ int conv_halo(spff_plan* p, int cls, double flops, double bytes, const Src2& x, 
     HIPCK(hipEventRecord(p->ev_halo, p->st2));
   }
   PROFB(p, cls, flops, bytes,
-        conv3d_run(x, p->F(p->wt), y, v, KD, Cin_w, Cout_w, dgrad, math, p->st, p->F(p->wg_ws),
-                   nullptr, 1));
+        conv3d_run(x, p->F(p->wcur), y, v, KD, Cin_w, Cout_w, dgrad, math, p->st, p->F(p->wg_ws),
+                   nullptr, 1, wmax));
   HIPCK(hipStreamWaitEvent(p->st, p->ev_halo, 0));
   PROFB(p, cls, 0.0, 0.0,
-        conv3d_run(x, p->F(p->wt), y, v, KD, Cin_w, Cout_w, dgrad, math, p->st, p->F(p->wg_ws),
-                   nullptr, 2));
+        conv3d_run(x, p->F(p->wcur), y, v, KD, Cin_w, Cout_w, dgrad, math, p->st, p->F(p->wg_ws),
+                   nullptr, 2, wmax));
   return SPFF_OK;
 }
 
@@ -813,10 +827,56 @@ int f16_in_max(spff_plan* p, const Blk& b, const Src2& in, const Vol& v) {
   PROFB(p, 7, 0.0, 4.0 * (double)nvox(v) * b.Cin, absmax_src(in, v, b.Cin, false, sl, p->st));
   return SPFF_OK;
 }
+// max |w| of conv 1 / 2 of block b for the conv kernels (SPFF_MATH_F16X3): batched plans
+// fill slot F16_W1 / F16_W2 whatever the sharding (weights are replicated); the others
+// pass f16_slot (null on sharded plans: conv3d_pack fills the image's own slot)
+const unsigned* w_slot(const spff_plan* p, const Blk& b, int k) {
+  if (p->cfg.math != SPFF_MATH_F16X3) return nullptr;
+  if (!p->pkb) return f16_slot(p, b, k);
+  return reinterpret_cast<const unsigned*>(p->ws + p->fsl) + 8 * (int)(&b - p->blk) + k;
+}
+// the parameter-derived operand data of a step, at the forward start.  Batched plans: the
+// maxima and bounds in one launch (prep_run), then every conv image -- forward and input
+// gradient, all 27 -- in one more (conv3d_pack_many); the weights do not change between
+// the forward and the backward of a step (the up-conv / head images are packed up front
+// the same way).  Otherwise per-tensor launches and conv3d_pack before each conv.
 int f16_param_slots(spff_plan* p) {
+  const int T = 9 * p->KD;
+  const int math = p->cfg.math;
+  if (p->pkb) {
+    PrepJobs pj;
+    PackJobs kj;
+    double bytes = 0.0;
+    if (math == SPFF_MATH_F16X3)
+      HIPCK(hipMemsetAsync(p->ws + p->fsl, 0, 7 * 8 * sizeof(unsigned), p->st));
+    for (int i = 0; i < 7; ++i) {
+      Blk& b = p->blk[i];
+      const Vol& v = p->vol[b.lvl];
+      unsigned* w1 = const_cast<unsigned*>(w_slot(p, b, F16_W1));
+      unsigned* w2 = const_cast<unsigned*>(w_slot(p, b, F16_W2));
+      bool ok = true;
+      if (math == SPFF_MATH_F16X3) {
+        ok = ok && prep_absmax(&pj, p->P(b.c1.w), (int64_t)b.C * b.Cin * T, w1);
+        ok = ok && prep_absmax(&pj, p->P(b.c2.w), (int64_t)b.C * b.C * T, w2);
+        bytes += 4.0 * b.C * (b.Cin + b.C) * T;
+        if (unsigned* a1 = f16_slot(p, b, F16_A1)) {
+          ok = ok && prep_act_bound(&pj, p->P(b.g1), p->P(b.b1), b.C, (double)v.D * v.H * v.W, a1);
+          bytes += 8.0 * b.C;
+        }
+      }
+      ok = ok && conv3d_pack_job(&kj, p->P(b.c1.w), p->F(b.pk[0]), p->KD, b.Cin, b.C, false, w1);
+      ok = ok && conv3d_pack_job(&kj, p->P(b.c2.w), p->F(b.pk[1]), p->KD, b.C, b.C, false, w2);
+      ok = ok && conv3d_pack_job(&kj, p->P(b.c2.w), p->F(b.pk[2]), p->KD, b.C, b.C, true, w2);
+      if (b.pk[3])
+        ok = ok && conv3d_pack_job(&kj, p->P(b.c1.w), p->F(b.pk[3]), p->KD, b.Cin, b.C, true, w1);
+      if (!ok) return fail(SPFF_EINVAL, "weight preparation table overflow");
+    }
+    if (pj.n) PROFB(p, 7, 0.0, bytes, prep_run(pj, p->st));
+    HIPCK(conv3d_pack_many(kj, math, p->st));
+    return SPFF_OK;
+  }
   if (!f16_slot(p, p->blk[0], 0)) return SPFF_OK;
   HIPCK(hipMemsetAsync(p->ws + p->fsl, 0, 7 * 8 * sizeof(unsigned), p->st));
-  const int T = 9 * p->KD;
   for (int i = 0; i < 7; ++i) {
     const Blk& b = p->blk[i];
     const Vol& v = p->vol[b.lvl];
@@ -829,6 +889,19 @@ int f16_param_slots(spff_plan* p) {
   }
   return SPFF_OK;
 }
+// the image of conv k of block b (0: c1 fwd, 1: c2 fwd, 2: c2 dgrad, 3: c1 dgrad) for the
+// next conv3d_run: the batched one, else packed now into the scratch image
+int conv_image(spff_plan* p, const Blk& b, int k, const Vol& v) {
+  if (p->pkb) {
+    p->wcur = b.pk[k];
+    return p->wcur ? SPFF_OK : fail(SPFF_EINVAL, "no batched image for this conv");
+  }
+  const bool c1 = k == 0 || k == 3;
+  HIPCK(conv3d_pack(p->P(c1 ? b.c1.w : b.c2.w), p->F(p->wt), v, p->KD, c1 ? b.Cin : b.C, b.C,
+                    k >= 2, p->cfg.math, p->st, f16_slot(p, b, c1 ? F16_W1 : F16_W2)));
+  p->wcur = p->wt;
+  return SPFF_OK;
+}
 
 // pool >= 0: encoder block b's output also feeds MaxPool3d((1,2,2)) into p->pool[pool]
 // (the output apply and the pool run as one pass where H and W are even)
@@ -836,15 +909,14 @@ int fwd_block(spff_plan* p, Blk& b, const Src2& in, int pool = -1) {
   const Vol& v = p->vol[b.lvl];
   const int C = b.C, KD = p->KD;
   const int math = p->cfg.math;
-  HIPCK(conv3d_pack(p->P(b.c1.w), p->F(p->wt), v, KD, b.Cin, C, false, math, p->st,
-                    f16_slot(p, b, F16_W1)));
+  CK(conv_image(p, b, 0, v));
   const double V = (double)nvox(v), T = 9.0 * KD;
   CK(f16_in_max(p, b, in, v));
   // InstanceNorm statistics fused into the conv epilogue where the split kernel
   // runs unsharded without split-K; otherwise the two slab_reduce passes
   const bool fuse1 = !p->co.on() && conv3d_fuses_stats(v, KD, b.Cin, C, math);
   CK(conv_halo(p, 0, 2.0 * V * b.Cin * C * T, cbytes(V, b.Cin, C, T), in, dst1(p->F(b.y1), C), v,
-               b.Cin, C, false, fuse1 ? p->F(p->cst) : nullptr, f16_slot(p, b, F16_W1)));
+               b.Cin, C, false, fuse1 ? p->F(p->cst) : nullptr, w_slot(p, b, F16_W1)));
   if (fuse1)
     HIPCK(conv3d_in_stats_fin(p->F(p->cst), v, KD, b.Cin, C, math, p->P(b.g1), p->P(b.b1),
                               p->F(b.mean1), p->F(b.rstd1), p->F(b.al1), p->F(b.de1), p->st));
@@ -854,12 +926,11 @@ int fwd_block(spff_plan* p, Blk& b, const Src2& in, int pool = -1) {
     PROFB(p, 5, 0.0, 8.0 * (double)nvox(v) * C,
           act_apply(p->F(b.y1), p->F(b.a1), p->F(b.al1), p->F(b.de1), nullptr, nullptr, v, C,
                     p->st));
-  HIPCK(conv3d_pack(p->P(b.c2.w), p->F(p->wt), v, KD, C, C, false, math, p->st,
-                    f16_slot(p, b, F16_W2)));
+  CK(conv_image(p, b, 1, v));
   const Src2 in2 = act_src(p, b);
   const bool fuse2 = !p->co.on() && conv3d_fuses_stats(v, KD, C, C, math);
   CK(conv_halo(p, 0, 2.0 * V * C * C * T, cbytes(V, C, C, T), in2, dst1(p->F(b.y2), C), v, C, C,
-               false, fuse2 ? p->F(p->cst) : nullptr, f16_slot(p, b, F16_W2)));
+               false, fuse2 ? p->F(p->cst) : nullptr, w_slot(p, b, F16_W2)));
   if (fuse2)
     HIPCK(conv3d_in_stats_fin(p->F(p->cst), v, KD, C, C, math, p->P(b.g2), p->P(b.b2), p->F(b.mean2),
                               p->F(b.rstd2), p->F(b.al2), p->F(b.de2), p->st));
@@ -1055,10 +1126,9 @@ int bwd_block(spff_plan* p, Blk& b, const float* dout, const Dst2* dx, const Src
   CK(conv_wgrad(p, 2.0 * V * C * C * T, cbytes(V, C, C, T), a1, dy2, p->DP(b.c2.w), v, C, C,
                 f16_slot(p, b, F16_A1), f16_slot(p, b, F16_DY2)));
   const int math = p->cfg.math;
-  HIPCK(conv3d_pack(p->P(b.c2.w), p->F(p->wt), v, KD, C, C, true, math, p->st,
-                    f16_slot(p, b, F16_W2)));
+  CK(conv_image(p, b, 2, v));
   CK(conv_halo(p, 1, 2.0 * V * C * C * T, cbytes(V, C, C, T), src1(dy2, C), dst1(da1, C), v, C, C,
-               true, nullptr, f16_slot(p, b, F16_W2)));
+               true, nullptr, w_slot(p, b, F16_W2)));
   {
     RedArgs a{};
     a.y = p->F(b.y1); a.g = da1; a.mean = p->F(b.mean1); a.rstd = p->F(b.rstd1);
@@ -1076,10 +1146,9 @@ int bwd_block(spff_plan* p, Blk& b, const float* dout, const Dst2* dx, const Src
   CK(conv_wgrad(p, 2.0 * V * b.Cin * C * T, cbytes(V, b.Cin, C, T), in, da1, p->DP(b.c1.w), v,
                 b.Cin, C, f16_in_slot(p, b), f16_slot(p, b, F16_DA1)));
   if (dx) {
-    HIPCK(conv3d_pack(p->P(b.c1.w), p->F(p->wt), v, KD, b.Cin, C, true, math, p->st,
-                      f16_slot(p, b, F16_W1)));
+    CK(conv_image(p, b, 3, v));
     CK(conv_halo(p, 1, 2.0 * V * b.Cin * C * T, cbytes(V, b.Cin, C, T), src1(da1, C), *dx, v,
-                 b.Cin, C, true, nullptr, f16_slot(p, b, F16_W1)));
+                 b.Cin, C, true, nullptr, w_slot(p, b, F16_W1)));
   }
   return SPFF_OK;
 }

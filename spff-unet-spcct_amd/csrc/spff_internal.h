@@ -101,6 +101,41 @@ size_t conv3d_pack_bytes(int KD, int Cin_w, int Cout_w);
 // (SPFF_MATH_F16X3: wmax = a precomputed max |w| slot, else computed into the image's tail)
 hipError_t conv3d_pack(const float* w, void* wpack, Vol vol, int KD, int Cin_w, int Cout_w,
                        bool dgrad, int math, hipStream_t s, const unsigned* wmax = nullptr);
+// A plan's weight preparation as one launch pair at the forward start, instead of one
+// max + one pack launch per conv: PrepJobs (max |w| of each weight tensor, the a1 bounds
+// act_bound computes) then PackJobs (every conv image, fwd and dgrad).  The tables travel
+// as kernel arguments.  conv3d_packs_batched: the math packs split images (else
+// conv3d_pack per conv).
+struct PrepJob {
+  const float* a;     // absmax: the tensor; act_bound: gamma
+  const float* b;     // act_bound: beta
+  unsigned* slot;     // zeroed by the caller (absmax: atomicMax; act_bound: stored)
+  int64_t n;          // absmax: elements; act_bound: channels
+  float sq;           // act_bound: sqrt(max(N - 1, 1))
+  int kind, blk0, nblk;  // kind 0 absmax, 1 act_bound
+};
+struct PrepJobs {
+  int n = 0, nblk = 0;
+  PrepJob j[32];
+};
+struct PackJob {
+  const float* w;
+  uint4* wp;
+  const unsigned* wmx;  // SPFF_MATH_F16X3: the filled max |w| slot
+  int Cout, Cin, T, T2, nkc, npad, BN, dgrad, blk0, nblk;
+};
+struct PackJobs {
+  int n = 0, nblk = 0;
+  PackJob j[40];  // 2568 B of kernel argument
+};
+bool conv3d_packs_batched(int math);
+bool prep_absmax(PrepJobs* J, const float* p, int64_t n, unsigned* slot);
+bool prep_act_bound(PrepJobs* J, const float* gamma, const float* beta, int C, double N,
+                    unsigned* slot);
+hipError_t prep_run(const PrepJobs& J, hipStream_t s);
+bool conv3d_pack_job(PackJobs* J, const float* w, void* wpack, int KD, int Cin_w, int Cout_w,
+                     bool dgrad, const unsigned* wmax);
+hipError_t conv3d_pack_many(const PackJobs& J, int math, hipStream_t s);
 // ws (optional, >= conv3d_splitk_bytes): scratch for split-K partial sums on
 // launches that would not fill the chip; null = no split
 // stats (optional, forward only, when conv3d_fuses_stats): the conv's epilogue also

@@ -70,6 +70,7 @@ struct RB {
   Lin c3;
   size_t y1, a1, y2, y3, out;
   size_t st[3][4];  // (mean, rstd, al, de) of the IN after conv1, conv2, conv3
+  size_t pk[4] = {0, 0, 0, 0};  // batched conv images: w1 fwd, w2 fwd, w2 dgrad, w1 dgrad
 };
 
 struct Up {
@@ -105,6 +106,8 @@ struct spff_swin {
   size_t x_cl = 0, t[5] = {}, hs[5] = {}, hmu[5] = {}, hrs[5] = {};
   size_t ones = 0, zeros = 0, dummy = 0, red_ws = 0, red_out = 0, kk1 = 0, kk2 = 0, wg_ws = 0,
          wt = 0, cst = 0;
+  bool pkb = false;  // conv images packed in one batch at the forward start (rb[i].pk)
+  size_t wsl = 0;    // SPFF_MATH_F16X3 max |w| per conv, [NRB][2] (batched plans)
   // backward scratch
   size_t G_out = 0, G_dz = 0, G_dy2 = 0, G_da1 = 0, G_up = 0;
   size_t d_enc[4] = {}, d_hs[5] = {}, dT[5] = {};
@@ -329,7 +332,19 @@ int build(spff_swin* p) {
   p->kk1 = p->alloc(fbytes((int64_t)B * maxC));
   p->kk2 = p->alloc(fbytes((int64_t)B * maxC));
   p->wg_ws = p->alloc(wg);
-  p->wt = p->alloc(wt);
+  p->pkb = conv3d_packs_batched(c.math);
+  if (p->pkb) {
+    for (int i = 0; i < NRB; ++i) {
+      RB& r = R[i];
+      r.pk[0] = p->alloc(conv3d_pack_bytes(3, r.Cin, r.C));
+      r.pk[1] = p->alloc(conv3d_pack_bytes(3, r.C, r.C));
+      r.pk[2] = p->alloc(conv3d_pack_bytes(3, r.C, r.C));
+      if (i > 0) r.pk[3] = p->alloc(conv3d_pack_bytes(3, r.Cin, r.C));  // enc0's input: no dx
+    }
+    p->wsl = p->alloc(NRB * 2 * sizeof(unsigned));
+  } else {
+    p->wt = p->alloc(wt);
+  }
   p->cst = p->alloc(cst);
   p->G_out = p->alloc(gmax);
   p->G_dz = p->alloc(gmax);
@@ -353,14 +368,68 @@ int in_stats(spff_swin* p, const Vol& v, int C, size_t y, const size_t* st4) {
   return SPFF_OK;
 }
 
-// 3x3x3 conv + (fused where the kernel allows) IN statistics
-int conv_in(spff_swin* p, const Src2& in, int64_t w, const Vol& v, int Cin, int C, size_t y,
-            const size_t* st4) {
+// batched plans: every conv's max |w| (f16x3) in one launch, then all 39 conv images
+// (forward and input gradient) in one more, at the forward start -- the weights do not
+// change between a step's forward and backward (the up-conv / linear images are packed up
+// front the same way).  Otherwise conv3d_pack before each conv (max + pack launches).
+int prep_weights(spff_swin* p) {
+  if (!p->pkb) return SPFF_OK;
   const int math = p->cfg.math;
-  SHIPCK(conv3d_pack(p->P(w), p->F(p->wt), v, 3, Cin, C, false, math, p->st));
+  const bool f16 = math == SPFF_MATH_F16X3;
+  unsigned* sl = reinterpret_cast<unsigned*>(p->ws + p->wsl);
+  PrepJobs pj;
+  PackJobs kj;
+  if (f16) SHIPCK(hipMemsetAsync(sl, 0, NRB * 2 * sizeof(unsigned), p->st));
+  for (int i = 0; i < NRB; ++i) {
+    RB& r = p->rb[i];
+    unsigned* w1 = f16 ? sl + 2 * i : nullptr;
+    unsigned* w2 = f16 ? sl + 2 * i + 1 : nullptr;
+    bool ok = true;
+    if (f16) {
+      ok = ok && prep_absmax(&pj, p->P(r.w1), (int64_t)r.C * r.Cin * 27, w1);
+      ok = ok && prep_absmax(&pj, p->P(r.w2), (int64_t)r.C * r.C * 27, w2);
+    }
+    ok = ok && conv3d_pack_job(&kj, p->P(r.w1), p->F(r.pk[0]), 3, r.Cin, r.C, false, w1);
+    ok = ok && conv3d_pack_job(&kj, p->P(r.w2), p->F(r.pk[1]), 3, r.C, r.C, false, w2);
+    ok = ok && conv3d_pack_job(&kj, p->P(r.w2), p->F(r.pk[2]), 3, r.C, r.C, true, w2);
+    if (r.pk[3]) ok = ok && conv3d_pack_job(&kj, p->P(r.w1), p->F(r.pk[3]), 3, r.Cin, r.C, true, w1);
+    if (!ok) return sfail(SPFF_EINVAL, "weight preparation table overflow");
+  }
+  SHIPCK(prep_run(pj, p->st));
+  SHIPCK(conv3d_pack_many(kj, math, p->st));
+  return SPFF_OK;
+}
+// conv k of residual block r (0: w1 fwd, 1: w2 fwd, 2: w2 dgrad, 3: w1 dgrad): its image
+// (the batched one, else packed now into the scratch image) and its max |w| slot
+int conv_image(spff_swin* p, const RB& r, int k, const Vol& v, const float** img,
+               const unsigned** wmax) {
+  const bool c1 = k == 0 || k == 3;
+  const int ri = (int)(&r - p->rb);
+  if (p->pkb) {
+    if (!r.pk[k]) return sfail(SPFF_EINVAL, "no batched image for this conv");
+    *img = p->F(r.pk[k]);
+    *wmax = p->cfg.math == SPFF_MATH_F16X3
+                ? reinterpret_cast<const unsigned*>(p->ws + p->wsl) + 2 * ri + (c1 ? 0 : 1)
+                : nullptr;
+    return SPFF_OK;
+  }
+  SHIPCK(conv3d_pack(p->P(c1 ? r.w1 : r.w2), p->F(p->wt), v, 3, c1 ? r.Cin : r.C, r.C, k >= 2,
+                     p->cfg.math, p->st));
+  *img = p->F(p->wt);
+  *wmax = nullptr;
+  return SPFF_OK;
+}
+
+// 3x3x3 conv k (0 / 1) of r + (fused where the kernel allows) IN statistics
+int conv_in(spff_swin* p, const Src2& in, const RB& r, int k, const Vol& v, int Cin, int C,
+            size_t y, const size_t* st4) {
+  const int math = p->cfg.math;
+  const float* img;
+  const unsigned* wmax;
+  SCK(conv_image(p, r, k, v, &img, &wmax));
   const bool fuse = conv3d_fuses_stats(v, 3, Cin, C, math);
-  SHIPCK(conv3d_run(in, p->F(p->wt), dst1(p->F(y), C), v, 3, Cin, C, false, math, p->st,
-                    p->F(p->wg_ws), fuse ? p->F(p->cst) : nullptr));
+  SHIPCK(conv3d_run(in, img, dst1(p->F(y), C), v, 3, Cin, C, false, math, p->st,
+                    p->F(p->wg_ws), fuse ? p->F(p->cst) : nullptr, 0, wmax));
   if (fuse) {
     SHIPCK(conv3d_in_stats_fin(p->F(p->cst), v, 3, Cin, C, math, p->F(p->ones), p->F(p->zeros),
                                p->F(st4[0]), p->F(st4[1]), p->F(st4[2]), p->F(st4[3]), p->st));
@@ -372,10 +441,10 @@ int conv_in(spff_swin* p, const Src2& in, int64_t w, const Vol& v, int Cin, int 
 int rb_fwd(spff_swin* p, RB& r, const Src2& in, const float* ident) {
   const Vol& v = p->vol[r.L];
   const int C = r.C;
-  SCK(conv_in(p, in, r.w1, v, r.Cin, C, r.y1, r.st[0]));
+  SCK(conv_in(p, in, r, 0, v, r.Cin, C, r.y1, r.st[0]));
   SHIPCK(act_apply(p->F(r.y1), p->F(r.a1), p->F(r.st[0][2]), p->F(r.st[0][3]), nullptr, nullptr, v,
                    C, p->st));
-  SCK(conv_in(p, src1(p->F(r.a1), C), r.w2, v, C, C, r.y2, r.st[1]));
+  SCK(conv_in(p, src1(p->F(r.a1), C), r, 1, v, C, C, r.y2, r.st[1]));
   if (r.has3) {
     float* pk = p->F(r.c3.pk);
     SHIPCK(head_pack(p->P(r.c3.w), pk, pk + head_pack_dgrad_offset(r.Cin, C), r.Cin, C, p->st));
@@ -417,15 +486,17 @@ int rb_bwd(spff_swin* p, RB& r, const float* dout, const Src2& in, const float* 
   SCK(in_bwd(p, v, C, r.y2, dz, dy2, r.st[1], 1.f));
   SHIPCK(conv3d_wgrad(src1(p->F(r.a1), C), dy2, C, p->DP(r.w2), v, 3, C, C, math, p->F(p->wg_ws),
                       p->st));
-  SHIPCK(conv3d_pack(p->P(r.w2), p->F(p->wt), v, 3, C, C, true, math, p->st));
-  SHIPCK(conv3d_run(src1(dy2, C), p->F(p->wt), dst1(da1, C), v, 3, C, C, true, math, p->st,
-                    p->F(p->wg_ws)));
+  const float* img;
+  const unsigned* wmax;
+  SCK(conv_image(p, r, 2, v, &img, &wmax));
+  SHIPCK(conv3d_run(src1(dy2, C), img, dst1(da1, C), v, 3, C, C, true, math, p->st,
+                    p->F(p->wg_ws), nullptr, 0, wmax));
   SCK(in_bwd(p, v, C, r.y1, da1, da1, r.st[0], 0.01f));
   SHIPCK(conv3d_wgrad(in, da1, C, p->DP(r.w1), v, 3, r.Cin, C, math, p->F(p->wg_ws), p->st));
   if (dsrc) {
-    SHIPCK(conv3d_pack(p->P(r.w1), p->F(p->wt), v, 3, r.Cin, C, true, math, p->st));
-    SHIPCK(conv3d_run(src1(da1, C), p->F(p->wt), *dsrc, v, 3, r.Cin, C, true, math, p->st,
-                      p->F(p->wg_ws)));
+    SCK(conv_image(p, r, 3, v, &img, &wmax));
+    SHIPCK(conv3d_run(src1(da1, C), img, *dsrc, v, 3, r.Cin, C, true, math, p->st,
+                      p->F(p->wg_ws), nullptr, 0, wmax));
   }
   if (r.has3) {
     SCK(in_bwd(p, v, C, r.y3, dz, dy2, r.st[2], 1.f));
@@ -544,6 +615,7 @@ int forward(spff_swin* p, const float* x, float* logits) {
     SHIPCK(ln_fwd(p->F(p->t[l]), C, C, nullptr, nullptr, p->F(p->hs[l]), C, p->F(p->hmu[l]),
                   p->F(p->hrs[l]), nvox(p->vol[l + 1]), st));
   }
+  SCK(prep_weights(p));
   RB* R = p->rb;
   SCK(rb_fwd(p, R[0], src1(p->F(p->x_cl), p->ldx), nullptr));
   for (int i = 1; i < 4; ++i) {

@@ -57,6 +57,7 @@ struct UBlk {
   int64_t rm1 = -1, rv1 = -1, rm2 = -1, rv2 = -1;                // buffers
   size_t y1, a1, y2, out;
   size_t mean1, rstd1, al1, de1, mean2, rstd2, al2, de2;
+  size_t pk[4] = {0, 0, 0, 0};  // batched conv images: w1 fwd, w2 fwd, w2 dgrad, w1 dgrad
 };
 
 struct UUp {
@@ -80,6 +81,8 @@ struct spff_unet3d {
   int64_t out_w = -1, out_b = -1;
   size_t head_pk = 0, x_cl = 0, pool[4] = {}, pidx[4] = {};
   size_t red_ws = 0, red_out = 0, kk1 = 0, kk2 = 0, wg_ws = 0, wt = 0;
+  bool pkb = false;  // conv images packed in one batch at the forward start (b.pk)
+  size_t wsl = 0;    // SPFF_MATH_F16X3 max |w| per conv, [NBLK][2] (batched plans)
   size_t G_out = 0, G_dy2 = 0, G_da1 = 0, G_dx = 0, dskip[4] = {}, logit_t = 0, dl_t = 0;
   size_t total = 0;
   bool last_training = true;
@@ -223,7 +226,19 @@ int build(spff_unet3d* p) {
   p->kk1 = p->alloc((size_t)B * 16 * f * sizeof(float));
   p->kk2 = p->alloc((size_t)B * 16 * f * sizeof(float));
   p->wg_ws = p->alloc(wg);
-  p->wt = p->alloc(wt);
+  p->pkb = conv3d_packs_batched(c.math);
+  if (p->pkb) {
+    for (int i = 0; i < NBLK; ++i) {
+      UBlk& b = p->blk[i];
+      b.pk[0] = p->alloc(conv3d_pack_bytes(3, b.Cin, b.C));
+      b.pk[1] = p->alloc(conv3d_pack_bytes(3, b.C, b.C));
+      b.pk[2] = p->alloc(conv3d_pack_bytes(3, b.C, b.C));
+      if (i > 0) b.pk[3] = p->alloc(conv3d_pack_bytes(3, b.Cin, b.C));  // enc1's input: no dx
+    }
+    p->wsl = p->alloc(NBLK * 2 * sizeof(unsigned));
+  } else {
+    p->wt = p->alloc(wt);
+  }
   size_t gmax = 0;  // max over levels of V_l * C_l (the bottleneck has 16 f channels)
   for (int l = 0; l < NLVL; ++l)
     gmax = std::max(gmax, (size_t)nvox(p->vol[l]) * (size_t)(f << l) * sizeof(float));
@@ -260,17 +275,72 @@ int bn_fwd(spff_unet3d* p, const Vol& v, int C, size_t y, size_t mean, size_t rs
   return SPFF_OK;
 }
 
+// batched plans: every conv's max |w| (f16x3) in one launch, then all 35 conv images
+// (forward and input gradient) in one more, at the forward start -- the weights do not
+// change between a step's forward and backward (the up-conv / head images are packed up
+// front the same way).  Otherwise conv3d_pack before each conv (max + pack launches).
+int prep_weights(spff_unet3d* p) {
+  if (!p->pkb) return SPFF_OK;
+  const int math = p->cfg.math;
+  const bool f16 = math == SPFF_MATH_F16X3;
+  unsigned* sl = reinterpret_cast<unsigned*>(p->ws + p->wsl);
+  PrepJobs pj;
+  PackJobs kj;
+  if (f16) UHIPCK(hipMemsetAsync(sl, 0, NBLK * 2 * sizeof(unsigned), p->st));
+  for (int i = 0; i < NBLK; ++i) {
+    UBlk& b = p->blk[i];
+    unsigned* w1 = f16 ? sl + 2 * i : nullptr;
+    unsigned* w2 = f16 ? sl + 2 * i + 1 : nullptr;
+    bool ok = true;
+    if (f16) {
+      ok = ok && prep_absmax(&pj, p->P(b.w1), (int64_t)b.C * b.Cin * 27, w1);
+      ok = ok && prep_absmax(&pj, p->P(b.w2), (int64_t)b.C * b.C * 27, w2);
+    }
+    ok = ok && conv3d_pack_job(&kj, p->P(b.w1), p->F(b.pk[0]), 3, b.Cin, b.C, false, w1);
+    ok = ok && conv3d_pack_job(&kj, p->P(b.w2), p->F(b.pk[1]), 3, b.C, b.C, false, w2);
+    ok = ok && conv3d_pack_job(&kj, p->P(b.w2), p->F(b.pk[2]), 3, b.C, b.C, true, w2);
+    if (b.pk[3]) ok = ok && conv3d_pack_job(&kj, p->P(b.w1), p->F(b.pk[3]), 3, b.Cin, b.C, true, w1);
+    if (!ok) return ufail(SPFF_EINVAL, "weight preparation table overflow");
+  }
+  UHIPCK(prep_run(pj, p->st));
+  UHIPCK(conv3d_pack_many(kj, math, p->st));
+  return SPFF_OK;
+}
+// conv k of block b (0: w1 fwd, 1: w2 fwd, 2: w2 dgrad, 3: w1 dgrad): its image (the
+// batched one, else packed now into the scratch image) and its max |w| slot
+int conv_image(spff_unet3d* p, const UBlk& b, int k, const Vol& v, const float** img,
+               const unsigned** wmax) {
+  const bool c1 = k == 0 || k == 3;
+  const int bi = (int)(&b - p->blk);
+  if (p->pkb) {
+    if (!b.pk[k]) return ufail(SPFF_EINVAL, "no batched image for this conv");
+    *img = p->F(b.pk[k]);
+    *wmax = p->cfg.math == SPFF_MATH_F16X3
+                ? reinterpret_cast<const unsigned*>(p->ws + p->wsl) + 2 * bi + (c1 ? 0 : 1)
+                : nullptr;
+    return SPFF_OK;
+  }
+  UHIPCK(conv3d_pack(p->P(c1 ? b.w1 : b.w2), p->F(p->wt), v, 3, c1 ? b.Cin : b.C, b.C, k >= 2,
+                     p->cfg.math, p->st));
+  *img = p->F(p->wt);
+  *wmax = nullptr;
+  return SPFF_OK;
+}
+
 int fwd_block(spff_unet3d* p, UBlk& b, const Src2& in, bool training) {
   const Vol& v = p->vol[b.lvl];
   const int C = b.C, math = p->cfg.math;
-  UHIPCK(conv3d_pack(p->P(b.w1), p->F(p->wt), v, 3, b.Cin, C, false, math, p->st));
-  UHIPCK(conv3d_run(in, p->F(p->wt), dst1(p->F(b.y1), C), v, 3, b.Cin, C, false, math, p->st, p->F(p->wg_ws)));
+  const float* img;
+  const unsigned* wmax;
+  UCK(conv_image(p, b, 0, v, &img, &wmax));
+  UHIPCK(conv3d_run(in, img, dst1(p->F(b.y1), C), v, 3, b.Cin, C, false, math, p->st,
+                    p->F(p->wg_ws), nullptr, 0, wmax));
   UCK(bn_fwd(p, v, C, b.y1, b.mean1, b.rstd1, b.al1, b.de1, b.g1, b.b1, b.rm1, b.rv1, training));
   UHIPCK(act_apply(p->F(b.y1), p->F(b.a1), p->F(b.al1), p->F(b.de1), nullptr, nullptr, v, C,
                    p->st, 0.f));
-  UHIPCK(conv3d_pack(p->P(b.w2), p->F(p->wt), v, 3, C, C, false, math, p->st));
-  UHIPCK(conv3d_run(src1(p->F(b.a1), C), p->F(p->wt), dst1(p->F(b.y2), C), v, 3, C, C, false,
-                    math, p->st, p->F(p->wg_ws)));
+  UCK(conv_image(p, b, 1, v, &img, &wmax));
+  UHIPCK(conv3d_run(src1(p->F(b.a1), C), img, dst1(p->F(b.y2), C), v, 3, C, C, false, math,
+                    p->st, p->F(p->wg_ws), nullptr, 0, wmax));
   UCK(bn_fwd(p, v, C, b.y2, b.mean2, b.rstd2, b.al2, b.de2, b.g2, b.b2, b.rm2, b.rv2, training));
   UHIPCK(act_apply(p->F(b.y2), p->F(b.out), p->F(b.al2), p->F(b.de2), nullptr, nullptr, v, C,
                    p->st, 0.f));
@@ -299,13 +369,17 @@ int bwd_block(spff_unet3d* p, UBlk& b, const float* dout, const Dst2* dx, const 
   UCK(bn_bwd(p, v, C, b.y2, dout, dy2, b.mean2, b.rstd2, b.al2, b.de2, b.g2, b.b2));
   UHIPCK(conv3d_wgrad(src1(p->F(b.a1), C), dy2, C, p->DP(b.w2), v, 3, C, C, math,
                       p->F(p->wg_ws), p->st));
-  UHIPCK(conv3d_pack(p->P(b.w2), p->F(p->wt), v, 3, C, C, true, math, p->st));
-  UHIPCK(conv3d_run(src1(dy2, C), p->F(p->wt), dst1(da1, C), v, 3, C, C, true, math, p->st, p->F(p->wg_ws)));
+  const float* img;
+  const unsigned* wmax;
+  UCK(conv_image(p, b, 2, v, &img, &wmax));
+  UHIPCK(conv3d_run(src1(dy2, C), img, dst1(da1, C), v, 3, C, C, true, math, p->st,
+                    p->F(p->wg_ws), nullptr, 0, wmax));
   UCK(bn_bwd(p, v, C, b.y1, da1, da1, b.mean1, b.rstd1, b.al1, b.de1, b.g1, b.b1));
   UHIPCK(conv3d_wgrad(in, da1, C, p->DP(b.w1), v, 3, b.Cin, C, math, p->F(p->wg_ws), p->st));
   if (dx) {
-    UHIPCK(conv3d_pack(p->P(b.w1), p->F(p->wt), v, 3, b.Cin, C, true, math, p->st));
-    UHIPCK(conv3d_run(src1(da1, C), p->F(p->wt), *dx, v, 3, b.Cin, C, true, math, p->st, p->F(p->wg_ws)));
+    UCK(conv_image(p, b, 3, v, &img, &wmax));
+    UHIPCK(conv3d_run(src1(da1, C), img, *dx, v, 3, b.Cin, C, true, math, p->st,
+                      p->F(p->wg_ws), nullptr, 0, wmax));
   }
   return SPFF_OK;
 }
@@ -319,6 +393,7 @@ int forward(spff_unet3d* p, const float* x, float* logits, bool training) {
                                    c.width, p->ldx, p->st));
   else
     UHIPCK(ncdhw_to_ndhwc(x, p->F(p->x_cl), v0, c.in_ch, p->ldx, p->st));
+  UCK(prep_weights(p));
   UBlk* B = p->blk;
   Src2 in = src1(p->F(p->x_cl), p->ldx);
   for (int l = 0; l < 4; ++l) {
