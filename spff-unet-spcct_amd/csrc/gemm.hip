@@ -1336,14 +1336,171 @@ static inline int head_fn(int K) { return cdiv(K, 32) * 32; }
 static inline int head_dk(int K) { return cdiv(K, G_BK) * G_BK; }
 static inline int head_dn(int Cin) { return cdiv(Cin, 32) * 32; }
 
+// Streaming head (Cin = 32 or 64, K <= 32): the head is memory-bound (Cin floats in, K out
+// per voxel) and the K <= 32 column MFMA GEMM ran it at ~3.3 TB/s.  A block takes 256
+// consecutive rows: a coalesced float4 pass stages them in LDS (the loader applies the
+// block-output activation, as LoadRowsAct does in the GEMM), each thread then forms its
+// row's K dot products in fp32 (c in order, the uniform weights through the scalar cache),
+// and a second coalesced pass stores the block's [256][K] outputs.  The input gradient is
+// the mirror image.  W = wd [K][dn] (head_pack's dgrad image, the reference layout).
+// (SPFF_HEAD_STREAM=0, diagnostics / A/B only: the GEMM path again)
+static bool head_stream_ok(int Cin, int K) {
+  static const bool off = [] {
+    const char* e = getenv("SPFF_HEAD_STREAM");
+    return e && e[0] == '0';
+  }();
+  return !off && (Cin == 32 || Cin == 64) && K >= 1 && K <= 32;
+}
+template <int C, int KM, class L>
+__global__ __launch_bounds__(256) void k_head_fwd_s(L A, const float* __restrict__ wd, int dn,
+                                                    const float* __restrict__ bias,
+                                                    float* __restrict__ y, int64_t V, int K) {
+  constexpr int CP = C + 1, Q = C / 4;
+  __shared__ float tile[256 * CP];
+  const int tid = threadIdx.x;
+  for (int64_t r0 = (int64_t)blockIdx.x * 256; r0 < V; r0 += (int64_t)gridDim.x * 256) {
+    const int nr = (int)(V - r0 < 256 ? V - r0 : 256);
+    float4 v[Q];
+#pragma unroll
+    for (int j = 0; j < Q; ++j) {  // Q quads per thread in flight
+      const int i = tid + j * 256, rr = i / Q;
+      v[j] = A.load4(A.prep(r0 + (rr < nr ? rr : 0)), 4 * (i % Q));
+    }
+#pragma unroll
+    for (int j = 0; j < Q; ++j) {
+      const int i = tid + j * 256;
+      float* t = tile + (i / Q) * CP + 4 * (i % Q);
+      t[0] = v[j].x; t[1] = v[j].y; t[2] = v[j].z; t[3] = v[j].w;
+    }
+    __syncthreads();
+    float o[KM];
+    {
+      float a[C];
+#pragma unroll
+      for (int c = 0; c < C; ++c) a[c] = tile[tid * CP + c];
+#pragma unroll
+      for (int k = 0; k < KM; ++k) {
+        float s = 0.f;
+        if (k < K) {
+#pragma unroll
+          for (int c = 0; c < C; ++c) s = fmaf(a[c], wd[k * dn + c], s);
+          s += bias ? bias[k] : 0.f;
+        }
+        o[k] = s;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < KM; ++k)
+      if (k < K) tile[tid * K + k] = o[k];
+    __syncthreads();
+    const int n = nr * K;
+    float* yb = y + r0 * K;  // 16-B aligned: r0 is a multiple of 256
+    for (int i = tid; i < n / 4; i += 256)
+      reinterpret_cast<float4*>(yb)[i] =
+          make_float4(tile[4 * i], tile[4 * i + 1], tile[4 * i + 2], tile[4 * i + 3]);
+    for (int i = (n / 4) * 4 + tid; i < n; i += 256) yb[i] = tile[i];
+    __syncthreads();
+  }
+}
+template <int C, int KM>
+__global__ __launch_bounds__(256) void k_head_dgrad_s(const float* __restrict__ dy,
+                                                      const float* __restrict__ wd, int dn,
+                                                      float* __restrict__ dx, int64_t V, int K) {
+  constexpr int CP = C + 1, NL = KM / 4;
+  __shared__ float tile[256 * CP];  // the block's dy rows [256][K], then its dx rows [256][CP]
+  const int tid = threadIdx.x;
+  for (int64_t r0 = (int64_t)blockIdx.x * 256; r0 < V; r0 += (int64_t)gridDim.x * 256) {
+    const int nr = (int)(V - r0 < 256 ? V - r0 : 256);
+    const int n = nr * K, n4 = n / 4;
+    const float* gb = dy + r0 * K;  // 16-B aligned: r0 is a multiple of 256
+    float4 gv[NL];
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {  // NL quads per thread in flight
+      const int i = tid + j * 256;
+      gv[j] = i < n4 ? reinterpret_cast<const float4*>(gb)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      const int i = tid + j * 256;
+      if (i < n4) {
+        tile[4 * i] = gv[j].x; tile[4 * i + 1] = gv[j].y;
+        tile[4 * i + 2] = gv[j].z; tile[4 * i + 3] = gv[j].w;
+      }
+    }
+    for (int i = n4 * 4 + tid; i < n; i += 256) tile[i] = gb[i];
+    __syncthreads();
+    float g[KM];
+#pragma unroll
+    for (int k = 0; k < KM; ++k) g[k] = (k < K && tid < nr) ? tile[tid * K + k] : 0.f;
+    __syncthreads();
+    float acc[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) acc[c] = 0.f;
+#pragma unroll
+    for (int k = 0; k < KM; ++k)
+      if (k < K) {
+#pragma unroll
+        for (int c = 0; c < C; ++c) acc[c] = fmaf(g[k], wd[k * dn + c], acc[c]);
+      }
+#pragma unroll
+    for (int c = 0; c < C; ++c) tile[tid * CP + c] = acc[c];
+    __syncthreads();
+    float* xb = dx + r0 * C;
+    for (int i = tid; i < nr * (C / 4); i += 256) {
+      const float* t = tile + (i / (C / 4)) * CP + 4 * (i % (C / 4));
+      reinterpret_cast<float4*>(xb)[i] = make_float4(t[0], t[1], t[2], t[3]);
+    }
+    __syncthreads();
+  }
+}
+static unsigned head_grid(int64_t V) {
+  return (unsigned)std::min<int64_t>((V + 255) / 256, 8192);
+}
+template <int C, int KM, class L>
+static hipError_t head_fwd_s(const L& A, const float* wd, int dn, const float* b, float* y,
+                             int64_t V, int K, hipStream_t s) {
+  hipLaunchKernelGGL((k_head_fwd_s<C, KM, L>), dim3(head_grid(V)), dim3(256), 0, s, A, wd, dn, b,
+                     y, V, K);
+  return hipGetLastError();
+}
+template <class L>
+static hipError_t head_fwd_stream(const L& A, const float* wd, int Cin, const float* b, float* y,
+                                  int64_t V, int K, hipStream_t s) {
+  const int dn = head_dn(Cin);
+  if (Cin == 32)
+    return K <= 16 ? head_fwd_s<32, 16>(A, wd, dn, b, y, V, K, s)
+                   : head_fwd_s<32, 32>(A, wd, dn, b, y, V, K, s);
+  return K <= 16 ? head_fwd_s<64, 16>(A, wd, dn, b, y, V, K, s)
+                 : head_fwd_s<64, 32>(A, wd, dn, b, y, V, K, s);
+}
+static hipError_t head_dgrad_stream(const float* dy, const float* wd, float* dx, int64_t V,
+                                    int Cin, int K, hipStream_t s) {
+  const int dn = head_dn(Cin);
+  const dim3 g(head_grid(V)), b(256);
+  if (Cin == 32) {
+    if (K <= 16) hipLaunchKernelGGL((k_head_dgrad_s<32, 16>), g, b, 0, s, dy, wd, dn, dx, V, K);
+    else hipLaunchKernelGGL((k_head_dgrad_s<32, 32>), g, b, 0, s, dy, wd, dn, dx, V, K);
+  } else {
+    if (K <= 16) hipLaunchKernelGGL((k_head_dgrad_s<64, 16>), g, b, 0, s, dy, wd, dn, dx, V, K);
+    else hipLaunchKernelGGL((k_head_dgrad_s<64, 32>), g, b, 0, s, dy, wd, dn, dx, V, K);
+  }
+  return hipGetLastError();
+}
+
 hipError_t head_fwd(const float* x, const float* wf, const float* b, float* y, int64_t V, int Cin,
                     int K, hipStream_t s, int math, const ActRows* act) {
   StoreRows C{y, K, K, b, V};
-  if (act) {
-    if (!act_ok(act, Cin)) return hipErrorInvalidValue;
+  if (act && !act_ok(act, Cin)) return hipErrorInvalidValue;
+  const bool y16 = !(reinterpret_cast<uintptr_t>(y) & 15);
+  if (head_stream_ok(Cin, K) && y16 && (act || !(reinterpret_cast<uintptr_t>(x) & 15))) {
+    const float* wd = wf + head_pack_dgrad_offset(Cin, K);
+    if (act) return head_fwd_stream(act_loader(*act, Cin, V), wd, Cin, b, y, V, K, s);
+    return head_fwd_stream(LoadRowsVec{x, Cin, Cin, V}, wd, Cin, b, y, V, K, s);
+  }
+  if (act)
     return launch_gemm(act_loader(*act, Cin, V), wf, C, V, head_fk(Cin), head_fn(K), s,
                        gemm_split(math));
-  }
   LoadRowsVec A{x, Cin, Cin, V};
   return launch_gemm(A, wf, C, V, head_fk(Cin), head_fn(K), s, gemm_split(math));
 }
@@ -1369,6 +1526,9 @@ size_t upconv_pack_dgrad_offset(int Cin, int Cout, int ns) {
 
 hipError_t head_dgrad(const float* dy, const float* wd, float* dx, int64_t V, int Cin, int K,
                       hipStream_t s, int math) {
+  if (head_stream_ok(Cin, K) &&
+      !((reinterpret_cast<uintptr_t>(dy) | reinterpret_cast<uintptr_t>(dx)) & 15))
+    return head_dgrad_stream(dy, wd, dx, V, Cin, K, s);
   LoadRowsScalar A{dy, K, K, V};
   StoreRows C{dx, Cin, Cin, nullptr, V};
   return launch_gemm(A, wd, C, V, head_dk(K), head_dn(Cin), s, gemm_split(math));

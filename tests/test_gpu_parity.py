@@ -321,6 +321,19 @@ def test_module_contract_generality(in_ch, K, base, mth):
     hidden 4/5/10/20).  Engine vs the oracle (pinned to the reference by the fixtures,
     including the reference-generated fx5_k40_base24): logits within 1e-3, argmax outside
     near-ties, loss, and every gradient against the kink-consistent fp64 oracle."""
+    _engine_vs_oracle(in_ch, K, base, mth)
+
+
+@pytest.mark.parametrize("in_ch,K,base,mth", [(5, 13, 32, "f16x3"), (5, 20, 32, "f32"),
+                                              (5, 13, 64, "bf16x6"), (5, 32, 64, "f16x3")])
+def test_streaming_head(in_ch, K, base, mth):
+    """The streaming 1x1x1 head (gemm.hip k_head_fwd_s / k_head_dgrad_s: Cin = base 32 or 64,
+    K <= 32; K <= 16 and 17..32 instantiations): logits, loss and every gradient (the head's
+    and, through its input gradient, the network's) against the oracle as above."""
+    _engine_vs_oracle(in_ch, K, base, mth)
+
+
+def _engine_vs_oracle(in_ch, K, base, mth):
     from innovative3D.synthetic import synthetic_batch
     from innovative3D.weightgen import synth_state
     B, D, H, W = 1, 4, 16, 16
