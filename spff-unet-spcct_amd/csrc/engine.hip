@@ -469,7 +469,8 @@ int build_plan(spff_plan* p) {
   p->kk1 = p->alloc((size_t)B * 8 * f * sizeof(float));
   p->kk2 = p->alloc((size_t)B * 8 * f * sizeof(float));
   p->wg_ws = p->alloc(wg);
-  p->pkb = conv3d_packs_batched(p->cfg.math);
+  // (the lean layout keeps the one scratch image: it trades time for the smallest footprint)
+  p->pkb = !p->lean && conv3d_packs_batched(p->cfg.math);
   if (p->pkb) {
     for (int i = 0; i < 7; ++i) {
       Blk& b = p->blk[i];
