@@ -1361,10 +1361,42 @@ __global__ __launch_bounds__(256) void k_head_fwd_s(L A, const float* __restrict
   for (int64_t r0 = (int64_t)blockIdx.x * 256; r0 < V; r0 += (int64_t)gridDim.x * 256) {
     const int nr = (int)(V - r0 < 256 ? V - r0 : 256);
     float4 v[Q];
+    bool done = false;
+    if constexpr (std::is_same<L, LoadRowsAct>::value) {
+      // HW % 256 == 0: the block's 256 rows share one (b, d), and thread tid always takes
+      // channel quad tid % Q, so its activation coefficients load once per block
+      if (A.HW % 256 == 0) {
+        const int64_t bd = r0 / A.HW, b = bd / A.D;
+        const int c = 4 * (tid % Q);
+        const float4 a = *reinterpret_cast<const float4*>(A.al + b * A.ld + c);
+        const float4 e = *reinterpret_cast<const float4*>(A.de + b * A.ld + c);
+        float4 pp = make_float4(1.f, 1.f, 1.f, 1.f), qq = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (A.PT) {
+          pp = *reinterpret_cast<const float4*>(A.PT + bd * A.ld + c);
+          qq = *reinterpret_cast<const float4*>(A.QT + bd * A.ld + c);
+        }
 #pragma unroll
-    for (int j = 0; j < Q; ++j) {  // Q quads per thread in flight
-      const int i = tid + j * 256, rr = i / Q;
-      v[j] = A.load4(A.prep(r0 + (rr < nr ? rr : 0)), 4 * (i % Q));
+        for (int j = 0; j < Q; ++j) {
+          const int rr = (tid + j * 256) / Q;
+          v[j] = *reinterpret_cast<const float4*>(A.p + (r0 + (rr < nr ? rr : 0)) * A.ld + c);
+        }
+        auto f = [&](float y, float a_, float e_, float p_, float q_) {  // LoadRowsAct::load4's
+          const float t = y * a_ + e_;
+          return (t > 0.f ? t : A.neg * t) * p_ + q_;
+        };
+#pragma unroll
+        for (int j = 0; j < Q; ++j)
+          v[j] = make_float4(f(v[j].x, a.x, e.x, pp.x, qq.x), f(v[j].y, a.y, e.y, pp.y, qq.y),
+                             f(v[j].z, a.z, e.z, pp.z, qq.z), f(v[j].w, a.w, e.w, pp.w, qq.w));
+        done = true;
+      }
+    }
+    if (!done) {
+#pragma unroll
+      for (int j = 0; j < Q; ++j) {  // Q quads per thread in flight
+        const int i = tid + j * 256, rr = i / Q;
+        v[j] = A.load4(A.prep(r0 + (rr < nr ? rr : 0)), 4 * (i % Q));
+      }
     }
 #pragma unroll
     for (int j = 0; j < Q; ++j) {
