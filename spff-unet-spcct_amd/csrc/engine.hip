@@ -1367,7 +1367,10 @@ int spff_forward(spff_plan* p, const float* x, const float* params, float* logit
     return fail(SPFF_EINVAL, "depth-sharded plan: call spff_plan_set_coll first");
   CK(ensure_pe(p));
   p->co.failed = nullptr;
-  return coll_status(p, forward(p, x, logits), "spff_forward");
+  p->halo_early = nullptr;  // never carried over from a step that failed after halo_begin
+  const int rc = forward(p, x, logits);
+  p->halo_early = nullptr;
+  return coll_status(p, rc, "spff_forward");
 }
 
 int spff_backward(spff_plan* p, const float* dlogits, const float* params, float* dparams,
@@ -1380,7 +1383,10 @@ int spff_backward(spff_plan* p, const float* dlogits, const float* params, float
   if (p->co.on() && !p->coll_set)
     return fail(SPFF_EINVAL, "depth-sharded plan: call spff_plan_set_coll first");
   p->co.failed = nullptr;
-  return coll_status(p, backward(p, dlogits), "spff_backward");
+  p->halo_early = nullptr;  //  a stale early halo would skip an exchange
+  const int rc = backward(p, dlogits);
+  p->halo_early = nullptr;
+  return coll_status(p, rc, "spff_backward");
 }
 
 int spff_saved_tensor(const spff_plan* p, void* ws, const char* name, const float** ptr,

@@ -14,8 +14,9 @@
 namespace spff {
 
 // K up to KMAX classes.  Up to KHIST_LDS the K x (K + 1) confusion histogram lives in LDS
-// (integer atomics there, flushed once per workgroup); above it each count goes straight
-// to the int64 matrix in HBM (integer atomics: still order-free and exact).
+// (integer atomics there, flushed once per workgroup); above it the counts go straight
+// to the int64 matrix in HBM, one atomic per distinct cell per wave (integer atomics:
+// still order-free and exact).
 constexpr int LOSS_GRID = 2048, LOSS_T = 256, KMAX = 128, KHIST_LDS = 64;
 
 __global__ void k_count_valid(const int64_t* __restrict__ lab, int64_t V, int ignore,
@@ -60,10 +61,8 @@ __global__ __launch_bounds__(LOSS_T) void k_loss(const float* __restrict__ x,
   if (lh)
     for (int i = threadIdx.x; i < K * K1; i += LOSS_T) hist[i] = 0;
   __syncthreads();
-  auto tally = [&](int i) {
-    if (lh) atomicAdd(&hist[i], 1u);
-    else atomicAdd(&conf[i], 1ull);
-  };
+  int cell;  // this lane's confusion cell in the current group, -1 for none
+  auto tally = [&](int i) { cell = i; };
   // clamp1: the 3DUNet's weighted CE divides by max(N_valid, 1) (models.py:796)
   const float invN =
       WITH_CE ? 1.f / (float)(clamp1 && *count < 1 ? (int64_t)1 : *count) : 0.f;
@@ -77,6 +76,7 @@ __global__ __launch_bounds__(LOSS_T) void k_loss(const float* __restrict__ x,
     const int nf = nv * K;
     wave_copy_rows(sx, x + v0 * K, nf, lane);
     wave_lds_sync();
+    cell = -1;
     if (lane < nv) {
       const int64_t v = v0 + lane;
       float* xr = sx + lane * K;
@@ -117,6 +117,21 @@ __global__ __launch_bounds__(LOSS_T) void k_loss(const float* __restrict__ x,
             for (int k = 0; k < K; ++k) xr[k] = 0.f;
           }
         }
+      }
+    }
+    if (lh) {
+      if (cell >= 0) atomicAdd(&hist[cell], 1u);
+    } else {
+      // K > KHIST_LDS: the counts go to HBM.  Labels are skewed (most voxels of a wave
+      // land in a few cells, e.g. background/background), so the wave issues ONE atomic
+      // per distinct cell with the number of its lanes in it, not one per voxel.
+      unsigned long long todo = __ballot(cell >= 0);
+      while (todo) {  // wave-uniform loop
+        const int leader = __builtin_ctzll(todo);
+        const int c = __shfl(cell, leader);
+        const unsigned long long same = __ballot(cell == c) & todo;
+        if (lane == leader) atomicAdd(&conf[c], (unsigned long long)__popcll(same));
+        todo &= ~same;
       }
     }
     wave_lds_sync();

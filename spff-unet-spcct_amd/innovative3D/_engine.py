@@ -328,8 +328,16 @@ class Plan:
         def _allreduce(ctx, buf, n, dt, stream):
             try:
                 t = view(buf, n, torch.float64 if dt == 1 else torch.float32)
-                _timed("allreduce", t.numel() * t.element_size(), stream, t.device,
-                       lambda: impl.allreduce(t))
+                nb = t.numel() * t.element_size()
+                cur = torch.cuda.current_stream(t.device)
+                if stream and stream != cur.cuda_stream:
+                    # issue the all-reduce on the stream the engine handed over (where
+                    # its timing events are recorded and the buffer is ordered), as
+                    # _halo does
+                    with torch.cuda.stream(torch.cuda.ExternalStream(stream, device=t.device)):
+                        _timed("allreduce", nb, stream, t.device, lambda: impl.allreduce(t))
+                else:
+                    _timed("allreduce", nb, stream, t.device, lambda: impl.allreduce(t))
                 return 0
             except Exception as e:  # noqa: BLE001 -- reported through the engine status
                 self.coll_error = e
@@ -532,19 +540,38 @@ def release_workspace(plan) -> None:
 
 
 def _alloc_workspace(plan, device) -> torch.Tensor:
-    """The plan's workspace.  If the device is out of memory, the workspaces of every
-    OTHER cached plan (validation shapes, a partial last batch: see _owned_plan) are
-    released, torch's cache is emptied and the allocation retried once; a second
-    failure raises.  SPFF_PLAN_CACHE=1 keeps one plan per module and tag (round 2's
-    behaviour: the previous shape's workspace is freed before a new shape's is built)."""
+    """The plan's workspace.  If the device is out of memory, the workspaces of the OTHER
+    cached plans on the same device (validation shapes, a partial last batch: see
+    _owned_plan) are released, torch's cache is emptied and the allocation retried:
+    first only plans with no backward pending on their workspace (``_pending_gen``, set
+    by the engine ops' autograd forward, cleared by their backward), then, as a last
+    resort, those too (their pending backward then fails loudly, see release_workspace).
+    A failure after that raises.  SPFF_PLAN_CACHE=1 keeps one plan per module and tag
+    (round 2's behaviour: the previous shape's workspace is freed before a new shape's
+    is built)."""
+    device = torch.device(device)
     try:
         return torch.empty(plan.ws_bytes, dtype=torch.uint8, device=device)
     except torch.OutOfMemoryError:
+        pass
+
+    def same_device(q):
+        ws = getattr(q, "_ws", None)
+        return ws is not None and ws.device == device
+
+    for last_resort in (False, True):
         for q in _all_plans():
-            if q is not plan:
-                release_workspace(q)
+            if q is plan or not same_device(q):
+                continue
+            if not last_resort and getattr(q, "_pending_gen", None) == getattr(q, "generation", 0):
+                continue
+            release_workspace(q)
         torch.cuda.empty_cache()
-        return torch.empty(plan.ws_bytes, dtype=torch.uint8, device=device)
+        try:
+            return torch.empty(plan.ws_bytes, dtype=torch.uint8, device=device)
+        except torch.OutOfMemoryError:
+            if last_resort:
+                raise
 
 
 def _device_bytes() -> int:

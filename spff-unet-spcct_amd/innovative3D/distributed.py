@@ -38,19 +38,27 @@ def world(group=None) -> int:
     return dist.get_world_size(group)
 
 
+def _multi(group, force: bool = False) -> bool:
+    """collectives are issued: more than one rank, or ``force`` on an initialised group"""
+    if world(group) > 1:
+        return True
+    return bool(force) and dist.is_available() and dist.is_initialized()
+
+
 def global_valid_count(labels: torch.Tensor, ignore_index: int = 255, group=None,
-                       count_fn: Optional[Callable] = None) -> torch.Tensor:
+                       count_fn: Optional[Callable] = None, force: bool = False) -> torch.Tensor:
     """All-reduced number of labels != ignore_index (int64 tensor on labels' device).
     ``count_fn`` defaults to the HIP counting kernel."""
     cnt = (count_fn or E.count_valid)(labels, ignore_index)
-    if world(group) > 1:
+    if _multi(group, force):
         dist.all_reduce(cnt, group=group)
     return cnt
 
 
-def allreduce_gradients(params: Iterable[torch.nn.Parameter], group=None) -> None:
+def allreduce_gradients(params: Iterable[torch.nn.Parameter], group=None,
+                        force: bool = False) -> None:
     """SUM-all-reduce every .grad with ONE collective over a flat buffer."""
-    if world(group) <= 1:
+    if not _multi(group, force):
         return
     gs: List[torch.Tensor] = [p.grad for p in params if p.grad is not None]
     if not gs:
@@ -71,7 +79,7 @@ def allreduce_confusion(conf: torch.Tensor, group=None) -> torch.Tensor:
 
 
 def global_loss(ce_share: torch.Tensor, conf: torch.Tensor, num_classes: int,
-                smooth: float = 1e-6, group=None):
+                smooth: float = 1e-6, group=None, force: bool = False):
     """(loss, ce, conf) of the whole global batch from this rank's CE share (CE
     normalised by the global valid count) and its confusion counts, with one
     fp64 all-reduce and no host sync.  loss = fp32(ce) + fp32(0.5 * dice_loss),
@@ -81,7 +89,7 @@ def global_loss(ce_share: torch.Tensor, conf: torch.Tensor, num_classes: int,
     K = int(num_classes)
     buf = torch.cat([ce_share.detach().reshape(1).to(torch.float64),
                      conf.detach().reshape(-1).to(torch.float64)])
-    if world(group) > 1:
+    if _multi(group, force):
         dist.all_reduce(buf, group=group)
     ce = buf[0].to(torch.float32)
     conf_g = buf[1:].round().to(torch.int64).view(conf.shape)
@@ -169,8 +177,14 @@ class DataParallelSPFF:
     after the backward instead, so ranks can never keep unreduced gradients."""
 
     def __init__(self, module: torch.nn.Module, num_classes: int, ignore_index: int = 255,
-                 group=None, bucket_bytes: int = 4 << 20, overlap: bool = True):
+                 group=None, bucket_bytes: int = 4 << 20, overlap: bool = True,
+                 force_collectives: bool = False):
+        """``force_collectives``: issue every collective even when the group has one rank
+        (a world-1 RCCL group then runs the whole device path -- the count, the bucketed
+        all-reduces on the engine's backward and the loss all-reduce -- on one GPU;
+        tests/test_gpu_dp.py::test_rccl_world1_bucketed_step)."""
         self.module, self.K, self.ignore, self.group = module, int(num_classes), ignore_index, group
+        self.force = bool(force_collectives)
         self.params = [p for p in module.parameters()]
         self.core = getattr(module, "model", module)
         self.bucketer = GradBucketer(group, bucket_bytes) if overlap else None
@@ -184,7 +198,8 @@ class DataParallelSPFF:
         for p in self.params:
             p.grad = None
         n = world(self.group)
-        hook = self.bucketer if (n > 1 and self.bucketer is not None) else None
+        multi = n > 1 or (self.force and dist.is_available() and dist.is_initialized())
+        hook = self.bucketer if (multi and self.bucketer is not None) else None
         begun = hook.begun if hook is not None else 0
         if hook is not None:
             hook.covered.clear()
@@ -192,23 +207,23 @@ class DataParallelSPFF:
         try:
             logits = self.module(x)
             self.last_logits = logits.detach()
-            cnt = global_valid_count(y, self.ignore, self.group) if n > 1 else None
+            cnt = global_valid_count(y, self.ignore, self.group, force=self.force) if multi else None
             loss_loc, conf, ce = ce_dice_parts(logits, y, self.K, self.ignore,
                                                count_override=cnt)
             loss_loc.backward()
         finally:
             self._set_hook(None)
-        if n > 1:
+        if multi:
             allreduce_uncovered(self.params, hook if (hook is not None and hook.begun != begun)
-                                else None, self.group)
-        if n == 1:
+                                else None, self.group, force=self.force)
+        if not multi:
             return loss_loc.detach(), conf
-        loss, _ce, conf_g = global_loss(ce, conf, self.K, group=self.group)
+        loss, _ce, conf_g = global_loss(ce, conf, self.K, group=self.group, force=self.force)
         return loss, conf_g
 
 
 def allreduce_uncovered(params: Iterable[torch.nn.Parameter], bucketer: Optional[GradBucketer],
-                        group=None) -> int:
+                        group=None, force: bool = False) -> int:
     """All-reduce (one flat collective) every .grad the bucketer did NOT reduce during
     the backward: the parameters no engine op reported through ``bucketer.cover`` (a
     parameter of a wrapper outside the plan, or all of them when no plan took the
@@ -216,5 +231,5 @@ def allreduce_uncovered(params: Iterable[torch.nn.Parameter], bucketer: Optional
     module structure and the same engine ops, so every rank issues the same call."""
     done = bucketer.covered if bucketer is not None else set()
     rest = [p for p in params if p.grad is not None and id(p) not in done]
-    allreduce_gradients(rest, group)
+    allreduce_gradients(rest, group, force=force)
     return len(rest)

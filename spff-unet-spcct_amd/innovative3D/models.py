@@ -202,6 +202,9 @@ class _SPFFFunction(torch.autograd.Function):
         ctx.plan = plan
         ctx.gen = plan.generation
         ctx.flat = flat
+        # a backward is pending on this workspace (E._alloc_workspace releases other
+        # plans' workspaces on OOM, pending ones only as a last resort)
+        plan._pending_gen = plan.generation if any(ctx.needs_input_grad) else None
         ctx.grad_hook = getattr(core, "grad_hook", None)
         ctx.param_ids = tuple(id(p) for p in params)
         ctx.slices = [(off, n, shape) for (_name, shape, off, n) in plan.params]
@@ -218,6 +221,7 @@ class _SPFFFunction(torch.autograd.Function):
         if not g_cl.is_contiguous():
             g_cl = g_cl.contiguous()
         dflat = plan.backward(g_cl, ctx.flat, grad_hook=ctx.grad_hook)
+        plan._pending_gen = None
         _mark_covered(ctx.grad_hook, ctx.param_ids)
         grads = [dflat[o:o + n].view(s) for (o, n, s) in ctx.slices]
         return (None, None, None, *grads)
@@ -529,6 +533,9 @@ class _UNet3DFunction(torch.autograd.Function):
     def forward(ctx, x, plan, flat, bufs, training, grad_hook, *params):
         logits_cl = plan.forward(x, flat, bufs, training)
         ctx.plan, ctx.gen, ctx.flat, ctx.grad_hook = plan, plan.generation, flat, grad_hook
+        # a backward is pending on this workspace (E._alloc_workspace releases other
+        # plans' workspaces on OOM, pending ones only as a last resort)
+        plan._pending_gen = plan.generation if any(ctx.needs_input_grad) else None
         ctx.param_ids = tuple(id(p) for p in params)
         ctx.slices = [(off, n, shape) for (_name, shape, off, n) in plan.params]
         return logits_cl.permute(0, 4, 1, 2, 3)
@@ -541,6 +548,7 @@ class _UNet3DFunction(torch.autograd.Function):
                               "backward of this one; the engine keeps one forward's activations")
         g_cl = g.permute(0, 2, 3, 4, 1).contiguous()
         dflat = plan.backward(g_cl, ctx.flat, grad_hook=ctx.grad_hook)
+        plan._pending_gen = None
         _mark_covered(ctx.grad_hook, ctx.param_ids)
         grads = [dflat[o:o + n].view(s) for (o, n, s) in ctx.slices]
         return (None, None, None, None, None, None, *grads)
@@ -807,6 +815,9 @@ class _SwinFunction(torch.autograd.Function):
     def forward(ctx, x, plan, flat, grad_hook, *params):
         logits_cl = plan.forward(x, flat)
         ctx.plan, ctx.gen, ctx.flat, ctx.grad_hook = plan, plan.generation, flat, grad_hook
+        # a backward is pending on this workspace (E._alloc_workspace releases other
+        # plans' workspaces on OOM, pending ones only as a last resort)
+        plan._pending_gen = plan.generation if any(ctx.needs_input_grad) else None
         ctx.param_ids = tuple(id(p) for p in params)
         ctx.slices = [(off, n, shape) for (_name, shape, off, n) in plan.params]
         return logits_cl.permute(0, 4, 1, 2, 3)
@@ -819,6 +830,7 @@ class _SwinFunction(torch.autograd.Function):
                               "backward of this one; the engine keeps one forward's activations")
         g_cl = g.permute(0, 2, 3, 4, 1).contiguous()
         dflat = plan.backward(g_cl, ctx.flat, grad_hook=ctx.grad_hook)
+        plan._pending_gen = None
         _mark_covered(ctx.grad_hook, ctx.param_ids)
         grads = [dflat[o:o + n].view(s) for (o, n, s) in ctx.slices]
         return (None, None, None, None, *grads)

@@ -161,11 +161,21 @@ class forced_branches:
     def __init__(self, masks):
         self.masks = masks
         self.npool = 0
+        self._dev = {}
+
+    def _m(self, key, like):
+        """The mask on the device the oracle runs on (moved once)."""
+        m = self.masks[key]
+        if m.device != like.device:
+            if key not in self._dev:
+                self._dev[key] = m.to(like.device)
+            m = self._dev[key]
+        return m
 
     def _lrelu(self, P, pre, inp, ksd):
         y = F.conv3d(inp, P[pre + ".0.weight"], None, padding=(ksd // 2, 1, 1))
         r = F.instance_norm(y, weight=P[pre + ".1.weight"], bias=P[pre + ".1.bias"], eps=1e-5)
-        return torch.where(self.masks[pre], r, 0.01 * r)
+        return torch.where(self._m(pre, r), r, 0.01 * r)
 
     def _pool(self, t):
         k = self.npool % 3
@@ -174,7 +184,7 @@ class forced_branches:
         v = t[..., :H_ // 2 * 2, :W_ // 2 * 2].reshape(B_, C_, D_, H_ // 2, 2, W_ // 2, 2)
         v = v.permute(0, 1, 2, 3, 5, 4, 6)
         v = v.reshape(B_, C_, D_, H_ // 2, W_ // 2, 4)
-        return v.gather(-1, self.masks[f"pool{k + 1}"].unsqueeze(-1)).squeeze(-1)
+        return v.gather(-1, self._m(f"pool{k + 1}", v).unsqueeze(-1)).squeeze(-1)
 
     def __enter__(self):
         self._orig = O.conv_in_lrelu, O.maxpool

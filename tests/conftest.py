@@ -47,3 +47,26 @@ def _heartbeat(request):
     th.start()
     yield
     stop.set()
+
+
+# Long tests last.  pytest collects files alphabetically, which put the minutes-long
+# baseline-size parity tests first: a run cut off by a time limit then lost the cheap
+# per-op / network / 3DUNet / Swin / train tests instead of the expensive ones.  Stable
+# sort: every other test keeps its order.
+_LONG = (
+    ("test_gpu_sharded.py", "test_depth_sharded_world8_f16x3_overlapped"),
+    ("test_gpu_volume512.py", None),
+    ("test_gpu_baseline_sizes.py", None),
+)
+
+
+def _long_rank(item):
+    fname = pathlib.Path(str(item.fspath)).name
+    for i, (f, name) in enumerate(_LONG):
+        if fname == f and (name is None or item.name.split("[")[0] == name):
+            return i + 1
+    return 0
+
+
+def pytest_collection_modifyitems(session, config, items):
+    items.sort(key=_long_rank)

@@ -227,8 +227,8 @@ def test_data_parallel_hooks_every_submodule_and_falls_back(monkeypatch):
     calls = []
     monkeypatch.setattr(Dd, "world", lambda group=None: 2)
     monkeypatch.setattr(Dd, "global_valid_count", lambda *a, **k: None)
-    monkeypatch.setattr(Dd, "allreduce_gradients", lambda params, group=None: calls.append(1))
-    monkeypatch.setattr(Dd, "global_loss", lambda ce, conf, K, group=None: (ce, ce, conf))
+    monkeypatch.setattr(Dd, "allreduce_gradients", lambda params, group=None, **k: calls.append(1))
+    monkeypatch.setattr(Dd, "global_loss", lambda ce, conf, K, group=None, **k: (ce, ce, conf))
     monkeypatch.setattr(Hh, "ce_dice_parts",
                         lambda lg, y, K, ig, count_override=None: (lg.sum(), None, lg.sum()))
     dp = Dd.DataParallelSPFF(m, 3)
@@ -271,8 +271,8 @@ def test_data_parallel_reduces_parameters_outside_the_plan(monkeypatch):
     monkeypatch.setattr(Dd, "world", lambda group=None: 2)
     monkeypatch.setattr(Dd, "global_valid_count", lambda *a, **k: None)
     monkeypatch.setattr(Dd, "allreduce_gradients",
-                        lambda params, group=None: reduced.append([id(p) for p in params]))
-    monkeypatch.setattr(Dd, "global_loss", lambda ce, conf, K, group=None: (ce, ce, conf))
+                        lambda params, group=None, **k: reduced.append([id(p) for p in params]))
+    monkeypatch.setattr(Dd, "global_loss", lambda ce, conf, K, group=None, **k: (ce, ce, conf))
     monkeypatch.setattr(Hh, "ce_dice_parts",
                         lambda lg, y, K, ig, count_override=None: (lg.sum(), None, lg.sum()))
     dp = Dd.DataParallelSPFF(m, 3)

@@ -8,7 +8,7 @@ Marked gpu; the CPU oracle runs on the host cores of the GPU box.
   tests/test_oracle_golden.py): logits within 1e-3 (north star), argmax
   identical except at near-ties (reference top-2 margin < 2 max|dlogit|;
   counted and printed), loss within 1e-5 relative, every parameter gradient
-  within 1e-3 relative L2 of a kink-consistent fp32 oracle backward (head/tail
+  within 1e-3 relative L2 of a kink-consistent fp64 oracle backward (head/tail
   elements printed).  Reference: models.py:693-701, helpers.py:797-803.
 * configs[3] path: the depth-sharded engine at production H = W = 512 --
   world 2 on one GPU through host-staged gloo, volume 1 x 5 x 16 x 512^2 --
@@ -27,7 +27,9 @@ config 2 against the unconstrained oracle).  So the logits, argmax and loss are
 checked against the unconstrained fp32 oracle, and the gradients against the
 fp64 oracle whose LeakyReLU signs and pool argmaxes are the engine's own
 (tests/test_gpu_parity.engine_branch_masks, tests/_kink.forced_branches),
-within max(1e-3, 4 x the fp32 oracle's own distance from it) relative L2.
+within 1e-3 relative L2 (GRAD_DEV below: where that fp64 backward is evaluated).
+
+The module's tests are the suite's longest; tests/conftest.py runs them last.
 """
 import os
 import socket
@@ -75,22 +77,33 @@ def _oracle_forward(st, x, y):
     return logits, float(loss)
 
 
+# Where the fp64 gradient oracle runs.  The restatement is CPU code (pinned to the
+# reference's fixtures on the CPU, tests/test_oracle_golden.py); at these sizes its fp64
+# backward takes ~130 s per case on the box's 16 host cores, so by default PyTorch
+# evaluates the same functions on the GPU in fp64 (vol2col + rocBLAS dgemm, hipFFT: no
+# MIOpen and no engine code), which tests/test_gpu_parity.py::
+# test_oracle_device_evaluation_matches_cpu pins to the CPU evaluation.  The logits,
+# argmax, loss and metrics are still judged against the fp32 oracle on the CPU.
+GRAD_DEV = os.environ.get("SPFF_ORACLE_GRAD_DEVICE", "cuda")
+
+
 def _oracle_grads(st, x, y, masks):
-    """fp64 and fp32 oracle gradients with the engine's LeakyReLU / MaxPool branch
-    decisions.  fp64 is the reference the engine is judged against; the fp32 run
-    measures how far the reference's own arithmetic lands from it at this size."""
+    """fp64 oracle gradients with the engine's LeakyReLU / MaxPool branch decisions
+    (the engine is judged against these, within 1e-3 relative L2).  Returns
+    (fp64 grads, None): the fp32 oracle backward that used to widen the tolerance is
+    not run (its distance from fp64 at these sizes was <= 1.3e-4, below the floor)."""
     from oracle import spff_oracle as O
     from _kink import forced_branches
     torch.set_num_threads(_threads())
-    out = []
-    for dt in (torch.float64, torch.float32):
-        P = O.params_from_state({k: v for k, v in st.items() if not k.endswith("._mask")},
-                                dtype=dt)
-        with forced_branches(masks):
-            O.fwd_bwd(P, x.to(dt), y, _oracle_cfg(x.shape[1]))
-        out.append({k: v.grad.clone() for k, v in P.items()})
-        del P
-    return out
+    P = O.params_from_state({k: v for k, v in st.items() if not k.endswith("._mask")},
+                            dtype=torch.float64, device=GRAD_DEV)
+    with forced_branches(masks):
+        O.fwd_bwd(P, x.to(GRAD_DEV, torch.float64), y.to(GRAD_DEV), _oracle_cfg(x.shape[1]))
+    g64 = {k: v.grad.detach().cpu() for k, v in P.items()}
+    del P
+    if GRAD_DEV != "cpu":
+        torch.cuda.empty_cache()
+    return g64, None
 
 
 def _engine_masks(core, xshape, st):
@@ -150,7 +163,7 @@ def _compare_metrics(tag, conf, labels, ref_logits, nflips, K=K13):
 
 def _compare(tag, lg, loss, grads, ref_logits, ref_loss, ref_grads, loss_rtol=1e-5, scales=None,
              conf=None, labels=None):
-    """``ref_grads`` = (fp64, fp32) kink-consistent oracle gradients: every engine
+    """``ref_grads`` = (fp64, fp32 or None) kink-consistent oracle gradients: every engine
     gradient within max(1e-3, 4 x the fp32 oracle's own distance) relative L2 of fp64
     (relative to ``scales[k]`` instead of |g64| where given).  ``conf`` (the engine's
     [K, K+1] confusion) + ``labels``: also the metric tuple (_compare_metrics)."""
@@ -175,7 +188,7 @@ def _compare(tag, lg, loss, grads, ref_logits, ref_loss, ref_grads, loss_rtol=1e
         r = g64.double().reshape(-1)
         nrm = max(float(r.norm()), (scales or {}).get(k, 0.0), 1e-30)
         rel = float((g - r).norm()) / nrm
-        rel32 = float((g32s[k].double().reshape(-1) - r).norm()) / nrm
+        rel32 = float((g32s[k].double().reshape(-1) - r).norm()) / nrm if g32s is not None else 0.0
         tol = max(1e-3, 4 * rel32)
         rows.append((rel, rel32, k, g[0].item(), r[0].item(), g[-1].item(), r[-1].item()))
         if rel > tol:

@@ -97,3 +97,66 @@ def test_dp_engine_matches_full_batch(tmp_path, bucket):
         e = float(np.abs(parts[0]["g_" + k] - g).max()) / sc
         assert e <= 1e-4, (k, e)
         np.testing.assert_array_equal(parts[1]["g_" + k], parts[0]["g_" + k])
+
+
+@pytest.mark.timeout(300)
+def test_rccl_world1_bucketed_step(tmp_path):
+    """The RCCL device path on the box's one GPU: a world-1 "nccl" process group
+    (RCCL on ROCm), one DataParallelSPFF step with every collective forced on -- the
+    valid-count all-reduce, the bucketed gradient all-reduces issued from the engine's
+    grad hook WHILE its backward is enqueued, the fp64 loss/confusion all-reduce -- and
+    TorchDepthColl's device branches (all_reduce on the engine's side stream; a halo
+    with no neighbour).  A SUM over one rank is the identity, so the gradients and the
+    confusion must equal the step without a process group BITWISE (the loss to 2e-7).  Two ranks on one
+    GPU are refused by RCCL (ncclInvalidUsage: Duplicate GPU), so the sharded halo's
+    device exchange between peers needs >= 2 GPUs."""
+    import innovative3D.helpers as Hh
+    from innovative3D.distributed import DataParallelSPFF
+    from innovative3D.sharded import TorchDepthColl
+    assert not dist.is_initialized()
+    torch.cuda.set_device(0)
+    lit = _model()
+    x, y = _data()
+    x, y = x[:1].cuda(), y[:1].cuda()
+    logits = lit(x)
+    loss0, conf0 = Hh.ce_dice_with_confusion(logits, y, K, 255)
+    loss0.backward()
+    torch.cuda.synchronize()
+    ref = {k: p.grad.clone() for k, p in lit.named_parameters() if p.grad is not None}
+    nflat = sum(g.numel() for g in ref.values())
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}",
+                            rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        backend = dist.get_backend()
+        print(f"backend {backend}, world {dist.get_world_size()}")
+        assert backend == "nccl"
+        dp = DataParallelSPFF(lit, K, 255, bucket_bytes=1 << 14, force_collectives=True)
+        loss, conf = dp.step(x, y)
+        torch.cuda.synchronize()
+        spans = sorted(dp.bucketer.launched)
+        print(f"{len(spans)} bucketed RCCL all-reduces; loss {float(loss):.8f} vs {float(loss0):.8f}")
+        assert dp.bucketer.begun == 1 and len(spans) > 3
+        assert spans[0][0] == 0 and all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+        assert spans[-1][1] == nflat
+        # the global loss is re-formed from the all-reduced fp64 [CE, confusion] buffer
+        # (distributed.global_loss): equal to the last fp32 bit or one ulp
+        assert abs(float(loss) - float(loss0)) <= 2e-7 * abs(float(loss0))
+        assert torch.equal(conf.cpu(), conf0.cpu().to(conf.dtype))
+        for k, p in lit.named_parameters():
+            if p.grad is not None:
+                assert torch.equal(p.grad, ref[k]), k
+        # TorchDepthColl's device branches, on a side stream as the engine hands them
+        coll = TorchDepthColl()
+        assert not coll.host
+        s2 = torch.cuda.Stream()
+        t = torch.randn(1000, dtype=torch.float64, device="cuda")
+        slab = torch.randn(6 * 64, device="cuda")
+        t0, slab0 = t.clone(), slab.clone()
+        s2.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s2):
+            coll.allreduce(t)
+            coll.halo(slab, 64, 4)
+        torch.cuda.synchronize()
+        assert torch.equal(t, t0) and torch.equal(slab, slab0)
+    finally:
+        dist.destroy_process_group()

@@ -94,7 +94,8 @@ def test_network_matches_reference(name, mth):
 
 def check_grads(grads, ref64, ref32, absb, st, mth):
     """Every engine gradient vs the kink-consistent fp64 oracle: max|g - g64| / scale
-    within max(1e-3, 8 x the fp32 oracle's own error) (bf16x3: max(5e-3, 64 x)); scale
+    within max(1e-3, 8 x the fp32 oracle's own error) (bf16x3: max(5e-3, 64 x); the
+    floor alone when ``ref32`` is None); scale
     = max over the tensor of sum_b |per-sample g_b| (absb); FourierGate mag_scale is
     judged against the sum of its absolute terms."""
     rows, bad = [], []
@@ -116,7 +117,7 @@ def check_grads(grads, ref64, ref32, absb, st, mth):
                            absb[mk].reshape(-1)).sum()
             scale = max(scale, float(terms) / max(mag, 1e-12))
         e_gpu = float(np.abs(g - g64).max()) / scale
-        e_32 = float(np.abs(ref32[kk] - g64).max()) / scale
+        e_32 = float(np.abs(ref32[kk] - g64).max()) / scale if ref32 is not None else 0.0
         tol = max(5e-3, 64 * e_32) if mth == "bf16x3" else max(1e-3, 8 * e_32)
         rows.append((e_gpu, e_32, kk))
         if e_gpu > tol:
@@ -186,8 +187,10 @@ def oracle_grads(d, masks):
     return oracle_grads_st(cfg_of(d["meta"]), state_of(d), d["x"], d["labels"], masks)
 
 
-def oracle_grads_st(cfg, st, x, labels, masks):
-    """fp64 and fp32 oracle parameter gradients (CPU) whose LeakyReLUs take the
+def oracle_grads_st(cfg, st, x, labels, masks, device="cpu", fp32=True):
+    """fp64 and fp32 oracle parameter gradients (CPU; ``device`` evaluates the same
+    restatement through PyTorch's fp64 device kernels, ``fp32=False`` skips the fp32
+    run and returns None for it) whose LeakyReLUs take the
     given sign patterns; also returns how many entries differ from the fp64
     oracle's own pattern (knife-edge flips) and sum_b |g_b| (fp64 per-sample
     gradients with the global CE normalisation; sum_b g_b = g exactly since
@@ -199,6 +202,7 @@ def oracle_grads_st(cfg, st, x, labels, masks):
     nflip = [0]
     orig, orig_pool = O.conv_in_lrelu, O.maxpool
     npool = [0]
+    masks = {k: v.to(device) for k, v in masks.items()}
 
     def pool_hooked(t):
         k = npool[0] % 3
@@ -223,24 +227,28 @@ def oracle_grads_st(cfg, st, x, labels, masks):
     O.conv_in_lrelu = hooked
     O.maxpool = pool_hooked
     try:
-        for dt in (torch.float64, torch.float32):
-            P = O.params_from_state(st, dtype=dt)
-            O.fwd_bwd(P, torch.from_numpy(d["x"]).to(dt), torch.from_numpy(d["labels"]), cfg)
-            out.append({k: v.grad.double().numpy() for k, v in P.items()})
+        for dt in ((torch.float64, torch.float32) if fp32 else (torch.float64,)):
+            P = O.params_from_state(st, dtype=dt, device=device)
+            O.fwd_bwd(P, torch.from_numpy(d["x"]).to(device, dt),
+                      torch.from_numpy(d["labels"]).to(device), cfg)
+            out.append({k: v.grad.double().cpu().numpy() for k, v in P.items()})
+            del P
+        if not fp32:
+            out.append(None)
         B = d["x"].shape[0]
         absb = {k: np.abs(v) for k, v in out[0].items()}
         if B > 1:
-            yall = torch.from_numpy(d["labels"])
+            yall = torch.from_numpy(d["labels"]).to(device)
             N = int((yall != 255).sum())
             full = dict(masks)
             absb = None
             for b in range(B):
                 for k in full:
                     masks[k] = full[k][b:b + 1]
-                P = O.params_from_state(st, dtype=torch.float64)
-                lg = O.forward(P, torch.from_numpy(d["x"][b:b + 1]).double(), cfg)
+                P = O.params_from_state(st, dtype=torch.float64, device=device)
+                lg = O.forward(P, torch.from_numpy(d["x"][b:b + 1]).to(device, torch.float64), cfg)
                 (F.cross_entropy(lg, yall[b:b + 1], ignore_index=255, reduction="sum") / N).backward()
-                gb = {k: np.abs(v.grad.numpy()) for k, v in P.items()}
+                gb = {k: np.abs(v.grad.cpu().numpy()) for k, v in P.items()}
                 absb = gb if absb is None else {k: absb[k] + gb[k] for k in absb}
             for k in full:
                 masks[k] = full[k]
@@ -369,3 +377,55 @@ def _engine_vs_oracle(in_ch, K, base, mth):
     ref64, ref32, nflip, absb = oracle_grads_st(cfg, st, x.numpy(), y.numpy(), masks)
     named = dict(core.named_parameters(remove_duplicate=False))
     check_grads({k: named[k].grad for k in ref64}, ref64, ref32, absb, st, mth)
+
+
+@pytest.mark.parametrize("case", ["fx3b_fgate_odd_b2", "registry_2x5x8x64x64"])
+def test_oracle_device_evaluation_matches_cpu(case):
+    """The full-size gradient checks (tests/test_gpu_baseline_sizes.py, the world-8
+    sharded test) evaluate the fp64 oracle through PyTorch's own fp64 device kernels
+    instead of the CPU: pin that evaluation to the CPU one -- the same restatement, the
+    same inputs, fp64 on both sides -- on a reference fixture (FourierGate at odd D,
+    batch 2) and on a registry-layout (K 13, base 32) batch at 64^2 with the engine's
+    own branch decisions forced on both (tests/_kink.forced_branches)."""
+    from _kink import forced_branches
+    if case.startswith("fx"):
+        d = load(case)
+        cfg, st = cfg_of(d["meta"]), state_of(d)
+        x, y = torch.from_numpy(d["x"]), torch.from_numpy(d["labels"])
+        masks = None
+    else:
+        from innovative3D.synthetic import synthetic_batch
+        from innovative3D.weightgen import synth_state
+        core = M.build_spct_energyfilm_fourier(num_classes=13, base=32, in_channels=5)
+        for b in core._blocks():
+            b.fgate._ensure_mask(8, "cpu")
+        st = synth_state([(k, tuple(v.shape)) for k, v in core.state_dict().items()], seed=3)
+        cfg = O.SpffCfg(in_ch=5, num_classes=13, base=32)
+        x, y = synthetic_batch(2, 5, 8, 64, 64, 13, ignore_frac=0.01, seed=3)
+        core.load_state_dict({k: torch.from_numpy(v) for k, v in st.items()})
+        core = core.to(DEV)
+        lg = core(x.to(DEV))
+        Hh.ce_dice_with_confusion(lg, y.to(DEV), 13, 255)[0].backward()
+        torch.cuda.synchronize()
+        masks = engine_branch_masks(core, tuple(x.shape), st, cfg)
+        del core, lg
+    st = {k: v for k, v in st.items() if not k.endswith("._mask")}
+    out = []
+    for dev in ("cpu", DEV):
+        P = O.params_from_state(st, dtype=torch.float64, device=dev)
+        if masks is None:
+            lg, loss, _ce, _dice = O.fwd_bwd(P, x.to(dev, torch.float64), y.to(dev), cfg)
+        else:
+            with forced_branches(masks):
+                lg, loss, _ce, _dice = O.fwd_bwd(P, x.to(dev, torch.float64), y.to(dev), cfg)
+        out.append((lg.cpu(), float(loss), {k: v.grad.cpu() for k, v in P.items()}))
+    (lc, lsc, gc), (ld, lsd, gd) = out
+    e = float((lc - ld).abs().max()) / float(lc.abs().max())
+    print(f"{case}: fp64 oracle on {DEV} vs cpu: logits {e:.2e} of max, loss {lsc:.15f} vs {lsd:.15f}")
+    assert e <= 1e-12 and abs(lsc - lsd) <= 1e-12 * abs(lsc)
+    worst = 0.0
+    for k in gc:
+        r = float((gc[k] - gd[k]).norm()) / max(float(gc[k].norm()), 1e-300)
+        worst = max(worst, r)
+        assert r <= 1e-8, f"{k}: {r:.2e}"
+    print(f"  worst gradient rel L2 {worst:.2e}")

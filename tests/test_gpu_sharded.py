@@ -99,12 +99,14 @@ def _gather_masks(parts, axis):
     return masks
 
 
-def _check_vs_oracle(parts, axis, st, cfg, x, y, mth):
+def _check_vs_oracle(parts, axis, st, cfg, x, y, mth, device="cpu"):
     """the sharded engine's gradients (rank 0; all ranks hold the same all-reduced
-    gradient) vs the fp64 oracle with the sharded engine's own branch decisions"""
+    gradient) vs the fp64 oracle with the sharded engine's own branch decisions
+    (``device`` != "cpu": the fp64 oracle alone, evaluated there, floor tolerance)"""
     from test_gpu_parity import check_grads, oracle_grads_st
     masks = _gather_masks(parts, axis)
-    ref64, ref32, nflip, absb = oracle_grads_st(cfg, st, x.numpy(), y.numpy(), masks)
+    ref64, ref32, nflip, absb = oracle_grads_st(cfg, st, x.numpy(), y.numpy(), masks,
+                                                device=device, fp32=device == "cpu")
     print(f"  branch decisions differing from the fp64 oracle's own: {nflip}")
     check_grads({k: parts[0]["g_" + k] for k in ref64}, ref64, ref32, absb, st, mth)
 
@@ -321,4 +323,4 @@ def test_depth_sharded_world8_f16x3_overlapped(tmp_path):
     for k in (f for f in parts[0].files if f.startswith("g_")):
         for p in parts[1:]:
             np.testing.assert_array_equal(p[k], parts[0][k])
-    _check_vs_oracle(parts, 2, st, _cfg(W8_K, W8_BASE, C), x, y, mth)
+    _check_vs_oracle(parts, 2, st, _cfg(W8_K, W8_BASE, C), x, y, mth, device="cuda")
