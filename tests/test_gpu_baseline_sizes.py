@@ -195,7 +195,8 @@ def _compare(tag, lg, loss, grads, ref_logits, ref_loss, ref_grads, loss_rtol=1e
             bad.append(f"{k}: rel L2 {rel:.2e} (fp32 oracle {rel32:.2e})")
     rows.sort(reverse=True)
     for rel, rel32, k, gh, rh, gt, rt in rows[:8]:
-        print(f"  {k:34s} relL2 {rel:.2e} (fp32 oracle {rel32:.2e}) head {gh:+.6e} vs {rh:+.6e} "
+        f32s = f"fp32 oracle {rel32:.2e}" if g32s is not None else "vs fp64"
+        print(f"  {k:34s} relL2 {rel:.2e} ({f32s}) head {gh:+.6e} vs {rh:+.6e} "
               f"tail {gt:+.6e} vs {rt:+.6e}")
     assert not bad, "; ".join(bad)
 
