@@ -107,13 +107,48 @@
 #ifndef SPFF_XPRIO
 #define SPFF_XPRIO 1
 #endif
+#ifndef SPFF_XFPIN
+// 1: the next chunk's halo loads (and the fused activation's coefficients) are issued right
+// after the chunk-boundary barrier, pinned there by a scheduling barrier.  Without it the
+// compiler sank them to the last k-step before the mid-chunk scale barrier (ISA: the loads
+// at MFMA 100-144 of the 144 before the vmcnt waits), so every wave waited out their whole
+// latency at that barrier
+#define SPFF_XFPIN 1
+#endif
+#ifndef SPFF_XPIPE
+// 1: the 16/32-wide X16 k-loop is software-pipelined by one row block: the A fragments of
+// row block rb + 1 (and, at the last row block, the next quad's B fragments and first A
+// fragments) are read from LDS before row block rb's MFMAs, kept in that order by
+// scheduling-group barriers.  Without it the compiler read each A fragment two MFMAs
+// (32 cycles) before its use and waited lgkmcnt(0) there, i.e. most of the LDS latency
+// exposed at every row block
+#define SPFF_XPIPE 1
+#endif
+#ifndef SPFF_XEARLYW
+// 1: the first chunk's weight DMA is issued at the kernel start, before the first halo
+// fetch, so its L2 latency overlaps the halo's HBM latency instead of following it at the
+// first chunk-boundary barrier (in-kernel stamps: prologue 9-13 us per tile, of which
+// 1-1.5 us that barrier and ~0.7 us the DMA issue)
+#define SPFF_XEARLYW 1
+#endif
 #ifndef SPFF_XSTORE
 // 1: the output tile goes through LDS (conflict-free [row][BN + 4] image in MFMA row order)
 // and leaves as 16-byte row stores, instead of one 4-byte store per accumulator element
 #define SPFF_XSTORE 1
 #endif
 
+#ifndef SPFF_XSTAMP
+// timing diagnostics only (variant builds): per workgroup of k_conv3d_fwd_x, s_memtime at
+// kernel start, first MFMA, end of the k-loop and end, plus s_memrealtime at start / end
+// and the CU it ran on, into g_xstamp; spff_debug_xstamps() copies them to the host
+#define SPFF_XSTAMP 0
+#endif
+
 namespace spff {
+#if SPFF_XSTAMP
+constexpr int XSTAMP_N = 1 << 15, XSTAMP_W = 16;
+__device__ unsigned long long g_xstamp[XSTAMP_N * XSTAMP_W];
+#endif
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -267,9 +302,9 @@ __host__ __device__ constexpr int xt_t2() {
 template <int BN, int KD, int NS, int TD, int TH>
 constexpr size_t xt_lds_bytes() {
   // operand images; the epilogue reuses the space for the output tile [TD TH 16][BN + 4]
-  // fp32 plus the fused statistics' [8 waves][BN] partials
+  // fp32 plus the fused statistics' two [NW][BN] partial-sum tables
   const size_t ops = (size_t)nplanes(NS) * (xt_npos<KD, TD, TH>() + xt_t2<KD>() * BN) * 16;
-  const size_t out = SPFF_XSTORE ? (size_t)TD * TH * 16 * (BN + 4) * 4 + 8 * BN * 4 : 0;
+  const size_t out = SPFF_XSTORE ? (size_t)TD * TH * 16 * (BN + 4) * 4 + 16 * BN * 4 : 0;
   return ops > out ? ops : out;
 }
 // tile depth of a BN-wide launch (host side: launches, fused-statistics layout)
@@ -296,6 +331,9 @@ static int ns_of(int math) {
   return math == SPFF_MATH_F16X3 ? NS_F16 : math == SPFF_MATH_BF16X3 ? 2 : 3;
 }
 
+// MFMAs per multiply-add of an NP-plane operand pair (the split products)
+__host__ __device__ constexpr int nprod(int np) { return np == 3 ? 6 : np == 2 ? 3 : 1; }
+
 // MFMA row r (0..15) of a 16-row block -> w within the W-row (see x_quads)
 __device__ __forceinline__ int x16_w(int r) {
   return (r >= 4 && r < 12) ? 2 * (r - 4) : (r < 4 ? 2 * r + 1 : 2 * r - 15);
@@ -311,6 +349,15 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : (BN <= 32 && NS == NS_F16 &&
     float* __restrict__ stats, int ntiles, int td0, int tds, int th0, int ths,
     const unsigned* __restrict__ wmx) {
   constexpr int XT_THREADS = NW * 64;
+#if SPFF_XSTAMP
+  const unsigned long long st_t0 = __builtin_amdgcn_s_memtime();
+  const unsigned long long st_r0 = __builtin_amdgcn_s_memrealtime();
+  unsigned long long st_t1 = 0, st_t2 = 0, st_pa = 0, st_pb = 0, st_pc = 0, st_c1a = 0,
+                     st_c1b = 0, st_c1c = 0, st_c1d = 0;
+#define XST(v) (v = __builtin_amdgcn_s_memtime())
+#else
+#define XST(v)
+#endif
   // planes per operand; HF: two fp16 planes of the scaled operands (NS_F16, bf16split.h)
   constexpr int NP = nplanes(NS);
   constexpr bool HF = NS == NS_F16;
@@ -447,6 +494,28 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : (BN <= 32 && NS == NS_F16 &&
       pok |= ok ? (1u << k) : 0u;
     }
   }
+  // the chunk's 8 (al, de) pairs of the fused input activation, loaded once per chunk from
+  // uniform addresses (scalar loads) and selected per lane: a thread's 4 channels are the
+  // lower or upper half (XT_THREADS is even: q = tid & 1 for all k).  Loaded per halo float4
+  // they became 9 dependent vector-memory round trips, each behind a vmcnt(0)
+  auto act_coef_kc = [&](int kc, float (&a)[4], float (&e)[4]) {
+    const int64_t o = __builtin_amdgcn_readfirstlane((int)((int64_t)b * x.ld0 + kc * 8));
+    const float* ap = x.al + o;
+    const float* dp = x.de + o;
+    const bool hi = tid & 1;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float alo = ap[j], ahi = ap[4 + j], elo = dp[j], ehi = dp[4 + j];
+      a[j] = hi ? ahi : alo;
+      e[j] = hi ? ehi : elo;
+    }
+  };
+  // (SPFF_XFPIN, HF 32-wide tiles) every chunk's coefficients staged in LDS once per tile
+  // (float4 q = the 4 channels 4q..4q+3): prep_max reads them there instead of issuing global
+  // loads of its own (which the scale barrier then waited for, or -- preloaded into registers
+  // with the halo -- which the register allocator waited for at the chunk start)
+  constexpr int XCF = 32;  // float4s per table: channels < 128 (launch_fwd_x checks)
+  __shared__ float4 scf[2][XCF];
   // live = false: a dummy fetch (every quad invalid, loads from clamped addresses) after the
   // last chunk, so that the fetch is unconditional: a conditional one left the registers'
   // old and new values to merge, and the compiler waited for the first loads at the merge
@@ -507,26 +576,18 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : (BN <= 32 && NS == NS_F16 &&
   };
   // HF: the fused input activation (32-wide tiles) and the zero padding applied to the
   // prefetched halo in place, and this thread's max |element| of it
-  // the chunk's 8 (al, de) pairs of the fused input activation, loaded once per chunk from
-  // uniform addresses (scalar loads) and selected per lane: a thread's 4 channels are the
-  // lower or upper half (XT_THREADS is even: q = tid & 1 for all k).  Loaded per halo float4
-  // they became 9 dependent vector-memory round trips, each behind a vmcnt(0)
-  auto act_coef = [&](float (&a)[4], float (&e)[4]) {
-    const int64_t o = __builtin_amdgcn_readfirstlane((int)((int64_t)b * x.ld0 + fkc * 8));
-    const float* ap = x.al + o;
-    const float* dp = x.de + o;
-    const bool hi = tid & 1;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float alo = ap[j], ahi = ap[4 + j], elo = dp[j], ehi = dp[4 + j];
-      a[j] = hi ? ahi : alo;
-      e[j] = hi ? ehi : elo;
-    }
-  };
   auto prep_max = [&]() {
     float m = 0.f;
     float ca[4] = {1.f, 1.f, 1.f, 1.f}, ce[4] = {0.f, 0.f, 0.f, 0.f};
-    if constexpr (BN == 32) if (x.al) act_coef(ca, ce);
+    if constexpr (BN == 32) if (x.al) {
+      if constexpr (HF && SPFF_XFPIN) {
+        const float4 fa = scf[0][2 * fkc + (tid & 1)], fe = scf[1][2 * fkc + (tid & 1)];
+        ca[0] = fa.x; ca[1] = fa.y; ca[2] = fa.z; ca[3] = fa.w;
+        ce[0] = fe.x; ce[1] = fe.y; ce[2] = fe.z; ce[3] = fe.w;
+      } else {
+        act_coef_kc(fkc, ca, ce);
+      }
+    }
 #pragma unroll
     for (int k = 0; k < RH; ++k) {
       const bool ok = (hvalid >> k) & 1u;
@@ -618,7 +679,7 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : (BN <= 32 && NS == NS_F16 &&
         reinterpret_cast<uint2*>(Xs + p * NPOS + (i >> 1))[i & 1] = hs[k][p];
     }
   };
-  auto stash = [&](int kc, bool first, bool halo = true) {
+  auto stash = [&](int kc, bool first, bool halo = true, bool wts = true) {
 #pragma unroll
     for (int k = 0; k < RH; ++k) {
       if (!halo) break;
@@ -635,6 +696,7 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : (BN <= 32 && NS == NS_F16 &&
     const uint4* src = wsrc + (int64_t)kc * NWU + lane;
 #pragma unroll
     for (int k = 0; k < (NPC + NW - 1) / NW; ++k) {
+      if (!wts) break;
       if (SPFF_XDIAG == 3 && !first) break;
       const int pc = wave + k * NW;
       if (k * NW + NW <= NPC || pc < NPC)
@@ -649,9 +711,24 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : (BN <= 32 && NS == NS_F16 &&
   // writes fp32 partial sums that k_splitk_reduce adds in a fixed order
   const int kc0 = part ? blockIdx.z * kps : 0;
   const int kc1 = part ? min(nkc, kc0 + kps) : nkc;
+  // (SPFF_XEARLYW) the first chunk's weights first: the Ws image is free at the start
+  if constexpr (SPFF_XEARLYW) stash(kc0, true, false, true);
   fetch(kc0);
+  // (after the halo loads are in flight: these loads overlap them)
+  if constexpr (BN == 32 && HF && SPFF_XFPIN) if (x.al) {
+    for (int i = tid; i < 2 * XCF; i += XT_THREADS) {
+      const int q = i % XCF, t = i / XCF;
+      float4 v = make_float4(t ? 0.f : 1.f, t ? 0.f : 1.f, t ? 0.f : 1.f, t ? 0.f : 1.f);
+      if (q < 2 * nkc) v = *reinterpret_cast<const float4*>((t ? x.de : x.al) + (int64_t)b * x.ld0 + 4 * q);
+      scf[t][q] = v;
+    }
+    __syncthreads();
+  }
   if constexpr (HF) {
-    exc = exn = block_scale(prep_max(), kc0 & 1);
+    const float m0 = prep_max();
+    XST(st_pa);
+    exc = exn = block_scale(m0, kc0 & 1);
+    XST(st_pb);
     sx = exp2i(exn);
   }
 #pragma unroll
@@ -674,6 +751,7 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : (BN <= 32 && NS == NS_F16 &&
         store_one(k);
       }
     }
+    if (kc == kc0 + 1) XST(st_c1a);
     if (kc != kc0) {
       // sign-alternating accumulation: odd chunks carry negated weights, so the
       // accumulator holds (-1)^kc x the partial sum; flip it at every chunk boundary
@@ -695,9 +773,54 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : (BN <= 32 && NS == NS_F16 &&
       exc = exn;
       if (!LATE) __syncthreads();
     }
-    if (SPFF_XDIAG != 1 || kc == kc0) stash(kc, kc == kc0, !(LATE && kc != kc0));
+    if (kc == kc0 + 1) XST(st_c1b);
+    if (SPFF_XDIAG != 1 || kc == kc0)
+      stash(kc, kc == kc0, !(LATE && kc != kc0), !(SPFF_XEARLYW && kc == kc0));
+    if (kc == kc0) XST(st_pc);
+    if (kc == kc0 + 1) XST(st_c1c);
     __syncthreads();  // (vmcnt(0): the weight DMA has landed)
+    if (kc == kc0 + 1) XST(st_c1d);
     fetch(kc + 1 < kc1 ? kc + 1 : kc, kc + 1 < kc1);
+    // (SPFF_XFPIN) issue those loads here, a whole J0 k-steps before the scale barrier needs
+    // them -- not where the scheduler would sink them, next to that barrier
+    if constexpr (SPFF_XFPIN) __builtin_amdgcn_sched_barrier(0x7);  // (ALU may cross)
+#if SPFF_XSTAMP
+    if (kc == kc0) st_t1 = __builtin_amdgcn_s_memtime();
+#endif
+    // (XPIPE) the fragments of the current row block, carried across the unrolled k-loop
+    constexpr bool XPIPE = X16 && SPFF_XPIPE && BN <= 32 && !HR;  // (HR: 249 -> 256 VGPRs, spills)
+    const bool pg1 = kg & 1, pg2 = kg & 2;
+    auto psel4 = [&](int c0, int c1, int c2, int c3) {
+      const int lo = pg1 ? c1 : c0, hi = pg1 ? c3 : c2;
+      return pg2 ? hi : lo;
+    };
+    auto ptoff = [&](int j) {
+      return psel4(toff_of(QT.src[4 * j]), toff_of(QT.src[4 * j + 1]), toff_of(QT.src[4 * j + 2]),
+                   toff_of(QT.src[4 * j + 3]));
+    };
+    auto pwtap = [&](int j) {
+      return psel4(QT.tap[4 * j], QT.tap[4 * j + 1], QT.tap[4 * j + 2], QT.tap[4 * j + 3]);
+    };
+    auto loadA = [&](bf16x8 (&a)[NP], int j, int rb) {
+      const int toff = ptoff(j);
+#pragma unroll
+      for (int p = 0; p < NP; ++p) a[p] = __builtin_bit_cast(bf16x8, Xs[p * NPOS + hpos[rb] + toff]);
+    };
+    auto loadB = [&](bf16x8 (&bb)[CB][NP], int j) {
+      const int wtap = pwtap(j);
+#pragma unroll
+      for (int p = 0; p < NP; ++p)
+#pragma unroll
+        for (int cb = 0; cb < CB; ++cb)
+          bb[cb][p] = __builtin_bit_cast(bf16x8, Ws[(p * T2 + wtap) * BN + cb * 16 + l16]);
+    };
+    bf16x8 pa[NP], pb[CB][NP];
+    if constexpr (XPIPE) {
+      if (SPFF_XDIAG != 2) {
+        loadB(pb, 0);
+        loadA(pa, 0, 0);
+      }
+    }
 #pragma unroll
     for (int j = 0; j < (SPFF_XDIAG == 2 ? 0 : NJ); ++j) {
       if constexpr (SPFF_XIGLP >= 0) __builtin_amdgcn_iglp_opt(SPFF_XIGLP);
@@ -723,7 +846,48 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : (BN <= 32 && NS == NS_F16 &&
           if ((j - J0) * SPJ + u < RH) split_one((j - J0) * SPJ + u);
         __builtin_amdgcn_sched_barrier(0x10C);
       }
-      if constexpr (X16) {
+      if constexpr (XPIPE) {
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) {
+          bf16x8 na[NP], nb[CB][NP];
+          const bool last = rb + 1 == RB, more = j + 1 < NJ;
+          // the next row block's reads, then this one's MFMAs: fenced so that neither DS
+          // reads nor MFMAs cross (VALU / SALU may: the halo split still interleaves)
+          __builtin_amdgcn_sched_barrier(0x6);
+          if (!last) {
+            loadA(na, j, rb + 1);
+          } else if (more) {
+            loadB(nb, j + 1);
+            loadA(na, j + 1, 0);
+          }
+          __builtin_amdgcn_sched_barrier(0x6);
+#pragma unroll
+          for (int cb = 0; cb < CB; ++cb) {
+            f32x4 c = acc[rb][cb];
+            if constexpr (NP == 3) {
+              c = mfma16x32<HF>(pa[1], pb[cb][1], c);
+              c = mfma16x32<HF>(pa[0], pb[cb][2], c);
+              c = mfma16x32<HF>(pa[2], pb[cb][0], c);
+            }
+            if constexpr (NP >= 2) {
+              c = mfma16x32<HF>(pa[0], pb[cb][1], c);
+              c = mfma16x32<HF>(pa[1], pb[cb][0], c);
+            }
+            c = mfma16x32<HF>(pa[0], pb[cb][0], c);
+            acc[rb][cb] = c;
+          }
+          if (!last || more) {
+#pragma unroll
+            for (int p = 0; p < NP; ++p) pa[p] = na[p];
+          }
+          if (last && more) {
+#pragma unroll
+            for (int p = 0; p < NP; ++p)
+#pragma unroll
+              for (int cb = 0; cb < CB; ++cb) pb[cb][p] = nb[cb][p];
+          }
+        }
+      } else if constexpr (X16) {
         // lane group kg takes slot 4j + kg of the quad schedule
         // (the four slots' table entries are indexed by the unrolled j only and selected per
         // lane group: a lane-varying index into the constexpr tables made the compiler load
@@ -811,6 +975,9 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : (BN <= 32 && NS == NS_F16 &&
     }
   }
 
+#if SPFF_XSTAMP
+  st_t2 = __builtin_amdgcn_s_memtime();
+#endif
   if ((kc1 - 1) & 1) {
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb)
@@ -831,10 +998,32 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : (BN <= 32 && NS == NS_F16 &&
   constexpr int NROW = TD * TH * TW;
   const bool vec = SPFF_XSTORE && !part && X16 && (Cout & 3) == 0 && (y.split & 3) == 0 &&
                    (y.ld0 & 3) == 0 && (y.ld1 & 3) == 0;
+  // fused InstanceNorm statistics of this output (replaces two HBM passes): per (tile,
+  // channel) the sum over the tile's valid voxels and the sum of squared deviations about
+  // the tile mean; merged per (b, c) in a fixed order by k_in_stats_fin (Chan).
+  // stats[(tile*npad + n)*2 + {0,1}], count[tile].  The column sums share the output
+  // image's barriers: [NW][CB][NCOL] partial sums, then the squared deviations', after the
+  // image when the epilogue staged it.
+  float* sred = reinterpret_cast<float*>(lds4) + (vec ? NROW * OP : 0);
+  float* sred2 = sred + NW * CB * NCOL;
+  const int nd = min(D - d0, TD), nh = min(H - h0, TH), nwv = min(W - w0, TW);
+  const float cnt = (float)(nd * nh * nwv);
+  // lanes holding the same column: 32x32 -- l and l+32; 16x16 -- l, l+16, l+32, l+48
+  auto colsum = [&](float v) {
+    v += __shfl_xor(v, 32);
+    if constexpr (X16) v += __shfl_xor(v, 16);
+    return v;
+  };
+  auto okrow = [&](int rb, int r) {
+    int td, th, tw;
+    vrow(wave * RB + rb, orow(r), td, th, tw);
+    return d0 + td < D && h0 + th < H && w0 + tw < W;
+  };
+  // every wave is past its last operand read
+  if (vec || stats) __syncthreads();
   if (vec) {
-    // every wave is past its last operand read; the image is in MFMA row order (row block
-    // q = wave RB + rb, row r), so a lane's 4 rows x 16 lanes hit 64 distinct banks
-    __syncthreads();
+    // the image is in MFMA row order (row block q = wave RB + rb, row r), so a lane's 4
+    // rows x 16 lanes hit 64 distinct banks
     float* ot = reinterpret_cast<float*>(lds4);
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb)
@@ -843,7 +1032,22 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : (BN <= 32 && NS == NS_F16 &&
 #pragma unroll
         for (int cb = 0; cb < CB; ++cb)
           ot[((wave * RB + rb) * 16 + orow(r)) * OP + cb * NCOL + lcol] = acc[rb][cb][r];
-    __syncthreads();
+  }
+  if (stats) {
+#pragma unroll
+    for (int cb = 0; cb < CB; ++cb) {
+      float sacc = 0.f;
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+        for (int r = 0; r < NREG; ++r) sacc += okrow(rb, r) ? acc[rb][cb][r] : 0.f;
+      sacc = colsum(sacc);
+      if (lane < NCOL) sred[(wave * CB + cb) * NCOL + lcol] = sacc;
+    }
+  }
+  if (vec || stats) __syncthreads();
+  if (vec) {
+    const float* ot = reinterpret_cast<const float*>(lds4);
     constexpr int Q4 = BN / 4;
     for (int i = tid; i < NROW * Q4; i += XT_THREADS) {
       const int row = i / Q4, q = i % Q4;
@@ -882,44 +1086,8 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : (BN <= 32 && NS == NS_F16 &&
       }
     }
   }
-
-  // ---- fused InstanceNorm statistics of this output (replaces two HBM passes):
-  // per (tile, channel) the sum over the tile's valid voxels and the sum of
-  // squared deviations about the tile mean; merged per (b, c) in a fixed order
-  // by k_in_stats_fin (Chan).  stats[(tile*npad + n)*2 + {0,1}], count[tile].
   if (stats) {
-    __syncthreads();  // every wave is past its last LDS operand read
-    // [NW][CB][NCOL], after the output image when the epilogue staged it
-    float* sred = reinterpret_cast<float*>(lds4) + (vec ? NROW * OP : 0);
-    const int nd = min(D - d0, TD), nh = min(H - h0, TH), nwv = min(W - w0, TW);
-    const float cnt = (float)(nd * nh * nwv);
-    bool ok[RB][NREG];
-#pragma unroll
-    for (int rb = 0; rb < RB; ++rb)
-#pragma unroll
-      for (int r = 0; r < NREG; ++r) {
-        int td, th, tw;
-        vrow(wave * RB + rb, orow(r), td, th, tw);
-        ok[rb][r] = d0 + td < D && h0 + th < H && w0 + tw < W;
-      }
-    // lanes holding the same column: 32x32 -- l and l+32; 16x16 -- l, l+16, l+32, l+48
-    auto colsum = [&](float v) {
-      v += __shfl_xor(v, 32);
-      if constexpr (X16) v += __shfl_xor(v, 16);
-      return v;
-    };
     float tsum[CB], mu[CB];
-#pragma unroll
-    for (int cb = 0; cb < CB; ++cb) {
-      float sacc = 0.f;
-#pragma unroll
-      for (int rb = 0; rb < RB; ++rb)
-#pragma unroll
-        for (int r = 0; r < NREG; ++r) sacc += ok[rb][r] ? acc[rb][cb][r] : 0.f;
-      sacc = colsum(sacc);
-      if (lane < NCOL) sred[(wave * CB + cb) * NCOL + lcol] = sacc;
-    }
-    __syncthreads();
 #pragma unroll
     for (int cb = 0; cb < CB; ++cb) {
       float t = 0.f;
@@ -927,7 +1095,6 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : (BN <= 32 && NS == NS_F16 &&
       tsum[cb] = t;
       mu[cb] = t / cnt;
     }
-    __syncthreads();
 #pragma unroll
     for (int cb = 0; cb < CB; ++cb) {
       float qacc = 0.f;
@@ -936,17 +1103,17 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : (BN <= 32 && NS == NS_F16 &&
 #pragma unroll
         for (int r = 0; r < NREG; ++r) {
           const float dl = acc[rb][cb][r] - mu[cb];
-          qacc += ok[rb][r] ? dl * dl : 0.f;
+          qacc += okrow(rb, r) ? dl * dl : 0.f;
         }
       qacc = colsum(qacc);
-      if (lane < NCOL) sred[(wave * CB + cb) * NCOL + lcol] = qacc;
+      if (lane < NCOL) sred2[(wave * CB + cb) * NCOL + lcol] = qacc;
     }
     __syncthreads();
     if (wave == 0 && lane < NCOL) {
 #pragma unroll
       for (int cb = 0; cb < CB; ++cb) {
         float q = 0.f;
-        for (int w = 0; w < NW; ++w) q += sred[(w * CB + cb) * NCOL + lcol];
+        for (int w = 0; w < NW; ++w) q += sred2[(w * CB + cb) * NCOL + lcol];
         const int n = n0 + cb * NCOL + lcol;
         if (n < Cout) {
           stats[((int64_t)tile * npad + n) * 2 + 0] = tsum[cb];
@@ -957,6 +1124,21 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : (BN <= 32 && NS == NS_F16 &&
     if (tid == 0 && nbk == 0)
       stats[(int64_t)ntiles * npad * 2 + tile] = cnt;
   }
+#if SPFF_XSTAMP
+  __syncthreads();
+  if (tid == 0 && blockIdx.x < (unsigned)XSTAMP_N && blockIdx.z == 0) {
+    unsigned long long* o = g_xstamp + (size_t)blockIdx.x * XSTAMP_W;
+    o[0] = st_t0; o[1] = st_t1; o[2] = st_t2; o[3] = __builtin_amdgcn_s_memtime();
+    o[4] = st_r0; o[5] = __builtin_amdgcn_s_memrealtime();
+    unsigned hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    unsigned xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    o[6] = hw; o[7] = xcc;
+    o[8] = st_pa; o[9] = st_pb; o[10] = st_pc;
+    o[11] = st_c1a; o[12] = st_c1b; o[13] = st_c1c; o[14] = st_c1d;
+  }
+#endif
 }
 
 // InstanceNorm3d statistics from the conv's per-tile partials (see the fused
@@ -1042,6 +1224,7 @@ static hipError_t launch_fwd_xh(const Src2& x, const uint4* wx, const Dst2& y, V
   constexpr size_t shm = xt_lds_bytes<BN, KD, NS, TD, TH>();
   static_assert(shm <= (NW == 8 ? 160 : 80) * 1024, "LDS budget");
   if (x.al && BN != 32) return hipErrorInvalidValue;  // fused activation: 32-wide tiles only
+  if (x.al && nkc > 16) return hipErrorInvalidValue;  // the kernel's LDS coefficient table
   // the 16/32-wide kernels hold halo voxel indices in 32 bits (with the halo slices)
   if (BN <= 32 && (int64_t)vol.B * (vol.D + 2 * vol.dh) * vol.H * vol.W >= (int64_t(1) << 31))
     return hipErrorInvalidValue;
@@ -1501,4 +1684,20 @@ hipError_t conv3d_run(const Src2& x, const void* wpack, const Dst2& y, Vol vol, 
                     rup(d.N, conv3d_bn(d.N)), s);
 }
 
+#if SPFF_XSTAMP
+}  // namespace spff
+extern "C" int spff_debug_xstamps_reset() {
+  void* p = nullptr;
+  hipError_t e = hipGetSymbolAddress(&p, HIP_SYMBOL(spff::g_xstamp));
+  if (e != hipSuccess) return (int)e;
+  return (int)hipMemset(p, 0, sizeof(spff::g_xstamp));
+}
+extern "C" int spff_debug_xstamps(unsigned long long* host, int n) {
+  if (n > spff::XSTAMP_N) n = spff::XSTAMP_N;
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(spff::g_xstamp),
+                                  sizeof(unsigned long long) * spff::XSTAMP_W * n, 0,
+                                  hipMemcpyDeviceToHost);
+}
+namespace spff {
+#endif
 }  // namespace spff
