@@ -438,10 +438,19 @@ class Plan:
         covered = [0]
         err = []
 
-        def _ready(_ctx, off, n, _stream_):
+        dev = dlogits_cl.device
+        main_stream = torch.cuda.current_stream(dev).cuda_stream
+
+        def _ready(_ctx, off, n, stream):
             try:
                 covered[0] += int(n)
-                grad_hook.ready(int(off), int(n))
+                if stream and stream != main_stream:
+                    # the engine's weight-gradient stream (those floats are final in its
+                    # order): the bucket's all-reduce is issued there
+                    with torch.cuda.stream(torch.cuda.ExternalStream(stream, device=dev)):
+                        grad_hook.ready(int(off), int(n))
+                else:
+                    grad_hook.ready(int(off), int(n))
                 return 0
             except Exception as e:  # noqa: BLE001 -- reported through the engine status
                 err.append(e)
