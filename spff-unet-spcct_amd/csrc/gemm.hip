@@ -974,7 +974,10 @@ __global__ __launch_bounds__(256) void k_xty(const float* __restrict__ X, int ld
 #pragma unroll
   for (int t = 0; t < TN; ++t) cs[t] = 0.f;
   const int64_t npairs = (ve - vb + 1) / 2;
-  constexpr int U = 4;  // voxel pairs per iteration, loads issued first
+  // voxel pairs per iteration, loads issued first: with one 32 x 32 output block (the head:
+  // 4-byte loads, 13 of 32 Y lanes live) 16 pairs keep ~4x the bytes in flight per wave that
+  // 4 did (the kernel streams x and dy once: bytes in flight, not issue, bound it)
+  constexpr int U = (TM == 1 && TN == 1) ? 16 : 8;
   uint32_t cbd = 0xffffffffu;  // ACT: the (b, d) slab the cached parameters belong to
   float ca[TM], ce[TM], cp[TM], cq[TM];
 #pragma unroll
@@ -1100,12 +1103,15 @@ static hipError_t launch_xty(const float* X, int ldx, int K1, const float* Y, in
 // One block = 32 outputs x 8 split groups; each group sums its splits in order,
 // then the 8 group sums are combined in order (deterministic).  Blocks past
 // nwb reduce the bias (column sums, also summed over ij for the upconv).
-__global__ __launch_bounds__(256) void k_atb_reduce(const float* __restrict__ part,
+constexpr int ATB_RG = 32;  // k-groups of k_atb_reduce: 32 x 32 threads per block
+__global__ __launch_bounds__(ATB_RG * 32) void k_atb_reduce(const float* __restrict__ part,
                                                     const float* __restrict__ csum,
                                                     float* __restrict__ dw, float* __restrict__ db,
                                                     int nsplit, int k1pad, int npad, int K1, int N,
                                                     int Cout, int mode, int nwb) {
-  __shared__ float red[8][33];
+  // thread group g sums slabs g, g + ATB_RG, ... of its block's 32 outputs (up to 1024 slabs:
+  // 32 loads each, many in flight), then group 0 adds the ATB_RG partials in order
+  __shared__ float red[ATB_RG][33];
   const int jl = threadIdx.x & 31, g = threadIdx.x >> 5;
   float s = 0.f;
   bool valid;
@@ -1118,14 +1124,14 @@ __global__ __launch_bounds__(256) void k_atb_reduce(const float* __restrict__ pa
     if (valid) {
       const int64_t stride = (int64_t)k1pad * npad;
 #pragma unroll 4
-      for (int k = g; k < nsplit; k += 8) s += part[k * stride + j];
+      for (int k = g; k < nsplit; k += ATB_RG) s += part[k * stride + j];
     }
   } else {
     co = (blockIdx.x - nwb) * 32 + jl;
     valid = co < Cout;
     if (valid) {
       const int nij = (mode == 0) ? 4 : (mode == 2) ? 8 : 1;
-      for (int k = g; k < nsplit; k += 8)
+      for (int k = g; k < nsplit; k += ATB_RG)
         for (int ij = 0; ij < nij; ++ij) s += csum[(int64_t)k * npad + ij * Cout + co];
     }
   }
@@ -1134,7 +1140,7 @@ __global__ __launch_bounds__(256) void k_atb_reduce(const float* __restrict__ pa
   if (g == 0 && valid) {
     float t = 0.f;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) t += red[q][jl];
+    for (int q = 0; q < ATB_RG; ++q) t += red[q][jl];
     if ((int)blockIdx.x >= nwb) {
       db[co] = t;
     } else if (mode == 0 || mode == 2) {
@@ -1186,7 +1192,7 @@ static hipError_t launch_xty(const float* X, int ldx, int K1, const float* Y, in
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const int nwb = cdiv(p.k1pad * p.npad, 32);
-  hipLaunchKernelGGL(k_atb_reduce, dim3(nwb + cdiv(Cout, 32)), dim3(256), 0, s, part, csum, dw,
+  hipLaunchKernelGGL(k_atb_reduce, dim3(nwb + cdiv(Cout, 32)), dim3(ATB_RG * 32), 0, s, part, csum, dw,
                      db, (int)p.nsplit, p.k1pad, p.npad, K1, N, Cout, mode, nwb);
   return hipGetLastError();
 }
@@ -1214,7 +1220,7 @@ static hipError_t launch_atb(const XL& X, const YL& Y, int64_t M, int K1, int N,
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const int nwb = cdiv(k1pad * npad, 32);
-  hipLaunchKernelGGL(k_atb_reduce, dim3(nwb + cdiv(Cout, 32)), dim3(256), 0, s, part, csum, dw,
+  hipLaunchKernelGGL(k_atb_reduce, dim3(nwb + cdiv(Cout, 32)), dim3(ATB_RG * 32), 0, s, part, csum, dw,
                      db, (int)nsplit, k1pad, npad, K1, N, Cout, mode, nwb);
   return hipGetLastError();
 }
