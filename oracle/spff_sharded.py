@@ -101,16 +101,16 @@ def fourier_gate(P, pre, x, sh: Shard, learn_phase: bool = False):
     if sh.axis == 3:   # s1 = mean over (c, h, w): partial sums over the local rows
         B, C, Fd, H, W = x.shape
         s_full = all_reduce(x.sum(dim=(1, 3, 4))) / (C * H * sh.world * W)
-        Sf = torch.fft.rfft(s_full, dim=1)
+        Sf = O.host_rfft(s_full, dim=1)
         M = (P[pre + ".freq_mask"] * P[pre + ".mag_scale"]).reshape(1, -1)
-        w = torch.fft.irfft(Sf * (M + 1j * 0.01) if learn_phase else Sf * M, n=Fd, dim=1)
+        w = O.host_irfft(Sf * (M + 1j * 0.01) if learn_phase else Sf * M, n=Fd, dim=1)
         return x * torch.sigmoid(w)[:, None, :, None, None]
     s = x.mean(dim=(1, 3, 4))                              # [B, D_loc]
     s_full = torch.cat(all_gather(s.contiguous()), dim=1)   # [B, D]
-    Sf = torch.fft.rfft(s_full, dim=1)
+    Sf = O.host_rfft(s_full, dim=1)
     M = (P[pre + ".freq_mask"] * P[pre + ".mag_scale"]).reshape(1, -1)
     Sf = Sf * (M + 1j * 0.01) if learn_phase else Sf * M
-    w = torch.fft.irfft(Sf, n=sh.D, dim=1)[:, sh.off:sh.off + sh.D_loc]
+    w = O.host_irfft(Sf, n=sh.D, dim=1)[:, sh.off:sh.off + sh.D_loc]
     return x * torch.sigmoid(w)[:, None, :, None, None]
 
 

@@ -117,6 +117,21 @@ class TorchDepthColl:
             op.wait()
 
 
+def _default_overlap(coll) -> bool:
+    """Bucketed gradient all-reduces during the backward, interleaved with the halo
+    exchanges.  On RCCL both go through the group's one communicator (batched
+    point-to-point selects the device's collective communicator, as all_reduce does)
+    and are issued from the host in the plan's fixed order, identical on every rank,
+    so they cannot cross.  That path has only run host-staged (gloo) and at world 1
+    on RCCL, so it stays opt-in for device collectives (SPFF_SHARD_OVERLAP=1) until a
+    multi-GPU run has exercised it; without it the flat gradient is all-reduced once
+    after the backward (allreduce_uncovered)."""
+    import os
+    if getattr(coll, "host", True):
+        return True
+    return os.environ.get("SPFF_SHARD_OVERLAP", "0") == "1"
+
+
 def height_bounds(H: int, world: int, rank: int):
     """(offset, rows) of rank's slab of a height-H volume (H / world a multiple of 8)."""
     if H % (8 * world):
@@ -143,9 +158,11 @@ class DepthShardedSPFF:
 
     def __init__(self, core: torch.nn.Module, num_classes: int, ignore_index: int = 255,
                  group=None, coll=None, timeout: float = 300.0, bucket_bytes: int = 4 << 20,
-                 overlap: bool = True):
+                 overlap: bool | None = None):
         self.core, self.K, self.ignore, self.group = core, int(num_classes), ignore_index, group
         self.coll = coll or TorchDepthColl(group, timeout=timeout)
+        if overlap is None:
+            overlap = _default_overlap(self.coll)
         core.shard = (self.coll.world, self.coll.rank, self.axis)
         core.shard_coll = self.coll
         self.params = [p for p in core.parameters()]

@@ -80,8 +80,9 @@ def _oracle_forward(st, x, y):
 # Where the fp64 gradient oracle runs.  The restatement is CPU code (pinned to the
 # reference's fixtures on the CPU, tests/test_oracle_golden.py); at these sizes its fp64
 # backward takes ~130 s per case on the box's 16 host cores, so by default PyTorch
-# evaluates the same functions on the GPU in fp64 (vol2col + rocBLAS dgemm, hipFFT: no
-# MIOpen and no engine code), which tests/test_gpu_parity.py::
+# evaluates the same functions on the GPU in fp64 (vol2col + rocBLAS dgemm; no MIOpen and
+# no engine code; the FourierGate's B x D spectra on the host, spff_oracle.host_rfft, since
+# rocFFT's were not repeatable inside the step), which tests/test_gpu_parity.py::
 # test_oracle_device_evaluation_matches_cpu pins to the CPU evaluation.  The logits,
 # argmax, loss and metrics are still judged against the fp32 oracle on the CPU.
 GRAD_DEV = os.environ.get("SPFF_ORACLE_GRAD_DEVICE", "cuda")
