@@ -577,7 +577,7 @@ def main():
                     help="0 (default) = time the CPU oracle on the whole batch; > 0 = sample 0, "
                          "depths [0, cpu-depth) only")
     ap.add_argument("--cpu-steps", type=int, default=3)
-    ap.add_argument("--pmc", default=str(ROOT / "profiles" / "r04_pmc_conv.json"),
+    ap.add_argument("--pmc", default=str(ROOT / "profiles" / "r05_pmc_conv.json"),
                     help="per-launch HBM traffic summary from rocprofv3 --pmc "
                          "(scripts/pmc_traffic.py); used only when its workload key matches")
     args = ap.parse_args()
