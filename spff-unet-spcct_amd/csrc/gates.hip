@@ -49,6 +49,11 @@ __device__ __forceinline__ double phase_term_t(int on, int k, int D, double Tre,
 int se_hidden(int C) { return C / 16 > 4 ? C / 16 : 4; }
 
 constexpr int GT = 1024;  // threads per gate workgroup
+#ifndef SPFF_GSPLIT_MIN
+// C x D from which the gate algebra runs as the channel-split kernels (grid C / 8 x B)
+// instead of one workgroup per sample
+#define SPFF_GSPLIT_MIN 8192
+#endif
 constexpr size_t GATE_LDS_MAX = 160 * 1024;
 
 // twiddles: twc[m] = cos(2 pi m / D), tws[m] = sin(2 pi m / D)
@@ -302,29 +307,6 @@ __global__ __launch_bounds__(GT) void k_gates_fwd(GateParams gp, const float* __
   }
 }
 
-hipError_t gates_fwd(const GateParams& gp, const float* Sa, GateSaved& sv, Vol vol, int C,
-                     float* scratch, hipStream_t s) {
-  (void)scratch;
-  const int D = vol.D, Hse = se_hidden(C);
-  const int efilm = gp.fw0 != nullptr;
-  if (efilm && !gp.efilm_ready) {
-    hipError_t e = efilm_fwd(gp, sv, C, D, s);
-    if (e != hipSuccess) return e;
-  }
-  const size_t shc = gates_fwd_shmem(C, D, Hse, true);
-  if (shc <= GATE_LDS_MAX) {
-    hipError_t e0 = hipFuncSetAttribute(reinterpret_cast<const void*>(k_gates_fwd<true>),
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)shc);
-    if (e0 != hipSuccess) return e0;
-    hipLaunchKernelGGL(k_gates_fwd<true>, dim3(vol.B), dim3(GT), shc, s, gp, Sa, sv, vol, C, Hse,
-                       efilm);
-  } else {
-    hipLaunchKernelGGL(k_gates_fwd<false>, dim3(vol.B), dim3(GT),
-                       gates_fwd_shmem(C, D, Hse, false), s, gp, Sa, sv, vol, C, Hse, efilm);
-  }
-  return hipGetLastError();
-}
-
 // ------------------------------------------------------------- gates bwd --
 // scratch layout (floats): dt[B][C][D], dbt[B][C][D], sw2p[B][C][Hse], sb2p[B][C],
 // sw0p[B][Hse][C], sb0p[B][Hse], dMr[B][L], dgb[2C][D], dh[EFiLM hidden][D]
@@ -345,11 +327,21 @@ static GScr gscr(float* base, int B, int C, int D, int Hse) {
   g.dh = g.dgb + (size_t)2 * C * D;
   return g;
 }
-size_t gates_scratch_bytes(Vol vol, int C) {
+static size_t gates_base_bytes(Vol vol, int C) {
   const int B = vol.B, D = vol.D, Hse = se_hidden(C), L = D / 2 + 1;
   size_t n = 2 * (size_t)B * C * D + (size_t)B * C * Hse + (size_t)B * C + (size_t)B * Hse * C +
              (size_t)B * Hse + (size_t)B * L + 2 * (size_t)C * D + EFH_MAX * (size_t)D;
-  return n * sizeof(float) + 256;
+  return (n * sizeof(float) + 256 + 255) / 256 * 256;
+}
+// (channel-split kernels, below) partial column sums [B][C/8][D] (double, twice), the SE
+// channel sums u and c0 [B][C], and the FourierGate / spectral-SE depth terms [B][D] (twice)
+static size_t gates_split_bytes(Vol vol, int C) {
+  const size_t B = vol.B, D = vol.D, nch = (C + 7) / 8;
+  return 2 * B * nch * D * sizeof(double) + 2 * B * C * sizeof(float) + 2 * B * D * sizeof(float) +
+         256;
+}
+size_t gates_scratch_bytes(Vol vol, int C) {
+  return gates_base_bytes(vol, C) + gates_split_bytes(vol, C);
 }
 
 struct GBShm {
@@ -652,12 +644,399 @@ static hipError_t gates_bwd_tail(const GateParams& gp, const GateSaved& sv, Gate
   return hipSuccess;
 }
 
+// ================================================ channel-split kernels ==
+// The one-workgroup-per-sample kernels above keep two CUs busy; at the deeper levels
+// (C x D up to 256 x 128 per sample) their [C][D] passes dominate (k_gates_bwd: 148 us for
+// the bottleneck block).  Here every [C][D] pass runs over 8-channel chunks, grid
+// (C / 8, B) -- column sums as fixed-order partials per chunk, row sums one wave per
+// channel -- and only the serial D-length chain (spectra, DFT, sigmoids) stays on one
+// workgroup per sample.  Same algebra as k_gates_fwd / k_gates_bwd.
+namespace {
+constexpr int GCH = 8;      // channels per chunk
+constexpr int GST = 256;    // threads of the chunk kernels
+struct GSplit {
+  double *ps1, *Tp;        // [B][nch][D]
+  float *u, *c0;           // [B][C]
+  float *ds2, *ds1;        // [B][D]
+};
+GSplit gsplit(float* scratch, Vol vol, int C) {
+  char* p = reinterpret_cast<char*>(scratch) + gates_base_bytes(vol, C);
+  const size_t B = vol.B, D = vol.D, nch = (C + GCH - 1) / GCH;
+  GSplit g;
+  g.ps1 = reinterpret_cast<double*>(p); p += B * nch * D * sizeof(double);
+  g.Tp = reinterpret_cast<double*>(p); p += B * nch * D * sizeof(double);
+  g.u = reinterpret_cast<float*>(p); p += B * C * sizeof(float);
+  g.c0 = reinterpret_cast<float*>(p); p += B * C * sizeof(float);
+  g.ds2 = reinterpret_cast<float*>(p); p += B * D * sizeof(float);
+  g.ds1 = reinterpret_cast<float*>(p);
+  return g;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+}  // namespace
+
+// split path for C x D >= SPFF_GSPLIT_MIN (C a multiple of 8, at most 1024 channels; the
+// chain kernels' LDS without the [C][D] caches fits for D <= 4096)
+static bool gates_split(int C, int D) {
+  return (int64_t)C * D >= SPFF_GSPLIT_MIN && C % GCH == 0 && C <= 1024 && D <= 4096;
+}
+
+// fwd 1: partial s1 numerators of one 8-channel chunk, ps1[b][ch][d] = sum_{c in ch} Z(c, d)
+__global__ __launch_bounds__(GST) void k_gfs_colsum(const float* __restrict__ Sa, GateSaved sv,
+                                                   Vol vol, int C, int efilm, GSplit sp) {
+  const int ch = blockIdx.x, b = blockIdx.y, nch = gridDim.x;
+  const int D = vol.D, HW = vol.H * vol.W;
+  const float* Sab = Sa + (int64_t)b * C * D;
+  const int c1 = min(C, (ch + 1) * GCH);
+  for (int d = threadIdx.x; d < D; d += GST) {
+    double acc = 0.0;
+    for (int c = ch * GCH; c < c1; ++c) {
+      const float sa = Sab[c * D + d];
+      acc += (double)(efilm ? (1.f + sv.t[c * D + d]) * sa + sv.bt[c * D + d] * (float)HW : sa);
+    }
+    sp.ps1[((int64_t)b * nch + ch) * D + d] = acc;
+  }
+}
+
+// fwd 2 (one workgroup per sample): s1 from the chunk partials (fixed order), the
+// FourierGate's DFT chain -> g1, the spectral SE -> sg2
+__global__ __launch_bounds__(GT) void k_gfs_chain(GateParams gp, GateSaved sv, Vol vol, int C,
+                                                  int nch, GSplit sp) {
+  const int b = blockIdx.x;
+  const int D = vol.D, HW = vol.H * vol.W, L = D / 2 + 1;
+  extern __shared__ double shd[];
+  GFShm m = gf_carve(shd, C, D, 0);
+  make_twiddles(m.twc, m.tws, D);
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    double acc = 0.0;
+    for (int ch = 0; ch < nch; ++ch) acc += sp.ps1[((int64_t)b * nch + ch) * D + d];
+    m.s1[d] = (float)(acc / ((double)C * HW));
+  }
+  __syncthreads();
+  if (gp.mask) {
+    rowsum(L, D, [&](int k, int d) { return (double)m.s1[d] * m.twc[(k * d) % D]; }, m.part, 1.0,
+           m.Sre);
+    rowsum(L, D, [&](int k, int d) { return -(double)m.s1[d] * m.tws[(k * d) % D]; }, m.part, 1.0,
+           m.Sim);
+    rowsum(D, L, [&](int d, int k) {
+      const int q = (k * d) % D;
+      const double Mk = (double)(gp.mask[k] * gp.mag[0]);
+      return ck_coef(k, D) * Mk * (m.Sre[k] * m.twc[q] - m.Sim[k] * m.tws[q]) +
+             phase_term(gp.fphase, k, D, m.Sre[k], m.Sim[k], m.twc[q], m.tws[q]);
+    }, m.part, 1.0 / D, m.tmp);
+    for (int d = threadIdx.x; d < D; d += blockDim.x) m.g1[d] = sigm((float)m.tmp[d]);
+  } else {
+    for (int d = threadIdx.x; d < D; d += blockDim.x) m.g1[d] = 1.f;
+  }
+  __syncthreads();
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    const float sg = gp.specse ? sigm(m.g1[d] * m.s1[d]) : 1.f;
+    sv.s1[b * D + d] = m.s1[d];
+    sv.g1[b * D + d] = m.g1[d];
+    sv.sg2[b * D + d] = sg;
+  }
+}
+
+// fwd 3 (SE): p[b][c] = sum_d g1 sg2 Z(c, d) / (D HW), one wave per channel
+__global__ __launch_bounds__(GST) void k_gfs_pool(const float* __restrict__ Sa, GateSaved sv,
+                                                 Vol vol, int C, int efilm) {
+  const int b = blockIdx.y, lane = threadIdx.x & 63;
+  const int c = blockIdx.x * (GST / 64) + (threadIdx.x >> 6);
+  if (c >= C) return;  // (whole wave)
+  const int D = vol.D, HW = vol.H * vol.W;
+  const float* Sab = Sa + (int64_t)b * C * D;
+  double acc = 0.0;
+  for (int d = lane; d < D; d += 64) {
+    const float sa = Sab[c * D + d];
+    const float z = efilm ? (1.f + sv.t[c * D + d]) * sa + sv.bt[c * D + d] * (float)HW : sa;
+    acc += (double)(sv.g1[b * D + d] * sv.sg2[b * D + d]) * (double)z;
+  }
+  acc = wave_sum_d(acc);
+  if (lane == 0) sv.p[b * C + c] = (float)(acc / ((double)D * HW));
+}
+
+// fwd 4: the SE MLP (each chunk recomputes the Hse hidden units from p, a C x Hse dot),
+// e of this chunk's channels, then P / Q (and the [B][D][C] copies) of its channels
+__global__ __launch_bounds__(GST) void k_gfs_apply(GateParams gp, GateSaved sv, Vol vol, int C,
+                                                  int Hse, int efilm) {
+  const int ch = blockIdx.x, b = blockIdx.y;
+  const int D = vol.D, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __shared__ float hs[64], es[GCH];
+  const int c0 = ch * GCH, c1 = min(C, c0 + GCH);
+  if (gp.sw0) {
+    for (int j = wave; j < Hse; j += GST / 64) {
+      float acc = 0.f;
+      for (int c = lane; c < C; c += 64) acc += gp.sw0[j * C + c] * sv.p[b * C + c];
+      acc = gate_wave_sum(acc);
+      if (lane == 0) hs[j] = acc + gp.sb0[j];
+    }
+    __syncthreads();
+    if (ch == 0)
+      for (int j = threadIdx.x; j < Hse; j += GST) sv.h[b * Hse + j] = hs[j];
+    for (int c = c0 + (int)threadIdx.x; c < c1; c += GST) {
+      float acc = 0.f;
+      for (int j = 0; j < Hse; ++j) acc += gp.sw2[c * Hse + j] * fmaxf(hs[j], 0.f);
+      const float ev = sigm(acc + gp.sb2[c]);
+      es[c - c0] = ev;
+      sv.e[b * C + c] = ev;
+    }
+  } else {
+    for (int c = c0 + (int)threadIdx.x; c < c1; c += GST) es[c - c0] = 1.f;
+  }
+  __syncthreads();
+  const int n = (c1 - c0) * D;
+  for (int i = threadIdx.x; i < n; i += GST) {
+    const int c = c0 + i / D, d = i % D;
+    const int cd = c * D + d;
+    const float G = sv.g1[b * D + d] * sv.sg2[b * D + d] * es[c - c0];
+    const float onept = efilm ? (1.f + sv.t[cd]) : 1.f;
+    const float btv = efilm ? sv.bt[cd] : 0.f;
+    sv.P[(int64_t)b * C * D + cd] = onept * G;
+    sv.Q[(int64_t)b * C * D + cd] = btv * G;
+    if (sv.PT) {
+      sv.PT[((int64_t)b * D + d) * C + c] = onept * G;
+      sv.QT[((int64_t)b * D + d) * C + c] = btv * G;
+    }
+  }
+}
+
+// bwd 1 (SE): u[b][c] = sum_d g1 sg2 R1(c, d), one wave per channel
+__global__ __launch_bounds__(GST) void k_gbs_rowsum(const float* __restrict__ Sg, GateSaved sv,
+                                                   Vol vol, int C, int efilm, GSplit sp) {
+  const int b = blockIdx.y, lane = threadIdx.x & 63;
+  const int c = blockIdx.x * (GST / 64) + (threadIdx.x >> 6);
+  if (c >= C) return;
+  const int D = vol.D;
+  const int64_t bo = (int64_t)b * C * D;
+  double acc = 0.0;
+  for (int d = lane; d < D; d += 64) {
+    const int64_t i = bo + c * D + d;
+    const float sgd = Sg[i * 2 + 0], sda = Sg[i * 2 + 1];
+    const float r1 = efilm ? (1.f + sv.t[c * D + d]) * sda + sv.bt[c * D + d] * sgd : sda;
+    acc += (double)(sv.g1[b * D + d] * sv.sg2[b * D + d]) * (double)r1;
+  }
+  acc = wave_sum_d(acc);
+  if (lane == 0) sp.u[b * C + c] = (float)acc;
+}
+
+// bwd 2: the SE backward (each chunk recomputes dh from all channels' dq, a C x Hse dot;
+// writes its channels' SE gradient partials, chunk 0 the hidden ones), c0 of its channels,
+// and the partial T[d] = sum_{c in chunk} (e R1 + c0 Z) for the spectral SE / FourierGate
+__global__ __launch_bounds__(GST) void k_gbs_colsum(GateParams gp, GateSaved sv,
+                                                   const float* __restrict__ Sa,
+                                                   const float* __restrict__ Sg, GScr gs, Vol vol,
+                                                   int C, int Hse, int efilm, GSplit sp) {
+  const int ch = blockIdx.x, b = blockIdx.y, nch = gridDim.x;
+  const int D = vol.D, HW = vol.H * vol.W, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __shared__ float dq[1024], dh[64], ec[GCH], cc[GCH];
+  const int c0 = ch * GCH, c1 = min(C, c0 + GCH);
+  const int64_t bo = (int64_t)b * C * D;
+  if (gp.sw0) {
+    for (int c = threadIdx.x; c < C; c += GST) {
+      const float ev = sv.e[b * C + c];
+      dq[c] = sp.u[b * C + c] * ev * (1.f - ev);
+    }
+    __syncthreads();
+    for (int j = wave; j < Hse; j += GST / 64) {
+      float acc = 0.f;
+      for (int c = lane; c < C; c += 64) acc += gp.sw2[c * Hse + j] * dq[c];
+      acc = gate_wave_sum(acc);
+      if (lane == 0) dh[j] = sv.h[b * Hse + j] > 0.f ? acc : 0.f;
+    }
+    __syncthreads();
+    if (ch == 0)
+      for (int j = threadIdx.x; j < Hse; j += GST) gs.sb0p[b * Hse + j] = dh[j];
+    for (int c = c0 + (int)threadIdx.x; c < c1; c += GST) {
+      gs.sb2p[b * C + c] = dq[c];
+      float acc = 0.f;
+      for (int j = 0; j < Hse; ++j) acc += gp.sw0[j * C + c] * dh[j];
+      const float c0v = acc / ((float)D * (float)HW);
+      cc[c - c0] = c0v;
+      ec[c - c0] = sv.e[b * C + c];
+      sp.c0[b * C + c] = c0v;
+    }
+    for (int i = threadIdx.x; i < (c1 - c0) * Hse; i += GST) {
+      const int c = c0 + i / Hse, j = i % Hse;
+      gs.sw2p[(int64_t)b * C * Hse + c * Hse + j] = dq[c] * fmaxf(sv.h[b * Hse + j], 0.f);
+    }
+    for (int i = threadIdx.x; i < Hse * (c1 - c0); i += GST) {
+      const int j = i / (c1 - c0), c = c0 + i % (c1 - c0);
+      gs.sw0p[(int64_t)b * Hse * C + j * C + c] = dh[j] * sv.p[b * C + c];
+    }
+  } else {
+    for (int c = c0 + (int)threadIdx.x; c < c1; c += GST) {
+      cc[c - c0] = 0.f;
+      ec[c - c0] = 1.f;
+      sp.c0[b * C + c] = 0.f;
+    }
+  }
+  if (!(gp.specse || gp.mask)) return;
+  __syncthreads();
+  for (int d = threadIdx.x; d < D; d += GST) {
+    double acc = 0.0;
+    for (int c = c0; c < c1; ++c) {
+      const int64_t i = bo + c * D + d;
+      const float sgd = Sg[i * 2 + 0], sda = Sg[i * 2 + 1];
+      const float tt = efilm ? sv.t[c * D + d] : 0.f;
+      const float r1 = efilm ? (1.f + tt) * sda + sv.bt[c * D + d] * sgd : sda;
+      const float sa = Sa[i];
+      const float z = efilm ? (1.f + tt) * sa + sv.bt[c * D + d] * (float)HW : sa;
+      acc += (double)ec[c - c0] * r1 + (double)cc[c - c0] * z;
+    }
+    sp.Tp[((int64_t)b * nch + ch) * D + d] = acc;
+  }
+}
+
+// bwd 3 (one workgroup per sample): T from the chunk partials, the spectral SE's ds2 and the
+// FourierGate's spectra / mask gradient partials / ds1
+__global__ __launch_bounds__(GT) void k_gbs_chain(GateParams gp, GateSaved sv, GScr gs, Vol vol,
+                                                  int C, int nch, GSplit sp) {
+  const int b = blockIdx.x;
+  const int D = vol.D, L = D / 2 + 1;
+  extern __shared__ double shd[];
+  GBShm m = gb_carve(shd, C, D, 0);
+  make_twiddles(m.twc, m.tws, D);
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    double acc = 0.0;
+    if (gp.specse || gp.mask)
+      for (int ch = 0; ch < nch; ++ch) acc += sp.Tp[((int64_t)b * nch + ch) * D + d];
+    m.tmp[d] = acc;
+    const float g1 = sv.g1[b * D + d], sg2 = sv.sg2[b * D + d];
+    m.g1[d] = g1;
+    m.sg2[d] = sg2;
+    const float ds2 = gp.specse ? sg2 * (1.f - sg2) * g1 * (float)acc : 0.f;
+    m.ds2[d] = ds2;
+    sp.ds2[b * D + d] = ds2;
+    if (!gp.mask) sp.ds1[b * D + d] = 0.f;
+  }
+  __syncthreads();
+  if (!gp.mask) return;
+  const float* s1 = sv.s1 + b * D;
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    const double t = (double)m.sg2[d] * m.tmp[d] + (double)m.ds2[d] * s1[d];
+    m.dw[d] = (float)t * m.g1[d] * (1.f - m.g1[d]);
+  }
+  __syncthreads();
+  rowsum(L, D, [&](int k, int d) { return (double)s1[d] * m.twc[(k * d) % D]; }, m.part, 1.0, m.Sre);
+  rowsum(L, D, [&](int k, int d) { return -(double)s1[d] * m.tws[(k * d) % D]; }, m.part, 1.0, m.Sim);
+  rowsum(L, D, [&](int k, int d) { return (double)m.dw[d] * m.twc[(k * d) % D]; }, m.part, 1.0, m.Tre);
+  rowsum(L, D, [&](int k, int d) { return (double)m.dw[d] * m.tws[(k * d) % D]; }, m.part, 1.0, m.Tim);
+  for (int k = threadIdx.x; k < L; k += blockDim.x)
+    gs.dMr[b * L + k] = (float)(ck_coef(k, D) / D * (m.Sre[k] * m.Tre[k] - m.Sim[k] * m.Tim[k]));
+  rowsum(D, L, [&](int d, int k) {
+    const int q = (k * d) % D;
+    const double Mk = (double)(gp.mask[k] * gp.mag[0]);
+    return ck_coef(k, D) * Mk * (m.twc[q] * m.Tre[k] + m.tws[q] * m.Tim[k]) +
+           phase_term_t(gp.fphase, k, D, m.Tre[k], m.Tim[k], m.twc[q], m.tws[q]);
+  }, m.part, 1.0 / D, m.tmp);
+  for (int d = threadIdx.x; d < D; d += blockDim.x) sp.ds1[b * D + d] = (float)m.tmp[d];
+}
+
+// bwd 4: A / B (and the EnergyFiLM partials dt, dbt) of this chunk's channels
+__global__ __launch_bounds__(GST) void k_gbs_apply(GateParams gp, GateSaved sv,
+                                                  const float* __restrict__ Sa,
+                                                  const float* __restrict__ Sg, GScr gs,
+                                                  float* __restrict__ Aout,
+                                                  float* __restrict__ Bout, Vol vol, int C,
+                                                  int efilm, GSplit sp) {
+  const int ch = blockIdx.x, b = blockIdx.y;
+  const int D = vol.D, HW = vol.H * vol.W;
+  const int c0 = ch * GCH, c1 = min(C, c0 + GCH);
+  const int64_t bo = (int64_t)b * C * D;
+  const float invCHW = 1.f / ((float)C * (float)HW);
+  const int n = (c1 - c0) * D;
+  for (int i = threadIdx.x; i < n; i += GST) {
+    const int c = c0 + i / D, d = i % D;
+    const int cd = c * D + d;
+    const float e = gp.sw0 ? sv.e[b * C + c] : 1.f;
+    const float sg2 = sv.sg2[b * D + d], g1 = sv.g1[b * D + d];
+    float al = e * sg2;
+    float be = sp.c0[b * C + c] * sg2 + sp.ds2[b * D + d] * invCHW;
+    if (gp.mask) {
+      al = al * g1;
+      be = be * g1 + sp.ds1[b * D + d] * invCHW;
+    }
+    if (efilm) {
+      const float sgd = Sg[(bo + cd) * 2 + 0], sda = Sg[(bo + cd) * 2 + 1];
+      gs.dt[bo + cd] = al * sda + be * Sa[bo + cd];
+      gs.dbt[bo + cd] = al * sgd + be * (float)HW;
+      const float onept = 1.f + sv.t[cd];
+      al *= onept;
+      be *= onept;
+    }
+    Aout[bo + cd] = al;
+    Bout[bo + cd] = be;
+  }
+}
+
+hipError_t gates_fwd(const GateParams& gp, const float* Sa, GateSaved& sv, Vol vol, int C,
+                     float* scratch, hipStream_t s) {
+  const int D = vol.D, Hse = se_hidden(C);
+  const int efilm = gp.fw0 != nullptr;
+  if (efilm && !gp.efilm_ready) {
+    hipError_t e = efilm_fwd(gp, sv, C, D, s);
+    if (e != hipSuccess) return e;
+  }
+  if (gates_split(C, D)) {
+    const GSplit sp = gsplit(scratch, vol, C);
+    const int nch = C / GCH;
+    hipLaunchKernelGGL(k_gfs_colsum, dim3(nch, vol.B), dim3(GST), 0, s, Sa, sv, vol, C, efilm, sp);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_gfs_chain, dim3(vol.B), dim3(GT), gates_fwd_shmem(C, D, 0, false), s, gp,
+                       sv, vol, C, nch, sp);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (gp.sw0) {
+      hipLaunchKernelGGL(k_gfs_pool, dim3(cdiv(C, GST / 64), vol.B), dim3(GST), 0, s, Sa, sv, vol, C,
+                         efilm);
+      if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(k_gfs_apply, dim3(nch, vol.B), dim3(GST), 0, s, gp, sv, vol, C, Hse, efilm);
+    return hipGetLastError();
+  }
+  const size_t shc = gates_fwd_shmem(C, D, Hse, true);
+  if (shc <= GATE_LDS_MAX) {
+    hipError_t e0 = hipFuncSetAttribute(reinterpret_cast<const void*>(k_gates_fwd<true>),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)shc);
+    if (e0 != hipSuccess) return e0;
+    hipLaunchKernelGGL(k_gates_fwd<true>, dim3(vol.B), dim3(GT), shc, s, gp, Sa, sv, vol, C, Hse,
+                       efilm);
+  } else {
+    hipLaunchKernelGGL(k_gates_fwd<false>, dim3(vol.B), dim3(GT),
+                       gates_fwd_shmem(C, D, Hse, false), s, gp, Sa, sv, vol, C, Hse, efilm);
+  }
+  return hipGetLastError();
+}
+
 hipError_t gates_bwd(const GateParams& gp, const GateSaved& sv, const float* Sa, const float* Sg,
                      GateGrads& gg, float* A, float* Bc, Vol vol, int C, float* scratch,
                      hipStream_t s) {
   const int D = vol.D, B = vol.B, Hse = se_hidden(C);
   const int efilm = gp.fw0 != nullptr;
   GScr g = gscr(scratch, B, C, D, Hse);
+  if (gates_split(C, D)) {
+    const GSplit sp = gsplit(scratch, vol, C);
+    const int nch = C / GCH;
+    hipError_t e;
+    if (gp.sw0) {
+      hipLaunchKernelGGL(k_gbs_rowsum, dim3(cdiv(C, GST / 64), B), dim3(GST), 0, s, Sg, sv, vol, C,
+                         efilm, sp);
+      if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(k_gbs_colsum, dim3(nch, B), dim3(GST), 0, s, gp, sv, Sa, Sg, g, vol, C, Hse,
+                       efilm, sp);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_gbs_chain, dim3(B), dim3(GT), gates_bwd_shmem(C, D, 0, 0), s, gp, sv, g,
+                       vol, C, nch, sp);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_gbs_apply, dim3(nch, B), dim3(GST), 0, s, gp, sv, Sa, Sg, g, A, Bc, vol, C,
+                       efilm, sp);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    return gates_bwd_tail(gp, sv, gg, g, B, C, D, D, Hse, s);
+  }
   int nc = 2;
   while (nc > 0 && gates_bwd_shmem(C, D, Hse, nc) > GATE_LDS_MAX) --nc;
   const size_t shm = gates_bwd_shmem(C, D, Hse, nc);
