@@ -516,7 +516,7 @@ __global__ void k_gates_bwd_final(GateParams gp, GateGrads gg, GScr gs, int B, i
                                   int Hse) {
   const int L = D / 2 + 1;
   const int n1 = C * Hse, n2 = C, n3 = Hse * C, n4 = Hse, n5 = L;
-  const int tot = (gp.sw0 ? n1 + n2 + n3 + n4 : 0) + (gp.mask ? n5 + 1 : 0);
+  const int tot = (gp.sw0 ? n1 + n2 + n3 + n4 : 0) + (gp.mask ? n5 : 0);
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += gridDim.x * blockDim.x) {
     int k = i;
     if (gp.sw0) {
@@ -530,19 +530,22 @@ __global__ void k_gates_bwd_final(GateParams gp, GateGrads gg, GScr gs, int B, i
       k -= n4;
     }
     // FourierGate: M = mask * mag
-    if (k < n5) {
+    float s = 0.f;
+    for (int b = 0; b < B; ++b) s += gs.dMr[b * L + k];
+    gg.mask[k] = s * gp.mag[0];
+  }
+  // d mag = sum_k mask_k sum_b dMr[b][k]: one wave, lanes over k, a fixed shuffle tree
+  // (a single thread walking the L x B terms took most of this kernel's 15 us)
+  if (gp.mask && blockIdx.x == 0 && threadIdx.x < 64) {
+    float t = 0.f;
+    for (int k = threadIdx.x; k < L; k += 64) {
       float s = 0.f;
       for (int b = 0; b < B; ++b) s += gs.dMr[b * L + k];
-      gg.mask[k] = s * gp.mag[0];
-    } else {
-      float tot2 = 0.f;
-      for (int kk = 0; kk < L; ++kk) {
-        float s = 0.f;
-        for (int b = 0; b < B; ++b) s += gs.dMr[b * L + kk];
-        tot2 += s * gp.mask[kk];
-      }
-      gg.mag[0] = tot2;
+      t += s * gp.mask[k];
     }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) t += __shfl_xor(t, o);
+    if (threadIdx.x == 0) gg.mag[0] = t;
   }
 }
 
