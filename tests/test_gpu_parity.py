@@ -341,11 +341,23 @@ def test_streaming_head(in_ch, K, base, mth):
     _engine_vs_oracle(in_ch, K, base, mth)
 
 
-def _engine_vs_oracle(in_ch, K, base, mth):
+@pytest.mark.parametrize("D,se,specse,mth", [(256, True, True, "f16x3"), (257, True, True, "f32"),
+                                               (256, False, True, "f16x3"),
+                                               (257, True, False, "f32")])
+def test_gate_channel_split_path(D, se, specse, mth):
+    """The channel-split gate kernels (gates.hip k_gfs_* / k_gbs_*, taken for C x D >= 8192):
+    depth 256 / 257 at base 32 puts every level on them (level 0: 32 x 256 = 8192), with
+    even and odd D (the FourierGate's Nyquist bin), and with the channel SE or the spectral
+    SE off (the kernels' sw0 / specse branches).  Engine vs the oracle as below."""
+    _engine_vs_oracle(5, 13, 32, mth, shape=(2, D, 8, 8), se=se, specse=specse)
+
+
+def _engine_vs_oracle(in_ch, K, base, mth, shape=(1, 4, 16, 16), se=True, specse=True):
     from innovative3D.synthetic import synthetic_batch
     from innovative3D.weightgen import synth_state
-    B, D, H, W = 1, 4, 16, 16
-    core = M.build_spct_energyfilm_fourier(num_classes=K, base=base, in_channels=in_ch)
+    B, D, H, W = shape
+    core = M.build_spct_energyfilm_fourier(num_classes=K, base=base, in_channels=in_ch,
+                                           use_se=se, use_specse=specse)
     for b in core._blocks():
         b.fgate._ensure_mask(D, "cpu")
     st = synth_state([(k, tuple(v.shape)) for k, v in core.state_dict().items()], seed=31,
@@ -358,7 +370,7 @@ def _engine_vs_oracle(in_ch, K, base, mth):
     loss, conf = Hh.ce_dice_with_confusion(logits, y.to(DEV), K, 255)
     loss.backward()
     torch.cuda.synchronize()
-    cfg = O.SpffCfg(in_ch=in_ch, num_classes=K, base=base)
+    cfg = O.SpffCfg(in_ch=in_ch, num_classes=K, base=base, se=se, specse=specse)
     P = O.params_from_state({k: v for k, v in st.items() if not k.endswith("._mask")},
                             requires_grad=False)
     with torch.no_grad():
