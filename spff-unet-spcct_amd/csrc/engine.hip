@@ -23,6 +23,11 @@
 // head's loaders +0.14 ms/step against dec1's 0.2 ms/step level-0 pass
 #define SPFF_OUTFUSE 1
 #endif
+#ifndef SPFF_POOL_FOLD
+// 1: the encoder blocks' output gradients (skip + MaxPool backward) are formed by their two
+// readers (PoolAdd: the tail reduction, the IN-backward apply) instead of k_maxpool_bwd_add
+#define SPFF_POOL_FOLD 1
+#endif
 #ifndef SPFF_RED_FUSE
 #define SPFF_RED_FUSE 1  // 0 (A/B diagnostics): separate tail and IN-backward reductions
 #endif
@@ -1046,7 +1051,7 @@ int hsh_gate_grads(spff_plan* p, const Blk& b, GateGrads& gg) {
 }
 
 int bwd_block(spff_plan* p, Blk& b, const float* dout, const Dst2* dx, const Src2& in_saved,
-              int dec_bi = -1) {
+              int dec_bi = -1, PoolAdd pa = {}) {
   const Vol& v = p->vol[b.lvl];
   const int C = b.C, KD = p->KD;
   Src2 in = in_saved;
@@ -1060,6 +1065,7 @@ int bwd_block(spff_plan* p, Blk& b, const float* dout, const Dst2* dx, const Src
     a.de = p->F(b.de2);
     a.mean = p->F(b.mean2);
     a.rstd = p->F(b.rstd2);
+    a.pa = pa;
     // (SPFF_RED_FUSE: the IN-backward sums of y2 in the same pass, RED_BWD_TAIL6)
     PROFB(p, 4, 0.0, 8.0 * (double)nvox(v) * C,
           SPFF_RED_FUSE ? slab_reduce(RED_BWD_TAIL6, a, v, C, p->F(p->red_out), p->F(p->red_ws),
@@ -1102,7 +1108,7 @@ int bwd_block(spff_plan* p, Blk& b, const float* dout, const Dst2* dx, const Src
   {
     RedArgs a{};
     a.y = p->F(b.y2); a.g = dout; a.mean = p->F(b.mean2); a.rstd = p->F(b.rstd2);
-    a.al = p->F(b.al2); a.de = p->F(b.de2); a.A = A; a.Bc = Bc;
+    a.al = p->F(b.al2); a.de = p->F(b.de2); a.A = A; a.Bc = Bc; a.pa = pa;
     if (b.tail() && SPFF_RED_FUSE)
       HIPCK(in_sums_from_tail(p->F(p->red_out4), A, Bc, p->F(p->red_out),
                               (int64_t)v.B * C * v.D, p->st));
@@ -1113,7 +1119,7 @@ int bwd_block(spff_plan* p, Blk& b, const float* dout, const Dst2* dx, const Src
     PROFB(p, 6, 0.0, 12.0 * (double)nvox(v) * C,
           in_bwd_apply(p->F(b.y2), dout, dy2, p->F(b.mean2), p->F(b.rstd2), p->F(b.al2),
                        p->F(b.de2), p->P(b.g2), A, Bc, p->F(p->kk1), p->F(p->kk2), v, C, p->st,
-                       0.01f, f16_slot(p, b, F16_DY2)));
+                       0.01f, f16_slot(p, b, F16_DY2), pa));
   }
   const double V = (double)nvox(v), T = 9.0 * KD;
   Src2 a1 = act_src(p, b);  // (fused: y1 and its halo as the forward left them)
@@ -1264,13 +1270,21 @@ int backward(spff_plan* p, const float* dl) {
   }
   for (int l = 2; l >= 0; --l) {
     const int C = f << l;
-    HIPCK(maxpool_bwd_add(p->F(p->G_dx), reinterpret_cast<const uint8_t*>(p->ws + p->pidx[l]),
-                          p->F(p->dskip[l]), C, p->F(p->dskip[l]), p->vol[l], C, p->st));
+    // the block's output gradient = skip gradient + the pool's backward of G_dx, formed by
+    // its two readers (PoolAdd) -- G_dx is overwritten only by this block's last dgrad
+    PoolAdd pa;
+    pa.dp = p->F(p->G_dx);
+    pa.idx = reinterpret_cast<const uint8_t*>(p->ws + p->pidx[l]);
+    if (!SPFF_POOL_FOLD) {
+      HIPCK(maxpool_bwd_add(pa.dp, pa.idx, p->F(p->dskip[l]), C, p->F(p->dskip[l]), p->vol[l], C,
+                            p->st));
+      pa = PoolAdd{};
+    }
     if (l > 0) {
       Dst2 dx = dst1(p->F(p->G_dx), C / 2);
-      CK(bwd_block(p, B[l], p->F(p->dskip[l]), &dx, src1(p->F(p->pool[l - 1]), C / 2)));
+      CK(bwd_block(p, B[l], p->F(p->dskip[l]), &dx, src1(p->F(p->pool[l - 1]), C / 2), -1, pa));
     } else {
-      CK(bwd_block(p, B[0], p->F(p->dskip[0]), nullptr, src1(p->F(p->x_cl), p->ldx)));
+      CK(bwd_block(p, B[0], p->F(p->dskip[0]), nullptr, src1(p->F(p->x_cl), p->ldx), -1, pa));
     }
     CK(block_grads_ready(p, B[l]));
   }

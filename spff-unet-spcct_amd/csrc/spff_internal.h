@@ -277,12 +277,21 @@ enum RedOp {
   // (s = slope(r)); in_sums_from_tail() turns out2 into RED_BWD_IN's [B][C][D][2]
   RED_BWD_TAIL6 = 5,
 };
+// An encoder block's output gradient formed where it is read: g (the skip gradient) plus
+// the MaxPool3d(1,2,2) backward of the pooled gradient dp [B][D][H/2][W/2][C] routed by the
+// argmax bytes idx (same layout) -- k_maxpool_bwd_add's sum, in its order, folded into its
+// two consumers (the tail reduction and the IN-backward apply) instead of a pass of its own
+struct PoolAdd {
+  const float* dp = nullptr;
+  const uint8_t* idx = nullptr;
+};
 struct RedArgs {
   const float* y; const float* g;     // y: [V][C] (ld = C), g: [V][C] (ld = C)
   const float* mean; const float* rstd; // [B][C]
   const float* al; const float* de;   // [B][C]
   const float* A; const float* Bc;    // [B][C][D] or null (identity)
   float neg = 0.01f;                  // activation negative slope (0: ReLU)
+  PoolAdd pa;                         // g += unpool(pa) (two-operand ops only)
 };
 // out: [B][C][D][nq] fp32, summed over h,w in a fixed order.
 size_t slab_reduce_ws_bytes(Vol vol, int C, int nq);
@@ -325,7 +334,7 @@ hipError_t in_bwd_apply(const float* y, const float* g, float* dy, const float* 
                         const float* rstd, const float* al, const float* de, const float* gamma,
                         const float* A, const float* Bc, const float* k1, const float* k2,
                         Vol vol, int C, hipStream_t s, float neg = 0.01f,
-                        unsigned* amax = nullptr);
+                        unsigned* amax = nullptr, PoolAdd pa = {});
 // (amax: also atomicMax the largest |dy| (float bits) into *amax -- an SPFF_MATH_F16X3 operand
 // scale for the convs that read dy; the caller zeroed it)
 // a bound on max |lrelu(IN(y))| from the parameters alone, into *slot (float bits): per
