@@ -33,9 +33,46 @@ __host__ __device__ inline int red_vpp(int tpv) {
 // elementwise block size: a multiple of C/4, so a thread's channel quad is fixed
 // over its grid-stride loop (256 for power-of-two C)
 static inline int ew_bs(int C) { return (C / 4) * (256 / (C / 4)); }
+#ifndef SPFF_NT
+#define SPFF_NT 0  // streaming passes: bit 0 nontemporal loads, bit 1 nontemporal stores (A/B)
+#endif
+typedef float nt_f4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 ld_s(const float* p) {
+  if constexpr ((SPFF_NT & 1) != 0) {
+    const nt_f4 v = __builtin_nontemporal_load(reinterpret_cast<const nt_f4*>(p));
+    return make_float4(v.x, v.y, v.z, v.w);
+  }
+  return *reinterpret_cast<const float4*>(p);
+}
+__device__ __forceinline__ void st_s(float* p, const float4& v) {
+  if constexpr ((SPFF_NT & 2) != 0) {
+    const nt_f4 w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, reinterpret_cast<nt_f4*>(p));
+  } else {
+    *reinterpret_cast<float4*>(p) = v;
+  }
+}
 // neg = negative slope: 0.01 for LeakyReLU (SPFF), 0 for ReLU (3DUNet)
 __device__ __forceinline__ float lrelu(float r, float neg) { return r > 0.f ? r : neg * r; }
 __device__ __forceinline__ float slope(float r, float neg) { return r > 0.f ? 1.f : neg; }
+// g + the pooled gradient routed to (h, w) of slab bd by its argmax byte (PoolAdd), as
+// k_maxpool_bwd_add adds it; odd extents: the last row / column has no pooled parent
+__device__ __forceinline__ float4 pool_add(float4 g, const PoolAdd& pa, int64_t bd, int hw,
+                                           const Vol& vol, int C, int c) {
+  const int h = hw / vol.W, w = hw - h * vol.W;
+  const int Ho = vol.H >> 1, Wo = vol.W >> 1, ho = h >> 1, wo = w >> 1;
+  if (ho < Ho && wo < Wo) {
+    const int64_t vo = (bd * Ho + ho) * Wo + wo;
+    const uint8_t k = (uint8_t)((h & 1) * 2 + (w & 1));
+    const uchar4 ix = *reinterpret_cast<const uchar4*>(pa.idx + vo * C + c);
+    const float4 d = *reinterpret_cast<const float4*>(pa.dp + vo * C + c);
+    if (ix.x == k) g.x += d.x;
+    if (ix.y == k) g.y += d.y;
+    if (ix.z == k) g.z += d.z;
+    if (ix.w == k) g.w += d.w;
+  }
+  return g;
+}
 
 namespace {
 struct RedPlan {
@@ -146,8 +183,9 @@ __global__ __launch_bounds__(256) void k_slab_reduce(RedArgs a, Vol vol, int C, 
       for (int k = 0; k < NB; ++k) {
         const int hw = hw0 + k * vpp;
         const int64_t off = (base + (hw < he ? hw : hw0)) * C + c;
-        yv[k] = *reinterpret_cast<const float4*>(a.y + off);
-        if (TWO) gv[k] = *reinterpret_cast<const float4*>(a.g + off);
+        yv[k] = ld_s(a.y + off);
+        if (TWO) gv[k] = ld_s(a.g + off);
+        if (TWO && a.pa.dp) gv[k] = pool_add(gv[k], a.pa, bd, hw < he ? hw : hw0, vol, C, c);
       }
 #pragma unroll
       for (int k = 0; k < NB; ++k) {
@@ -579,14 +617,14 @@ __global__ __launch_bounds__(256) void k_act_apply(const float* __restrict__ y, 
   }
   float m = 0.f;
   for (int i = i0; i < n4; i += gridDim.x * blockDim.x) {
-    const float4 v = *reinterpret_cast<const float4*>(y + base + 4 * (int64_t)i);
+    const float4 v = ld_s(y + base + 4 * (int64_t)i);
     float r[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       r[j] = lrelu(r[j] * pa[j] + pd[j], neg) * pp[j] + pq[j];
       m = fmaxf(m, fabsf(r[j]));
     }
-    *reinterpret_cast<float4*>(out + base + 4 * (int64_t)i) = make_float4(r[0], r[1], r[2], r[3]);
+    st_s(out + base + 4 * (int64_t)i, make_float4(r[0], r[1], r[2], r[3]));
   }
   if (amax) block_amax(m, amax);
 }
@@ -638,7 +676,7 @@ __global__ __launch_bounds__(256) void k_act_apply_pool(
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int64_t vv = vin + (k >> 1) * vol.W + (k & 1);
-      const float4 v = *reinterpret_cast<const float4*>(y + vv * C + c);
+      const float4 v = ld_s(y + vv * C + c);
       float r[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -651,7 +689,7 @@ __global__ __launch_bounds__(256) void k_act_apply_pool(
           bi[j] = (uint8_t)k;
         }
       }
-      *reinterpret_cast<float4*>(out + vv * C + c) = make_float4(r[0], r[1], r[2], r[3]);
+      st_s(out + vv * C + c, make_float4(r[0], r[1], r[2], r[3]));
     }
     const int64_t vo = ((int64_t)bd * Ho + ho) * Wo + wo;
     *reinterpret_cast<float4*>(pooled + vo * C + c) = make_float4(best[0], best[1], best[2], best[3]);
@@ -676,7 +714,7 @@ __global__ __launch_bounds__(256) void k_in_bwd_apply(
     const float* __restrict__ rstd, const float* __restrict__ al, const float* __restrict__ de,
     const float* __restrict__ gamma, const float* __restrict__ A, const float* __restrict__ Bc,
     const float* __restrict__ k1, const float* __restrict__ k2, Vol vol, int C, float neg,
-    unsigned* __restrict__ amax) {
+    unsigned* __restrict__ amax, PoolAdd pa) {
   const int bd = blockIdx.y, b = bd / vol.D, d = bd % vol.D;
   const int n4 = vol.H * vol.W * (C >> 2);
   const int64_t base = (int64_t)bd * vol.H * vol.W * C;
@@ -693,8 +731,9 @@ __global__ __launch_bounds__(256) void k_in_bwd_apply(
   }
   float m = 0.f;
   for (int i = i0; i < n4; i += gridDim.x * blockDim.x) {
-    const float4 yv = *reinterpret_cast<const float4*>(y + base + 4 * (int64_t)i);
-    const float4 gv = *reinterpret_cast<const float4*>(g + base + 4 * (int64_t)i);
+    const float4 yv = ld_s(y + base + 4 * (int64_t)i);
+    float4 gv = ld_s(g + base + 4 * (int64_t)i);
+    if (pa.dp) gv = pool_add(gv, pa, bd, i / (C >> 2), vol, C, c);
     const float ys[4] = {yv.x, yv.y, yv.z, yv.w};
     const float gs[4] = {gv.x, gv.y, gv.z, gv.w};
     float o[4];
@@ -706,7 +745,7 @@ __global__ __launch_bounds__(256) void k_in_bwd_apply(
       o[j] = psc[j] * (dr - pk1[j] - xh * pk2[j]);
       m = fmaxf(m, fabsf(o[j]));
     }
-    *reinterpret_cast<float4*>(dy + base + 4 * (int64_t)i) = make_float4(o[0], o[1], o[2], o[3]);
+    st_s(dy + base + 4 * (int64_t)i, make_float4(o[0], o[1], o[2], o[3]));
   }
   if (amax) block_amax(m, amax);
 }
@@ -743,9 +782,9 @@ hipError_t act_bound(const float* gamma, const float* beta, int C, double N, uns
 hipError_t in_bwd_apply(const float* y, const float* g, float* dy, const float* mean,
                         const float* rstd, const float* al, const float* de, const float* gamma,
                         const float* A, const float* Bc, const float* k1, const float* k2, Vol vol,
-                        int C, hipStream_t s, float neg, unsigned* amax) {
+                        int C, hipStream_t s, float neg, unsigned* amax, PoolAdd pa) {
   hipLaunchKernelGGL(k_in_bwd_apply, ew_grid(vol, C), dim3(ew_bs(C)), 0, s, y, g, dy, mean, rstd, al,
-                     de, gamma, A, Bc, k1, k2, vol, C, neg, amax);
+                     de, gamma, A, Bc, k1, k2, vol, C, neg, amax, pa);
   return hipGetLastError();
 }
 
