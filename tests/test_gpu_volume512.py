@@ -142,7 +142,9 @@ def test_volume512_depth_sharded_8_ranks_matches_one_gpu():
         assert err <= 1e-4 * amax
         assert abs(loss8 - loss1) <= 1e-5 * abs(loss1)
         assert nflip == nflip_tie, f"{nflip - nflip_tie} argmax flips outside near-ties"
-        assert rows[0][0] <= 5e-2, rows[:3]
+        # two fp32 sums over 134 M voxels in different orders, plus the knife-edge branches
+        # each run takes on its own (no oracle to force them at this size): observed 3.6e-3
+        assert rows[0][0] <= 1e-2, rows[:3]
     finally:
         for f in files:
             try:
