@@ -97,6 +97,55 @@ __device__ void rowsum(int NI, int NJ, Fn f, double* part, double scale, double*
   __syncthreads();
 }
 
+// N row sums over the same (NI, NJ) index space in one pass (f(i, j, v) fills v[0..N-1]);
+// part holds N x blockDim.x doubles.  Same slice partition and combine order as rowsum.
+template <int N, class Fn>
+__device__ void rowsum_n(int NI, int NJ, Fn f, double* part, double scale, double* const* out) {
+  const int t = threadIdx.x, nt = (int)blockDim.x;
+  const int S = NI >= nt ? 1 : nt / NI;
+  double acc[N];
+#pragma unroll
+  for (int q = 0; q < N; ++q) acc[q] = 0.0;
+  if (NI >= nt) {
+    for (int i = t; i < NI; i += nt) {
+#pragma unroll
+      for (int q = 0; q < N; ++q) acc[q] = 0.0;
+      for (int j = 0; j < NJ; ++j) {
+        double v[N];
+        f(i, j, v);
+#pragma unroll
+        for (int q = 0; q < N; ++q) acc[q] += v[q];
+      }
+#pragma unroll
+      for (int q = 0; q < N; ++q) out[q][i] = acc[q] * scale;
+    }
+    __syncthreads();
+    return;
+  }
+  if (t < NI * S) {
+    const int i = t / S, sl = t % S;
+    for (int j = sl; j < NJ; j += S) {
+      double v[N];
+      f(i, j, v);
+#pragma unroll
+      for (int q = 0; q < N; ++q) acc[q] += v[q];
+    }
+  }
+  __syncthreads();
+  if (t < NI * S)
+#pragma unroll
+    for (int q = 0; q < N; ++q) part[q * nt + t] = acc[q];
+  __syncthreads();
+  for (int i = t; i < NI; i += nt)
+#pragma unroll
+    for (int q = 0; q < N; ++q) {
+      double sum = 0.0;
+      for (int k = 0; k < S; ++k) sum += part[q * nt + i * S + k];
+      out[q][i] = sum * scale;
+    }
+  __syncthreads();
+}
+
 // ------------------------------------------------------------- EFiLM fwd --
 // hid[j][d] = fw0[j] . pe[:,d] + fb0[j]; gb[o][d] = fw2[o] . relu(hid[:,d]) + fb2[o]
 // (H hidden units, P code rows: EnergyFiLM3D(hidden, pe_dims), 32 and 16 by default)
@@ -682,9 +731,10 @@ __device__ __forceinline__ double wave_sum_d(double v) {
 }  // namespace
 
 // split path for C x D >= SPFF_GSPLIT_MIN (C a multiple of 8, at most 1024 channels; the
-// chain kernels' LDS without the [C][D] caches fits for D <= 4096)
+// chain kernels' LDS -- twiddles, spectra and the 2 / 4 x GT partials of the merged row
+// sums, no [C][D] caches -- fits for D <= 1024)
 static bool gates_split(int C, int D) {
-  return (int64_t)C * D >= SPFF_GSPLIT_MIN && C % GCH == 0 && C <= 1024 && D <= 4096;
+  return (int64_t)C * D >= SPFF_GSPLIT_MIN && C % GCH == 0 && C <= 1024 && D <= 1024;
 }
 
 // fwd 1: partial s1 numerators of one 8-channel chunk, ps1[b][ch][d] = sum_{c in ch} Z(c, d)
@@ -707,11 +757,12 @@ __global__ __launch_bounds__(GST) void k_gfs_colsum(const float* __restrict__ Sa
 // fwd 2 (one workgroup per sample): s1 from the chunk partials (fixed order), the
 // FourierGate's DFT chain -> g1, the spectral SE -> sg2
 __global__ __launch_bounds__(GT) void k_gfs_chain(GateParams gp, GateSaved sv, Vol vol, int C,
-                                                  int nch, GSplit sp) {
+                                                  int nch, GSplit sp, int part_off) {
   const int b = blockIdx.x;
   const int D = vol.D, HW = vol.H * vol.W, L = D / 2 + 1;
   extern __shared__ double shd[];
   GFShm m = gf_carve(shd, C, D, 0);
+  double* part4 = shd + part_off;  // 2 x GT doubles after the carve
   make_twiddles(m.twc, m.tws, D);
   for (int d = threadIdx.x; d < D; d += blockDim.x) {
     double acc = 0.0;
@@ -720,10 +771,12 @@ __global__ __launch_bounds__(GT) void k_gfs_chain(GateParams gp, GateSaved sv, V
   }
   __syncthreads();
   if (gp.mask) {
-    rowsum(L, D, [&](int k, int d) { return (double)m.s1[d] * m.twc[(k * d) % D]; }, m.part, 1.0,
-           m.Sre);
-    rowsum(L, D, [&](int k, int d) { return -(double)m.s1[d] * m.tws[(k * d) % D]; }, m.part, 1.0,
-           m.Sim);
+    double* outs[2] = {m.Sre, m.Sim};
+    rowsum_n<2>(L, D, [&](int k, int d, double* v) {
+      const int q = (k * d) % D;
+      v[0] = (double)m.s1[d] * m.twc[q];
+      v[1] = -(double)m.s1[d] * m.tws[q];
+    }, part4, 1.0, outs);
     rowsum(D, L, [&](int d, int k) {
       const int q = (k * d) % D;
       const double Mk = (double)(gp.mask[k] * gp.mag[0]);
@@ -896,7 +949,7 @@ __global__ __launch_bounds__(GST) void k_gbs_colsum(GateParams gp, GateSaved sv,
 // bwd 3 (one workgroup per sample): T from the chunk partials, the spectral SE's ds2 and the
 // FourierGate's spectra / mask gradient partials / ds1
 __global__ __launch_bounds__(GT) void k_gbs_chain(GateParams gp, GateSaved sv, GScr gs, Vol vol,
-                                                  int C, int nch, GSplit sp) {
+                                                  int C, int nch, GSplit sp, int part_off) {
   const int b = blockIdx.x;
   const int D = vol.D, L = D / 2 + 1;
   extern __shared__ double shd[];
@@ -923,10 +976,18 @@ __global__ __launch_bounds__(GT) void k_gbs_chain(GateParams gp, GateSaved sv, G
     m.dw[d] = (float)t * m.g1[d] * (1.f - m.g1[d]);
   }
   __syncthreads();
-  rowsum(L, D, [&](int k, int d) { return (double)s1[d] * m.twc[(k * d) % D]; }, m.part, 1.0, m.Sre);
-  rowsum(L, D, [&](int k, int d) { return -(double)s1[d] * m.tws[(k * d) % D]; }, m.part, 1.0, m.Sim);
-  rowsum(L, D, [&](int k, int d) { return (double)m.dw[d] * m.twc[(k * d) % D]; }, m.part, 1.0, m.Tre);
-  rowsum(L, D, [&](int k, int d) { return (double)m.dw[d] * m.tws[(k * d) % D]; }, m.part, 1.0, m.Tim);
+  {
+    double* part4 = shd + part_off;  // 4 x GT doubles after the carve
+    double* outs[4] = {m.Sre, m.Sim, m.Tre, m.Tim};
+    rowsum_n<4>(L, D, [&](int k, int d, double* v) {
+      const int q = (k * d) % D;
+      const double c = m.twc[q], sn = m.tws[q];
+      v[0] = (double)s1[d] * c;
+      v[1] = -(double)s1[d] * sn;
+      v[2] = (double)m.dw[d] * c;
+      v[3] = (double)m.dw[d] * sn;
+    }, part4, 1.0, outs);
+  }
   for (int k = threadIdx.x; k < L; k += blockDim.x)
     gs.dMr[b * L + k] = (float)(ck_coef(k, D) / D * (m.Sre[k] * m.Tre[k] - m.Sim[k] * m.Tim[k]));
   rowsum(D, L, [&](int d, int k) {
@@ -989,8 +1050,13 @@ hipError_t gates_fwd(const GateParams& gp, const float* Sa, GateSaved& sv, Vol v
     hipLaunchKernelGGL(k_gfs_colsum, dim3(nch, vol.B), dim3(GST), 0, s, Sa, sv, vol, C, efilm, sp);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_gfs_chain, dim3(vol.B), dim3(GT), gates_fwd_shmem(C, D, 0, false), s, gp,
-                       sv, vol, C, nch, sp);
+    const int off = (int)((gates_fwd_shmem(C, D, 0, false) + 15) / 16 * 2);  // (doubles)
+    const size_t shm = (off + 2 * GT) * sizeof(double);
+    if (shm > 64 * 1024 &&
+        (e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_gfs_chain),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm)) != hipSuccess)
+      return e;
+    hipLaunchKernelGGL(k_gfs_chain, dim3(vol.B), dim3(GT), shm, s, gp, sv, vol, C, nch, sp, off);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (gp.sw0) {
       hipLaunchKernelGGL(k_gfs_pool, dim3(cdiv(C, GST / 64), vol.B), dim3(GST), 0, s, Sa, sv, vol, C,
@@ -1032,8 +1098,14 @@ hipError_t gates_bwd(const GateParams& gp, const GateSaved& sv, const float* Sa,
     hipLaunchKernelGGL(k_gbs_colsum, dim3(nch, B), dim3(GST), 0, s, gp, sv, Sa, Sg, g, vol, C, Hse,
                        efilm, sp);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_gbs_chain, dim3(B), dim3(GT), gates_bwd_shmem(C, D, 0, 0), s, gp, sv, g,
-                       vol, C, nch, sp);
+    const int off = (int)((gates_bwd_shmem(C, D, 0, 0) + 15) / 16 * 2);  // (doubles)
+    const size_t shm = (off + 4 * GT) * sizeof(double);
+    if (shm > 64 * 1024) {
+      e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_gbs_chain),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+      if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(k_gbs_chain, dim3(B), dim3(GT), shm, s, gp, sv, g, vol, C, nch, sp, off);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     hipLaunchKernelGGL(k_gbs_apply, dim3(nch, B), dim3(GST), 0, s, gp, sv, Sa, Sg, g, A, Bc, vol, C,
                        efilm, sp);
