@@ -524,6 +524,33 @@ def cpu_baseline_swin(st, K, steps):
                       f"{steps} steps after 1 warm-up ({med:.2f} s/step)"}
 
 
+def time_loss_pass(xshape, y, K, device, reps=10):
+    """The loss pass (k_loss + its finaliser: K*4 B logits and an 8 B label read, K*4 B
+    dlogits written per voxel -- SURVEY §8(d)'s fourth memory-bound pass), timed with HIP
+    events on the stream it runs on, on channel-last logits of this step's shape and the
+    step's labels, with the global valid count given as the data-parallel runner gives it.
+    Outside the timed step (the engine's own call, same sizes)."""
+    from innovative3D import _engine as E
+    B, _c, D, H, W = xshape
+    g = torch.Generator(device=device).manual_seed(7)
+    lcl = torch.randn(B, D, H, W, K, device=device, generator=g)
+    cnt = (y != 255).sum().reshape(1).to(torch.int64)
+    E.ce_dice_forward(lcl, y, K, 255, 1e-6, cnt)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        E.ce_dice_forward(lcl, y, K, 255, 1e-6, cnt)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    by = float(B * D * H * W) * (K * 4 + 8 + K * 4)
+    del lcl
+    return {"achieved_GBps": by / (ms * 1e-3) / 1e9, "frac": by / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "ms_per_call": ms, "algorithmic_bytes_per_call": by,
+            "note": "timed after the step loop on logits of the step's shape (one call per step)"}
+
+
 def rank_report(elapsed_local, steps, device):
     """World size, backend and every rank's own ms/step (all ranks must call)."""
     t = torch.tensor([elapsed_local], dtype=torch.float64, device=device)
@@ -751,6 +778,8 @@ def main():
                       "ms_per_step": ms_k / args.steps}
             tb += by
             tm += ms_k
+    if not (sharded or registry):
+        mem["loss"] = time_loss_pass(tuple(x.shape), y, K, device)
     roof["memory_bound"] = {
         "peak_GBps": HBM_PEAK_GBS, "kernels": mem,
         "aggregate": {"achieved_GBps": tb / (tm * 1e-3) / 1e9 if tm else None,
@@ -758,7 +787,8 @@ def main():
         "note": ("slab_reduce = per-(b,c,d) hw-reductions (IN statistics, gate sums; C*4 B per "
                  "input tensor per voxel, incl. the split combine); act_apply = IN/gate apply "
                  "(8*C B/voxel); in_bwd_apply = IN backward apply (12*C B/voxel); HIP events "
-                 "on the engine stream")}
+                 "on the engine stream; loss = k_loss + finaliser (K*4 + 8 + K*4 B/voxel), not "
+                 "in the aggregate")}
     if registry:
         cfg = {"workload": f"SPFF-UNet fwd+ce_plus_macro_dice+bwd, batch {B} x 1ch x 5 x {HW} x "
                            f"{HW} (registry layout) height-sharded into {world} x {Hl}-row slabs, "

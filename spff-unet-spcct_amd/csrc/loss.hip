@@ -17,13 +17,32 @@ namespace spff {
 // (integer atomics there, flushed once per workgroup); above it the counts go straight
 // to the int64 matrix in HBM, one atomic per distinct cell per wave (integer atomics:
 // still order-free and exact).
-constexpr int LOSS_GRID = 2048, LOSS_T = 256, KMAX = 128, KHIST_LDS = 64;
+#ifndef SPFF_LOSS_GRID
+#define SPFF_LOSS_GRID 1024  // (2048: 124.8 us per k_loss, 1024: 116.8, 512: 174.9 at 2 x 128^3, K 13)
+#endif
+constexpr int LOSS_GRID = SPFF_LOSS_GRID, LOSS_T = 256, KMAX = 128, KHIST_LDS = 64;
+#ifndef SPFF_LOSS_HOIST
+#define SPFF_LOSS_HOIST 1
+#endif
 
+// 16-B label pairs, four in flight per thread (one 8-B load per trip ran at ~1 TB/s)
 __global__ void k_count_valid(const int64_t* __restrict__ lab, int64_t V, int ignore,
                               unsigned long long* __restrict__ cnt) {
   unsigned long long c = 0;
-  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < V;
-       v += (int64_t)gridDim.x * blockDim.x)
+  const int64_t np = ((uintptr_t)lab & 15) == 0 ? V / 2 : 0;  // aligned pairs
+  const longlong2* lp = reinterpret_cast<const longlong2*>(lab);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t p0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p0 < np; p0 += 4 * stride) {
+    longlong2 r[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (p0 + u * stride < np) r[u] = lp[p0 + u * stride];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (p0 + u * stride < np)
+        c += (r[u].x != ignore ? 1ull : 0ull) + (r[u].y != ignore ? 1ull : 0ull);
+  }
+  for (int64_t v = 2 * np + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < V; v += stride)
     c += (lab[v] != ignore) ? 1ull : 0ull;
   __shared__ unsigned long long red[LOSS_T];
   red[threadIdx.x] = c;
@@ -74,11 +93,13 @@ __global__ __launch_bounds__(LOSS_T) void k_loss(const float* __restrict__ x,
     const int64_t v0 = grp * 64;
     const int nv = (int)(V - v0 < 64 ? V - v0 : 64);
     const int nf = nv * K;
+    // (SPFF_LOSS_HOIST) the label first: its load then overlaps the row copy's
+    int64_t y = (SPFF_LOSS_HOIST && lane < nv) ? lab[v0 + lane] : (int64_t)ignore;
     wave_copy_rows(sx, x + v0 * K, nf, lane);
     wave_lds_sync();
     cell = -1;
     if (lane < nv) {
-      const int64_t v = v0 + lane;
+      if (!SPFF_LOSS_HOIST) y = lab[v0 + lane];
       float* xr = sx + lane * K;
       float m = xr[0];
       int am = 0;
@@ -86,7 +107,6 @@ __global__ __launch_bounds__(LOSS_T) void k_loss(const float* __restrict__ x,
         const float t = xr[k];
         if (t > m || (isnan(t) && !isnan(m))) { m = t; am = k; }
       }
-      const int64_t y = lab[v];
       const bool valid = (y != ignore);
       if (valid && (y < 0 || y >= K)) {
         ++bad;
@@ -221,7 +241,9 @@ hipError_t count_valid(const int64_t* labels, int64_t V, int ignore, int64_t* co
                        hipStream_t s) {
   hipError_t e = hipMemsetAsync(count, 0, sizeof(int64_t), s);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_count_valid, dim3(LOSS_GRID), dim3(LOSS_T), 0, s, labels, V, ignore,
+  // 256 workgroups: each ends in one 64-bit atomic on the same counter, and 2048 of them
+  // queued on that one address took most of the kernel's ~30 us
+  hipLaunchKernelGGL(k_count_valid, dim3(256), dim3(LOSS_T), 0, s, labels, V, ignore,
                      reinterpret_cast<unsigned long long*>(count));
   return hipGetLastError();
 }

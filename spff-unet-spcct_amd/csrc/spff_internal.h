@@ -508,13 +508,49 @@ hipError_t confusion_only(const float* logits, const int64_t* labels, int64_t V,
 // row in LDS.  wave_lds_sync orders one wave's LDS writes before its reads by
 // other lanes (LDS executes a wave's instructions in order; the fence and
 // wave_barrier keep the compiler from moving accesses across it).
+// Up to 4 quads (or 4 floats) per lane are loaded before any is stored, so a run of up to
+// 1024 floats (K <= 16) costs one memory latency, not one per loop trip.
+#ifndef SPFF_COPY_BATCH
+#define SPFF_COPY_BATCH 1
+#endif
 __device__ __forceinline__ void wave_copy_rows(float* __restrict__ dst,
                                                const float* __restrict__ src, int n, int lane) {
+  if (!SPFF_COPY_BATCH) {
+    if ((((uintptr_t)src | (uintptr_t)dst) & 15) == 0 && (n & 3) == 0) {
+      for (int i = lane; i < (n >> 2); i += 64)
+        reinterpret_cast<float4*>(dst)[i] = reinterpret_cast<const float4*>(src)[i];
+    } else {
+      for (int i = lane; i < n; i += 64) dst[i] = src[i];
+    }
+    return;
+  }
+  // (clamped unconditional loads, predicated stores: a conditionally loaded register array
+  // went to scratch)
   if ((((uintptr_t)src | (uintptr_t)dst) & 15) == 0 && (n & 3) == 0) {
-    for (int i = lane; i < (n >> 2); i += 64)
-      reinterpret_cast<float4*>(dst)[i] = reinterpret_cast<const float4*>(src)[i];
+    const int n4 = n >> 2;
+    const float4* s4 = reinterpret_cast<const float4*>(src);
+    float4* d4 = reinterpret_cast<float4*>(dst);
+    for (int i0 = lane; i0 < n4; i0 += 256) {
+      const float4 r0 = s4[i0];
+      const float4 r1 = s4[min(i0 + 64, n4 - 1)];
+      const float4 r2 = s4[min(i0 + 128, n4 - 1)];
+      const float4 r3 = s4[min(i0 + 192, n4 - 1)];
+      d4[i0] = r0;
+      if (i0 + 64 < n4) d4[i0 + 64] = r1;
+      if (i0 + 128 < n4) d4[i0 + 128] = r2;
+      if (i0 + 192 < n4) d4[i0 + 192] = r3;
+    }
   } else {
-    for (int i = lane; i < n; i += 64) dst[i] = src[i];
+    for (int i0 = lane; i0 < n; i0 += 256) {
+      const float r0 = src[i0];
+      const float r1 = src[min(i0 + 64, n - 1)];
+      const float r2 = src[min(i0 + 128, n - 1)];
+      const float r3 = src[min(i0 + 192, n - 1)];
+      dst[i0] = r0;
+      if (i0 + 64 < n) dst[i0 + 64] = r1;
+      if (i0 + 128 < n) dst[i0 + 128] = r2;
+      if (i0 + 192 < n) dst[i0 + 192] = r3;
+    }
   }
 }
 __device__ __forceinline__ void wave_lds_sync() {
