@@ -21,6 +21,9 @@ namespace spff {
 #define SPFF_LOSS_GRID 1024  // (2048: 124.8 us per k_loss, 1024: 116.8, 512: 174.9 at 2 x 128^3, K 13)
 #endif
 constexpr int LOSS_GRID = SPFF_LOSS_GRID, LOSS_T = 256, KMAX = 128, KHIST_LDS = 64;
+#ifndef SPFF_LOSS_PF
+#define SPFF_LOSS_PF 1
+#endif
 #ifndef SPFF_LOSS_HOIST
 #define SPFF_LOSS_HOIST 1
 #endif
@@ -88,15 +91,56 @@ __global__ __launch_bounds__(LOSS_T) void k_loss(const float* __restrict__ x,
   double ce = 0.0;
   unsigned int bad = 0;
   const int64_t ngroups = (V + 63) / 64;
-  for (int64_t grp = (int64_t)blockIdx.x * LOSS_WAVES + wv; grp < ngroups;
-       grp += (int64_t)gridDim.x * LOSS_WAVES) {
+  const int64_t gstride = (int64_t)gridDim.x * LOSS_WAVES;
+  // (SPFF_LOSS_PF) the next group's rows (K <= 16: at most 4 quads per lane) and labels are
+  // loaded into registers while this group is worked on; the LDS orderings of this path
+  // wait for LDS only, so those loads stay in flight across them
+  const bool pf = SPFF_LOSS_PF && K <= 16 && (((uintptr_t)x & 15) == 0);
+  float4 q0 = {}, q1 = {}, q2 = {}, q3 = {};
+  int64_t ypf = ignore, pgrp = -1;
+  auto prefetch = [&](int64_t g) {
+    pgrp = -1;
+    if (g >= ngroups) return;
+    const int64_t w0 = g * 64;
+    const int nv2 = (int)(V - w0 < 64 ? V - w0 : 64);
+    if ((nv2 * K) & 3) return;  // (a ragged last run takes the plain copy)
+    const int n4 = (nv2 * K) >> 2;
+    const float4* s4 = reinterpret_cast<const float4*>(x + w0 * K);
+    q0 = s4[min(lane, n4 - 1)];
+    q1 = s4[min(lane + 64, n4 - 1)];
+    q2 = s4[min(lane + 128, n4 - 1)];
+    q3 = s4[min(lane + 192, n4 - 1)];
+    ypf = lane < nv2 ? lab[w0 + lane] : (int64_t)ignore;
+    pgrp = g;
+  };
+  auto lds_only_sync = [&]() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+  };
+  for (int64_t grp = (int64_t)blockIdx.x * LOSS_WAVES + wv; grp < ngroups; grp += gstride) {
     const int64_t v0 = grp * 64;
     const int nv = (int)(V - v0 < 64 ? V - v0 : 64);
     const int nf = nv * K;
-    // (SPFF_LOSS_HOIST) the label first: its load then overlaps the row copy's
-    int64_t y = (SPFF_LOSS_HOIST && lane < nv) ? lab[v0 + lane] : (int64_t)ignore;
-    wave_copy_rows(sx, x + v0 * K, nf, lane);
-    wave_lds_sync();
+    int64_t y;
+    if (pf && pgrp == grp) {
+      const int n4 = nf >> 2;
+      float4* d4 = reinterpret_cast<float4*>(sx);
+      if (lane < n4) d4[lane] = q0;
+      if (lane + 64 < n4) d4[lane + 64] = q1;
+      if (lane + 128 < n4) d4[lane + 128] = q2;
+      if (lane + 192 < n4) d4[lane + 192] = q3;
+      y = ypf;
+    } else {
+      // (SPFF_LOSS_HOIST) the label first: its load then overlaps the row copy's
+      y = (SPFF_LOSS_HOIST && lane < nv) ? lab[v0 + lane] : (int64_t)ignore;
+      wave_copy_rows(sx, x + v0 * K, nf, lane);
+    }
+    if (pf) {
+      lds_only_sync();
+      prefetch(grp + gstride);
+    } else {
+      wave_lds_sync();
+    }
     cell = -1;
     if (lane < nv) {
       if (!SPFF_LOSS_HOIST) y = lab[v0 + lane];
@@ -154,9 +198,9 @@ __global__ __launch_bounds__(LOSS_T) void k_loss(const float* __restrict__ x,
         todo &= ~same;
       }
     }
-    wave_lds_sync();
+    if (pf) lds_only_sync(); else wave_lds_sync();
     if (WITH_CE) wave_copy_rows(dx + v0 * K, sx, nf, lane);
-    wave_lds_sync();  // the next group overwrites the slice
+    if (pf) lds_only_sync(); else wave_lds_sync();  // the next group overwrites the slice
   }
   if (WITH_CE) {
     red[threadIdx.x] = ce;
