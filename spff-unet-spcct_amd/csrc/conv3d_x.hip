@@ -124,6 +124,9 @@
 // exposed at every row block
 #define SPFF_XPIPE 1
 #endif
+#ifndef SPFF_XPIPE64
+#define SPFF_XPIPE64 1  // the XPIPE row-block pipeline in the 64-wide tiles too (A/B 35.53 -> 35.40; 0: 32-wide only)
+#endif
 #ifndef SPFF_XEARLYW
 // 1: the first chunk's weight DMA is issued at the kernel start, before the first halo
 // fetch, so its L2 latency overlaps the halo's HBM latency instead of following it at the
@@ -788,7 +791,7 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : (BN <= 32 && NS == NS_F16 &&
     if (kc == kc0) st_t1 = __builtin_amdgcn_s_memtime();
 #endif
     // (XPIPE) the fragments of the current row block, carried across the unrolled k-loop
-    constexpr bool XPIPE = X16 && SPFF_XPIPE && BN <= 32 && !HR;  // (HR: 249 -> 256 VGPRs, spills)
+    constexpr bool XPIPE = X16 && SPFF_XPIPE && (BN <= 32 || SPFF_XPIPE64) && !HR;  // (HR: 249 -> 256 VGPRs, spills)
     const bool pg1 = kg & 1, pg2 = kg & 2;
     auto psel4 = [&](int c0, int c1, int c2, int c3) {
       const int lo = pg1 ? c1 : c0, hi = pg1 ? c3 : c2;
