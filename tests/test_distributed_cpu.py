@@ -282,3 +282,22 @@ def test_data_parallel_reduces_parameters_outside_the_plan(monkeypatch):
     reduced.clear()
     dp.step(torch.ones(3), None)
     assert reduced == [[id(m.extra)]]
+
+
+def test_sharded_overlap_default(monkeypatch):
+    """the sharded runners overlap the bucketed gradient all-reduces with
+    the backward by default only when the halo collectives are host-staged (the tested path);
+    device (RCCL) collectives need SPFF_SHARD_OVERLAP=1 until a multi-GPU run has exercised
+    them (innovative3D/sharded.py _default_overlap)."""
+    from innovative3D.sharded import _default_overlap
+
+    class Coll:
+        def __init__(self, host):
+            self.host = host
+
+    monkeypatch.delenv("SPFF_SHARD_OVERLAP", raising=False)
+    assert _default_overlap(Coll(True)) is True
+    assert _default_overlap(Coll(False)) is False
+    assert _default_overlap(object()) is True  # a custom coll without the attribute
+    monkeypatch.setenv("SPFF_SHARD_OVERLAP", "1")
+    assert _default_overlap(Coll(False)) is True
