@@ -144,10 +144,15 @@ def test_conv3d_f16x3_operand_scaling(amp):
 
 
 @pytest.mark.parametrize("K,shape", [(13, (2, 5, 16, 16)), (9, (1, 16, 32, 32)), (2, (1, 3, 8, 8)),
-                                     (100, (1, 4, 32, 33)), (128, (1, 3, 16, 16))])
+                                     (100, (1, 4, 32, 33)), (128, (1, 3, 16, 16)),
+                                     (13, (2, 33, 65, 67)), (4, (1, 65, 65, 66)),
+                                     (3, (2, 3, 11, 13))])
 def test_loss_matches_oracle(K, shape):
     """K > 64 takes the HBM confusion path (wave-aggregated atomics): labels and argmax
-    skewed onto a few cells there, as segmentation labels are."""
+    skewed onto a few cells there, as segmentation labels are.  The last three: more 64-voxel
+    runs than the grid has waves, so runs come from the register prefetch (loss.hip
+    SPFF_LOSS_PF), with a ragged last run of 6 rows (K 13: plain copy), of 2 rows (K 4: the
+    prefetch path's partial quad run) and a small ragged case."""
     g = torch.Generator().manual_seed(K)
     logits = torch.randn(shape[0], K, *shape[1:], generator=g) * 2
     y = torch.randint(0, K, shape, generator=g)
