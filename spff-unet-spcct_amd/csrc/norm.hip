@@ -18,6 +18,12 @@
 #ifndef SPFF_EW_GX
 #define SPFF_EW_GX 4  // blocks per (b,d) slab: fewer, longer streams measured fastest (64 -> 4: -20 %)
 #endif
+#ifndef SPFF_EW_MINWG
+// Floor on a whole launch's workgroups: with few (b,d) slabs (the registry's D = 5 depth)
+// SPFF_EW_GX blocks per slab leave most of the 256 CUs idle (B D 4 = 40 workgroups), so the
+// blocks per slab grow until the launch has this many.  The 128^3 patch (B D = 256) keeps 4.
+#define SPFF_EW_MINWG 1024
+#endif
 
 namespace spff {
 
@@ -629,10 +635,16 @@ __global__ __launch_bounds__(256) void k_act_apply(const float* __restrict__ y, 
   if (amax) block_amax(m, amax);
 }
 
+// Blocks per slab: SPFF_EW_GX, raised to reach SPFF_EW_MINWG workgroups in all, at most
+// one float4 per thread.  Any count keeps a thread's channel quad fixed (see above).
+static int ew_gx(int n4, int C, int slabs) {
+  const int want = std::max(SPFF_EW_GX, cdiv(SPFF_EW_MINWG, std::max(slabs, 1)));
+  return std::max(1, std::min(cdiv(n4, ew_bs(C)), want));
+}
+
 static dim3 ew_grid(Vol vol, int C) {
   const int n4 = vol.H * vol.W * (C / 4);
-  int gx = std::min(cdiv(n4, ew_bs(C)), SPFF_EW_GX);
-  return dim3(gx, vol.B * vol.D);
+  return dim3(ew_gx(n4, C, vol.B * vol.D), vol.B * vol.D);
 }
 
 hipError_t act_apply(const float* y, float* out, const float* al, const float* de, const float* P,
@@ -703,7 +715,7 @@ hipError_t act_apply_pool(const float* y, float* out, const float* al, const flo
                           int C, hipStream_t s, float neg, unsigned* amax) {
   if ((vol.H | vol.W) & 1 || C % 4) return hipErrorInvalidValue;
   const int n4 = (vol.H / 2) * (vol.W / 2) * (C / 4);
-  const dim3 grid(std::min(cdiv(n4, ew_bs(C)), SPFF_EW_GX), vol.B * vol.D);
+  const dim3 grid(ew_gx(n4, C, vol.B * vol.D), vol.B * vol.D);
   hipLaunchKernelGGL(k_act_apply_pool, grid, dim3(ew_bs(C)), 0, s, y, out, al, de, P, Q, pooled,
                      idx, vol, C, neg, amax);
   return hipGetLastError();
