@@ -1545,9 +1545,17 @@ bool conv3d_packs_batched(int math) {
   }();
   return !off && use_split(Vol{}, math, false) && use_split(Vol{}, math, true);
 }
+// Blocks per job: the largest weights (the 3DUNet's 320 x 320 x 27) set the launch's time,
+// so a job's cap is several blocks per CU, not the 64 (a quarter of the CUs) of round 4.
+#ifndef SPFF_PREP_NB
+#define SPFF_PREP_NB 256
+#endif
+#ifndef SPFF_PACK_NB
+#define SPFF_PACK_NB 512
+#endif
 bool prep_absmax(PrepJobs* J, const float* p, int64_t n, unsigned* slot) {
   if (J->n == 32 || n <= 0) return false;
-  const int nb = (int)std::min<int64_t>(64, std::max<int64_t>(1, (n + 8191) / 8192));
+  const int nb = (int)std::min<int64_t>(SPFF_PREP_NB, std::max<int64_t>(1, (n + 4095) / 4096));
   J->j[J->n++] = PrepJob{p, nullptr, slot, n, 0.f, 0, J->nblk, nb};
   J->nblk += nb;
   return true;
@@ -1570,7 +1578,7 @@ bool conv3d_pack_job(PackJobs* J, const float* w, void* wpack, int KD, int Cin_w
   if (J->n == 40) return false;
   const XDims d = xdims(KD, Cin_w, Cout_w, dgrad);
   const int64_t total = (int64_t)d.nkc * d.T2 * d.npad;
-  const int nb = (int)std::min<int64_t>(64, (total + 255) / 256);
+  const int nb = (int)std::min<int64_t>(SPFF_PACK_NB, (total + 255) / 256);
   J->j[J->n++] = PackJob{w, static_cast<uint4*>(wpack), wmax, Cout_w, Cin_w, d.T, d.T2, d.nkc,
                          d.npad, d.BN, dgrad ? 1 : 0, J->nblk, nb};
   J->nblk += nb;
