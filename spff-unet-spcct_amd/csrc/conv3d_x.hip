@@ -1217,6 +1217,18 @@ __global__ void k_splitk_reduce(const float* __restrict__ part, int nsplit, int6
   }
 }
 
+// 2-deep 32-wide tiles where the 4-deep ones waste more depth planes: D mod 4 = 1 or 2
+// (the registry's D = 5 computes 6 planes instead of 8).  Every host-side tile count
+// (xt_ntiles: fused statistics, split-K, depth / height splits) takes the same choice.
+#ifndef SPFF_X32SHALLOW
+#define SPFF_X32SHALLOW 1
+#endif
+static bool xt_shallow(Vol vol, int BN, int ns) {
+  return SPFF_X32SHALLOW && xt_d4(BN, ns) && (vol.D % 4 == 1 || vol.D % 4 == 2);
+}
+static int xt_td_v(Vol vol, int BN, int ns) { return xt_shallow(vol, BN, ns) ? XT_D : xt_td(BN, ns); }
+static int xt_mb_v(Vol vol, int BN, int ns) { return xt_shallow(vol, BN, ns) ? 2 : xt_mb(BN, ns); }
+
 template <int BN, int KD, int NS, bool HR, int MB = xt_mb(BN, NS), int NW = xt_nw(BN, NS),
           int TD = xt_td(BN, NS)>
 static hipError_t launch_fwd_xh(const Src2& x, const uint4* wx, const Dst2& y, Vol vol, int K,
@@ -1265,6 +1277,14 @@ template <int BN, int KD, int NS>
 static hipError_t launch_fwd_x(const Src2& x, const uint4* wx, const Dst2& y, Vol vol, int K,
                                int nkc, int N, int npad, hipStream_t s, float* part, int nsplit,
                                int kps, float* stats, int dpart, const unsigned* wmx) {
+  if constexpr (xt_d4(BN, NS)) {
+    constexpr int NW = xt_nw(BN, NS);
+    if (xt_shallow(vol, BN, NS))
+      return x.rows() ? launch_fwd_xh<BN, KD, NS, true, 2, NW, XT_D>(
+                            x, wx, y, vol, K, nkc, N, npad, s, part, nsplit, kps, stats, dpart, wmx)
+                      : launch_fwd_xh<BN, KD, NS, false, 2, NW, XT_D>(
+                            x, wx, y, vol, K, nkc, N, npad, s, part, nsplit, kps, stats, dpart, wmx);
+  }
   return x.rows() ? launch_fwd_xh<BN, KD, NS, true>(x, wx, y, vol, K, nkc, N, npad, s, part,
                                                     nsplit, kps, stats, dpart, wmx)
                   : launch_fwd_xh<BN, KD, NS, false>(x, wx, y, vol, K, nkc, N, npad, s, part,
@@ -1315,7 +1335,8 @@ bool conv3d_fuses_act(int math, int C) {
 // tiles of a BN-wide launch (the fused IN statistics are per (tile, out channel))
 static int64_t xt_ntiles(Vol vol, int BN, int ns) {
   const int nw = xt_nw(BN, ns);
-  const int td = xt_td(BN, ns), th = SPFF_X16 ? 2 * nw * xt_mb(BN, ns) / td : nw * xt_mb(BN, ns);
+  const int td = xt_td_v(vol, BN, ns), mb = xt_mb_v(vol, BN, ns);
+  const int th = SPFF_X16 ? 2 * nw * mb / td : nw * mb;
   return (int64_t)vol.B * cdiv(vol.D, td) * cdiv(vol.H, th) * cdiv(vol.W, XT_W);
 }
 namespace {
@@ -1639,13 +1660,14 @@ size_t conv3d_splitk_bytes(Vol vol, int KD, int Cin, int Cout) {
 bool conv3d_splits_depth(Vol vol, int KD, int Cin_w, int Cout_w, bool dgrad, int math) {
   const XDims d = xdims(KD, Cin_w, Cout_w, dgrad);
   return KD == 3 && use_split(vol, math, dgrad) && splitk_plan(vol, d, ns_of(math)).nsplit == 1 &&
-         cdiv(vol.D, xt_td(d.BN, ns_of(math))) >= 3;
+         cdiv(vol.D, xt_td_v(vol, d.BN, ns_of(math))) >= 3;
 }
 bool conv3d_splits_height(Vol vol, int KD, int Cin_w, int Cout_w, bool dgrad, int math) {
   const XDims d = xdims(KD, Cin_w, Cout_w, dgrad);
   const int nw = xt_nw(d.BN, ns_of(math));
   const int ns = ns_of(math);
-  const int th = SPFF_X16 ? 2 * nw * xt_mb(d.BN, ns) / xt_td(d.BN, ns) : nw * xt_mb(d.BN, ns);
+  const int th = SPFF_X16 ? 2 * nw * xt_mb_v(vol, d.BN, ns) / xt_td_v(vol, d.BN, ns)
+                          : nw * xt_mb_v(vol, d.BN, ns);
   return use_split(vol, math, dgrad) && splitk_plan(vol, d, ns_of(math)).nsplit == 1 &&
          cdiv(vol.H, th) >= 3;
 }
