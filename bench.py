@@ -4,8 +4,13 @@ backward (weight grads; optimizer step excluded, as in the metric's
 definition) on a batch of 2 x 5-channel 128^3 patches (K=13,
 base 32) per GPU, synthetic data resident in HBM before the timed region.
 
-    python bench.py [--gpus N --steps K --warmup W]
+    python bench.py [--gpus N --steps K --warmup W]     (N > 1: starts its own N ranks)
     torchrun --nproc-per-node N bench.py --gpus N ...   (data parallel, RCCL)
+
+With --gpus N > 1 and no launcher (WORLD_SIZE unset) the parent process starts N fresh
+children with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT set
+(`launch_ranks`) before any device call and exits with the first non-zero child code.
+Under a launcher, --gpus must equal WORLD_SIZE.
 
 One process per GPU; N > 1 is batch data parallelism (weak scaling): each rank
 runs its own batch, the valid-voxel count is all-reduced before the loss so
@@ -329,6 +334,7 @@ def bench_unet3d(args, world, rank, device):
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    ranks = rank_report(elapsed, args.steps, device) if world > 1 else None
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -355,6 +361,8 @@ def bench_unet3d(args, world, rank, device):
         "algorithmic_flops_per_step": fl,
         "cpu_baseline": None,
     }
+    if ranks:
+        out["ranks"] = ranks
     if rank == 0 and world == 1 and args.cpu_baseline == "auto":
         out["cpu_baseline"] = cpu_baseline_unet3d(st, K, args.cpu_steps)
         out["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
@@ -467,6 +475,7 @@ def bench_swin(args, world, rank, device):
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    ranks = rank_report(elapsed, args.steps, device) if world > 1 else None
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -493,6 +502,8 @@ def bench_swin(args, world, rank, device):
         "parity": "unpinned (MONAI absent offline); engine vs the restated oracle: tests/test_gpu_swin.py",
         "cpu_baseline": None,
     }
+    if ranks:
+        out["ranks"] = ranks
     if rank == 0 and world == 1 and args.cpu_baseline == "auto":
         out["cpu_baseline"] = cpu_baseline_swin(st, K, args.cpu_steps)
         out["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
@@ -560,6 +571,49 @@ def rank_report(elapsed_local, steps, device):
             "ms_per_step_by_rank": [float(v.item()) / steps * 1e3 for v in ts]}
 
 
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv, child_cmd=None, env=None):
+    """`bench.py --gpus N` without an external launcher: start N FRESH child processes
+    (`sys.executable bench.py <argv>`), one per GPU, with RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_ADDR (127.0.0.1) / MASTER_PORT set, exactly what `torch.distributed.run` would
+    set, then wait for all of them.  The parent never touches the GPU (no torch.cuda call
+    before or after), so each child initialises HIP and RCCL on its own device.  Returns
+    the first non-zero child exit code (in rank order), else 0; when one child fails the
+    others are given the process-group timeout to fail their collectives, then killed."""
+    import subprocess
+    cmd = list(child_cmd or [sys.executable, str(pathlib.Path(__file__).resolve())]) + list(argv)
+    base = dict(os.environ if env is None else env)
+    base.setdefault("MASTER_ADDR", "127.0.0.1")
+    base.setdefault("MASTER_PORT", str(_free_port()))
+    procs = []
+    for r in range(n):
+        e = dict(base, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                 LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", SPFF_BENCH_LAUNCHED="1")
+        procs.append(subprocess.Popen(cmd, env=e))
+    rcs = [None] * n
+    deadline = None
+    while any(rc is None for rc in rcs):
+        for i, p in enumerate(procs):
+            if rcs[i] is None:
+                rcs[i] = p.poll()
+        if deadline is None and any(rc not in (None, 0) for rc in rcs):
+            deadline = time.time() + float(base.get("SPFF_BENCH_KILL_AFTER", "120"))
+        if deadline is not None and time.time() > deadline:
+            for i, p in enumerate(procs):
+                if rcs[i] is None:
+                    p.kill()
+                    rcs[i] = p.wait()
+        time.sleep(0.05)
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -609,9 +663,28 @@ def main():
                          "(scripts/pmc_traffic.py); used only when its workload key matches")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:
+            # no external launcher: start the N ranks here, before anything touches the GPU
+            raise SystemExit(launch_ranks(args.gpus, sys.argv[1:]))
+    elif int(os.environ["WORLD_SIZE"]) != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE="
+                         f"{os.environ['WORLD_SIZE']} ranks")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("SPFF_BENCH_STUB") == "1":
+        # launcher test hook (tests/test_bench_launch_cpu.py): report the rank layout and
+        # stop before any device call
+        print(json.dumps({"stub": True, "rank": rank, "local_rank": local, "world_size": world,
+                          "launched": os.environ.get("SPFF_BENCH_LAUNCHED") == "1",
+                          "master": [os.environ.get("MASTER_ADDR"),
+                                     os.environ.get("MASTER_PORT")]}), flush=True)
+        return
+    if world > 1 and not args.one_gpu:
+        n_dev = torch.cuda.device_count()  # does not initialise HIP on this image
+        if local >= n_dev:
+            raise SystemExit(f"bench.py: rank {rank} needs device {local}, {n_dev} visible")
     device = torch.device("cuda", 0 if args.one_gpu else local)
     torch.cuda.set_device(device)
     if world > 1:
