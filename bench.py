@@ -326,6 +326,8 @@ def bench_unet3d(args, world, rank, device):
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
+    from innovative3D import _engine as E
+    E.conv_prof_enable(True)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -334,6 +336,8 @@ def bench_unet3d(args, world, rank, device):
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    cprof = E.conv_prof_collect()
+    E.conv_prof_enable(False)
     ranks = rank_report(elapsed, args.steps, device) if world > 1 else None
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
     if world > 1:
@@ -359,6 +363,7 @@ def bench_unet3d(args, world, rank, device):
         "backbone_voxels_per_s": value * 16 / D0,
         "step_tflops": fl * world * args.steps / elapsed / 1e12 / world,
         "algorithmic_flops_per_step": fl,
+        "roofline": conv_class_roofline(cprof, args.steps, args.math, elapsed / args.steps * 1e3),
         "cpu_baseline": None,
     }
     if ranks:
@@ -370,6 +375,31 @@ def bench_unet3d(args, world, rank, device):
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def conv_class_roofline(prof, steps, math, step_ms):
+    """`roofline` of a workload whose step is not an SPFF plan (3DUNet, SwinUNETR): the 3x3x3
+    fwd/dgrad conv launches (the same k_conv3d_fwd_x kernel as the headline's dominant
+    kernel), timed live with HIP events on their stream by the library-wide conv profiler
+    (spff_conv_prof_*), algorithmic fp32 flops 2 V Cin Cout 27 per launch; the weight
+    gradient and each class's share of the step beside it."""
+    ms = prof["conv_fwd"][0] + prof["conv_dgrad"][0]
+    fl = prof["conv_fwd"][1] + prof["conv_dgrad"][1]
+    nl = prof["conv_fwd"][2] + prof["conv_dgrad"][2]
+    achieved = fl / (ms * 1e-3) / 1e12 if ms > 0 else None
+    peak = MATH_PEAK[math]
+    return {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+            "frac": (achieved / peak) if achieved else None, "traffic": None,
+            "kernel": MATH_KERNEL[math], "avg_launch_ms": ms / max(1, nl), "launches": int(nl),
+            "algorithmic_flops_per_launch": fl / max(1, nl),
+            "per_class_ms_per_step": {k: v[0] / steps for k, v in prof.items()},
+            "per_class_tflops": {k: (v[1] / (v[0] * 1e-3) / 1e12 if v[0] > 0 else None)
+                                 for k, v in prof.items()},
+            "conv_share_of_step": sum(v[0] for v in prof.values()) / steps / step_ms,
+            "note": ("3x3x3 conv classes timed by the library-wide conv profiler (HIP events "
+                     "around each launch on its stream, spff_conv_prof_*); achieved = fwd + "
+                     "dgrad algorithmic flops / their summed durations; traffic not "
+                     "collected for this workload")}
 
 
 def cpu_baseline_unet3d(st, K, steps):
@@ -467,6 +497,8 @@ def bench_swin(args, world, rank, device):
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
+    from innovative3D import _engine as E
+    E.conv_prof_enable(True)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -475,6 +507,8 @@ def bench_swin(args, world, rank, device):
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    cprof = E.conv_prof_collect()
+    E.conv_prof_enable(False)
     ranks = rank_report(elapsed, args.steps, device) if world > 1 else None
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
     if world > 1:
@@ -500,6 +534,7 @@ def bench_swin(args, world, rank, device):
         "step_tflops": fl * args.steps / elapsed / 1e12,
         "algorithmic_flops_per_step": fl,
         "parity": "unpinned (MONAI absent offline); engine vs the restated oracle: tests/test_gpu_swin.py",
+        "roofline": conv_class_roofline(cprof, args.steps, args.math, elapsed / args.steps * 1e3),
         "cpu_baseline": None,
     }
     if ranks:

@@ -172,6 +172,13 @@ int spff_debug_set(spff_plan* plan, int key, int value);
  * once, result written once)}. */
 int spff_prof_enable(spff_plan* plan, int on);
 int spff_prof_collect(spff_plan* plan, double* out, int nclass);
+/* Library-wide conv timing: HIP events around every 3x3x3 conv launch (forward, input
+ * gradient, weight gradient) on the stream it runs on, whichever plan or op entry point
+ * issues it (the 3DUNet / SwinUNETR plans included).  collect: out[4 c + {0,1,2,3}] =
+ * (ms, algorithmic fp32 flops 2 V Cin Cout T, launches, 0) for class c = 0 fwd, 1 dgrad,
+ * 2 wgrad; synchronises on the recorded events and resets the record. */
+int spff_conv_prof_enable(int on);
+int spff_conv_prof_collect(double* out, int nclass);
 
 /* ce_plus_macro_dice_loss (helpers.py:797-803) on channel-last logits [V][K].
  * out4 (device) = [ce, ce + 0.5*hard_dice_loss, hard_dice_loss, n_valid];

@@ -103,8 +103,18 @@ for r in range(reps):
     for k, v in cur.items():
         ref = first[k]
         d = float((v - ref).abs().max() / ref.abs().max().clamp_min(1e-300))
+        l2 = float((v - ref).norm() / ref.norm().clamp_min(1e-300))
         if d > 1e-12:
-            bad.append((k, d))
-    print(f"run {r}: loss {float(loss):.12f}; {len(bad)} records differ from run 0", flush=True)
-    for k, d in bad[:14]:
-        print(f"    {k:40s} {d:.3e}", flush=True)
+            bad.append((d, l2, k))
+    # largest first (insertion order listed only the early activation records),
+    # then every parameter-gradient record that moved -- the oracle's own gradients
+    bad.sort(reverse=True)
+    print(f"run {r}: loss {float(loss):.12f}; {len(bad)} records differ from run 0 "
+          f"(max|diff|/max|ref|, rel L2), largest first:", flush=True)
+    for d, l2, k in bad[:14]:
+        print(f"    {k:40s} {d:.3e}  {l2:.3e}", flush=True)
+    grads = [b for b in bad if b[2].startswith("grad ")]
+    print(f"  parameter-gradient records that differ: {len(grads)} of "
+          f"{sum(1 for k in cur if k.startswith('grad '))}", flush=True)
+    for d, l2, k in grads[:10]:
+        print(f"    {k:40s} {d:.3e}  {l2:.3e}", flush=True)

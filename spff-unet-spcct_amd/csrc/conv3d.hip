@@ -504,9 +504,20 @@ hipError_t conv3d_wgrad_reduce(const float* part, float* dw, int nsplit, int T, 
   return hipGetLastError();
 }
 
+static hipError_t conv3d_wgrad_(const Src2& x, const float* dy, int lddy, float* dw, Vol vol,
+                                int KD, int Cin, int Cout, int math, float* ws, hipStream_t s,
+                                const unsigned* xmax, const unsigned* ymax);
 hipError_t conv3d_wgrad(const Src2& x, const float* dy, int lddy, float* dw, Vol vol, int KD,
                         int Cin, int Cout, int math, float* ws, hipStream_t s,
                         const unsigned* xmax, const unsigned* ymax) {
+  CProf pr(2, 2.0 * (double)nvox(vol) * Cin * Cout * 9 * KD, s);
+  const hipError_t e = conv3d_wgrad_(x, dy, lddy, dw, vol, KD, Cin, Cout, math, ws, s, xmax, ymax);
+  pr.end(s);
+  return e;
+}
+static hipError_t conv3d_wgrad_(const Src2& x, const float* dy, int lddy, float* dw, Vol vol,
+                                int KD, int Cin, int Cout, int math, float* ws, hipStream_t s,
+                                const unsigned* xmax, const unsigned* ymax) {
   if (math != SPFF_MATH_F32 && debug_split_wgrad())
     return conv3d_wgrad_x(x, dy, lddy, dw, vol, KD, Cin, Cout, math, ws, s, xmax, ymax);
   if (lddy % 4) return hipErrorInvalidValue;

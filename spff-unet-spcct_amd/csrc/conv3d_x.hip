@@ -44,6 +44,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <type_traits>
+#include <vector>
 
 #ifndef SPFF_XDIAG
 #define SPFF_XDIAG 0  // timing diagnostics only: 1 = no restaging, 2 = no MFMA loop,
@@ -381,6 +382,9 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : (BN <= 32 && NS == NS_F16 &&
   constexpr int NWU = NP * T2 * BN;  // pre-split weight units (16 B) per chunk
   static_assert(NWU % 64 == 0, "weight image must be whole 1 KiB DMA pieces");
   static_assert(!X16 || TD * TH == NW * RB, "X16: one W-row per 16-row block");
+  // the epilogue's two fused-statistics tables [NW][CB][NCOL] (= NW BN floats each) live in
+  // the 16 BN floats xt_lds_bytes reserves beside the output tile
+  static_assert(NW <= 8, "fused-statistics tables: at most 8 waves");
   // the k-step from which the next chunk's halo is split (HF: after its block max), and the
   // halo float4 split per k-step from there on
   constexpr int J0 = (NS == NS_F16 && SPFF_XSCALEJ >= 0 && SPFF_XSCALEJ < NJ) ? SPFF_XSCALEJ : NJ / 2;
@@ -1237,7 +1241,9 @@ static hipError_t launch_fwd_xh(const Src2& x, const uint4* wx, const Dst2& y, V
   constexpr int TH = SPFF_X16 ? 2 * NW * MB / TD : NW * MB;
   static_assert(NW == 8 || TD == XT_D || xt_d4(BN, NS), "xt_ntiles: tile shape");
   constexpr size_t shm = xt_lds_bytes<BN, KD, NS, TD, TH>();
-  static_assert(shm <= (NW == 8 ? 160 : 80) * 1024, "LDS budget");
+  // (+ the kernel's static tables: the fused activation's scf[2][32] float4 and the per-wave
+  // scale slots smx[2][NW])
+  static_assert(shm + 2 * 32 * 16 + 2 * NW * 4 <= (NW == 8 ? 160 : 80) * 1024, "LDS budget");
   if (x.al && BN != 32) return hipErrorInvalidValue;  // fused activation: 32-wide tiles only
   if (x.al && nkc > 16) return hipErrorInvalidValue;  // the kernel's LDS coefficient table
   // the 16/32-wide kernels hold halo voxel indices in 32 bits (with the halo slices)
@@ -1690,9 +1696,71 @@ hipError_t conv3d_in_stats_fin(const float* stats, Vol vol, int KD, int Cin, int
   return hipGetLastError();
 }
 
+namespace {
+struct CProfRec {
+  hipEvent_t a = nullptr, b = nullptr;
+  int cls = 0;
+  double flops = 0.0;
+};
+std::vector<CProfRec> g_cprof;
+size_t g_cprof_n = 0;
+bool g_cprof_on = false;
+}  // namespace
+CProf::CProf(int cls, double flops, hipStream_t s) {
+  if (!g_cprof_on) return;
+  if (g_cprof_n == g_cprof.size()) {
+    CProfRec r;
+    if (hipEventCreate(&r.a) != hipSuccess || hipEventCreate(&r.b) != hipSuccess) return;
+    g_cprof.push_back(r);
+  }
+  CProfRec& r = g_cprof[g_cprof_n];
+  r.cls = cls;
+  r.flops = flops;
+  if (hipEventRecord(r.a, s) != hipSuccess) return;
+  rec = (int)g_cprof_n++;
+}
+void CProf::end(hipStream_t s) {
+  if (rec >= 0) (void)hipEventRecord(g_cprof[rec].b, s);
+  rec = -1;
+}
+void conv_prof_enable(bool on) {
+  g_cprof_on = on;
+  g_cprof_n = 0;
+}
+hipError_t conv_prof_collect(double* out, int nclass) {
+  for (int i = 0; i < 4 * nclass; ++i) out[i] = 0.0;
+  for (size_t i = 0; i < g_cprof_n; ++i) {
+    CProfRec& r = g_cprof[i];
+    hipError_t e = hipEventSynchronize(r.b);
+    if (e != hipSuccess) return e;
+    float ms = 0.f;
+    e = hipEventElapsedTime(&ms, r.a, r.b);
+    if (e != hipSuccess) return e;
+    if (r.cls < nclass) {
+      out[4 * r.cls + 0] += ms;
+      out[4 * r.cls + 1] += r.flops;
+      out[4 * r.cls + 2] += 1.0;
+    }
+  }
+  g_cprof_n = 0;
+  return hipSuccess;
+}
+
+static hipError_t conv3d_run_(const Src2& x, const void* wpack, const Dst2& y, Vol vol, int KD,
+                              int Cin_w, int Cout_w, bool dgrad, int math, hipStream_t s,
+                              float* ws, float* stats, int dpart, const unsigned* wmax);
 hipError_t conv3d_run(const Src2& x, const void* wpack, const Dst2& y, Vol vol, int KD,
                       int Cin_w, int Cout_w, bool dgrad, int math, hipStream_t s, float* ws,
                       float* stats, int dpart, const unsigned* wmax) {
+  CProf pr(dgrad ? 1 : 0, 2.0 * (double)nvox(vol) * Cin_w * Cout_w * 9 * KD, s);
+  const hipError_t e = conv3d_run_(x, wpack, y, vol, KD, Cin_w, Cout_w, dgrad, math, s, ws,
+                                   stats, dpart, wmax);
+  pr.end(s);
+  return e;
+}
+static hipError_t conv3d_run_(const Src2& x, const void* wpack, const Dst2& y, Vol vol, int KD,
+                              int Cin_w, int Cout_w, bool dgrad, int math, hipStream_t s,
+                              float* ws, float* stats, int dpart, const unsigned* wmax) {
   const XDims d = xdims(KD, Cin_w, Cout_w, dgrad);
   if (stats && (dgrad || !conv3d_fuses_stats(vol, KD, Cin_w, Cout_w, math)))
     return hipErrorInvalidValue;

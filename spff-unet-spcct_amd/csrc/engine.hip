@@ -167,6 +167,7 @@ struct spff_plan {
   int dbg_stop = -1;  // debug: stop backward after this many blocks (-1 = off)
   bool efilm_ready = false;  // this forward's EFiLM coefficients are computed (all blocks)
   bool keep_out = false;  // debug: store the fused block outputs too (saved views)
+  bool pool_fold = SPFF_POOL_FOLD;  // PoolAdd in the encoder backward (debug key 2: off)
   // per call
   char* ws = nullptr;
   const float* prm = nullptr;
@@ -1105,6 +1106,11 @@ int bwd_block(spff_plan* p, Blk& b, const float* dout, const Dst2* dx, const Src
   }
   float* dy2 = p->F(p->G_dy2);
   float* da1 = p->F(p->G_da1);
+  // PoolAdd reads the pooled gradient (in G_dx) up to this block's IN-backward apply of dy2;
+  // only the block's last dgrad (into dx) may overwrite it, so neither dy2 nor da1 may live
+  // there (a placement change would corrupt the encoder gradients silently)
+  if (pa.dp && (pa.dp == dy2 || pa.dp == da1))
+    return fail(SPFF_EINVAL, "PoolAdd gradient aliases a scratch the block writes first");
   {
     RedArgs a{};
     a.y = p->F(b.y2); a.g = dout; a.mean = p->F(b.mean2); a.rstd = p->F(b.rstd2);
@@ -1275,7 +1281,7 @@ int backward(spff_plan* p, const float* dl) {
     PoolAdd pa;
     pa.dp = p->F(p->G_dx);
     pa.idx = reinterpret_cast<const uint8_t*>(p->ws + p->pidx[l]);
-    if (!SPFF_POOL_FOLD) {
+    if (!p->pool_fold) {
       HIPCK(maxpool_bwd_add(pa.dp, pa.idx, p->F(p->dskip[l]), C, p->F(p->dskip[l]), p->vol[l], C,
                             p->st));
       pa = PoolAdd{};
@@ -1461,6 +1467,7 @@ int spff_debug_set(spff_plan* p, int key, int value) {
   if (!p) return fail(SPFF_EINVAL, "null plan");
   if (key == 0) p->dbg_stop = value;
   if (key == 1) p->keep_out = value != 0;  // store the GEMM-applied block outputs too
+  if (key == 2) p->pool_fold = value != 0;  // 0: k_maxpool_bwd_add pass instead of PoolAdd
   return SPFF_OK;
 }
 
@@ -1487,6 +1494,17 @@ int spff_prof_collect(spff_plan* p, double* out, int nclass) {
     }
   }
   p->prof_n = 0;
+  return SPFF_OK;
+}
+
+int spff_conv_prof_enable(int on) {
+  conv_prof_enable(on != 0);
+  return SPFF_OK;
+}
+
+int spff_conv_prof_collect(double* out, int nclass) {
+  if (!out || nclass < 0) return fail(SPFF_EINVAL, "null argument");
+  HIPCK(conv_prof_collect(out, nclass));
   return SPFF_OK;
 }
 

@@ -169,6 +169,17 @@ hipError_t conv3d_wgrad(const Src2& x, const float* dy, int lddy, float* dw, Vol
                         const unsigned* xmax = nullptr, const unsigned* ymax = nullptr);
 size_t conv3d_wgrad_x_ws_bytes(Vol vol, int KD, int Cin, int Cout);
 bool debug_split_wgrad();  // SPFF_DEBUG_SPLIT (conv3d_x.hip)
+// Library-wide conv timing (spff_conv_prof_*, conv3d_x.hip): when on, conv3d_run and
+// conv3d_wgrad bracket their launches with HIP events on the stream they run on, whichever
+// plan (SPFF, 3DUNet, SwinUNETR) or the op-level ABI calls them.  Classes: 0 fwd,
+// 1 dgrad, 2 wgrad; flops = 2 V Cin Cout T (algorithmic, fp32).
+struct CProf {
+  int rec = -1;
+  CProf(int cls, double flops, hipStream_t s);
+  void end(hipStream_t s);
+};
+void conv_prof_enable(bool on);
+hipError_t conv_prof_collect(double* out, int nclass);
 // the split-bf16 fwd and wgrad kernels apply Src2::al / de to a C-channel conv input of
 // a C -> C conv (conv3d_x.hip: the 32-wide tiles, so C == 32)
 bool conv3d_fuses_act(int math, int C);

@@ -130,6 +130,8 @@ _SIGS = {
     "spff_debug_set": (_I, [_P, _I, _I]),
     "spff_prof_enable": (_I, [_P, _I]),
     "spff_prof_collect": (_I, [_P, ctypes.POINTER(ctypes.c_double), _I]),
+    "spff_conv_prof_enable": (_I, [_I]),
+    "spff_conv_prof_collect": (_I, [ctypes.POINTER(ctypes.c_double), _I]),
     "spff_loss_ws_bytes": (_S, [_L, _I]),
     "spff_loss": (_I, [_P, _P, _L, _I, _I, ctypes.c_double, _P, _P, _P, _P, _P, _P]),
     "spff_confusion": (_I, [_P, _P, _L, _I, _I, _P, _P]),
@@ -498,7 +500,8 @@ class Plan:
 
     def debug_set(self, key: int, value: int):
         """spff_debug_set: key 0 = stop the backward after N decoder blocks, key 1 = store
-        the GEMM-applied block outputs too (saved("dec1.out") etc.)."""
+        the GEMM-applied block outputs too (saved("dec1.out") etc.), key 2 = 0: the encoder
+        output gradients by a k_maxpool_bwd_add pass instead of PoolAdd in their readers."""
         check(lib().spff_debug_set(self._h, int(key), int(value)), "spff_debug_set")
 
     def saved(self, name: str) -> torch.Tensor:
@@ -1007,3 +1010,21 @@ def scale_(x: torch.Tensor, scale: torch.Tensor) -> torch.Tensor:
 def to_channels_last(t: torch.Tensor) -> torch.Tensor:
     """[B,C,D,H,W] -> contiguous [B,D,H,W,C] (a free view for channels_last_3d)."""
     return t.permute(0, 2, 3, 4, 1).contiguous()
+
+
+CONV_PROF_CLASSES = ("conv_fwd", "conv_dgrad", "conv_wgrad")
+
+
+def conv_prof_enable(on: bool = True) -> None:
+    """Library-wide conv timing (every 3x3x3 conv launch of any plan; HIP events on the
+    launch's stream) -- the 3DUNet / SwinUNETR bench lines' roofline source."""
+    check(lib().spff_conv_prof_enable(int(bool(on))), "spff_conv_prof_enable")
+
+
+def conv_prof_collect() -> Dict[str, Tuple[float, float, int]]:
+    """{class: (ms, algorithmic fp32 flops, launches)} since the last enable / collect."""
+    n = len(CONV_PROF_CLASSES)
+    buf = (ctypes.c_double * (4 * n))()
+    check(lib().spff_conv_prof_collect(buf, n), "spff_conv_prof_collect")
+    return {c: (buf[4 * i], buf[4 * i + 1], int(buf[4 * i + 2]))
+            for i, c in enumerate(CONV_PROF_CLASSES)}

@@ -110,7 +110,7 @@ class GradBucketer:
     def __init__(self, group=None, bucket_bytes: int = 4 << 20):
         self.group, self.bucket_floats = group, max(1, bucket_bytes // 4)
         self.flat: Optional[torch.Tensor] = None
-        self.runs: List[List[int]] = []   # pending [start, end) runs, disjoint
+        self.runs: List[list] = []        # pending [start, end, stream] runs, disjoint
         self.works = []
         self.launched: List[tuple] = []   # (start, end) of every issued all-reduce
         self.begun = 0                    # begin() calls (DataParallelSPFF checks coverage)
@@ -135,29 +135,44 @@ class GradBucketer:
             except Exception:  # noqa: BLE001 -- the original error is what propagates
                 pass
 
-    def _launch(self, a: int, b: int) -> None:
+    def _stream_key(self):
+        """the stream ready() was called on (device tensors; None on the host): a run's
+        all-reduce is ordered after the work of the stream that reported it, so runs
+        reported on different streams are never merged"""
+        f = self.flat
+        if f is None or not f.is_cuda:
+            return None
+        return torch.cuda.current_stream(f.device).cuda_stream
+
+    def _launch(self, a: int, b: int, key=None) -> None:
         self.launched.append((a, b))
-        self.works.append(dist.all_reduce(self.flat[a:b], group=self.group, async_op=True))
+        f = self.flat
+        if key is not None and key != self._stream_key():
+            with torch.cuda.stream(torch.cuda.ExternalStream(key, device=f.device)):
+                self.works.append(dist.all_reduce(f[a:b], group=self.group, async_op=True))
+            return
+        self.works.append(dist.all_reduce(f[a:b], group=self.group, async_op=True))
 
     def ready(self, off: int, n: int) -> None:
         a, b = int(off), int(off) + int(n)
+        key = self._stream_key()
         keep = []
         for r in self.runs:
-            if r[1] == a:
+            if r[2] == key and r[1] == a:
                 a = r[0]
-            elif r[0] == b:
+            elif r[2] == key and r[0] == b:
                 b = r[1]
             else:
                 keep.append(r)
         if b - a >= self.bucket_floats:
             self.runs = keep
-            self._launch(a, b)
+            self._launch(a, b, key)
         else:
-            self.runs = keep + [[a, b]]
+            self.runs = keep + [[a, b, key]]
 
     def finish(self) -> None:
-        for a, b in sorted(self.runs):
-            self._launch(a, b)
+        for a, b, key in sorted(self.runs, key=lambda r: r[0]):
+            self._launch(a, b, key)
         self.runs = []
         for w in self.works:
             w.wait()

@@ -31,6 +31,7 @@ within 1e-3 relative L2 (GRAD_DEV below: where that fp64 backward is evaluated).
 
 The module's tests are the suite's longest; tests/conftest.py runs them last.
 """
+import json
 import os
 import socket
 
@@ -202,6 +203,21 @@ def _compare(tag, lg, loss, grads, ref_logits, ref_loss, ref_grads, loss_rtol=1e
     assert not bad, "; ".join(bad)
 
 
+def _oracle_forward64(st, x):
+    """fp64 oracle logits (the exact reference of both the fp32 oracle and the engine),
+    evaluated where the fp64 gradient oracle runs (GRAD_DEV)."""
+    from oracle import spff_oracle as O
+    torch.set_num_threads(_threads())
+    P = O.params_from_state({k: v for k, v in st.items() if not k.endswith("._mask")},
+                            requires_grad=False, dtype=torch.float64, device=GRAD_DEV)
+    with torch.no_grad():
+        lg = O.forward(P, x.to(GRAD_DEV, torch.float64), _oracle_cfg(x.shape[1])).cpu()
+    del P
+    if GRAD_DEV != "cpu":
+        torch.cuda.empty_cache()
+    return lg
+
+
 @pytest.fixture(scope="module")
 def config2_oracle():
     from innovative3D.synthetic import synthetic_batch
@@ -211,13 +227,34 @@ def config2_oracle():
     return st, x, y, logits, loss
 
 
+@pytest.fixture(scope="module")
+def config2_fp64(config2_oracle):
+    """The fp32 oracle's own argmax stability: its flips against the fp64 oracle on the
+    same inputs (the reference's arithmetic is fp32 PyTorch-CPU: this is how far the
+    reference itself is from exact argmax masks at config 2)."""
+    st, x, _y, ref_logits, _loss = config2_oracle
+    lg64 = _oracle_forward64(st, x)
+    am64 = lg64.argmax(1)
+    flips32 = int((ref_logits.argmax(1) != am64).sum())
+    err32 = float((ref_logits.double() - lg64).abs().max())
+    print(f"config2 fp32 oracle vs fp64 oracle: max|dlogit| {err32:.3e}, argmax flips "
+          f"{flips32} of {am64.numel()}")
+    return lg64, am64, flips32, err32
+
+
+# the engine's argmax flips against the fp64 oracle may not exceed this multiple of the fp32
+# reference's own (plus a floor of 8 for a reference that happens to flip almost none)
+FLIP_MULTIPLE, FLIP_FLOOR = 2.0, 8
+
+
 @pytest.mark.timeout(600)
 # all three arithmetics at full size: f16x3 (the default), the f32 MFMA path and
 # bf16x6 (the exact 3-plane split, round 2's default)
 @pytest.mark.parametrize("mth", ["f16x3", "f32", "bf16x6"])
-def test_config2_headline_matches_oracle(config2_oracle, mth):
+def test_config2_headline_matches_oracle(config2_oracle, config2_fp64, mth):
     import innovative3D.helpers as Hh
     st, x, y, ref_logits, ref_loss = config2_oracle
+    lg64, am64, flips32, err32 = config2_fp64
     core, _ = _spff_state(128)
     core.load_state_dict({k: torch.from_numpy(v) for k, v in st.items()})
     core = core.to(DEV)
@@ -227,10 +264,38 @@ def test_config2_headline_matches_oracle(config2_oracle, mth):
     loss.backward()
     torch.cuda.synchronize()
     grads = {k: p.grad for k, p in core.named_parameters(remove_duplicate=False)}
+    lg = logits.detach().cpu()
+    # argmax stability against the exact (fp64) logits, beside the fp32 reference's own
+    flips64 = int((lg.argmax(1) != am64).sum())
+    err64 = float((lg.double() - lg64).abs().max())
+    n_ref_flips = int((lg.argmax(1) != ref_logits.argmax(1)).sum())
     ref_grads = _oracle_grads(st, x, y, _engine_masks(core, tuple(x.shape), st))
-    _compare(f"config2 2x5x128^3 {mth}", logits.detach().cpu(), float(loss), grads, ref_logits,
+    _compare(f"config2 2x5x128^3 {mth}", lg, float(loss), grads, ref_logits,
              ref_loss, ref_grads, scales=_mag_scales(st, ref_grads[0]),
              conf=conf.cpu().numpy(), labels=y)
+    import innovative3D.models as M
+    from oracle import spff_oracle as O
+    met = M.metrics_from_confusion(conf.cpu().numpy(), K13, int(y.numel()))
+    ref_met = O.metrics_from_confusion(O.confusion(ref_logits, y, K13, 255), K13, int(y.numel()))
+    rec = {"math": mth, "engine_vs_fp32_oracle": {"max_abs_dlogit": float((lg - ref_logits).abs().max()),
+                                                  "argmax_flips": n_ref_flips},
+           "engine_vs_fp64_oracle": {"max_abs_dlogit": err64, "argmax_flips": flips64},
+           "fp32_oracle_vs_fp64_oracle": {"max_abs_dlogit": err32, "argmax_flips": flips32},
+           "macro_dice": met[3], "macro_dice_fp32_oracle": ref_met[3],
+           "abs_d_macro_dice": abs(met[3] - ref_met[3]), "loss": float(loss),
+           "loss_fp32_oracle": ref_loss, "voxels": int(am64.numel()),
+           "flip_bound": FLIP_MULTIPLE * max(flips32, FLIP_FLOOR)}
+    print("config2 record: " + json.dumps(rec))
+    try:
+        import pathlib
+        out = pathlib.Path(__file__).resolve().parents[1] / "gpurun_out"
+        if out.is_dir():
+            with open(out / "config2_parity.jsonl", "a") as f:
+                f.write(json.dumps(rec) + "\n")
+    except OSError:
+        pass
+    assert flips64 <= FLIP_MULTIPLE * max(flips32, FLIP_FLOOR), (
+        f"engine flips {flips64} argmaxes of the fp64 oracle; the fp32 reference flips {flips32}")
 
 
 # ------------------------------------------------- configs[3] path (sharded)

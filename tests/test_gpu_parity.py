@@ -441,3 +441,38 @@ def test_oracle_device_evaluation_matches_cpu(case):
         worst = max(worst, r)
         assert r <= 1e-8, f"{k}: {r:.2e}"
     print(f"  worst gradient rel L2 {worst:.2e}")
+
+
+@pytest.mark.parametrize("mth", ["f16x3", "f32"])
+def test_pool_fold_bitwise(mth):
+    """the encoder blocks' output gradient formed by its readers (PoolAdd:
+    skip gradient + the MaxPool backward of the pooled gradient, read by the tail reduction
+    and the IN-backward apply) against the k_maxpool_bwd_add pass it replaced (debug key 2
+    = 0).  Same sum in the same order: every parameter gradient bitwise equal."""
+    from innovative3D.synthetic import synthetic_batch
+    from innovative3D.weightgen import synth_state
+    K = 13
+    core = M.build_spct_energyfilm_fourier(num_classes=K, base=16, in_channels=5)
+    for b in core._blocks():
+        b.fgate._ensure_mask(8, "cpu")
+    st = synth_state([(k, tuple(v.shape)) for k, v in core.state_dict().items()], seed=5)
+    core.load_state_dict({k: torch.from_numpy(v) for k, v in st.items()})
+    core = core.to(DEV)
+    core.math = mth
+    x, y = synthetic_batch(2, 5, 8, 32, 48, num_classes=K, ignore_frac=0.02, seed=6)
+    x, y = x.to(DEV), y.to(DEV)
+    grads = []
+    for fold in (1, 0):
+        for p in core.parameters():
+            p.grad = None
+        logits = core(x)
+        core._plan.debug_set(2, fold)
+        loss, _conf = Hh.ce_dice_with_confusion(logits, y, K, 255)
+        loss.backward()
+        torch.cuda.synchronize()
+        grads.append({k: p.grad.detach().clone() for k, p in core.named_parameters()
+                      if p.grad is not None})
+    core._plan.debug_set(2, 1)
+    assert grads[0].keys() == grads[1].keys() and len(grads[0]) > 20
+    for k in grads[0]:
+        assert torch.equal(grads[0][k], grads[1][k]), k

@@ -324,3 +324,63 @@ def test_depth_sharded_world8_f16x3_overlapped(tmp_path):
         for p in parts[1:]:
             np.testing.assert_array_equal(p[k], parts[0][k])
     _check_vs_oracle(parts, 2, st, _cfg(W8_K, W8_BASE, C), x, y, mth, device="cuda")
+
+
+# ---- RCCL on >= 2 GPUs: device halos + the bucketed gradient all-reduces
+# interleaved with them (SPFF_SHARD_OVERLAP=1), one GPU per rank.  The driver's GPU test box
+# has one GPU, where this skips; on a multi-GPU node it is the sharded RCCL path's check.
+def _rccl_worker(rank, world, port, out, overlap):
+    import pathlib
+    import sys
+    root = pathlib.Path(__file__).resolve().parents[1]
+    sys.path[:0] = [str(root), str(root / "tests"), str(root / "spff-unet-spcct_amd")]
+    os.environ["SPFF_SHARD_OVERLAP"] = "1" if overlap else "0"
+    from innovative3D.sharded import DepthShardedSPFF, shard_bounds
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dev = torch.device("cuda", rank)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    depth = 16
+    core = _model("f16x3", depth).to(dev)
+    x, y = _data(depth)
+    off, d = shard_bounds(depth, world, rank)
+    step = DepthShardedSPFF(core, K, 255)
+    assert (step.bucketer is not None) == overlap
+    loss, conf = step.step(x[:, :, off:off + d].contiguous().to(dev),
+                           y[:, off:off + d].contiguous().to(dev))
+    torch.cuda.synchronize()
+    mk = _save_masks(core, (SHAPE[0], SHAPE[1], d, SHAPE[3], SHAPE[4]), _cfg())
+    np.savez(f"{out}.{rank}.npz", logits=step.last_logits.cpu().numpy(), loss=float(loss),
+             conf=conf.cpu().numpy(), **mk,
+             **{"g_" + k: p.grad.cpu().numpy() for k, p in core.named_parameters(remove_duplicate=False)
+                if p.grad is not None})
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs >= 2 GPUs (one rank per GPU, RCCL)")
+@pytest.mark.parametrize("overlap", [True, False])
+def test_depth_sharded_rccl_two_gpus(tmp_path, overlap):
+    import innovative3D.helpers as Hh
+    depth = 16
+    core = _model("f16x3", depth)
+    st = core._synth_state
+    x, y = _data(depth)
+    logits = core(x.cuda())
+    loss, _conf = Hh.ce_dice_with_confusion(logits, y.cuda(), K, 255)
+    loss.backward()
+    ref, loss_ref = logits.detach().cpu().numpy(), float(loss)
+    del core, logits, loss
+    out = str(tmp_path / "rccl")
+    mp.spawn(_rccl_worker, args=(2, _free_port(), out, overlap), nprocs=2, join=True)
+    parts = [np.load(f"{out}.{r}.npz") for r in range(2)]
+    lg = np.concatenate([p["logits"] for p in parts], axis=2)
+    e = float(np.abs(lg - ref).max())
+    print(f"RCCL world 2 overlap={overlap}: max|dlogit| {e:.2e}, loss {float(parts[0]['loss']):.7f} "
+          f"vs {loss_ref:.7f}")
+    assert e <= 1e-4 * float(np.abs(ref).max())
+    assert abs(float(parts[0]["loss"]) - loss_ref) <= 1e-5 * abs(loss_ref)
+    for k in (f for f in parts[0].files if f.startswith("g_")):
+        np.testing.assert_array_equal(parts[1][k], parts[0][k])
+    _check_vs_oracle(parts, 2, st, _cfg(), x, y, "f16x3")
