@@ -225,6 +225,19 @@ int spff_conv3d_wgrad(const float* x, int ldx, const float* dy, float* dw, int B
 int spff_conv3d_wgrad_ex(const float* x, int ldx, const float* dy, float* dw, int B, int D,
                          int H, int W, int cin, int cout, int ksd, int math, void* ws,
                          void* stream);
+/* Op-level ConvTranspose3d(cin -> cout, kernel = stride = (1,2,2)) + bias (reference
+ * models.py:668-672, the decoder up-convolutions) on channel-last tensors: x [B][D][H][W][cin]
+ * low resolution, y [B][D][2H][2W][cout]; weight W[cin][cout][1][2][2], bias [cout].
+ * math = SPFF_MATH_*: the GEMM arithmetic (f32 MFMA, the exact bf16x6 split, or f16x3 with
+ * per-chunk power-of-two scales).  dgrad: dx = the input gradient of dy; wgrad: dw, db
+ * (overwritten).  ws >= spff_upconv_ws_bytes(...). */
+size_t spff_upconv_ws_bytes(int B, int D, int H, int W, int cin, int cout);
+int spff_upconv_fwd(const float* x, const float* w, const float* b, float* y, int B, int D, int H,
+                    int W, int cin, int cout, int math, void* ws, void* stream);
+int spff_upconv_dgrad(const float* dy, const float* w, float* dx, int B, int D, int H, int W,
+                      int cin, int cout, int math, void* ws, void* stream);
+int spff_upconv_wgrad(const float* x, const float* dy, float* dw, float* db, int B, int D, int H,
+                      int W, int cin, int cout, int math, void* ws, void* stream);
 
 /* ---------------------------------------------------------------------------
  * 3D U-Net baseline variant (BASELINE config 3; registry entry "3DUNet",

@@ -1497,6 +1497,50 @@ int spff_prof_collect(spff_plan* p, double* out, int nclass) {
   return SPFF_OK;
 }
 
+// ---- op-level up-convolution (tests / INTEGRATION): ws = [forward pack | dgrad pack |
+// wgrad partial slabs]
+size_t spff_upconv_ws_bytes(int B, int D, int H, int W, int cin, int cout) {
+  const Vol low{B, D, H, W};
+  return upconv_pack_floats(cin, cout) * sizeof(float) + 256 +
+         upconv_wgrad_ws_bytes(low, cin, cout);
+}
+static int upconv_args(int cin, int cout, int math) {
+  if (cin % 4 || cout % 4 || cin <= 0 || cout <= 0)
+    return fail(SPFF_EINVAL, "cin and cout must be positive multiples of 4");
+  if (math < SPFF_MATH_F32 || math > SPFF_MATH_F16X3) return fail(SPFF_EINVAL, "bad math");
+  return SPFF_OK;
+}
+int spff_upconv_fwd(const float* x, const float* w, const float* b, float* y, int B, int D, int H,
+                    int W, int cin, int cout, int math, void* ws, void* stream) {
+  if (!x || !w || !b || !y || !ws) return fail(SPFF_EINVAL, "null argument");
+  CK(upconv_args(cin, cout, math));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  float* wf = static_cast<float*>(ws);
+  HIPCK(upconv_pack(w, wf, wf + upconv_pack_dgrad_offset(cin, cout), cin, cout, s));
+  HIPCK(upconv_fwd(x, wf, b, y, Vol{B, D, H, W}, cin, cout, s, 4, math));
+  return SPFF_OK;
+}
+int spff_upconv_dgrad(const float* dy, const float* w, float* dx, int B, int D, int H, int W,
+                      int cin, int cout, int math, void* ws, void* stream) {
+  if (!dy || !w || !dx || !ws) return fail(SPFF_EINVAL, "null argument");
+  CK(upconv_args(cin, cout, math));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  float* wf = static_cast<float*>(ws);
+  HIPCK(upconv_pack(w, wf, wf + upconv_pack_dgrad_offset(cin, cout), cin, cout, s));
+  HIPCK(upconv_dgrad(dy, cout, wf + upconv_pack_dgrad_offset(cin, cout), dx, Vol{B, D, H, W}, cin,
+                     cout, s, 4, math));
+  return SPFF_OK;
+}
+int spff_upconv_wgrad(const float* x, const float* dy, float* dw, float* db, int B, int D, int H,
+                      int W, int cin, int cout, int math, void* ws, void* stream) {
+  if (!x || !dy || !dw || !db || !ws) return fail(SPFF_EINVAL, "null argument");
+  CK(upconv_args(cin, cout, math));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  float* part = static_cast<float*>(ws) + upconv_pack_floats(cin, cout) + 64;
+  HIPCK(upconv_wgrad(x, dy, cout, dw, db, Vol{B, D, H, W}, cin, cout, part, s, 4, math));
+  return SPFF_OK;
+}
+
 int spff_conv_prof_enable(int on) {
   conv_prof_enable(on != 0);
   return SPFF_OK;

@@ -35,9 +35,17 @@ static int num_cus() {
 #ifndef SPFF_GEMM_PERSIST
 #define SPFF_GEMM_PERSIST 1
 #endif
-// (SPFF_MATH_F16X3 is a conv arithmetic: the GEMMs take the bf16x6 split with it)
-static inline bool gemm_split(int math) {
-  return SPFF_GEMM_SPLIT && (math == SPFF_MATH_BF16X6 || math == SPFF_MATH_F16X3);
+// SPFF_GEMM_F16=0 (A/B diagnostics): the GEMMs take the bf16x6 split under SPFF_MATH_F16X3
+#ifndef SPFF_GEMM_F16
+#define SPFF_GEMM_F16 1
+#endif
+// GEMM arithmetic of a conv math mode: 0 = fp32 MFMA (k_gemm / k_atb), 1 = the exact
+// 3-plane bf16 split (bf16x6), 2 = scaled fp16 planes (f16x3, per-chunk scales, below)
+enum { GM_F32 = 0, GM_BF16X6 = 1, GM_F16X3 = 2 };
+static inline int gemm_split(int math) {
+  if (!SPFF_GEMM_SPLIT) return GM_F32;
+  if (math == SPFF_MATH_F16X3) return SPFF_GEMM_F16 ? GM_F16X3 : GM_BF16X6;
+  return math == SPFF_MATH_BF16X6 ? GM_BF16X6 : GM_F32;
 }
 static inline int64_t cdiv64(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
@@ -483,13 +491,82 @@ __device__ __forceinline__ int gx_bsw(int k) {
   constexpr int L = BN == 128 ? 0 : BN == 64 ? 1 : 2;
   return ((k & 3) >> L) | (((k >> 3) & 1) << (2 - L));
 }
-template <class AL, class CS, int BN, bool V4>
+// |largest element| of a float4
+__device__ __forceinline__ float amax4(const float4& v) {
+  return fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)));
+}
+__device__ __forceinline__ float4 ldexp4(const float4& v, int e) {
+  return make_float4(ldexpf(v.x, e), ldexpf(v.y, e), ldexpf(v.z, e), ldexpf(v.w, e));
+}
+// float4 -> the NS planes of the split GEMMs (3 bf16 planes, or NS_F16: 2 fp16 planes of the
+// already scaled values)
+template <int NS>
+__device__ __forceinline__ void gsplit(const float4& v, uint2 (&o)[nplanes(NS)]) {
+  split4_pk<NS>(v, o);
+}
+// f16x3 GEMM chunk scales (NS_F16): the workgroup's largest |element| of the A (X) and B (Y)
+// chunk it is about to stage, from every thread's registers -> the chunk's exponents ea, eb
+// (f16_scale_exp: max |v| 2^e < 2^14), and the accumulator moved to the units of the new
+// chunk's products, 2^(ea + eb).  The exponent may rise by at most 64 per chunk (ea lowered
+// by the excess), so the rescaled accumulator cannot overflow; a chunk whose elements are
+// that much smaller than everything summed before it then keeps 2^-39 of that bound as
+// its fp16 floor, below the fp32 rounding of the sum it joins.  Every thread must call it
+// (one workgroup barrier, which also separates the previous chunk's LDS reads from this
+// chunk's stores).  The per-(tile, chunk) scales follow the conv kernels' (conv3d_x.hip);
+// the weights carry their own per chunk here, so no operand needs a precomputed maximum.
+template <int NW, int NACC>
+__device__ __forceinline__ void gemm_chunk_scale(float ma, float mb, unsigned (&slot)[2][NW],
+                                                 bool first, int& ecur, int& ea, int& eb,
+                                                 f32x4g (&acc)[NACC]) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    ma = fmaxf(ma, __shfl_xor(ma, o));
+    mb = fmaxf(mb, __shfl_xor(mb, o));
+  }
+  if (lane == 0) {
+    slot[0][wave] = __float_as_uint(ma);
+    slot[1][wave] = __float_as_uint(mb);
+  }
+  __syncthreads();
+  unsigned ba = 0, bb = 0;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) {
+    ba = max(ba, slot[0][w]);
+    bb = max(bb, slot[1][w]);
+  }
+  ea = f16_scale_exp(__builtin_amdgcn_readfirstlane(ba));
+  eb = f16_scale_exp(__builtin_amdgcn_readfirstlane(bb));
+  int e = ea + eb;
+  if (first) {
+    ecur = e;
+    return;
+  }
+  if (e > ecur + 64) {
+    ea -= e - (ecur + 64);
+    e = ecur + 64;
+  }
+  if (e != ecur) {
+    const int d = e - ecur;
+#pragma unroll
+    for (int i = 0; i < NACC; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[i][r] = ldexpf(acc[i][r], d);
+    ecur = e;
+  }
+}
+
+template <class AL, class CS, int BN, bool V4, int NS = 3>
 __global__ __launch_bounds__(256, 2) void k_gemm_x(AL A, const float* __restrict__ B, CS C,
                                                    int kpad, int npad) {
   constexpr int CB = BN / 16, NRB = BN / 32;  // 16-wide col blocks; B float4 per thread
   constexpr int APL = G_BM * G_BK, BPL = G_BK * BN;  // bf16 per plane
-  __shared__ __attribute__((aligned(16))) unsigned short As[3 * APL];
-  __shared__ __attribute__((aligned(16))) unsigned short Bs[3 * BPL];
+  constexpr bool HF = NS == NS_F16;
+  constexpr int NP = nplanes(NS);
+  __shared__ __attribute__((aligned(16))) unsigned short As[NP * APL];
+  __shared__ __attribute__((aligned(16))) unsigned short Bs[NP * BPL];
+  __shared__ unsigned gmx[2][4];  // HF: per-wave max |A|, |B| of the chunk
+  int ecur = 0, ea = 0, eb = 0;   // HF: accumulator unit 2^ecur; the chunk's A / B exponents
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, l16 = lane & 15;
   // persistent over row tiles blockIdx.x, + gridDim.x, ...: the next tile's first
@@ -532,22 +609,25 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x(AL A, const float* __restrict
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int m = arow + 32 * j;
-      uint2 o[3];
-      gsplit4(zero_unless(ra[j], (am >> j) & 1u), o);
+      uint2 o[NP];
+      float4 v = zero_unless(ra[j], (am >> j) & 1u);
+      if constexpr (HF) v = ldexp4(v, ea);
+      gsplit<NS>(v, o);
       const int off = m * G_BK + 8 * ((aq >> 1) ^ ((m & 8) >> 2)) + 4 * (aq & 1);
 #pragma unroll
-      for (int p = 0; p < 3; ++p) *reinterpret_cast<uint2*>(As + p * APL + off) = o[p];
+      for (int p = 0; p < NP; ++p) *reinterpret_cast<uint2*>(As + p * APL + off) = o[p];
     }
 #pragma unroll
     for (int j = 0; j < NRB; ++j) {
       const int i = tid + 256 * j, r = i / (BN / 4), c4 = i % (BN / 4);
       float4 v = rb[j];
       if (neg) v = make_float4(-v.x, -v.y, -v.z, -v.w);
-      uint2 o[3];
-      gsplit4(v, o);
+      if constexpr (HF) v = ldexp4(v, eb);
+      uint2 o[NP];
+      gsplit<NS>(v, o);
       const int off = r * BN + 16 * ((c4 >> 2) ^ gx_bsw<BN>(r)) + 4 * (c4 & 3);
 #pragma unroll
-      for (int p = 0; p < 3; ++p) *reinterpret_cast<uint2*>(Bs + p * BPL + off) = o[p];
+      for (int p = 0; p < NP; ++p) *reinterpret_cast<uint2*>(Bs + p * BPL + off) = o[p];
     }
   };
   // A fragment: row 16 rb + l16 of this wave's 32, k-chunk g (8 bf16 = 16 B)
@@ -574,7 +654,18 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x(AL A, const float* __restrict
 #pragma unroll
         for (int cb = 0; cb < CB; ++cb) acc[rb][cb] = -acc[rb][cb];
     }
-    if (!first) __syncthreads();  // every wave is past its reads of the previous chunk
+    if constexpr (HF) {
+      // this chunk's scales (its barrier also orders the previous chunk's LDS reads)
+      float ma = 0.f, mb = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ma = fmaxf(ma, (am >> j) & 1u ? amax4(ra[j]) : 0.f);
+#pragma unroll
+      for (int j = 0; j < NRB; ++j) mb = fmaxf(mb, amax4(rb[j]));
+      gemm_chunk_scale<4, 2 * CB>(ma, mb, gmx, kc == 0, ecur, ea, eb,
+                                  reinterpret_cast<f32x4g(&)[2 * CB]>(acc));
+    } else {
+      if (!first) __syncthreads();  // every wave is past its reads of the previous chunk
+    }
     first = false;
     stash(kc & 1);
     __syncthreads();
@@ -585,17 +676,17 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x(AL A, const float* __restrict
       if (last && tn < ntl) prep_rows(tn);
       fetch(last ? 0 : (kc + 1) * G_BK);
     }
-    bf16x8g a[2][3];
+    bf16x8g a[2][NP];
 #pragma unroll
     for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
-      for (int p = 0; p < 3; ++p)
+      for (int p = 0; p < NP; ++p)
         a[rb][p] = *reinterpret_cast<const bf16x8g*>(As + p * APL + aoff[rb]);
 #pragma unroll
     for (int cb = 0; cb < CB; ++cb) {
-      bf16x8g b[3];
+      bf16x8g b[NP];
 #pragma unroll
-      for (int p = 0; p < 3; ++p) {
+      for (int p = 0; p < NP; ++p) {
         const unsigned short* b0 = Bs + p * BPL + kr0 * BN + 16 * (cb ^ gx_bsw<BN>(kr0)) + 4 * pp;
         const unsigned short* b1 = Bs + p * BPL + kr1 * BN + 16 * (cb ^ gx_bsw<BN>(kr1)) + 4 * pp;
         const i16x4g lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4g*)b0);
@@ -607,23 +698,30 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x(AL A, const float* __restrict
       // of one row, stored as one 16-B write (the epilogue is store-issue bound otherwise);
       // else the lane holds 4 rows of one column (row-contiguous lanes for narrow pitches)
       auto mf = [](const bf16x8g& x, const bf16x8g& y, f32x4g c) {
-        return V4 ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(y, x, c, 0, 0, 0)
-                  : __builtin_amdgcn_mfma_f32_16x16x32_bf16(x, y, c, 0, 0, 0);
+        return V4 ? mfma16x32<HF>(y, x, c) : mfma16x32<HF>(x, y, c);
       };
 #pragma unroll
       for (int rb = 0; rb < 2; ++rb) {
         f32x4g c = acc[rb][cb];
-        c = mf(a[rb][1], b[1], c);
-        c = mf(a[rb][0], b[2], c);
-        c = mf(a[rb][2], b[0], c);
-        c = mf(a[rb][0], b[1], c);
-        c = mf(a[rb][1], b[0], c);
-        c = mf(a[rb][0], b[0], c);
+        if constexpr (HF) {  // hl, lh, hh (the dropped ll <= 2^-22 |ab|)
+          c = mf(a[rb][0], b[1], c);
+          c = mf(a[rb][1], b[0], c);
+          c = mf(a[rb][0], b[0], c);
+        } else {
+          c = mf(a[rb][1], b[NP - 2], c);
+          c = mf(a[rb][0], b[NP - 1], c);
+          c = mf(a[rb][NP - 1], b[0], c);
+          c = mf(a[rb][0], b[1], c);
+          c = mf(a[rb][1], b[0], c);
+          c = mf(a[rb][0], b[0], c);
+        }
         acc[rb][cb] = c;
       }
     }
   }
   const float sg = ((nkc - 1) & 1) ? -1.f : 1.f;
+  // (HF: the accumulator is in units of 2^ecur -- moved back by an exact ldexp)
+  auto unscale = [&](float v) { return HF ? ldexpf(v, -ecur) : v; };
   if constexpr (V4) {
     // lane: row 16 rb + l16 of the wave's 32, columns n0 + 16 cb + 4 g + (0..3)
     int64_t rh[2];
@@ -637,8 +735,10 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x(AL A, const float* __restrict
 #pragma unroll
       for (int rb = 0; rb < 2; ++rb)
         if (rh[rb] >= 0 && c0 >= 0) {
-          const float4 v = make_float4(sg * acc[rb][cb][0] + bq.x, sg * acc[rb][cb][1] + bq.y,
-                                       sg * acc[rb][cb][2] + bq.z, sg * acc[rb][cb][3] + bq.w);
+          const float4 v = make_float4(sg * unscale(acc[rb][cb][0]) + bq.x,
+                                       sg * unscale(acc[rb][cb][1]) + bq.y,
+                                       sg * unscale(acc[rb][cb][2]) + bq.z,
+                                       sg * unscale(acc[rb][cb][3]) + bq.w);
           C.put4(rh[rb] + c0, v);
           if constexpr (cs_amax<CS>::value)
             amx = fmaxf(amx, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
@@ -662,7 +762,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x(AL A, const float* __restrict
 #pragma unroll
         for (int cb = 0; cb < CB; ++cb)
           if (cc[cb] >= 0) {
-            const float v = sg * acc[rb][cb][r] + bv[cb];
+            const float v = sg * unscale(acc[rb][cb][r]) + bv[cb];
             C.put(rh + cc[cb], v);
             if constexpr (cs_amax<CS>::value) amx = fmaxf(amx, fabsf(v));
           }
@@ -684,10 +784,10 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x(AL A, const float* __restrict
 }
 
 // persistent row tiles: as many workgroups as fit the chip at once
-template <int BN, bool V4, class AL, class CS>
+template <int BN, bool V4, int NS, class AL, class CS>
 static void launch_gemm_x(const AL& A, const float* B, const CS& C, dim3 grid, int kpad, int npad,
                           hipStream_t s) {
-  auto kern = k_gemm_x<AL, CS, BN, V4>;
+  auto kern = k_gemm_x<AL, CS, BN, V4, NS>;
   static int per_cu = 0;
   if (!per_cu &&
       hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0) != hipSuccess)
@@ -698,22 +798,32 @@ static void launch_gemm_x(const AL& A, const float* B, const CS& C, dim3 grid, i
   hipLaunchKernelGGL(kern, gx, dim3(256), 0, s, A, B, C, kpad, npad);
 }
 
-// split = true: k_gemm_x (split bf16, SPFF_MATH_BF16X6); false: fp32 MFMA k_gemm
+template <int NS, class AL, class CS>
+static void launch_gemm_xs(const AL& A, const float* B, const CS& C, dim3 grid, int BN, int kpad,
+                           int npad, hipStream_t s) {
+  // 16-B stores of column quads where the output functor and its pitch allow
+  const bool v4 = CS::kVec && C.vec_ok();
+  if (BN == 128) v4 ? launch_gemm_x<128, true, NS>(A, B, C, grid, kpad, npad, s)
+                    : launch_gemm_x<128, false, NS>(A, B, C, grid, kpad, npad, s);
+  else if (BN == 64) v4 ? launch_gemm_x<64, true, NS>(A, B, C, grid, kpad, npad, s)
+                        : launch_gemm_x<64, false, NS>(A, B, C, grid, kpad, npad, s);
+  else v4 ? launch_gemm_x<32, true, NS>(A, B, C, grid, kpad, npad, s)
+          : launch_gemm_x<32, false, NS>(A, B, C, grid, kpad, npad, s);
+}
+// mode (gemm_split): GM_BF16X6 / GM_F16X3 = k_gemm_x with 3 bf16 / 2 scaled fp16 planes;
+// GM_F32 = fp32 MFMA k_gemm
 template <class AL, class CS>
 static hipError_t launch_gemm(const AL& A, const float* B, const CS& C, int64_t M, int kpad,
-                              int npad, hipStream_t s, bool split = false) {
+                              int npad, hipStream_t s, int mode = GM_F32) {
   if (kpad % G_BK || npad % 32 || M >= (int64_t(1) << 31)) return hipErrorInvalidValue;
   const int BN = npad % 128 == 0 ? 128 : npad % 64 == 0 ? 64 : 32;
   dim3 grid((unsigned)cdiv64(M, G_BM), npad / BN);
-  if (split) {
-    // 16-B stores of column quads where the output functor and its pitch allow
-    const bool v4 = CS::kVec && C.vec_ok();
-    if (BN == 128) v4 ? launch_gemm_x<128, true>(A, B, C, grid, kpad, npad, s)
-                      : launch_gemm_x<128, false>(A, B, C, grid, kpad, npad, s);
-    else if (BN == 64) v4 ? launch_gemm_x<64, true>(A, B, C, grid, kpad, npad, s)
-                          : launch_gemm_x<64, false>(A, B, C, grid, kpad, npad, s);
-    else v4 ? launch_gemm_x<32, true>(A, B, C, grid, kpad, npad, s)
-            : launch_gemm_x<32, false>(A, B, C, grid, kpad, npad, s);
+  if (mode == GM_F16X3) {
+    launch_gemm_xs<NS_F16>(A, B, C, grid, BN, kpad, npad, s);
+    return hipGetLastError();
+  }
+  if (mode == GM_BF16X6) {
+    launch_gemm_xs<3>(A, B, C, grid, BN, kpad, npad, s);
     return hipGetLastError();
   }
   if (BN == 128)
@@ -793,13 +903,18 @@ __global__ __launch_bounds__(256) void k_atb(XL X, YL Y, float* __restrict__ par
 // MFMA operands are gathered with ds_read_b64_tr_b16 (m is the reduction axis of
 // both).  Odd chunks stage -Y and the accumulator is negated at every chunk
 // boundary.  The bias column sums are taken in fp32 from the staged registers.
-template <class XL, class YL>
+// (NS_F16: 2 scaled fp16 planes and 3 products, per-chunk scales of X and Y as in k_gemm_x)
+template <class XL, class YL, int NS = 3>
 __global__ __launch_bounds__(256, 2) void k_atb_x(XL X, YL Y, float* __restrict__ part,
                                                   float* __restrict__ csum, int64_t M, int64_t rps,
                                                   int k1pad, int npad) {
   constexpr int PL = T_BM * 64;  // bf16 per plane
-  __shared__ __attribute__((aligned(16))) unsigned short Xs[3 * PL];
-  __shared__ __attribute__((aligned(16))) unsigned short Ys[3 * PL];
+  constexpr bool HF = NS == NS_F16;
+  constexpr int NP = nplanes(NS);
+  __shared__ __attribute__((aligned(16))) unsigned short Xs[NP * PL];
+  __shared__ __attribute__((aligned(16))) unsigned short Ys[NP * PL];
+  __shared__ unsigned gmx[2][4];  // HF: per-wave max |X|, |Y| of the chunk
+  int ecur = 0, ex = 0, ey = 0;   // HF: accumulator unit 2^ecur; the chunk's exponents
   __shared__ float4 cred[16][16];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, l16 = lane & 15, q = l16 >> 2, pp = l16 & 3;
@@ -835,16 +950,19 @@ __global__ __launch_bounds__(256, 2) void k_atb_x(XL X, YL Y, float* __restrict_
     for (int j = 0; j < 4; ++j) {
       const int m = sr + 16 * j;
       const int off = m * 64 + 16 * ((sq >> 2) ^ gx_bsw<64>(m)) + 4 * (sq & 3);
-      uint2 o[3];
-      gsplit4(zero_unless(xr[j], (xm >> j) & 1u), o);
+      uint2 o[NP];
+      float4 x = zero_unless(xr[j], (xm >> j) & 1u);
+      if constexpr (HF) x = ldexp4(x, ex);
+      gsplit<NS>(x, o);
 #pragma unroll
-      for (int p = 0; p < 3; ++p) *reinterpret_cast<uint2*>(Xs + p * PL + off) = o[p];
+      for (int p = 0; p < NP; ++p) *reinterpret_cast<uint2*>(Xs + p * PL + off) = o[p];
       float4 y = zero_unless(yr[j], (ym >> j) & 1u);
       if (do_cs) { cs.x += y.x; cs.y += y.y; cs.z += y.z; cs.w += y.w; }
       if (neg) y = make_float4(-y.x, -y.y, -y.z, -y.w);
-      gsplit4(y, o);
+      if constexpr (HF) y = ldexp4(y, ey);
+      gsplit<NS>(y, o);
 #pragma unroll
-      for (int p = 0; p < 3; ++p) *reinterpret_cast<uint2*>(Ys + p * PL + off) = o[p];
+      for (int p = 0; p < NP; ++p) *reinterpret_cast<uint2*>(Ys + p * PL + off) = o[p];
     }
   };
   // operand of row block i (16 columns of X or Y at c0 + 16 i): lane 4q + p of k-group
@@ -866,18 +984,30 @@ __global__ __launch_bounds__(256, 2) void k_atb_x(XL X, YL Y, float* __restrict_
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = -acc[i][j];
-      __syncthreads();
+    }
+    if constexpr (HF) {
+      // this chunk's scales (the barrier inside also orders the previous chunk's reads)
+      float mx = 0.f, my = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        mx = fmaxf(mx, (xm >> j) & 1u ? amax4(xr[j]) : 0.f);
+        my = fmaxf(my, (ym >> j) & 1u ? amax4(yr[j]) : 0.f);
+      }
+      gemm_chunk_scale<4, 4>(mx, my, gmx, kc == 0, ecur, ex, ey,
+                             reinterpret_cast<f32x4g(&)[4]>(acc));
+    } else {
+      if (kc) __syncthreads();
     }
     stash(kc & 1);
     __syncthreads();
     fetch(m0 + T_BM);  // (unconditional: past the split's rows every quad is masked)
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      bf16x8g a[2][3], b[2][3];
+      bf16x8g a[2][NP], b[2][NP];
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int p = 0; p < 3; ++p) {
+        for (int p = 0; p < NP; ++p) {
           a[i][p] = frag(Xs + p * PL, ks, 2 * wr + i);
           b[i][p] = frag(Ys + p * PL, ks, 2 * wc + i);
         }
@@ -886,12 +1016,18 @@ __global__ __launch_bounds__(256, 2) void k_atb_x(XL X, YL Y, float* __restrict_
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           f32x4g c = acc[i][j];
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][1], b[j][1], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[j][2], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][2], b[j][0], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[j][1], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][1], b[j][0], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[j][0], c, 0, 0, 0);
+          if constexpr (HF) {  // hl, lh, hh
+            c = mfma16x32<true>(a[i][0], b[j][1], c);
+            c = mfma16x32<true>(a[i][1], b[j][0], c);
+            c = mfma16x32<true>(a[i][0], b[j][0], c);
+          } else {
+            c = mfma16x32<false>(a[i][1], b[j][1], c);
+            c = mfma16x32<false>(a[i][0], b[j][NP - 1], c);
+            c = mfma16x32<false>(a[i][NP - 1], b[j][0], c);
+            c = mfma16x32<false>(a[i][0], b[j][1], c);
+            c = mfma16x32<false>(a[i][1], b[j][0], c);
+            c = mfma16x32<false>(a[i][0], b[j][0], c);
+          }
           acc[i][j] = c;
         }
     }
@@ -905,7 +1041,7 @@ __global__ __launch_bounds__(256, 2) void k_atb_x(XL X, YL Y, float* __restrict_
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         part[((int64_t)split * k1pad + k10 + 32 * wr + 16 * i + 4 * g + r) * npad + n0 + 32 * wc +
-             16 * j + l16] = sg * acc[i][j][r];
+             16 * j + l16] = sg * (HF ? ldexpf(acc[i][j][r], -ecur) : acc[i][j][r]);
   if (do_cs) {
     cred[sr][sq] = cs;
     __syncthreads();
@@ -1200,7 +1336,7 @@ static hipError_t launch_xty(const float* X, int ldx, int K1, const float* Y, in
 template <class XL, class YL>
 static hipError_t launch_atb(const XL& X, const YL& Y, int64_t M, int K1, int N, int Cout,
                              int mode, float* dw, float* db, float* ws, hipStream_t s,
-                             bool split = false) {
+                             int split = GM_F32) {
   if (M >= (int64_t(1) << 31)) return hipErrorInvalidValue;
   const int k1pad = cdiv(K1, 64) * 64, npad = cdiv(N, 64) * 64;
   const int nout = (k1pad / 64) * (npad / 64);
@@ -1211,7 +1347,10 @@ static hipError_t launch_atb(const XL& X, const YL& Y, int64_t M, int K1, int N,
   float* part = ws;
   float* csum = ws + nsplit * k1pad * npad;
   dim3 grid((unsigned)nsplit, k1pad / 64, npad / 64);
-  if (split)
+  if (split == GM_F16X3)
+    hipLaunchKernelGGL((k_atb_x<XL, YL, NS_F16>), grid, dim3(256), 0, s, X, Y, part, csum, M, rps,
+                       k1pad, npad);
+  else if (split == GM_BF16X6)
     hipLaunchKernelGGL((k_atb_x<XL, YL>), grid, dim3(256), 0, s, X, Y, part, csum, M, rps, k1pad,
                        npad);
   else

@@ -130,6 +130,10 @@ _SIGS = {
     "spff_debug_set": (_I, [_P, _I, _I]),
     "spff_prof_enable": (_I, [_P, _I]),
     "spff_prof_collect": (_I, [_P, ctypes.POINTER(ctypes.c_double), _I]),
+    "spff_upconv_ws_bytes": (ctypes.c_size_t, [_I, _I, _I, _I, _I, _I]),
+    "spff_upconv_fwd": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
+    "spff_upconv_dgrad": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
+    "spff_upconv_wgrad": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
     "spff_conv_prof_enable": (_I, [_I]),
     "spff_conv_prof_collect": (_I, [ctypes.POINTER(ctypes.c_double), _I]),
     "spff_loss_ws_bytes": (_S, [_L, _I]),
