@@ -277,11 +277,13 @@ def bench_unet3d(args, world, rank, device):
     registry "3DUNet") on batch 4 x 1 x 5 x 96 x 96 per GPU: train-mode forward,
     the wrapper's weighted CE, backward (optimizer excluded, as in the headline
     metric).  N > 1: batch data parallelism (per-replica BatchNorm statistics,
-    as DDP without SyncBN), global valid count, gradient all-reduce."""
+    synchronised BatchNorm (innovative3D.distributed.sync_batchnorm: the batch moments
+    and the backward's per-channel sums all-reduced, so N ranks normalise exactly as one
+    device on the N x 4 batch), global valid count, gradient all-reduce."""
     import innovative3D.models as M
     from innovative3D.weightgen import synth_state
     from innovative3D.synthetic import synthetic_batch
-    from innovative3D.distributed import allreduce_gradients, global_valid_count
+    from innovative3D.distributed import allreduce_gradients, global_valid_count, sync_batchnorm
     K, Bt, D0, HW = args.classes, 4, 5, 96
     m = M.LitCicek3DUNet_DepthAdapter_Published(num_classes=K)
     sd = m.state_dict()
@@ -289,6 +291,7 @@ def bench_unet3d(args, world, rank, device):
     m.load_state_dict({k: torch.from_numpy(v) for k, v in st.items()})
     m = m.to(device).train()
     m.backbone.math = args.math
+    sync_batchnorm(m)  # (world 1: nothing to synchronise)
     x, y = synthetic_batch(Bt, 1, D0, HW, HW, K, ignore_frac=0.01, seed=1000 + rank, device=device)
     params = list(m.parameters())
 
@@ -356,7 +359,9 @@ def bench_unet3d(args, world, rank, device):
         "data": "synthetic (x~N(0,1), labels U[0,K) with 1% ignore=255; weights from weightgen seed 0)",
         "config": {"workload": f"3DUNet fwd+weighted CE+bwd, batch {Bt} x 1ch x {D0} x {HW} x {HW} "
                                f"per GPU (backbone at 16 x {HW} x {HW}), K={K}, base 32, "
-                               "BatchNorm train mode (BASELINE configs[2])",
+                               "BatchNorm train mode" + (", synchronised over the ranks"
+                                                         if world > 1 else "") +
+                               " (BASELINE configs[2])",
                    "global_batch": Bt * world, "shape": [Bt, 1, D0, HW, HW],
                    "parallelism": f"dp{world}"},
         "loss": float(loss.item()),

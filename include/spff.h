@@ -283,6 +283,14 @@ int spff_unet3d_forward(spff_unet3d* net, const float* x, const float* params, f
 /* backward of the last forward: dlogits [B][D][H][W][K] -> dparams (every entry written) */
 int spff_unet3d_backward(spff_unet3d* net, const float* dlogits, const float* params,
                          float* dparams, void* workspace, void* stream);
+/* Synchronised BatchNorm for data parallelism (torch.nn.SyncBatchNorm semantics): with a
+ * table (only its allreduce is used; in-place fp64 sum over the group, in stream order) and
+ * world > 1, every train-mode BatchNorm3d all-reduces its per-channel batch moments and its
+ * backward's two per-channel sums, so each rank normalises with the global batch statistics
+ * and updates identical running statistics; the BN weight / bias gradients stay this
+ * rank's partial sums (the caller SUM-all-reduces the flat gradient).  Every rank must run
+ * the plan's shape.  NULL or world <= 1: per-replica statistics (the default). */
+int spff_unet3d_set_sync_bn(spff_unet3d* net, const spff_coll* coll, int world);
 int spff_unet3d_saved_tensor(const spff_unet3d* net, void* workspace, const char* name,
                              const float** ptr, int64_t* nvox, int* channels);
 

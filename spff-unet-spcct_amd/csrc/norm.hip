@@ -573,6 +573,92 @@ __global__ void k_bn_bwd_stats(const float* __restrict__ sums, float* __restrict
   if (dbeta) dbeta[c] = (float)s0;
 }
 
+// ---- SyncBatchNorm: the same per-channel fp64 sums, over the data-parallel group ----
+__global__ void k_bn_partial(const float* __restrict__ sums, double* __restrict__ part, Vol vol,
+                             int C, int nq) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  for (int q = 0; q < nq; ++q) {
+    double s = 0.0;
+    for (int b = 0; b < vol.B; ++b)
+      for (int d = 0; d < vol.D; ++d) s += sums[(((int64_t)b * C + c) * vol.D + d) * nq + q];
+    part[(int64_t)q * C + c] = s;
+  }
+}
+__global__ void k_bn_mean_fin(const double* __restrict__ part, float* __restrict__ mean, int B,
+                              int C, double N) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float m = (float)(part[c] / N);
+  for (int b = 0; b < B; ++b) mean[b * C + c] = m;
+}
+__global__ void k_bn_rstd_fin(const double* __restrict__ part, const float* __restrict__ gamma,
+                              const float* __restrict__ beta, const float* __restrict__ mean,
+                              float* __restrict__ rstd, float* __restrict__ al,
+                              float* __restrict__ de, float* __restrict__ rmean,
+                              float* __restrict__ rvar, double mom, double eps, int B, int C,
+                              double N) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const double s = part[c];
+  const double var = s / N;
+  const float rs = (float)(1.0 / sqrt(var + eps));
+  const float mu = mean[c];
+  const float g = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+  const float a = g * rs;
+  for (int b = 0; b < B; ++b) {
+    rstd[b * C + c] = rs;
+    al[b * C + c] = a;
+    de[b * C + c] = bt - mu * a;
+  }
+  if (rmean) {
+    rmean[c] = (float)(mom * (double)mu + (1.0 - mom) * (double)rmean[c]);
+    const double uv = N > 1.0 ? s / (N - 1.0) : var;
+    rvar[c] = (float)(mom * uv + (1.0 - mom) * (double)rvar[c]);
+  }
+}
+__global__ void k_bn_bwd_dgb_part(const double* __restrict__ part, float* __restrict__ dgamma,
+                                  float* __restrict__ dbeta, int C) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  if (dgamma) dgamma[c] = (float)part[C + c];
+  if (dbeta) dbeta[c] = (float)part[c];
+}
+__global__ void k_bn_bwd_fin(const double* __restrict__ part, float* __restrict__ k1,
+                             float* __restrict__ k2, int B, int C, double N) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float a = (float)(part[c] / N), b2 = (float)(part[C + c] / N);
+  for (int b = 0; b < B; ++b) {
+    k1[b * C + c] = a;
+    k2[b * C + c] = b2;
+  }
+}
+hipError_t bn_partial(const float* sums, double* part, Vol vol, int C, int nq, hipStream_t s) {
+  hipLaunchKernelGGL(k_bn_partial, dim3(cdiv(C, 64)), dim3(64), 0, s, sums, part, vol, C, nq);
+  return hipGetLastError();
+}
+hipError_t bn_mean_fin(const double* part, float* mean, int B, int C, double N, hipStream_t s) {
+  hipLaunchKernelGGL(k_bn_mean_fin, dim3(cdiv(C, 64)), dim3(64), 0, s, part, mean, B, C, N);
+  return hipGetLastError();
+}
+hipError_t bn_rstd_fin(const double* part, const float* gamma, const float* beta,
+                       const float* mean, float* rstd, float* al, float* de, float* rmean,
+                       float* rvar, double mom, double eps, int B, int C, double N, hipStream_t s) {
+  hipLaunchKernelGGL(k_bn_rstd_fin, dim3(cdiv(C, 64)), dim3(64), 0, s, part, gamma, beta, mean,
+                     rstd, al, de, rmean, rvar, mom, eps, B, C, N);
+  return hipGetLastError();
+}
+hipError_t bn_bwd_dgb_part(const double* part, float* dgamma, float* dbeta, int C, hipStream_t s) {
+  hipLaunchKernelGGL(k_bn_bwd_dgb_part, dim3(cdiv(C, 64)), dim3(64), 0, s, part, dgamma, dbeta, C);
+  return hipGetLastError();
+}
+hipError_t bn_bwd_fin(const double* part, float* k1, float* k2, int B, int C, double N,
+                      hipStream_t s) {
+  hipLaunchKernelGGL(k_bn_bwd_fin, dim3(cdiv(C, 64)), dim3(64), 0, s, part, k1, k2, B, C, N);
+  return hipGetLastError();
+}
+
 hipError_t bn_mean(const float* sums, float* mean, Vol vol, int C, hipStream_t s) {
   hipLaunchKernelGGL(k_bn_mean, dim3(cdiv(C, 64)), dim3(64), 0, s, sums, mean, vol, C);
   return hipGetLastError();

@@ -362,6 +362,19 @@ hipError_t bn_rstd(const float* sqsums, const float* gamma, const float* beta, c
 hipError_t bn_eval(const float* rmean, const float* rvar, const float* gamma, const float* beta,
                    float* mean, float* rstd, float* al, float* de, double eps, int B, int C,
                    hipStream_t s);
+// SyncBatchNorm (data-parallel 3DUNet, unet3d.hip): per-channel fp64 partials of the
+// per-(b,c,d) slab sums, part[q][c] = sum over (b, d) of sums[b][c][d][q] (nq = 1 or 2; the
+// order of bn_mean / bn_bwd_stats), all-reduced by the caller, then finalised with the
+// group's voxel count N (the running statistics as bn_rstd)
+hipError_t bn_partial(const float* sums, double* part, Vol vol, int C, int nq, hipStream_t s);
+hipError_t bn_mean_fin(const double* part, float* mean, int B, int C, double N, hipStream_t s);
+hipError_t bn_rstd_fin(const double* part, const float* gamma, const float* beta,
+                       const float* mean, float* rstd, float* al, float* de, float* rmean,
+                       float* rvar, double mom, double eps, int B, int C, double N, hipStream_t s);
+// dgamma[c] = part[1][c], dbeta[c] = part[0][c] (this rank's share), before the all-reduce
+hipError_t bn_bwd_dgb_part(const double* part, float* dgamma, float* dbeta, int C, hipStream_t s);
+hipError_t bn_bwd_fin(const double* part, float* k1, float* k2, int B, int C, double N,
+                      hipStream_t s);
 // eval = 1: backward of the running-statistics transform (k1 = k2 = 0)
 hipError_t bn_bwd_stats(const float* sums, float* dgamma, float* dbeta, float* k1, float* k2,
                         Vol vol, int C, hipStream_t s, int eval = 0);

@@ -86,6 +86,12 @@ struct spff_unet3d {
   size_t G_out = 0, G_dy2 = 0, G_da1 = 0, G_dx = 0, dskip[4] = {}, logit_t = 0, dl_t = 0;
   size_t total = 0;
   bool last_training = true;
+  // synchronised BatchNorm (spff_unet3d_set_sync_bn): the per-channel batch moments and the
+  // backward's two per-channel sums are all-reduced (fp64) over the data-parallel group, so
+  // every rank normalises with the GLOBAL batch statistics (torch.nn.SyncBatchNorm); world
+  // 1 or no table: per-replica statistics, as DDP without SyncBN
+  Coll co;
+  size_t bnp = 0;  // fp64 per-channel partials [2][16 f]
   // per call
   char* ws = nullptr;
   const float* prm = nullptr;
@@ -225,6 +231,7 @@ int build(spff_unet3d* p) {
   p->red_out = p->alloc(red_out);
   p->kk1 = p->alloc((size_t)B * 16 * f * sizeof(float));
   p->kk2 = p->alloc((size_t)B * 16 * f * sizeof(float));
+  p->bnp = p->alloc((size_t)2 * 16 * f * sizeof(double));
   p->wg_ws = p->alloc(wg);
   p->pkb = conv3d_packs_batched(c.math);
   if (p->pkb) {
@@ -267,6 +274,20 @@ int bn_fwd(spff_unet3d* p, const Vol& v, int C, size_t y, size_t mean, size_t rs
   RedArgs a{};
   a.y = p->F(y);
   UHIPCK(slab_reduce(RED_SUM, a, v, C, p->F(p->red_out), p->F(p->red_ws), p->st));
+  if (p->co.on()) {  // SyncBN: global moments (same fp64 per-channel sums, then the group's)
+    double* part = reinterpret_cast<double*>(p->ws + p->bnp);
+    const double N = (double)nvox(v) * p->co.world;  // every rank runs the plan's shape
+    UHIPCK(bn_partial(p->F(p->red_out), part, v, C, 1, p->st));
+    UHIPCK(p->co.sum_f64(part, C, p->st));
+    UHIPCK(bn_mean_fin(part, p->F(mean), v.B, C, N, p->st));
+    a.mean = p->F(mean);
+    UHIPCK(slab_reduce(RED_SQDEV, a, v, C, p->F(p->red_out), p->F(p->red_ws), p->st));
+    UHIPCK(bn_partial(p->F(p->red_out), part, v, C, 1, p->st));
+    UHIPCK(p->co.sum_f64(part, C, p->st));
+    UHIPCK(bn_rstd_fin(part, p->P(g), p->P(b), p->F(mean), p->F(rstd), p->F(al), p->F(de),
+                       p->BF(rm), p->BF(rv), BN_MOM, BN_EPS, v.B, C, N, p->st));
+    return SPFF_OK;
+  }
   UHIPCK(bn_mean(p->F(p->red_out), p->F(mean), v, C, p->st));
   a.mean = p->F(mean);
   UHIPCK(slab_reduce(RED_SQDEV, a, v, C, p->F(p->red_out), p->F(p->red_ws), p->st));
@@ -354,8 +375,19 @@ int bn_bwd(spff_unet3d* p, const Vol& v, int C, size_t y, const float* g, float*
   a.y = p->F(y); a.g = g; a.mean = p->F(mean); a.rstd = p->F(rstd);
   a.al = p->F(al); a.de = p->F(de); a.neg = 0.f;
   UHIPCK(slab_reduce(RED_BWD_IN, a, v, C, p->F(p->red_out), p->F(p->red_ws), p->st));
-  UHIPCK(bn_bwd_stats(p->F(p->red_out), p->DP(gamma), p->DP(beta), p->F(p->kk1), p->F(p->kk2), v,
-                      C, p->st, p->last_training ? 0 : 1));
+  if (p->co.on() && p->last_training) {
+    // SyncBN: k1, k2 from the group's sums; dgamma / dbeta are this rank's partial sums
+    // (the flat gradient is SUM-all-reduced afterwards, like every other parameter's)
+    double* part = reinterpret_cast<double*>(p->ws + p->bnp);
+    UHIPCK(bn_partial(p->F(p->red_out), part, v, C, 2, p->st));
+    UHIPCK(bn_bwd_dgb_part(part, p->DP(gamma), p->DP(beta), C, p->st));
+    UHIPCK(p->co.sum_f64(part, 2 * (int64_t)C, p->st));
+    UHIPCK(bn_bwd_fin(part, p->F(p->kk1), p->F(p->kk2), v.B, C, (double)nvox(v) * p->co.world,
+                      p->st));
+  } else {
+    UHIPCK(bn_bwd_stats(p->F(p->red_out), p->DP(gamma), p->DP(beta), p->F(p->kk1), p->F(p->kk2),
+                        v, C, p->st, p->last_training ? 0 : 1));
+  }
   UHIPCK(in_bwd_apply(p->F(y), g, dy, p->F(mean), p->F(rstd), p->F(al), p->F(de), p->P(gamma),
                       nullptr, nullptr, p->F(p->kk1), p->F(p->kk2), v, C, p->st, 0.f));
   return SPFF_OK;
@@ -535,7 +567,25 @@ int spff_unet3d_forward(spff_unet3d* p, const float* x, const float* params, flo
   p->dprm = nullptr;
   p->buf = buffers;
   p->st = static_cast<hipStream_t>(stream);
-  return forward(p, x, logits, training != 0);
+  p->co.failed = nullptr;
+  const int rc = forward(p, x, logits, training != 0);
+  if (p->co.failed) return ufail(SPFF_ECOLL, std::string("SyncBN ") + p->co.failed + " failed");
+  return rc;
+}
+
+int spff_unet3d_set_sync_bn(spff_unet3d* p, const spff_coll* coll, int world) {
+  if (!p) return ufail(SPFF_EINVAL, "null plan");
+  if (!coll || world <= 1) {
+    p->co = Coll{};
+    return SPFF_OK;
+  }
+  if (!coll->allreduce) return ufail(SPFF_EINVAL, "spff_coll needs allreduce");
+  p->co = Coll{};
+  p->co.world = world;
+  p->co.ctx = coll->ctx;
+  p->co.allreduce = coll->allreduce;
+  p->co.halo = coll->halo;
+  return SPFF_OK;
 }
 
 int spff_unet3d_backward(spff_unet3d* p, const float* dlogits, const float* params,
@@ -545,7 +595,10 @@ int spff_unet3d_backward(spff_unet3d* p, const float* dlogits, const float* para
   p->prm = params;
   p->dprm = dparams;
   p->st = static_cast<hipStream_t>(stream);
-  return backward(p, dlogits);
+  p->co.failed = nullptr;
+  const int rc = backward(p, dlogits);
+  if (p->co.failed) return ufail(SPFF_ECOLL, std::string("SyncBN ") + p->co.failed + " failed");
+  return rc;
 }
 
 int spff_unet3d_saved_tensor(const spff_unet3d* p, void* ws, const char* name, const float** ptr,

@@ -134,6 +134,7 @@ _SIGS = {
     "spff_upconv_fwd": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
     "spff_upconv_dgrad": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
     "spff_upconv_wgrad": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
+    "spff_unet3d_set_sync_bn": (_I, [_P, _P, _I]),
     "spff_conv_prof_enable": (_I, [_I]),
     "spff_conv_prof_collect": (_I, [ctypes.POINTER(ctypes.c_double), _I]),
     "spff_loss_ws_bytes": (_S, [_L, _I]),
@@ -707,6 +708,44 @@ class UNet3DPlan:
         if self._ws is None or self._ws.device != device:
             self._ws = _alloc_workspace(self, device)
         return self._ws
+
+    def set_sync_bn(self, impl) -> None:
+        """Synchronised BatchNorm over a data-parallel group (spff_unet3d_set_sync_bn):
+        ``impl`` has ``allreduce(t)`` (in-place sum of a device tensor over the group) and
+        ``world``, e.g. innovative3D.sharded.TorchDepthColl; None restores per-replica
+        statistics."""
+        L = lib()
+        if impl is None or int(getattr(impl, "world", 1)) <= 1:
+            check(L.spff_unet3d_set_sync_bn(self._h, None, 1), "spff_unet3d_set_sync_bn")
+            self._sync = None
+            return
+
+        def _allreduce(ctx, buf, n, dt, stream):
+            try:
+                ws = self._ws
+                off = buf - ws.data_ptr()
+                esz = 8 if dt == 1 else 4
+                if off < 0 or off % esz or off + n * esz > ws.numel():
+                    raise SpffError("collective buffer outside the plan workspace")
+                t = ws[off:off + n * esz].view(torch.float64 if dt == 1 else torch.float32)
+                cur = torch.cuda.current_stream(t.device)
+                if stream and stream != cur.cuda_stream:
+                    with torch.cuda.stream(torch.cuda.ExternalStream(stream, device=t.device)):
+                        impl.allreduce(t)
+                else:
+                    impl.allreduce(t)
+                return 0
+            except Exception as e:  # noqa: BLE001 -- reported through the engine status
+                self.coll_error = e
+                return 1
+
+        def _no_halo(ctx, interior, sl, d_local, stream):
+            return 1
+        self._sync_fns = (ALLREDUCE_FN(_allreduce), HALO_FN(_no_halo))  # keep alive
+        self._sync = spff_coll(None, self._sync_fns[0], self._sync_fns[1])
+        self.coll_error = None
+        check(L.spff_unet3d_set_sync_bn(self._h, ctypes.byref(self._sync), int(impl.world)),
+              "spff_unet3d_set_sync_bn")
 
     def forward(self, x: torch.Tensor, flat: torch.Tensor, bufs: torch.Tensor, training: bool,
                 out: Optional[torch.Tensor] = None) -> torch.Tensor:

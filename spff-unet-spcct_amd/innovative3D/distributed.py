@@ -248,3 +248,30 @@ def allreduce_uncovered(params: Iterable[torch.nn.Parameter], bucketer: Optional
     rest = [p for p in params if p.grad is not None and id(p) not in done]
     allreduce_gradients(rest, group, force=force)
     return len(rest)
+
+
+def sync_batchnorm(module: torch.nn.Module, group=None, host_staged=None):
+    """Synchronised BatchNorm for the 3DUNet variant's data parallelism: every engine
+    BatchNorm3d of ``module`` (the Cicek3DUNet backbone, or the Lit wrapper around it)
+    all-reduces its batch moments over ``group`` in the forward and its two per-channel
+    sums in the backward (spff_unet3d_set_sync_bn), so a step on N ranks of B samples
+    normalises exactly as one device on the N B-sample batch and every rank keeps the same
+    running statistics (torch.nn.SyncBatchNorm semantics).  The
+    BN weight / bias gradients stay per-rank partial sums, SUM-all-reduced with the rest of
+    the gradient.  World 1: nothing to synchronise (returns None).  Returns the collective
+    (innovative3D.sharded.TorchDepthColl: RCCL on device tensors, host-staged for gloo)."""
+    from .sharded import TorchDepthColl
+    if world(group) <= 1:
+        for m in module.modules():
+            if hasattr(m, "_bn_modules"):
+                m.sync_bn = None
+        return None
+    coll = TorchDepthColl(group, host_staged=host_staged)
+    n = 0
+    for m in module.modules():
+        if hasattr(m, "_bn_modules"):  # the engine backbone (models.Cicek3DUNet)
+            m.sync_bn = coll
+            n += 1
+    if not n:
+        raise ValueError("sync_batchnorm: no engine 3DUNet backbone in the module")
+    return coll

@@ -667,6 +667,14 @@ class Cicek3DUNet(nn.Module):
         params = self._engine_params(plan)
         flat = self._ensure_flat(plan, params, x.device)
         bufs = self._ensure_bufs(plan, x.device)
+        plan.workspace(x.device)
+        # data parallelism with synchronised BatchNorm: ``self.sync_bn`` = a collective with
+        # allreduce(t) / world over the group (innovative3D.distributed.SyncBNGroup); None:
+        # per-replica statistics (DDP without SyncBN, the reference's Lightning default)
+        sync = getattr(self, "sync_bn", None)
+        if getattr(plan, "_sync_impl", None) is not sync:
+            plan.set_sync_bn(sync)
+            plan._sync_impl = sync
         training = bool(self.training)
         if training:
             with torch.no_grad():

@@ -187,3 +187,108 @@ def test_unet3d_config3_shape_step():
     assert abs(float(loss) - math.log(13)) < 1.0
     for n, p in m.named_parameters():
         assert p.grad is not None and torch.isfinite(p.grad).all(), n
+
+
+# ---- data parallelism with synchronised BatchNorm ----
+SB_SHAPE, SB_K = (4, 1, 5, 32, 32), 9
+
+
+def _sb_model(seed=3):
+    from innovative3D.weightgen import synth_state
+    m = M.LitCicek3DUNet_DepthAdapter_Published(num_classes=SB_K)
+    sd = m.state_dict()
+    st = synth_state([(k, tuple(v.shape)) for k, v in sd.items()], seed=seed)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in st.items()})
+    return m.to(DEV).train()
+
+
+def _sb_data():
+    g = torch.Generator().manual_seed(21)
+    x = torch.randn(*SB_SHAPE, generator=g)
+    G = torch.randn(SB_SHAPE[0], SB_K, *SB_SHAPE[2:], generator=g)  # d loss / d logits
+    return x, G
+
+
+def _sb_step(m, x, G):
+    """forward (train mode) + a loss that is a plain sum over samples, so the batch's
+    gradient is the SUM of the ranks' gradients with no loss normalisation in between"""
+    for p in m.parameters():
+        p.grad = None
+    logits = m(x.to(DEV))
+    (logits * G.to(DEV)).sum().backward()
+    torch.cuda.synchronize()
+    return logits.detach().cpu()
+
+
+def _sb_worker(rank, world, port, out, sync):
+    import os
+    import pathlib
+    import sys
+    import torch.distributed as dist
+    root = pathlib.Path(__file__).resolve().parents[1]
+    sys.path[:0] = [str(root), str(root / "tests"), str(root / "spff-unet-spcct_amd")]
+    from innovative3D.distributed import allreduce_gradients, sync_batchnorm
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    m = _sb_model()
+    if sync:
+        sync_batchnorm(m)
+    x, G = _sb_data()
+    n = SB_SHAPE[0] // world
+    lg = _sb_step(m, x[rank * n:(rank + 1) * n], G[rank * n:(rank + 1) * n])
+    allreduce_gradients(list(m.parameters()))  # host-staged gloo: CPU copies
+    bufs = {k: v.detach().cpu().numpy() for k, v in m.named_buffers() if "running" in k}
+    np.savez(f"{out}.{rank}.npz", logits=lg.numpy(), **{"b_" + k: v for k, v in bufs.items()},
+             **{"g_" + k: p.grad.cpu().numpy() for k, p in m.named_parameters()})
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("mth", ["f32", "f16x3"])
+def test_sync_batchnorm_world2_matches_single_batch(tmp_path, mth, monkeypatch):
+    """(2 + 2) x 1 x 5 x 32^2 on two ranks with synchronised BatchNorm (host-staged gloo,
+    both ranks on this GPU) against ONE process on the batch of 4: logits, running
+    statistics and the all-reduced gradients.  Without SyncBN the ranks normalise with
+    their own half-batch statistics, and the logits differ by O(1) (checked too)."""
+    import torch.multiprocessing as mp
+    monkeypatch.setenv("SPFF_MATH", mth)
+    m = _sb_model()
+    x, G = _sb_data()
+    ref = _sb_step(m, x, G).numpy()
+    ref_g = {k: p.grad.cpu().numpy() for k, p in m.named_parameters()}
+    ref_b = {k: v.detach().cpu().numpy() for k, v in m.named_buffers() if "running" in k}
+    del m
+    res = {}
+    for sync in (True, False):
+        out = str(tmp_path / f"sb{int(sync)}")
+        mp.spawn(_sb_worker, args=(2, _free_port(), out, sync), nprocs=2, join=True)
+        parts = [np.load(f"{out}.{r}.npz") for r in range(2)]
+        res[sync] = parts
+    parts = res[True]
+    lg = np.concatenate([p["logits"] for p in parts], axis=0)
+    e = float(np.abs(lg - ref).max()) / float(np.abs(ref).max())
+    e_nosync = float(np.abs(np.concatenate([p["logits"] for p in res[False]], 0) - ref).max()) \
+        / float(np.abs(ref).max())
+    worst_b = max(float(np.abs(parts[r]["b_" + k] - v).max() / max(np.abs(v).max(), 1e-30))
+                  for k, v in ref_b.items() for r in range(2))
+    worst_g = max(float(np.abs(parts[0]["g_" + k] - v).max() / max(np.abs(v).max(), 1e-30))
+                  for k, v in ref_g.items())
+    print(f"SyncBN world 2 {mth}: logits rel {e:.2e} (per-replica BN: {e_nosync:.2e}), running "
+          f"stats rel {worst_b:.2e}, gradients rel {worst_g:.2e}")
+    assert e <= 1e-5, e
+    assert e_nosync > 1e-2  # the test discriminates: per-replica statistics differ
+    assert worst_b <= 1e-5, worst_b
+    assert worst_g <= 1e-4, worst_g
+    for k in ref_g:  # every rank holds the same reduced gradient
+        np.testing.assert_array_equal(parts[0]["g_" + k], parts[1]["g_" + k])
