@@ -141,6 +141,12 @@
 #define SPFF_XSTORE 1
 #endif
 
+#ifndef SPFF_XBSTAT
+// 1: the input-gradient conv into da1 also forms the IN-backward sums of its output in the
+// epilogue (BStat), replacing a RED_BWD_IN slab_reduce pass (0: that pass, A/B)
+#define SPFF_XBSTAT 1
+#endif
+
 #ifndef SPFF_XSTAMP
 // timing diagnostics only (variant builds): per workgroup of k_conv3d_fwd_x, s_memtime at
 // kernel start, first MFMA, end of the k-loop and end, plus s_memrealtime at start / end
@@ -351,7 +357,7 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : (BN <= 32 && NS == NS_F16 &&
     Src2 x, const uint4* __restrict__ wp, Dst2 y, Vol vol, int Cin, int nkc, int Cout, int npad,
     int tilesD, int tilesH, int tilesW, float* __restrict__ part, int kps,
     float* __restrict__ stats, int ntiles, int td0, int tds, int th0, int ths,
-    const unsigned* __restrict__ wmx) {
+    const unsigned* __restrict__ wmx, BStat bst) {
   constexpr int XT_THREADS = NW * 64;
 #if SPFF_XSTAMP
   const unsigned long long st_t0 = __builtin_amdgcn_s_memtime();
@@ -1026,6 +1032,26 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : (BN <= 32 && NS == NS_F16 &&
     vrow(wave * RB + rb, orow(r), td, th, tw);
     return d0 + td < D && h0 + th < H && w0 + tw < W;
   };
+  // (bst, input gradient with fused IN-backward sums): this thread's channel quad is fixed
+  // in the row-major store loop below (XT_THREADS is a multiple of BN / 4); its y loads are
+  // issued here, before the image barrier, so their latency overlaps it
+  constexpr int Q4 = BN / 4;
+  constexpr int NIT = NROW * Q4 / XT_THREADS;
+  static_assert(XT_THREADS % Q4 == 0 && (NROW * Q4) % XT_THREADS == 0, "store loop shape");
+  const bool bsm = SPFF_XBSTAT && !HR && vec && bst.y != nullptr;  // (uniform; unsharded only)
+  float4 byv[NIT];
+  if (bsm) {
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int i = tid + it * XT_THREADS, row = i / Q4, q = i % Q4;
+      int td, th, tw;
+      vrow(row >> 4, row & 15, td, th, tw);
+      const int gd = d0 + td, gh = h0 + th, gw = w0 + tw, n = n0 + 4 * q;
+      const bool ok = gd < D && gh < H && gw < W && n < Cout;
+      const int64_t vox = ok ? (((int64_t)b * D + gd) * H + gh) * W + gw : 0;
+      byv[it] = *reinterpret_cast<const float4*>(bst.y + vox * bst.ld + (ok ? n : 0));
+    }
+  }
   // every wave is past its last operand read
   if (vec || stats) __syncthreads();
   if (vec) {
@@ -1053,9 +1079,69 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : (BN <= 32 && NS == NS_F16 &&
     }
   }
   if (vec || stats) __syncthreads();
-  if (vec) {
+  if (bsm) {
     const float* ot = reinterpret_cast<const float*>(lds4);
-    constexpr int Q4 = BN / 4;
+    const int qf = tid % Q4, nf = n0 + 4 * qf;
+    float ca[4], cd[4], cm[4], cr[4], s0[4], s1[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t bc = (int64_t)b * bst.ld + (nf < Cout ? nf : 0) + j;
+      ca[j] = bst.al[bc];
+      cd[j] = bst.de[bc];
+      cm[j] = bst.mean[bc];
+      cr[j] = bst.rstd[bc];
+      s0[j] = 0.f;
+      s1[j] = 0.f;
+    }
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int i = tid + it * XT_THREADS, row = i / Q4;
+      int td, th, tw;
+      vrow(row >> 4, row & 15, td, th, tw);
+      const int gd = d0 + td, gh = h0 + th, gw = w0 + tw;
+      if (gd >= D || gh >= H || gw >= W || nf >= Cout) continue;
+      const int64_t vox = (((int64_t)b * D + gd) * H + gh) * W + gw;
+      const float4 v = *reinterpret_cast<const float4*>(ot + row * OP + 4 * qf);
+      float* pp = nf < y.split ? y.p0 + vox * y.ld0 + nf : y.p1 + vox * y.ld1 + (nf - y.split);
+      *reinterpret_cast<float4*>(pp) = v;
+      const float vv[4] = {v.x, v.y, v.z, v.w};
+      const float yy[4] = {byv[it].x, byv[it].y, byv[it].z, byv[it].w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {  // RED_BWD_IN's terms (norm.hip), without the gate A, Bc
+        const float r = yy[j] * ca[j] + cd[j];
+        const float dr = vv[j] * (r > 0.f ? 1.f : bst.neg);
+        const float xh = (yy[j] - cm[j]) * cr[j];
+        s0[j] += dr;
+        s1[j] += dr * xh;
+      }
+    }
+    // the lanes of a wave holding the same channel quad (lane mod Q4), then the waves in
+    // order: a fixed reduction tree
+#pragma unroll
+    for (int o = Q4; o < 64; o <<= 1)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        s0[j] += __shfl_xor(s0[j], o);
+        s1[j] += __shfl_xor(s1[j], o);
+      }
+    if (lane < Q4) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        sred[(wave * Q4 + lane) * 8 + j] = s0[j];
+        sred[(wave * Q4 + lane) * 8 + 4 + j] = s1[j];
+      }
+    }
+    __syncthreads();
+    if (wave == 0 && lane < Q4 && n0 + 4 * lane < Cout) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float t = 0.f;
+        for (int w = 0; w < NW; ++w) t += sred[(w * Q4 + lane) * 8 + j];
+        bst.out[((int64_t)tile * npad + n0 + 4 * lane + (j & 3)) * 2 + (j >> 2)] = t;
+      }
+    }
+  } else if (vec) {
+    const float* ot = reinterpret_cast<const float*>(lds4);
     for (int i = tid; i < NROW * Q4; i += XT_THREADS) {
       const int row = i / Q4, q = i % Q4;
       int td, th, tw;
@@ -1237,7 +1323,8 @@ template <int BN, int KD, int NS, bool HR, int MB = xt_mb(BN, NS), int NW = xt_n
           int TD = xt_td(BN, NS)>
 static hipError_t launch_fwd_xh(const Src2& x, const uint4* wx, const Dst2& y, Vol vol, int K,
                                 int nkc, int N, int npad, hipStream_t s, float* part, int nsplit,
-                                int kps, float* stats, int dpart, const unsigned* wmx) {
+                                int kps, float* stats, int dpart, const unsigned* wmx,
+                                const BStat& bst) {
   constexpr int TH = SPFF_X16 ? 2 * NW * MB / TD : NW * MB;
   static_assert(NW == 8 || TD == XT_D || xt_d4(BN, NS), "xt_ntiles: tile shape");
   constexpr size_t shm = xt_lds_bytes<BN, KD, NS, TD, TH>();
@@ -1271,7 +1358,7 @@ static hipError_t launch_fwd_xh(const Src2& x, const uint4* wx, const Dst2& y, V
   dim3 grid(8 * cdiv(ntiles, 8) * (npad / BN), 1, part ? nsplit : 1);
   hipLaunchKernelGGL(kern, grid, dim3(NW * 64), shm, s, x, wx, y, vol, K, nkc, N, npad, tilesD,
                      tilesH, tilesW, part, part ? kps : nkc, part ? nullptr : stats, ntiles, td0,
-                     tds, th0, ths, wmx);
+                     tds, th0, ths, wmx, bst);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || !part) return e;
   const int64_t total = nvox(vol) * N;
@@ -1282,19 +1369,22 @@ static hipError_t launch_fwd_xh(const Src2& x, const uint4* wx, const Dst2& y, V
 template <int BN, int KD, int NS>
 static hipError_t launch_fwd_x(const Src2& x, const uint4* wx, const Dst2& y, Vol vol, int K,
                                int nkc, int N, int npad, hipStream_t s, float* part, int nsplit,
-                               int kps, float* stats, int dpart, const unsigned* wmx) {
+                               int kps, float* stats, int dpart, const unsigned* wmx,
+                               const BStat& bst) {
   if constexpr (xt_d4(BN, NS)) {
     constexpr int NW = xt_nw(BN, NS);
     if (xt_shallow(vol, BN, NS))
       return x.rows() ? launch_fwd_xh<BN, KD, NS, true, 2, NW, XT_D>(
-                            x, wx, y, vol, K, nkc, N, npad, s, part, nsplit, kps, stats, dpart, wmx)
+                            x, wx, y, vol, K, nkc, N, npad, s, part, nsplit, kps, stats, dpart, wmx,
+                            bst)
                       : launch_fwd_xh<BN, KD, NS, false, 2, NW, XT_D>(
-                            x, wx, y, vol, K, nkc, N, npad, s, part, nsplit, kps, stats, dpart, wmx);
+                            x, wx, y, vol, K, nkc, N, npad, s, part, nsplit, kps, stats, dpart, wmx,
+                            bst);
   }
   return x.rows() ? launch_fwd_xh<BN, KD, NS, true>(x, wx, y, vol, K, nkc, N, npad, s, part,
-                                                    nsplit, kps, stats, dpart, wmx)
+                                                    nsplit, kps, stats, dpart, wmx, bst)
                   : launch_fwd_xh<BN, KD, NS, false>(x, wx, y, vol, K, nkc, N, npad, s, part,
-                                                     nsplit, kps, stats, dpart, wmx);
+                                                     nsplit, kps, stats, dpart, wmx, bst);
 }
 
 namespace {
@@ -1629,7 +1719,7 @@ hipError_t conv3d_pack_many(const PackJobs& J, int math, hipStream_t s) {
 template <int NS>
 static hipError_t run_x(const Src2& x, const uint4* wu, const Dst2& y, Vol vol, int KD,
                         const XDims& d, hipStream_t s, float* ws, float* stats, int dpart,
-                        const unsigned* wmx) {
+                        const unsigned* wmx, const BStat& bst) {
   // (32x32x16, MB = 4, 2 x 32 x 16 tiles for Cout <= 32: fits LDS but spills 91 VGPRs)
   // (32x32x16 schedule, NW = 4 waves, 2 x 8 x 16 tiles: measured 6 % slower; the 16x16x32
   // schedule takes NW = 4 for BN 32 by default, SPFF_X32NW)
@@ -1638,16 +1728,16 @@ static hipError_t run_x(const Src2& x, const uint4* wu, const Dst2& y, Vol vol, 
   if (d.BN == 64)
     return KD == 3
                ? launch_fwd_x<64, 3, NS>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s, part,
-                                                k.nsplit, k.kps, stats, dpart, wmx)
+                                                k.nsplit, k.kps, stats, dpart, wmx, bst)
                : launch_fwd_x<64, 1, NS>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s, part,
-                                                k.nsplit, k.kps, stats, dpart, wmx);
+                                                k.nsplit, k.kps, stats, dpart, wmx, bst);
   if (d.BN == 16)
     return launch_fwd_x<16, 3, NS>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s, part, k.nsplit,
-                                   k.kps, stats, dpart, wmx);
+                                   k.kps, stats, dpart, wmx, bst);
   return KD == 3 ? launch_fwd_x<32, 3, NS>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s,
-                                                  part, k.nsplit, k.kps, stats, dpart, wmx)
+                                                  part, k.nsplit, k.kps, stats, dpart, wmx, bst)
                  : launch_fwd_x<32, 1, NS>(x, wu, y, vol, d.K, d.nkc, d.N, d.npad, s,
-                                                  part, k.nsplit, k.kps, stats, dpart, wmx);
+                                                  part, k.nsplit, k.kps, stats, dpart, wmx, bst);
 }
 
 
@@ -1681,6 +1771,63 @@ size_t conv3d_stats_bytes(Vol vol, int KD, int Cin, int Cout) {
   const XDims d = xdims(KD, Cin, Cout, false);
   const int64_t nt = std::max(xt_ntiles(vol, d.BN, 3), xt_ntiles(vol, d.BN, NS_F16));
   return (size_t)nt * (2 * d.npad + 1) * sizeof(float);
+}
+// the input gradient's epilogue with the IN-backward sums (BStat): the split kernel, one
+// launch (no split-K, unsharded), 16-B row stores (the X16 LDS-staged epilogue)
+bool conv3d_fuses_bwd_stats(Vol vol, int KD, int Cin_w, int Cout_w, int math) {
+  const XDims d = xdims(KD, Cin_w, Cout_w, true);
+  return SPFF_XBSTAT && SPFF_X16 && SPFF_XSTORE && use_split(vol, math, true) && vol.dh == 0 &&
+         (d.N & 3) == 0 && splitk_plan(vol, d, ns_of(math)).nsplit == 1;
+}
+// per (b, c): sum dr, sum dr xhat over the sample's tiles in a fixed order (fp64) -> k1, k2
+// (/ N) and dgamma, dbeta (summed over b) -- k_in_bwd_stats' outputs
+__global__ __launch_bounds__(256) void k_in_bwd_stats_tiles(const float* __restrict__ part,
+                                                            int tpb, int npad, int B, int C,
+                                                            double N, float* __restrict__ dgamma,
+                                                            float* __restrict__ dbeta,
+                                                            float* __restrict__ k1,
+                                                            float* __restrict__ k2) {
+  __shared__ double r0[256], r1[256];
+  const int c = blockIdx.x, tid = threadIdx.x;
+  double tg = 0.0, tb = 0.0;
+  for (int b = 0; b < B; ++b) {
+    double s0 = 0.0, s1 = 0.0;
+    for (int t = b * tpb + tid; t < (b + 1) * tpb; t += 256) {
+      const float2 v = *reinterpret_cast<const float2*>(part + ((int64_t)t * npad + c) * 2);
+      s0 += v.x;
+      s1 += v.y;
+    }
+    r0[tid] = s0;
+    r1[tid] = s1;
+    __syncthreads();
+    for (int st = 128; st > 0; st >>= 1) {
+      if (tid < st) {
+        r0[tid] += r0[tid + st];
+        r1[tid] += r1[tid + st];
+      }
+      __syncthreads();
+    }
+    if (tid == 0) {
+      k1[b * C + c] = (float)(r0[0] / N);
+      k2[b * C + c] = (float)(r1[0] / N);
+    }
+    tb += r0[0];
+    tg += r1[0];
+    __syncthreads();
+  }
+  if (tid == 0) {
+    if (dgamma) dgamma[c] = (float)tg;
+    if (dbeta) dbeta[c] = (float)tb;
+  }
+}
+hipError_t conv3d_in_bwd_stats_fin(const float* part, Vol vol, int KD, int Cin_w, int Cout_w,
+                                   int math, float* dgamma, float* dbeta, float* k1, float* k2,
+                                   hipStream_t s) {
+  const XDims d = xdims(KD, Cin_w, Cout_w, true);
+  const int64_t nt = xt_ntiles(vol, d.BN, ns_of(math));
+  hipLaunchKernelGGL(k_in_bwd_stats_tiles, dim3(d.N), dim3(256), 0, s, part, (int)(nt / vol.B),
+                     d.npad, vol.B, d.N, (double)vol.D * vol.H * vol.W, dgamma, dbeta, k1, k2);
+  return hipGetLastError();
 }
 bool conv3d_fuses_stats(Vol vol, int KD, int Cin, int Cout, int math) {
   const XDims d = xdims(KD, Cin, Cout, false);
@@ -1748,20 +1895,27 @@ hipError_t conv_prof_collect(double* out, int nclass) {
 
 static hipError_t conv3d_run_(const Src2& x, const void* wpack, const Dst2& y, Vol vol, int KD,
                               int Cin_w, int Cout_w, bool dgrad, int math, hipStream_t s,
-                              float* ws, float* stats, int dpart, const unsigned* wmax);
+                              float* ws, float* stats, int dpart, const unsigned* wmax,
+                              const BStat* bst);
 hipError_t conv3d_run(const Src2& x, const void* wpack, const Dst2& y, Vol vol, int KD,
                       int Cin_w, int Cout_w, bool dgrad, int math, hipStream_t s, float* ws,
-                      float* stats, int dpart, const unsigned* wmax) {
+                      float* stats, int dpart, const unsigned* wmax, const BStat* bst) {
   CProf pr(dgrad ? 1 : 0, 2.0 * (double)nvox(vol) * Cin_w * Cout_w * 9 * KD, s);
   const hipError_t e = conv3d_run_(x, wpack, y, vol, KD, Cin_w, Cout_w, dgrad, math, s, ws,
-                                   stats, dpart, wmax);
+                                   stats, dpart, wmax, bst);
   pr.end(s);
   return e;
 }
 static hipError_t conv3d_run_(const Src2& x, const void* wpack, const Dst2& y, Vol vol, int KD,
                               int Cin_w, int Cout_w, bool dgrad, int math, hipStream_t s,
-                              float* ws, float* stats, int dpart, const unsigned* wmax) {
+                              float* ws, float* stats, int dpart, const unsigned* wmax,
+                              const BStat* bst) {
   const XDims d = xdims(KD, Cin_w, Cout_w, dgrad);
+  if (bst && (dpart != 0 || x.rows() || !conv3d_fuses_bwd_stats(vol, KD, Cin_w, Cout_w, math) ||
+              (y.split & 3) || (y.ld0 & 3) || (y.ld1 & 3) || (bst->ld & 3) || !bst->y ||
+              !bst->out))
+    return hipErrorInvalidValue;
+  const BStat bs = bst ? *bst : BStat{};
   if (stats && (dgrad || !conv3d_fuses_stats(vol, KD, Cin_w, Cout_w, math)))
     return hipErrorInvalidValue;
   if ((dpart == 1 || dpart == 2) && !conv3d_splits_depth(vol, KD, Cin_w, Cout_w, dgrad, math))
@@ -1775,11 +1929,11 @@ static hipError_t conv3d_run_(const Src2& x, const void* wpack, const Dst2& y, V
       // the input's scale is taken per (tile, chunk) inside the kernel; the weights' from
       // the caller's precomputed max |w| or the one conv3d_pack left in the image's slot 0
       unsigned* sl = f16_slots(wpack, KD, Cin_w, Cout_w);
-      return run_x<NS_F16>(x, wu, y, vol, KD, d, s, ws, stats, dpart, wmax ? wmax : sl);
+      return run_x<NS_F16>(x, wu, y, vol, KD, d, s, ws, stats, dpart, wmax ? wmax : sl, bs);
     }
     return math == SPFF_MATH_BF16X3
-               ? run_x<2>(x, wu, y, vol, KD, d, s, ws, stats, dpart, nullptr)
-               : run_x<3>(x, wu, y, vol, KD, d, s, ws, stats, dpart, nullptr);
+               ? run_x<2>(x, wu, y, vol, KD, d, s, ws, stats, dpart, nullptr, bs)
+               : run_x<3>(x, wu, y, vol, KD, d, s, ws, stats, dpart, nullptr, bs);
   }
   return conv3d_fwd(x, static_cast<const float*>(wpack), y, vol, KD, d.K, rup(d.K, 8), d.N,
                     rup(d.N, conv3d_bn(d.N)), s);

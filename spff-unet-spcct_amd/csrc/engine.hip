@@ -168,6 +168,7 @@ struct spff_plan {
   bool efilm_ready = false;  // this forward's EFiLM coefficients are computed (all blocks)
   bool keep_out = false;  // debug: store the fused block outputs too (saved views)
   bool pool_fold = SPFF_POOL_FOLD;  // PoolAdd in the encoder backward (debug key 2: off)
+  bool bst_fuse = true;  // conv1's IN-backward sums in the dgrad epilogue (debug key 3: off)
   // per call
   char* ws = nullptr;
   const float* prm = nullptr;
@@ -711,8 +712,12 @@ int halo_begin(spff_plan* p, const float* x, const Vol& v, int C) {
 // scale is per (tile, chunk), inside the conv kernel)
 int conv_halo(spff_plan* p, int cls, double flops, double bytes, const Src2& x, const Dst2& y,
               const Vol& v, int Cin_w, int Cout_w, bool dgrad, float* stats,
-              const unsigned* wmax = nullptr) {
-  if (p->hsh) return conv_h(p, cls, flops, bytes, x, y, v, Cin_w, Cout_w, dgrad, wmax);
+              const unsigned* wmax = nullptr, const BStat* bst = nullptr) {
+  if (p->hsh) {
+    if (bst) return fail(SPFF_EINVAL, "fused IN-backward sums: unsharded plans only");
+    return conv_h(p, cls, flops, bytes, x, y, v, Cin_w, Cout_w, dgrad, wmax);
+  }
+  if (bst && v.dh) return fail(SPFF_EINVAL, "fused IN-backward sums: unsharded plans only");
   const int KD = p->KD, math = p->cfg.math;
   const bool ovl = v.dh && !stats && conv3d_splits_depth(v, KD, Cin_w, Cout_w, dgrad, math);
   const bool early = p->halo_early && p->halo_early == x.p0 && x.p1 == x.p0;
@@ -724,7 +729,7 @@ int conv_halo(spff_plan* p, int cls, double flops, double bytes, const Src2& x, 
       CK(halo_src(p, x, v));
     PROFB(p, cls, flops, bytes,
           conv3d_run(x, p->F(p->wcur), y, v, KD, Cin_w, Cout_w, dgrad, math, p->st, p->F(p->wg_ws),
-                     stats, 0, wmax));
+                     stats, 0, wmax, bst));
     return SPFF_OK;
   }
   if (!early) {
@@ -1140,15 +1145,34 @@ int bwd_block(spff_plan* p, Blk& b, const float* dout, const Dst2* dx, const Src
                 f16_slot(p, b, F16_A1), f16_slot(p, b, F16_DY2)));
   const int math = p->cfg.math;
   CK(conv_image(p, b, 2, v));
+  // the IN-backward sums of conv1 (sum dr, sum dr xhat over da1, y1) in the epilogue of the
+  // input-gradient conv that writes da1 (BStat), instead of a RED_BWD_IN pass over both
+  const bool bfuse = p->bst_fuse && !p->co.on() && !p->hsh &&
+                     conv3d_fuses_bwd_stats(v, KD, C, C, math);
+  BStat bs;
+  if (bfuse) {
+    bs.y = p->F(b.y1);
+    bs.al = p->F(b.al1);
+    bs.de = p->F(b.de1);
+    bs.mean = p->F(b.mean1);
+    bs.rstd = p->F(b.rstd1);
+    bs.out = p->F(p->cst);
+    bs.ld = C;
+  }
   CK(conv_halo(p, 1, 2.0 * V * C * C * T, cbytes(V, C, C, T), src1(dy2, C), dst1(da1, C), v, C, C,
-               true, nullptr, w_slot(p, b, F16_W2)));
+               true, nullptr, w_slot(p, b, F16_W2), bfuse ? &bs : nullptr));
   {
     RedArgs a{};
     a.y = p->F(b.y1); a.g = da1; a.mean = p->F(b.mean1); a.rstd = p->F(b.rstd1);
     a.al = p->F(b.al1); a.de = p->F(b.de1);
-    PROFB(p, 4, 0.0, 8.0 * (double)nvox(v) * C,
-        slab_reduce(RED_BWD_IN, a, v, C, p->F(p->red_out), p->F(p->red_ws), p->st));
-    CK(in_bwd(p, v, C, b.g1, b.b1));
+    if (bfuse) {
+      HIPCK(conv3d_in_bwd_stats_fin(p->F(p->cst), v, KD, C, C, math, p->DP(b.g1), p->DP(b.b1),
+                                    p->F(p->kk1), p->F(p->kk2), p->st));
+    } else {
+      PROFB(p, 4, 0.0, 8.0 * (double)nvox(v) * C,
+            slab_reduce(RED_BWD_IN, a, v, C, p->F(p->red_out), p->F(p->red_ws), p->st));
+      CK(in_bwd(p, v, C, b.g1, b.b1));
+    }
     PROFB(p, 6, 0.0, 12.0 * (double)nvox(v) * C,
           in_bwd_apply(p->F(b.y1), da1, da1, p->F(b.mean1), p->F(b.rstd1), p->F(b.al1),
                        p->F(b.de1), p->P(b.g1), nullptr, nullptr, p->F(p->kk1), p->F(p->kk2), v,
@@ -1468,6 +1492,7 @@ int spff_debug_set(spff_plan* p, int key, int value) {
   if (key == 0) p->dbg_stop = value;
   if (key == 1) p->keep_out = value != 0;  // store the GEMM-applied block outputs too
   if (key == 2) p->pool_fold = value != 0;  // 0: k_maxpool_bwd_add pass instead of PoolAdd
+  if (key == 3) p->bst_fuse = value != 0;   // 0: conv1's IN-backward sums by a slab_reduce pass
   return SPFF_OK;
 }
 

@@ -147,10 +147,29 @@ hipError_t conv3d_pack_many(const PackJobs& J, int math, hipStream_t s);
 // depth tiles; 0 = all.  1 and 2 together write exactly what 0 writes.  3 / 4: the same
 // for the H tiles of a height-sharded conv (conv3d_splits_height: interior tiles read no
 // boundary row; 3 and 4 together write what 0 writes).
+// bst (optional, input gradient only, when conv3d_fuses_bwd_stats): the output dx is the
+// gradient entering an InstanceNorm + LeakyReLU whose input was bst.y; the epilogue also
+// writes per-(tile, channel) partials of sum dr and sum dr xhat (dr = dx slope(y al + de),
+// xhat = (y - mean) rstd -- RED_BWD_IN's sums) that conv3d_in_bwd_stats_fin turns into the
+// IN backward's k1, k2, dgamma, dbeta, replacing that slab_reduce pass
+struct BStat {
+  const float* y = nullptr;     // [V][ld], the layout of the conv output
+  const float* al = nullptr;    // [B][ld]
+  const float* de = nullptr;
+  const float* mean = nullptr;
+  const float* rstd = nullptr;
+  float* out = nullptr;         // >= conv3d_stats_bytes(vol, KD, Cin_w, Cout_w)
+  int ld = 0;
+  float neg = 0.01f;
+};
 hipError_t conv3d_run(const Src2& x, const void* wpack, const Dst2& y, Vol vol, int KD,
                       int Cin_w, int Cout_w, bool dgrad, int math, hipStream_t s,
                       float* ws = nullptr, float* stats = nullptr, int dpart = 0,
-                      const unsigned* wmax = nullptr);
+                      const unsigned* wmax = nullptr, const BStat* bst = nullptr);
+bool conv3d_fuses_bwd_stats(Vol vol, int KD, int Cin_w, int Cout_w, int math);
+hipError_t conv3d_in_bwd_stats_fin(const float* part, Vol vol, int KD, int Cin_w, int Cout_w,
+                                   int math, float* dgamma, float* dbeta, float* k1, float* k2,
+                                   hipStream_t s);
 bool conv3d_splits_depth(Vol vol, int KD, int Cin_w, int Cout_w, bool dgrad, int math);
 bool conv3d_splits_height(Vol vol, int KD, int Cin_w, int Cout_w, bool dgrad, int math);
 bool conv3d_fuses_stats(Vol vol, int KD, int Cin, int Cout, int math);

@@ -289,7 +289,7 @@ def test_upconv_gemm_arithmetics(cin, cout, outliers):
         for (bb, d, h, ww) in ((0, 1, 3, 5), (1, 2, 20, 33)):
             x[bb, d, h, ww, :4] = 1e10
             dy[bb, d, 2 * h, 2 * ww, :4] = -3e10
-            far_x[bb, d, max(h - 8, 0):h + 9, :, :] = False  # rows sharing a GEMM tile
+            far_x[bb, d, max(h - 8, 0):h + 9, :] = False  # rows sharing a GEMM tile
     y64 = _upconv_ref(x, w, b)
     ya = _upconv_ref(x.abs(), w.abs(), b.abs())
     # dgrad: dx[v][ci] = sum_{ij, co} dy[high(v, ij)][co] W[ci][co][ij]

@@ -476,3 +476,45 @@ def test_pool_fold_bitwise(mth):
     assert grads[0].keys() == grads[1].keys() and len(grads[0]) > 20
     for k in grads[0]:
         assert torch.equal(grads[0][k], grads[1][k]), k
+
+
+@pytest.mark.parametrize("mth", ["f16x3", "bf16x6"])
+@pytest.mark.parametrize("shape", [(2, 8, 32, 48), (1, 5, 24, 40)])
+def test_fused_in_backward_sums(mth, shape):
+    """conv1's InstanceNorm-backward sums (sum dr, sum dr xhat) formed in the epilogue of the
+    input-gradient conv that writes da1 (conv3d_x.hip BStat) against the RED_BWD_IN
+    slab_reduce pass they replace (debug key 3 = 0).  Same terms, another summation order
+    (per tile then fp64 over tiles, vs per (b, c, d) slab then fp64 over d): every parameter
+    gradient within 1e-5 of its tensor's max; the forward is untouched (logits bitwise).
+    The ragged case (D = 5, H = 24: partial tiles) checks the epilogue's row masking."""
+    from innovative3D.synthetic import synthetic_batch
+    from innovative3D.weightgen import synth_state
+    K = 13
+    B, D, H, W = shape
+    core = M.build_spct_energyfilm_fourier(num_classes=K, base=16, in_channels=5)
+    for b in core._blocks():
+        b.fgate._ensure_mask(D, "cpu")
+    st = synth_state([(k, tuple(v.shape)) for k, v in core.state_dict().items()], seed=9)
+    core.load_state_dict({k: torch.from_numpy(v) for k, v in st.items()})
+    core = core.to(DEV)
+    core.math = mth
+    x, y = synthetic_batch(B, 5, D, H, W, num_classes=K, ignore_frac=0.02, seed=10)
+    x, y = x.to(DEV), y.to(DEV)
+    grads, logits = [], []
+    for fused in (1, 0):
+        for p in core.parameters():
+            p.grad = None
+        lg = core(x)
+        core._plan.debug_set(3, fused)
+        loss, _conf = Hh.ce_dice_with_confusion(lg, y, K, 255)
+        loss.backward()
+        torch.cuda.synchronize()
+        logits.append(lg.detach().clone())
+        grads.append({k: p.grad.detach().clone() for k, p in core.named_parameters()
+                      if p.grad is not None})
+    core._plan.debug_set(3, 1)
+    assert torch.equal(logits[0], logits[1])
+    worst = max(float((grads[0][k] - grads[1][k]).abs().max() /
+                      grads[1][k].abs().max().clamp_min(1e-30)) for k in grads[1])
+    print(f"fused IN-backward sums {mth} {shape}: worst gradient difference {worst:.2e} of max|g|")
+    assert worst <= 1e-5, worst
