@@ -92,44 +92,56 @@ __global__ __launch_bounds__(LOSS_T) void k_loss(const float* __restrict__ x,
   unsigned int bad = 0;
   const int64_t ngroups = (V + 63) / 64;
   const int64_t gstride = (int64_t)gridDim.x * LOSS_WAVES;
-  // (SPFF_LOSS_PF) the next group's rows (K <= 16: at most 4 quads per lane) and labels are
-  // loaded into registers while this group is worked on; the LDS orderings of this path
-  // wait for LDS only, so those loads stay in flight across them
+  // (SPFF_LOSS_PF) the rows (K <= 16: at most 4 quads per lane) and labels of the wave's
+  // next TWO groups are in flight in registers while this group is worked on (two register
+  // sets, used alternately: a wave spends ~2 us of HBM latency per group and only a few
+  // hundred cycles of work on it, so one group in flight per wave left the pass latency-
+  // bound); the LDS orderings of this path wait for LDS only, so the loads stay in flight
   const bool pf = SPFF_LOSS_PF && K <= 16 && (((uintptr_t)x & 15) == 0);
-  float4 q0 = {}, q1 = {}, q2 = {}, q3 = {};
-  int64_t ypf = ignore, pgrp = -1;
-  auto prefetch = [&](int64_t g) {
-    pgrp = -1;
-    if (g >= ngroups) return;
+  struct PF {
+    float4 q0, q1, q2, q3;
+    int64_t y, g;
+  };
+  auto prefetch = [&](int64_t g) __attribute__((always_inline)) {
+    PF f;
+    f.q0 = f.q1 = f.q2 = f.q3 = make_float4(0.f, 0.f, 0.f, 0.f);
+    f.y = ignore;
+    f.g = -1;
+    if (!pf || g >= ngroups) return f;
     const int64_t w0 = g * 64;
     const int nv2 = (int)(V - w0 < 64 ? V - w0 : 64);
-    if ((nv2 * K) & 3) return;  // (a ragged last run takes the plain copy)
+    if ((nv2 * K) & 3) return f;  // (a ragged last run takes the plain copy)
     const int n4 = (nv2 * K) >> 2;
     const float4* s4 = reinterpret_cast<const float4*>(x + w0 * K);
-    q0 = s4[min(lane, n4 - 1)];
-    q1 = s4[min(lane + 64, n4 - 1)];
-    q2 = s4[min(lane + 128, n4 - 1)];
-    q3 = s4[min(lane + 192, n4 - 1)];
-    ypf = lane < nv2 ? lab[w0 + lane] : (int64_t)ignore;
-    pgrp = g;
+    f.q0 = s4[min(lane, n4 - 1)];
+    f.q1 = s4[min(lane + 64, n4 - 1)];
+    f.q2 = s4[min(lane + 128, n4 - 1)];
+    f.q3 = s4[min(lane + 192, n4 - 1)];
+    f.y = lane < nv2 ? lab[w0 + lane] : (int64_t)ignore;
+    f.g = g;
+    return f;
   };
   auto lds_only_sync = [&]() {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
   };
-  for (int64_t grp = (int64_t)blockIdx.x * LOSS_WAVES + wv; grp < ngroups; grp += gstride) {
+  // one group: its rows into the wave's LDS slice (from the register set f when it holds
+  // them), then set f refilled with group g2, the loss / dlogits / confusion of the rows,
+  // and the dlogits run stored
+  auto group = [&](int64_t grp, PF f, int64_t g2) __attribute__((always_inline)) {
+    PF nx;
     const int64_t v0 = grp * 64;
     const int nv = (int)(V - v0 < 64 ? V - v0 : 64);
     const int nf = nv * K;
     int64_t y;
-    if (pf && pgrp == grp) {
+    if (pf && f.g == grp) {
       const int n4 = nf >> 2;
       float4* d4 = reinterpret_cast<float4*>(sx);
-      if (lane < n4) d4[lane] = q0;
-      if (lane + 64 < n4) d4[lane + 64] = q1;
-      if (lane + 128 < n4) d4[lane + 128] = q2;
-      if (lane + 192 < n4) d4[lane + 192] = q3;
-      y = ypf;
+      if (lane < n4) d4[lane] = f.q0;
+      if (lane + 64 < n4) d4[lane + 64] = f.q1;
+      if (lane + 128 < n4) d4[lane + 128] = f.q2;
+      if (lane + 192 < n4) d4[lane + 192] = f.q3;
+      y = f.y;
     } else {
       // (SPFF_LOSS_HOIST) the label first: its load then overlaps the row copy's
       y = (SPFF_LOSS_HOIST && lane < nv) ? lab[v0 + lane] : (int64_t)ignore;
@@ -137,9 +149,10 @@ __global__ __launch_bounds__(LOSS_T) void k_loss(const float* __restrict__ x,
     }
     if (pf) {
       lds_only_sync();
-      prefetch(grp + gstride);
+      nx = prefetch(g2);
     } else {
       wave_lds_sync();
+      nx = prefetch(ngroups);  // (no prefetch)
     }
     cell = -1;
     if (lane < nv) {
@@ -201,6 +214,14 @@ __global__ __launch_bounds__(LOSS_T) void k_loss(const float* __restrict__ x,
     if (pf) lds_only_sync(); else wave_lds_sync();
     if (WITH_CE) wave_copy_rows(dx + v0 * K, sx, nf, lane);
     if (pf) lds_only_sync(); else wave_lds_sync();  // the next group overwrites the slice
+    return nx;
+  };
+  const int64_t g0 = (int64_t)blockIdx.x * LOSS_WAVES + wv;
+  PF fa = prefetch(g0);
+  PF fb = prefetch(g0 + gstride);
+  for (int64_t grp = g0; grp < ngroups; grp += 2 * gstride) {
+    fa = group(grp, fa, grp + 2 * gstride);
+    if (grp + gstride < ngroups) fb = group(grp + gstride, fb, grp + 3 * gstride);
   }
   if (WITH_CE) {
     red[threadIdx.x] = ce;
@@ -292,7 +313,7 @@ hipError_t count_valid(const int64_t* labels, int64_t V, int ignore, int64_t* co
   return hipGetLastError();
 }
 
-// ws: [LOSS_GRID doubles][int64 count][uint64 nbad]
+// ws: [LOSS_GRID doubles][int64 count]
 hipError_t loss_fwd(const float* logits, const int64_t* labels, int64_t V, int K, int ignore,
                     double smooth, const int64_t* count_override, float* out4, float* dlogits,
                     int64_t* conf, float* ws, hipStream_t s, const float* class_w,
@@ -300,7 +321,6 @@ hipError_t loss_fwd(const float* logits, const int64_t* labels, int64_t V, int K
   if (K > KMAX || K < 1) return hipErrorInvalidValue;
   double* part = reinterpret_cast<double*>(ws);
   int64_t* cnt = reinterpret_cast<int64_t*>(part + LOSS_GRID);
-  unsigned long long* nbad = reinterpret_cast<unsigned long long*>(cnt + 1);
   hipError_t e;
   const int64_t* cptr = count_override;
   if (!cptr) {
@@ -308,11 +328,10 @@ hipError_t loss_fwd(const float* logits, const int64_t* labels, int64_t V, int K
     cptr = cnt;
   }
   if ((e = hipMemsetAsync(conf, 0, sizeof(int64_t) * K * (K + 1), s)) != hipSuccess) return e;
-  if ((e = hipMemsetAsync(nbad, 0, sizeof(unsigned long long), s)) != hipSuccess) return e;
   if ((e = loss_lds_attr<true>(K)) != hipSuccess) return e;
   hipLaunchKernelGGL(k_loss<true>, dim3(LOSS_GRID), dim3(LOSS_T), loss_lds(K), s, logits, labels,
                      V, K, ignore, cptr, dlogits, reinterpret_cast<unsigned long long*>(conf),
-                     part, nbad, class_w, clamp1);
+                     part, nullptr, class_w, clamp1);  // (bad labels: conf column K)
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(k_loss_final, dim3(1), dim3(LOSS_T), 0, s, part, LOSS_GRID, cptr,
                      reinterpret_cast<unsigned long long*>(conf), K, smooth, out4, clamp1);
