@@ -1055,7 +1055,7 @@ def to_channels_last(t: torch.Tensor) -> torch.Tensor:
     return t.permute(0, 2, 3, 4, 1).contiguous()
 
 
-CONV_PROF_CLASSES = ("conv_fwd", "conv_dgrad", "conv_wgrad")
+CONV_PROF_CLASSES = ("conv_fwd", "conv_dgrad", "conv_wgrad", "loss_pass", "k_loss")
 
 
 def conv_prof_enable(on: bool = True) -> None:
