@@ -705,6 +705,9 @@ def main():
                     help="0 (default) = time the CPU oracle on the whole batch; > 0 = sample 0, "
                          "depths [0, cpu-depth) only")
     ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--graph", action="store_true",
+                    help="time the step as a captured HIP graph replayed K times (patch / "
+                         "volume512 / registry at N = 1; the eager time is reported beside it)")
     ap.add_argument("--pmc", default=str(ROOT / "profiles" / "r05_pmc_conv.json"),
                     help="per-launch HBM traffic summary from rocprofv3 --pmc "
                          "(scripts/pmc_traffic.py); used only when its workload key matches")
@@ -745,6 +748,8 @@ def main():
             dist.init_process_group("nccl", device_id=device,
                                     timeout=datetime.timedelta(seconds=args.coll_timeout))
 
+    if args.graph and (world > 1 or args.workload in ("unet3d", "swin")):
+        raise SystemExit("bench.py --graph: one GPU, SPFF workloads")
     if args.workload == "unet3d":
         return bench_unet3d(args, world, rank, device)
     if args.workload == "swin":
@@ -821,11 +826,43 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    elapsed_local = elapsed
     prof = plan.prof_collect()
     plan.prof_enable(False)
     coll = plan.coll_collect() if plan.coll_timing else {}
     plan.coll_timing = False
+    graph_rec = None
+    if args.graph:
+        # the step captured once into a HIP graph (torch.cuda.CUDAGraph over the engine's
+        # launches: no host syncs, static shapes, the plan's workspace fixed) and replayed:
+        # the same kernels with their launch overhead and inter-kernel gaps cut.  The
+        # per-class timing above is the eager run's (its HIP events are not captured)
+        eager = elapsed
+        side = torch.cuda.Stream(device)
+        side.wait_stream(torch.cuda.current_stream(device))
+        with torch.cuda.stream(side):
+            step()
+        torch.cuda.current_stream(device).wait_stream(side)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            gloss = step()
+        for _ in range(2):
+            g.replay()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            g.replay()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        loss = gloss
+        graph_rec = {"eager_ms_per_step": eager / args.steps * 1e3,
+                     "graph_ms_per_step": elapsed / args.steps * 1e3}
+    elapsed_local = elapsed
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -949,6 +986,8 @@ def main():
         "cpu_baseline": None,
         "build": build_record(),
     }
+    if graph_rec:
+        out["hip_graph"] = graph_rec
     if world > 1:
         out["ranks"] = rank_report(elapsed_local, args.steps, device)
         bk = getattr(runner, "bucketer", None)
