@@ -705,9 +705,10 @@ def main():
                     help="0 (default) = time the CPU oracle on the whole batch; > 0 = sample 0, "
                          "depths [0, cpu-depth) only")
     ap.add_argument("--cpu-steps", type=int, default=3)
-    ap.add_argument("--graph", action="store_true",
-                    help="time the step as a captured HIP graph replayed K times (patch / "
-                         "volume512 / registry at N = 1; the eager time is reported beside it)")
+    ap.add_argument("--graph", choices=("auto", "on", "off"), default="auto",
+                    help="time the step as a captured HIP graph replayed K times (one GPU, SPFF "
+                         "workloads; the eager time of the same steps is reported beside it); "
+                         "auto = on for the headline patch128 at N = 1")
     ap.add_argument("--pmc", default=str(ROOT / "profiles" / "r05_pmc_conv.json"),
                     help="per-launch HBM traffic summary from rocprofv3 --pmc "
                          "(scripts/pmc_traffic.py); used only when its workload key matches")
@@ -748,8 +749,10 @@ def main():
             dist.init_process_group("nccl", device_id=device,
                                     timeout=datetime.timedelta(seconds=args.coll_timeout))
 
-    if args.graph and (world > 1 or args.workload in ("unet3d", "swin")):
-        raise SystemExit("bench.py --graph: one GPU, SPFF workloads")
+    if args.graph == "on" and (world > 1 or args.workload in ("unet3d", "swin")):
+        raise SystemExit("bench.py --graph on: one GPU, SPFF workloads")
+    use_graph = args.graph == "on" or (args.graph == "auto" and world == 1 and
+                                       args.workload == "patch128")
     if args.workload == "unet3d":
         return bench_unet3d(args, world, rank, device)
     if args.workload == "swin":
@@ -810,32 +813,29 @@ def main():
         step()
     torch.cuda.synchronize()
     plan = core._plan
-    plan.prof_enable(True)
-    plan.prof_collect()
-    # the shard group's collective callbacks (halo exchanges, statistics all-reduces), timed
-    # with HIP events on the stream each one's work runs on
-    plan.coll_timing = world > 1 and (sharded or registry)
-    plan.coll_collect()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        loss = step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    prof = plan.prof_collect()
-    plan.prof_enable(False)
-    coll = plan.coll_collect() if plan.coll_timing else {}
-    plan.coll_timing = False
+
+    def timed(fn, n):
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        r = None
+        for _ in range(n):
+            r = fn()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        return time.perf_counter() - t0, r
+
+    # 1. the timed region: K steps with nothing but the step's own launches in it (the
+    #    per-class HIP events of 2. add a queue packet before and after every profiled launch,
+    #    ~1 ms per step of gaps: measured separately, never inside the timed region)
+    elapsed, loss = timed(step, args.steps)
     graph_rec = None
-    if args.graph:
+    if use_graph:
         # the step captured once into a HIP graph (torch.cuda.CUDAGraph over the engine's
         # launches: no host syncs, static shapes, the plan's workspace fixed) and replayed:
-        # the same kernels with their launch overhead and inter-kernel gaps cut.  The
-        # per-class timing above is the eager run's (its HIP events are not captured)
+        # the same kernels, without the host round trips between them
         eager = elapsed
         side = torch.cuda.Stream(device)
         side.wait_stream(torch.cuda.current_stream(device))
@@ -848,20 +848,23 @@ def main():
             gloss = step()
         for _ in range(2):
             g.replay()
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            g.replay()
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        elapsed = time.perf_counter() - t0
+        elapsed, _ = timed(g.replay, args.steps)
         loss = gloss
         graph_rec = {"eager_ms_per_step": eager / args.steps * 1e3,
-                     "graph_ms_per_step": elapsed / args.steps * 1e3}
+                     "graph_ms_per_step": elapsed / args.steps * 1e3,
+                     "note": "value = the graph replays; the eager loop of the same steps "
+                             "beside it (both without profiling events)"}
+    # 2. per-class kernel timing: a separate pass of K eager steps with HIP events around the
+    #    engine's launches on its stream (and, sharded, around the collective callbacks)
+    plan.prof_enable(True)
+    plan.prof_collect()
+    plan.coll_timing = world > 1 and (sharded or registry)
+    plan.coll_collect()
+    prof_elapsed, _ = timed(step, args.steps)
+    prof = plan.prof_collect()
+    plan.prof_enable(False)
+    coll = plan.coll_collect() if plan.coll_timing else {}
+    plan.coll_timing = False
     elapsed_local = elapsed
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
     if world > 1:
@@ -988,6 +991,7 @@ def main():
     }
     if graph_rec:
         out["hip_graph"] = graph_rec
+    out["profiled_pass_ms_per_step"] = prof_elapsed / args.steps * 1e3
     if world > 1:
         out["ranks"] = rank_report(elapsed_local, args.steps, device)
         bk = getattr(runner, "bucketer", None)
