@@ -35,11 +35,6 @@ static int num_cus() {
 #ifndef SPFF_GEMM_PERSIST
 #define SPFF_GEMM_PERSIST 1
 #endif
-// workgroups of a C = X^T Y launch (split-M slabs): 3 per CU -- k_atb_x with two voxel
-// chunks in flight per thread holds ~160 VGPRs, so a 4th would wait for a second round
-#ifndef SPFF_ATB_WGS
-#define SPFF_ATB_WGS 768
-#endif
 // SPFF_GEMM_F16=0 (A/B diagnostics): the GEMMs take the bf16x6 split under SPFF_MATH_F16X3
 #ifndef SPFF_GEMM_F16
 #define SPFF_GEMM_F16 1
@@ -933,42 +928,35 @@ __global__ __launch_bounds__(256, 2) void k_atb_x(XL X, YL Y, float* __restrict_
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4g{0.f, 0.f, 0.f, 0.f};
   float4 cs = make_float4(0.f, 0.f, 0.f, 0.f);  // columns n0 + 4 (tid & 15) .. + 3
   const int sq = tid & 15, sr = tid >> 4;      // staging: col quad, row (+ 16 j)
-  // the voxel chunks' X / Y quads in flight in registers: TWO chunks ahead (two sets used
-  // alternately) -- a split walks 4 .. 32 chunks of 64 rows back to back, and with one chunk
-  // in flight each chunk waited out most of a memory latency behind its few MFMAs
-  struct XY {
-    float4 x[4], y[4];
-    unsigned xm, ym;  // validity bits (zeroed at the stash)
-  };
+  float4 xr[4], yr[4];
+  unsigned xm = 0, ym = 0;  // validity bits of xr / yr (zeroed at the stash)
   const int64_t mb = (int64_t)split * rps, me = min(M, mb + rps);
-  auto fetch = [&](int64_t m0) __attribute__((always_inline)) {
-    XY f;
-    f.xm = f.ym = 0;
+  auto fetch = [&](int64_t m0) {
+    xm = ym = 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int64_t m = m0 + sr + 16 * j;
       const bool ok = m < me;
       const int64_t mm = ok ? m : mb;  // (a row of this split: prep in range)
       bool ox, oy;
-      f.x[j] = ld4(X, X.prep(mm), k10 + 4 * sq, ox);
-      f.y[j] = ld4(Y, Y.prep(mm), n0 + 4 * sq, oy);
-      f.xm |= (ok && ox) ? 1u << j : 0u;
-      f.ym |= (ok && oy) ? 1u << j : 0u;
+      xr[j] = ld4(X, X.prep(mm), k10 + 4 * sq, ox);
+      yr[j] = ld4(Y, Y.prep(mm), n0 + 4 * sq, oy);
+      xm |= (ok && ox) ? 1u << j : 0u;
+      ym |= (ok && oy) ? 1u << j : 0u;
     }
-    return f;
   };
-  auto stash = [&](const XY& f, bool neg) __attribute__((always_inline)) {
+  auto stash = [&](bool neg) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int m = sr + 16 * j;
       const int off = m * 64 + 16 * ((sq >> 2) ^ gx_bsw<64>(m)) + 4 * (sq & 3);
       uint2 o[NP];
-      float4 x = zero_unless(f.x[j], (f.xm >> j) & 1u);
+      float4 x = zero_unless(xr[j], (xm >> j) & 1u);
       if constexpr (HF) x = ldexp4(x, ex);
       gsplit<NS>(x, o);
 #pragma unroll
       for (int p = 0; p < NP; ++p) *reinterpret_cast<uint2*>(Xs + p * PL + off) = o[p];
-      float4 y = zero_unless(f.y[j], (f.ym >> j) & 1u);
+      float4 y = zero_unless(yr[j], (ym >> j) & 1u);
       if (do_cs) { cs.x += y.x; cs.y += y.y; cs.z += y.z; cs.w += y.w; }
       if (neg) y = make_float4(-y.x, -y.y, -y.z, -y.w);
       if constexpr (HF) y = ldexp4(y, ey);
@@ -988,9 +976,9 @@ __global__ __launch_bounds__(256, 2) void k_atb_x(XL X, YL Y, float* __restrict_
     const i16x8g v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
     return __builtin_bit_cast(bf16x8g, v);
   };
+  if (mb < me) fetch(mb);
   int kc = 0;
-  // chunk kc from set cur, whose registers are then refilled with chunk nxt
-  auto run_chunk = [&](XY cur, int64_t nxt) __attribute__((always_inline)) {
+  for (int64_t m0 = mb; m0 < me; m0 += T_BM, ++kc) {
     if (kc) {
 #pragma unroll
       for (int i = 0; i < 2; ++i)
@@ -1002,17 +990,17 @@ __global__ __launch_bounds__(256, 2) void k_atb_x(XL X, YL Y, float* __restrict_
       float mx = 0.f, my = 0.f;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        mx = fmaxf(mx, (cur.xm >> j) & 1u ? amax4(cur.x[j]) : 0.f);
-        my = fmaxf(my, (cur.ym >> j) & 1u ? amax4(cur.y[j]) : 0.f);
+        mx = fmaxf(mx, (xm >> j) & 1u ? amax4(xr[j]) : 0.f);
+        my = fmaxf(my, (ym >> j) & 1u ? amax4(yr[j]) : 0.f);
       }
       gemm_chunk_scale<4, 4>(mx, my, gmx, kc == 0, ecur, ex, ey,
                              reinterpret_cast<f32x4g(&)[4]>(acc));
     } else {
       if (kc) __syncthreads();
     }
-    stash(cur, kc & 1);
+    stash(kc & 1);
     __syncthreads();
-    const XY f = fetch(nxt);  // (unconditional: past the split's rows every quad is masked)
+    fetch(m0 + T_BM);  // (unconditional: past the split's rows every quad is masked)
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       bf16x8g a[2][NP], b[2][NP];
@@ -1042,17 +1030,6 @@ __global__ __launch_bounds__(256, 2) void k_atb_x(XL X, YL Y, float* __restrict_
           }
           acc[i][j] = c;
         }
-    }
-    ++kc;
-    return f;
-  };
-  if (mb < me) {
-    XY cur = fetch(mb);
-    XY nxt = fetch(mb + T_BM);
-    for (int64_t m0 = mb; m0 < me; m0 += T_BM) {  // (one call site: the sets rotate)
-      const XY f = run_chunk(cur, m0 + 2 * T_BM);
-      cur = nxt;
-      nxt = f;
     }
   }
   const float sg = (kc > 0 && ((kc - 1) & 1)) ? -1.f : 1.f;
@@ -1363,7 +1340,7 @@ static hipError_t launch_atb(const XL& X, const YL& Y, int64_t M, int K1, int N,
   if (M >= (int64_t(1) << 31)) return hipErrorInvalidValue;
   const int k1pad = cdiv(K1, 64) * 64, npad = cdiv(N, 64) * 64;
   const int nout = (k1pad / 64) * (npad / 64);
-  int64_t nsplit = std::max<int64_t>(1, cdiv64(SPFF_ATB_WGS, nout));
+  int64_t nsplit = std::max<int64_t>(1, cdiv64(1024, nout));
   nsplit = std::min<int64_t>(nsplit, std::max<int64_t>(1, cdiv64(M, 4 * T_BM)));
   int64_t rps = cdiv64(cdiv64(M, nsplit), T_BM) * T_BM;
   nsplit = cdiv64(M, rps);
@@ -1390,7 +1367,7 @@ static hipError_t launch_atb(const XL& X, const YL& Y, int64_t M, int K1, int N,
 static size_t atb_ws_bytes(int64_t M, int K1, int N) {
   const int k1pad = cdiv(K1, 64) * 64, npad = cdiv(N, 64) * 64;
   const int nout = (k1pad / 64) * (npad / 64);
-  int64_t nsplit = std::max<int64_t>(1, cdiv64(SPFF_ATB_WGS, nout));
+  int64_t nsplit = std::max<int64_t>(1, cdiv64(1024, nout));
   nsplit = std::min<int64_t>(nsplit, std::max<int64_t>(1, cdiv64(M, 4 * T_BM)));
   int64_t rps = cdiv64(cdiv64(M, nsplit), T_BM) * T_BM;
   nsplit = cdiv64(M, rps);
