@@ -388,6 +388,7 @@ def conv_class_roofline(prof, steps, math, step_ms):
     kernel), timed live with HIP events on their stream by the library-wide conv profiler
     (spff_conv_prof_*), algorithmic fp32 flops 2 V Cin Cout 27 per launch; the weight
     gradient and each class's share of the step beside it."""
+    prof = {k: v for k, v in prof.items() if k.startswith("conv_")}
     ms = prof["conv_fwd"][0] + prof["conv_dgrad"][0]
     fl = prof["conv_fwd"][1] + prof["conv_dgrad"][1]
     nl = prof["conv_fwd"][2] + prof["conv_dgrad"][2]
