@@ -1252,9 +1252,25 @@ __global__ __launch_bounds__(256) void k_in_stats_fin(const float* __restrict__ 
   const int bc = blockIdx.x, b = bc / C, c = bc % C, tid = threadIdx.x;
   const float* cnt = stats + (int64_t)ntiles * npad * 2;
   double s = 0.0, n = 0.0;
-  for (int t = b * tpb + tid; t < (b + 1) * tpb; t += 256) {
-    s += stats[((int64_t)t * npad + c) * 2];
-    n += cnt[t];
+  const int tend = (b + 1) * tpb;
+  // (8 tiles' loads issued before any is added -- the same summation order as one at a
+  //  time, which waited out a load latency per tile)
+  for (int t0 = b * tpb + tid; t0 < tend; t0 += 256 * 8) {
+    float sv[8], nv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int t = t0 + 256 * u;
+      const bool ok = t < tend;
+      sv[u] = ok ? stats[((int64_t)t * npad + c) * 2] : 0.f;
+      nv[u] = ok ? cnt[t] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (t0 + 256 * u < tend) {
+        s += sv[u];
+        n += nv[u];
+      }
+    }
   }
   r0[tid] = s;
   r1[tid] = n;
@@ -1269,11 +1285,25 @@ __global__ __launch_bounds__(256) void k_in_stats_fin(const float* __restrict__ 
   const double N = r1[0], mu = r0[0] / N;
   __syncthreads();
   double q = 0.0;
-  for (int t = b * tpb + tid; t < (b + 1) * tpb; t += 256) {
-    const double nt = cnt[t];
-    if (nt <= 0.0) continue;
-    const double dl = stats[((int64_t)t * npad + c) * 2] / nt - mu;
-    q += stats[((int64_t)t * npad + c) * 2 + 1] + nt * dl * dl;
+  for (int t0 = b * tpb + tid; t0 < tend; t0 += 256 * 8) {
+    float sv[8], qv[8], nv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int t = t0 + 256 * u;
+      const bool ok = t < tend;
+      const float2 v = ok ? *reinterpret_cast<const float2*>(stats + ((int64_t)t * npad + c) * 2)
+                          : make_float2(0.f, 0.f);
+      sv[u] = v.x;
+      qv[u] = v.y;
+      nv[u] = ok ? cnt[t] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const double nt = nv[u];
+      if (t0 + 256 * u >= tend || nt <= 0.0) continue;
+      const double dl = sv[u] / nt - mu;
+      q += qv[u] + nt * dl * dl;
+    }
   }
   r0[tid] = q;
   __syncthreads();
@@ -1792,10 +1822,20 @@ __global__ __launch_bounds__(256) void k_in_bwd_stats_tiles(const float* __restr
   double tg = 0.0, tb = 0.0;
   for (int b = 0; b < B; ++b) {
     double s0 = 0.0, s1 = 0.0;
-    for (int t = b * tpb + tid; t < (b + 1) * tpb; t += 256) {
-      const float2 v = *reinterpret_cast<const float2*>(part + ((int64_t)t * npad + c) * 2);
-      s0 += v.x;
-      s1 += v.y;
+    const int tend = (b + 1) * tpb;
+    for (int t0 = b * tpb + tid; t0 < tend; t0 += 256 * 8) {
+      float2 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int t = t0 + 256 * u;
+        v[u] = t < tend ? *reinterpret_cast<const float2*>(part + ((int64_t)t * npad + c) * 2)
+                        : make_float2(0.f, 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        s0 += v[u].x;
+        s1 += v[u].y;
+      }
     }
     r0[tid] = s0;
     r1[tid] = s1;

@@ -1159,8 +1159,10 @@ int bwd_block(spff_plan* p, Blk& b, const float* dout, const Dst2* dx, const Src
     bs.out = p->F(p->cst);
     bs.ld = C;
   }
-  CK(conv_halo(p, 1, 2.0 * V * C * C * T, cbytes(V, C, C, T), src1(dy2, C), dst1(da1, C), v, C, C,
-               true, nullptr, w_slot(p, b, F16_W2), bfuse ? &bs : nullptr));
+  // (compulsory bytes: + y1, which the fused epilogue reads once)
+  CK(conv_halo(p, 1, 2.0 * V * C * C * T, cbytes(V, C, C, T) + (bfuse ? 4.0 * V * C : 0.0),
+               src1(dy2, C), dst1(da1, C), v, C, C, true, nullptr, w_slot(p, b, F16_W2),
+               bfuse ? &bs : nullptr));
   {
     RedArgs a{};
     a.y = p->F(b.y1); a.g = da1; a.mean = p->F(b.mean1); a.rstd = p->F(b.rstd1);
