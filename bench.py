@@ -706,10 +706,12 @@ def main():
                     help="0 (default) = time the CPU oracle on the whole batch; > 0 = sample 0, "
                          "depths [0, cpu-depth) only")
     ap.add_argument("--cpu-steps", type=int, default=3)
-    ap.add_argument("--graph", choices=("auto", "on", "off"), default="auto",
-                    help="time the step as a captured HIP graph replayed K times (one GPU, SPFF "
-                         "workloads; the eager time of the same steps is reported beside it); "
-                         "auto = on for the headline patch128 at N = 1")
+    ap.add_argument("--graph", choices=("auto", "on", "off"), default="off",
+                    help="diagnostic: also time the step as a captured HIP graph replayed K "
+                         "times (one GPU, SPFF workloads; value = the replays, the eager time "
+                         "beside it).  Off by default: a probe with new inputs copied into the "
+                         "captured buffers did not reproduce the eager step (DESIGN §5); "
+                         "auto = on for patch128 at N = 1")
     ap.add_argument("--pmc", default=str(ROOT / "profiles" / "r05_pmc_conv.json"),
                     help="per-launch HBM traffic summary from rocprofv3 --pmc "
                          "(scripts/pmc_traffic.py); used only when its workload key matches")
