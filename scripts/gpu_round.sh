@@ -38,8 +38,7 @@ for step in "$@"; do
     profu3d) (cd "$GRAFT_REPO_ROOT" && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profu3d -o run --output-format csv -- python3 bench.py --workload unet3d --steps 3 --warmup 1 --cpu-baseline skip > gpurun_out/profu3d.log 2>&1); rc=$? ;;
     graph) timeout -k 10 600 python bench.py --steps 10 --warmup 3 --cpu-baseline skip --graph on > gpurun_out/bench_graph.log 2>&1; rc=$? ;;
     dry2) (timeout -k 10 400 python bench.py --gpus 2 --one-gpu --size 64 --steps 2 --warmup 1 > gpurun_out/dry2_patch.log 2>&1 && timeout -k 10 400 python bench.py --gpus 2 --one-gpu --workload unet3d --steps 2 --warmup 1 > gpurun_out/dry2_unet3d.log 2>&1); rc=$? ;;
-    gprobe) (timeout -k 10 300 python -u scripts/graph_probe2.py f16x3 > gpurun_out/gprobe.log 2>&1; timeout -k 10 300 python -u scripts/graph_probe2.py f16x3 2 >> gpurun_out/gprobe.log 2>&1; timeout -k 10 300 python -u scripts/graph_probe2.py f32 2 >> gpurun_out/gprobe.log 2>&1); rc=$? ;;
-    gprobe3) timeout -k 10 300 python -u scripts/graph_probe3.py > gpurun_out/gprobe3.log 2>&1; rc=$? ;;
+    gprobe3) timeout -k 10 300 python -u scripts/graph_probe3.py f16x3 > gpurun_out/gprobe3.log 2>&1 && timeout -k 10 300 python -u scripts/graph_probe3.py f32 >> gpurun_out/gprobe3.log 2>&1; rc=$? ;;
     probe) timeout -k 10 600 python -u scripts/oracle_det_probe.py 4 > gpurun_out/oracle_det_probe.log 2>&1; rc=$? ;;
     *) echo "unknown step $step"; rc=2 ;;
   esac

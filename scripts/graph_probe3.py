@@ -6,6 +6,8 @@ import sys
 
 import torch
 
+MATH = sys.argv[1] if len(sys.argv) > 1 else "f16x3"
+
 ROOT = pathlib.Path(__file__).resolve().parents[1]
 sys.path[:0] = [str(ROOT), str(ROOT / "spff-unet-spcct_amd")]
 import innovative3D.models as M  # noqa: E402
@@ -20,7 +22,7 @@ for b in core._blocks():
 st = synth_state([(k, tuple(v.shape)) for k, v in core.state_dict().items()], seed=11)
 core.load_state_dict({k: torch.from_numpy(v) for k, v in st.items()})
 core = core.to("cuda")
-core.math = "f16x3"
+core.math = MATH
 runner = DataParallelSPFF(core, K, 255)
 x1, y1 = synthetic_batch(2, 5, D, 32, 48, num_classes=K, ignore_frac=0.02, seed=1)
 x2, y2 = synthetic_batch(2, 5, D, 32, 48, num_classes=K, ignore_frac=0.02, seed=2)
@@ -55,14 +57,48 @@ g = torch.cuda.CUDAGraph()
 with torch.cuda.graph(g):
     gl, gc = runner.step(x, y)
 glg = runner.last_logits
-print("captured", flush=True)
+print("captured", MATH, flush=True)
+plan = core._plan
+ws = plan._ws
+
+
+def ranges(a, b):
+    """coalesced differing 4-byte word ranges of two byte tensors"""
+    d = (a.view(torch.int32) != b.view(torch.int32)).nonzero().flatten().cpu().tolist()
+    out = []
+    for i in d:
+        if out and i <= out[-1][1] + 64:
+            out[-1][1] = i
+        else:
+            out.append([i, i])
+    return [(4 * lo, 4 * (hi - lo + 1)) for lo, hi in out]
+
+
+x.copy_(x1)
+y.copy_(y1)
+runner.step(x, y)
+torch.cuda.synchronize()
+ws_e = ws.clone()
+flat_e = core._flat.clone()
 for tag, (xx, yy) in (("x1", (x1, y1)), ("x1", (x1, y1)), ("x2", (x2, y2)), ("x1", (x1, y1))):
     x.copy_(xx)
     y.copy_(yy)
     g.replay()
     torch.cuda.synchronize()
     r = refs[tag]
+    if tag == "x1":
+        rg = ranges(ws, ws_e)
+        print(f"  ws diff vs eager x1: {len(rg)} ranges {rg[:12]} flat equal "
+              f"{torch.equal(core._flat, flat_e)}", flush=True)
     dl = float((glg - r[2]).abs().max())
     dg = max(float((p.grad - r[3][k]).abs().max()) for k, p in core.named_parameters())
     print(f"replay {tag}: loss {float(gl):.7f} (eager {r[0]:.7f}) |dlogit| {dl:.3e} conf "
           f"{torch.equal(gc, r[1])} max|dgrad| {dg:.3e}", flush=True)
+x.copy_(x1)
+y.copy_(y1)
+l, c = runner.step(x, y)
+torch.cuda.synchronize()
+print(f"eager after replays x1: loss {float(l):.7f} logits equal "
+      f"{torch.equal(runner.last_logits, refs['x1'][2])} ws ranges {ranges(ws, ws_e)[:12]}",
+      flush=True)
+print("ws bytes", ws.numel(), flush=True)

@@ -747,7 +747,7 @@ hipError_t conv3d_wgrad_x(const Src2& x, const float* dy, int lddy, float* dw, V
   if (hf) {  // operand maxima: the caller's precomputed slots, else computed here
     if (!SPFF_WX16) return hipErrorInvalidValue;
     if (!xmax || !ymax) {
-      hipError_t e = hipMemsetAsync(sl, 0, 2 * sizeof(unsigned), s);
+      hipError_t e = spff::zero_async(sl, 2 * sizeof(unsigned), s);
       if (e != hipSuccess) return e;
     }
     if (!xmax) {

@@ -1625,7 +1625,7 @@ hipError_t conv3d_pack(const float* w, void* wpack, Vol vol, int KD, int Cin_w, 
     unsigned* sl = f16_slots(wpack, KD, Cin_w, Cout_w);
     if (math == SPFF_MATH_F16X3) {
       if (!wmax) {  // max |w| into the image's slot 0 (else the caller's precomputed slot)
-        hipError_t e = hipMemsetAsync(sl, 0, sizeof(unsigned), s);
+        hipError_t e = spff::zero_async(sl, sizeof(unsigned), s);
         if (e != hipSuccess) return e;
         e = absmax_f32(w, (int64_t)Cout_w * Cin_w * d.T, sl, s);
         if (e != hipSuccess) return e;

@@ -597,9 +597,9 @@ int halo(spff_plan* p, const float* interior, const Vol& v, int C, hipStream_t s
   if (!st) st = p->st;
   const int64_t sl = (int64_t)v.H * v.W * C;
   float* in = const_cast<float*>(interior);
-  if (p->co.rank == 0) HIPCK(hipMemsetAsync(in - sl, 0, sl * sizeof(float), st));
+  if (p->co.rank == 0) HIPCK(spff::zero_async(in - sl, sl * sizeof(float), st));
   if (p->co.rank == p->co.world - 1)
-    HIPCK(hipMemsetAsync(in + v.D * sl, 0, sl * sizeof(float), st));
+    HIPCK(spff::zero_async(in + v.D * sl, sl * sizeof(float), st));
   if (p->co.do_halo(in, sl, v.D, st) != 0) return fail(SPFF_ECOLL, "halo exchange failed");
   return SPFF_OK;
 }
@@ -674,7 +674,7 @@ int conv_wgrad(spff_plan* p, double flops, double bytes, const Src2& x, const fl
     // sharded plans: the operand maxima of this launch (x with the halo slices / boundary
     // rows it reads, dy), timed as class 7 like the unsharded plans' precomputed ones
     unsigned* sl = reinterpret_cast<unsigned*>(p->ws + p->fsl) + F16_SHARD_SLOTS;
-    HIPCK(hipMemsetAsync(sl, 0, 2 * sizeof(unsigned), p->st));
+    HIPCK(spff::zero_async(sl, 2 * sizeof(unsigned), p->st));
     PROFB(p, 7, 0.0, 4.0 * (double)nvox(v) * Cin, absmax_src(xr, v, Cin, true, sl, p->st));
     PROFB(p, 7, 0.0, 4.0 * (double)nvox(v) * Cout,
           absmax_src(src1(dy, Cout), v, Cout, false, sl + 1, p->st));
@@ -860,7 +860,7 @@ int f16_param_slots(spff_plan* p) {
     PackJobs kj;
     double bytes = 0.0;
     if (math == SPFF_MATH_F16X3)
-      HIPCK(hipMemsetAsync(p->ws + p->fsl, 0, 7 * 8 * sizeof(unsigned), p->st));
+      HIPCK(spff::zero_async(p->ws + p->fsl, 7 * 8 * sizeof(unsigned), p->st));
     for (int i = 0; i < 7; ++i) {
       Blk& b = p->blk[i];
       const Vol& v = p->vol[b.lvl];
@@ -888,7 +888,7 @@ int f16_param_slots(spff_plan* p) {
     return SPFF_OK;
   }
   if (!f16_slot(p, p->blk[0], 0)) return SPFF_OK;
-  HIPCK(hipMemsetAsync(p->ws + p->fsl, 0, 7 * 8 * sizeof(unsigned), p->st));
+  HIPCK(spff::zero_async(p->ws + p->fsl, 7 * 8 * sizeof(unsigned), p->st));
   for (int i = 0; i < 7; ++i) {
     const Blk& b = p->blk[i];
     const Vol& v = p->vol[b.lvl];
@@ -1050,9 +1050,9 @@ int hsh_gate_grads(spff_plan* p, const Blk& b, GateGrads& gg) {
   mv(gg.fb2, b.fb2, false); mv(gg.mask, b.mask, false); mv(gg.mag, b.mag, false);
   mv(gg.sw0, b.sw0, true); mv(gg.sb0, b.sb0, true); mv(gg.sw2, b.sw2, true);
   mv(gg.sb2, b.sb2, true);
-  if (span > 0) HIPCK(hipMemsetAsync(p->DP(g0), 0, span * sizeof(float), p->st));
+  if (span > 0) HIPCK(spff::zero_async(p->DP(g0), span * sizeof(float), p->st));
   if (b.se1 > b.se0)
-    HIPCK(hipMemsetAsync(p->DP(b.se0), 0, (b.se1 - b.se0) * sizeof(float), p->st));
+    HIPCK(spff::zero_async(p->DP(b.se0), (b.se1 - b.se0) * sizeof(float), p->st));
   return SPFF_OK;
 }
 

@@ -310,7 +310,7 @@ size_t loss_ws_bytes(int64_t V, int K) {
 
 hipError_t count_valid(const int64_t* labels, int64_t V, int ignore, int64_t* count,
                        hipStream_t s) {
-  hipError_t e = hipMemsetAsync(count, 0, sizeof(int64_t), s);
+  hipError_t e = spff::zero_async(count, sizeof(int64_t), s);
   if (e != hipSuccess) return e;
   // 256 workgroups: each ends in one 64-bit atomic on the same counter, and 2048 of them
   // queued on that one address took most of the kernel's ~30 us
@@ -336,7 +336,7 @@ hipError_t loss_fwd(const float* logits, const int64_t* labels, int64_t V, int K
   // (library-wide timing, spff_conv_prof_*: class 3 = the pass as launched here -- confusion
   // zeroing, k_loss, finaliser; class 4 = k_loss alone)
   CProf whole(3, 0.0, s);
-  if ((e = hipMemsetAsync(conf, 0, sizeof(int64_t) * K * (K + 1), s)) != hipSuccess) return e;
+  if ((e = spff::zero_async(conf, sizeof(int64_t) * K * (K + 1), s)) != hipSuccess) return e;
   if ((e = loss_lds_attr<true>(K)) != hipSuccess) return e;
   CProf kern(4, 0.0, s);
   hipLaunchKernelGGL(k_loss<true>, dim3(LOSS_GRID), dim3(LOSS_T), loss_lds(K), s, logits, labels,
@@ -353,7 +353,7 @@ hipError_t loss_fwd(const float* logits, const int64_t* labels, int64_t V, int K
 hipError_t confusion_only(const float* logits, const int64_t* labels, int64_t V, int K, int ignore,
                           int64_t* conf, hipStream_t s) {
   if (K > KMAX || K < 1) return hipErrorInvalidValue;
-  hipError_t e = hipMemsetAsync(conf, 0, sizeof(int64_t) * K * (K + 1), s);
+  hipError_t e = spff::zero_async(conf, sizeof(int64_t) * K * (K + 1), s);
   if (e != hipSuccess) return e;
   if ((e = loss_lds_attr<false>(K)) != hipSuccess) return e;
   hipLaunchKernelGGL(k_loss<false>, dim3(LOSS_GRID), dim3(LOSS_T), loss_lds(K), s, logits, labels,

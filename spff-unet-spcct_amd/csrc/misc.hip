@@ -467,4 +467,33 @@ hipError_t scale_by_dev(float* x, int64_t n, const float* scale, hipStream_t s) 
   return hipGetLastError();
 }
 
+// hipMemsetAsync replacement for the step's stream-ordered zeroing (counters, amax slots,
+// accumulators): a kernel node, so that a HIP-graph capture of the step replays it like the
+// step's other kernels (scripts/graph_probe3.py: with hipMemsetAsync inside the captured
+// step, the first replay matched the eager step and later ones read stale counters and
+// amax slots).  bytes and p must be multiples of 4.
+template <typename T>
+__global__ void k_fill(T* __restrict__ p, int64_t n, T v) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    p[i] = v;
+}
+
+hipError_t fill32_async(void* p, size_t bytes, unsigned value, hipStream_t s) {
+  if (bytes == 0) return hipSuccess;
+  if ((bytes & 3) || (reinterpret_cast<uintptr_t>(p) & 3)) return hipErrorInvalidValue;
+  if (!((bytes | reinterpret_cast<uintptr_t>(p)) & 15)) {
+    const int64_t n = (int64_t)(bytes / 16);
+    const int grid = (int)std::min<int64_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_fill<uint4>, dim3(grid), dim3(256), 0, s, static_cast<uint4*>(p), n,
+                       make_uint4(value, value, value, value));
+  } else {
+    const int64_t n = (int64_t)(bytes / 4);
+    const int grid = (int)std::min<int64_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_fill<unsigned>, dim3(grid), dim3(256), 0, s, static_cast<unsigned*>(p),
+                       n, value);
+  }
+  return hipGetLastError();
+}
+
 }  // namespace spff

@@ -510,6 +510,12 @@ hipError_t maxpool_fwd(const float* x, float* y, uint8_t* idx, Vol in, int C, hi
 hipError_t maxpool_bwd_add(const float* dp, const uint8_t* idx, const float* dskip, int ldskip,
                            float* dx, Vol in, int C, hipStream_t s);
 hipError_t scale_by_dev(float* x, int64_t n, const float* scale, hipStream_t s);
+// stream-ordered fill of 32-bit words by a kernel (graph-capturable in place of
+// hipMemsetAsync); bytes and p multiples of 4
+hipError_t fill32_async(void* p, size_t bytes, unsigned value, hipStream_t s);
+inline hipError_t zero_async(void* p, size_t bytes, hipStream_t s) {
+  return fill32_async(p, bytes, 0u, s);
+}
 // the decoder's _cat fallback (models.py:687-691): F.interpolate(up, skip size, trilinear,
 // align_corners=False) from (D, Hi, Wi) to (D, Ho, Wo) -- the D factor is exactly 1 --
 // and its backward (gather form, fixed order).  Channel-last, ld = C (multiple of 4).

@@ -379,7 +379,7 @@ int prep_weights(spff_swin* p) {
   unsigned* sl = reinterpret_cast<unsigned*>(p->ws + p->wsl);
   PrepJobs pj;
   PackJobs kj;
-  if (f16) SHIPCK(hipMemsetAsync(sl, 0, NRB * 2 * sizeof(unsigned), p->st));
+  if (f16) SHIPCK(spff::zero_async(sl, NRB * 2 * sizeof(unsigned), p->st));
   for (int i = 0; i < NRB; ++i) {
     RB& r = p->rb[i];
     unsigned* w1 = f16 ? sl + 2 * i : nullptr;
@@ -582,7 +582,7 @@ int stage_bwd(spff_swin* p, Stage& S, const float* tin, const float* dtout, floa
   // the qkv weight gradient reuses wg: take the padded tokens' bias part first
   SHIPCK(linear_dgrad(dq, 3 * C, 3 * C, wd(S.qkv), Bf, C, C, T, nullptr, st));  // Bf = d n1
   float* dpad = p->F(p->dummy);  // [3C] padded-token k / v bias grads
-  SHIPCK(hipMemsetAsync(dpad, 0, fbytes(3 * C), st));
+  SHIPCK(spff::zero_async(dpad, fbytes(3 * C), st));
   SHIPCK(swin_attn_pad_grad(S.g, wg, dpad, st));
   SHIPCK(hipMemcpyAsync(A, dpad, fbytes(3 * C), hipMemcpyDeviceToDevice, st));  // A free again
   SHIPCK(linear_wgrad(p->F(S.n1), C, C, dq, 3 * C, 3 * C, p->DP(S.qkv.w), p->DP(S.qkv.b), T, wg,
@@ -599,9 +599,8 @@ int forward(spff_swin* p, const float* x, float* logits) {
   const int f = p->f;
   const Vol& v0 = p->vol[0];
   hipStream_t st = p->st;
-  SHIPCK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(p->F(p->ones)), 0x3f800000,
-                           (size_t)p->maxC, st));
-  SHIPCK(hipMemsetAsync(p->F(p->zeros), 0, fbytes(p->maxC), st));
+  SHIPCK(spff::fill32_async(p->F(p->ones), (size_t)p->maxC * 4, 0x3f800000u, st));
+  SHIPCK(spff::zero_async(p->F(p->zeros), fbytes(p->maxC), st));
   SHIPCK(ncdhw_to_ndhwc(x, p->F(p->x_cl), v0, c.in_ch, p->ldx, st));
   // patch embedding -> t0 (L1, f); hs0 = LN(t0)
   float* pk = p->F(p->pe_pk);

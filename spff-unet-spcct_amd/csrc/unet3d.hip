@@ -307,7 +307,7 @@ int prep_weights(spff_unet3d* p) {
   unsigned* sl = reinterpret_cast<unsigned*>(p->ws + p->wsl);
   PrepJobs pj;
   PackJobs kj;
-  if (f16) UHIPCK(hipMemsetAsync(sl, 0, NBLK * 2 * sizeof(unsigned), p->st));
+  if (f16) UHIPCK(spff::zero_async(sl, NBLK * 2 * sizeof(unsigned), p->st));
   for (int i = 0; i < NBLK; ++i) {
     UBlk& b = p->blk[i];
     unsigned* w1 = f16 ? sl + 2 * i : nullptr;
