@@ -711,7 +711,7 @@ def main():
                          "workloads), the eager loop of the same K steps beside it; auto = on "
                          "for patch128 at N = 1.  The replay's loss must equal the eager "
                          "step's bit for bit, else value falls back to the eager time")
-    ap.add_argument("--pmc", default=str(ROOT / "profiles" / "r05_pmc_conv.json"),
+    ap.add_argument("--pmc", default=str(ROOT / "profiles" / "r06_pmc_conv.json"),
                     help="per-launch HBM traffic summary from rocprofv3 --pmc "
                          "(scripts/pmc_traffic.py); used only when its workload key matches")
     args = ap.parse_args()
