@@ -839,33 +839,42 @@ def main():
         # launches: no host syncs, static shapes, the plan's workspace fixed) and replayed:
         # the same kernels, without the host round trips between them
         eager = elapsed
-        side = torch.cuda.Stream(device)
-        side.wait_stream(torch.cuda.current_stream(device))
-        with torch.cuda.stream(side):
-            step()
-        torch.cuda.current_stream(device).wait_stream(side)
-        torch.cuda.synchronize()
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            gloss = step()
-        for _ in range(2):
-            g.replay()
-        g_elapsed, _ = timed(g.replay, args.steps)
-        # the engine is deterministic: a replay on the same inputs reproduces the eager
-        # step's loss bit for bit (tests/test_gpu_graph.py); anything else means the
-        # capture missed work, and the eager time stands
-        same = float(gloss) == float(loss)
-        graph_rec = {"eager_ms_per_step": eager / args.steps * 1e3,
-                     "graph_ms_per_step": g_elapsed / args.steps * 1e3,
-                     "replay_loss_equals_eager": same,
-                     "note": ("value = the graph replays" if same else
-                              "value = the EAGER loop: the replay's loss differed") +
-                             "; both loops without profiling events"}
-        if same:
-            elapsed, loss = g_elapsed, gloss
-        else:
-            print(f"bench.py: HIP-graph replay loss {float(gloss)!r} != eager {float(loss)!r}; "
-                  "reporting the eager time", file=sys.stderr, flush=True)
+        try:
+            side = torch.cuda.Stream(device)
+            side.wait_stream(torch.cuda.current_stream(device))
+            with torch.cuda.stream(side):
+                step()
+            torch.cuda.current_stream(device).wait_stream(side)
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                gloss = step()
+            for _ in range(2):
+                g.replay()
+            g_elapsed, _ = timed(g.replay, args.steps)
+            # the engine is deterministic: a replay on the same inputs reproduces the eager
+            # step's loss bit for bit (tests/test_gpu_graph.py); anything else means the
+            # capture missed work, and the eager time stands
+            same = float(gloss) == float(loss)
+            graph_rec = {"eager_ms_per_step": eager / args.steps * 1e3,
+                         "graph_ms_per_step": g_elapsed / args.steps * 1e3,
+                         "replay_loss_equals_eager": same,
+                         "note": ("value = the graph replays" if same else
+                                  "value = the EAGER loop: the replay's loss differed") +
+                                 "; both loops without profiling events"}
+            if same:
+                elapsed, loss = g_elapsed, gloss
+            else:
+                print(f"bench.py: HIP-graph replay loss {float(gloss)!r} != eager {float(loss)!r}; "
+                      "reporting the eager time", file=sys.stderr, flush=True)
+        except RuntimeError as e:
+            # a capture the runtime refuses: the eager loop above stands (and says why)
+            torch.cuda.synchronize()
+            graph_rec = {"eager_ms_per_step": eager / args.steps * 1e3, "error": repr(e)[:300],
+                         "note": "value = the EAGER loop: the HIP-graph capture failed"}
+            print(f"bench.py: HIP-graph capture failed ({e!r}); reporting the eager time",
+                  file=sys.stderr, flush=True)
+
     # 2. per-class kernel timing: a separate pass of K eager steps with HIP events around the
     #    engine's launches on its stream (and, sharded, around the collective callbacks)
     plan.prof_enable(True)
