@@ -16,6 +16,9 @@ namespace spff {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+#ifndef SPFF_XTY_U1
+#define SPFF_XTY_U1 16  // voxel pairs in flight per wave of the one-block k_xty (the head wgrad)
+#endif
 // SPFF_GEMM_SPLIT=0 (A/B diagnostics): the fp32 MFMA GEMMs for every math
 #ifndef SPFF_GEMM_SPLIT
 #define SPFF_GEMM_SPLIT 1
@@ -1113,34 +1116,60 @@ __global__ __launch_bounds__(256) void k_xty(const float* __restrict__ X, int ld
   // voxel pairs per iteration, loads issued first: with one 32 x 32 output block (the head:
   // 4-byte loads, 13 of 32 Y lanes live) 16 pairs keep ~4x the bytes in flight per wave that
   // 4 did (the kernel streams x and dy once: bytes in flight, not issue, bound it)
-  constexpr int U = (TM == 1 && TN == 1) ? 16 : 8;
+  constexpr int U = (TM == 1 && TN == 1) ? SPFF_XTY_U1 : 8;
   uint32_t cbd = 0xffffffffu;  // ACT: the (b, d) slab the cached parameters belong to
   float ca[TM], ce[TM], cp[TM], cq[TM];
 #pragma unroll
   for (int t = 0; t < TM; ++t) { ca[t] = 1.f; ce[t] = 0.f; cp[t] = 1.f; cq[t] = 0.f; }
-  for (int64_t p0 = wave; p0 < npairs; p0 += 4 * U) {
+  // !UP: a pair's rows start at a wave-uniform address (scalar registers) and every lane's
+  // offset into them is loop-invariant (32 bits): one VGPR per column block instead of a
+  // 64-bit address per load in flight (180 -> fewer VGPRs, more waves per CU)
+  uint32_t xo[TM], yo[TN];
+#pragma unroll
+  for (int t = 0; t < TM; ++t) {
+    const int col = k10 + 32 * t + l32;
+    xo[t] = col < xsplit ? (uint32_t)(khalf * ldx + col) : (uint32_t)(khalf * ldx2 + col - xsplit);
+  }
+#pragma unroll
+  for (int t = 0; t < TN; ++t) yo[t] = (uint32_t)(khalf * ldy + noff[t]);
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  for (int64_t p0 = wv; p0 < npairs; p0 += 4 * U) {
     float xa[U][TM], yb[U][TN];
     uint32_t vbd[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int64_t v = vb + 2 * (p0 + 4 * u) + khalf;
+      const int64_t v0 = vb + 2 * (p0 + 4 * u);  // the pair's first voxel (uniform)
+      const int64_t v = v0 + khalf;
       const bool vok = (p0 + 4 * u < npairs) && v < ve;
       if constexpr (ACT) {
         uint32_t r;
         udivmod_s((uint32_t)(vok ? v : vb), (uint32_t)act.HW, act.hwsh, vbd[u], r);
       }
-      int64_t yr = 0;
-      if (vok) yr = UP ? up_high_base((uint32_t)v, g.D, g.Hl, g.Wl, g.nsub) * ldy : v * ldy;
+      if constexpr (UP) {
+        int64_t yr = 0;
+        if (vok) yr = up_high_base((uint32_t)v, g.D, g.Hl, g.Wl, g.nsub) * ldy;
 #pragma unroll
-      for (int t = 0; t < TM; ++t) {
-        // X columns >= xsplit come from the second source (torch.cat([X, X2], 1) rows)
-        const int col = k10 + 32 * t + l32;
-        xa[u][t] = (vok && kok[t])
-                       ? (col < xsplit ? X[v * ldx + col] : X2[v * ldx2 + (col - xsplit)])
-                       : 0.f;
+        for (int t = 0; t < TM; ++t) {
+          // X columns >= xsplit come from the second source (torch.cat([X, X2], 1) rows)
+          const int col = k10 + 32 * t + l32;
+          xa[u][t] = (vok && kok[t])
+                         ? (col < xsplit ? X[v * ldx + col] : X2[v * ldx2 + (col - xsplit)])
+                         : 0.f;
+        }
+#pragma unroll
+        for (int t = 0; t < TN; ++t) yb[u][t] = (vok && nok[t]) ? Y[yr + noff[t]] : 0.f;
+      } else {
+        const float* xr = X + v0 * ldx;
+        const float* x2r = X2 + v0 * ldx2;
+        const float* yr = Y + v0 * ldy;
+#pragma unroll
+        for (int t = 0; t < TM; ++t) {
+          const int col = k10 + 32 * t + l32;
+          xa[u][t] = (vok && kok[t]) ? (col < xsplit ? xr[xo[t]] : x2r[xo[t]]) : 0.f;
+        }
+#pragma unroll
+        for (int t = 0; t < TN; ++t) yb[u][t] = (vok && nok[t]) ? yr[yo[t]] : 0.f;
       }
-#pragma unroll
-      for (int t = 0; t < TN; ++t) yb[u][t] = (vok && nok[t]) ? Y[yr + noff[t]] : 0.f;
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
