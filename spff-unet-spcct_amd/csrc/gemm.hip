@@ -16,6 +16,12 @@ namespace spff {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+#ifndef SPFF_GEMM_OCC3_BN
+// k_gemm_x column blocks up to this width are compiled for 3 workgroups per CU (<= 168
+// VGPRs; the 64-wide up-conv dgrad went 176 -> 168 with 2 spilled): A/B gemm class
+// 2.14 -> 2.10 ms/step.  The 128-wide blocks keep 2 (their accumulators alone are 64 VGPRs)
+#define SPFF_GEMM_OCC3_BN 64
+#endif
 #ifndef SPFF_XTY_U1
 #define SPFF_XTY_U1 16  // voxel pairs in flight per wave of the one-block k_xty (the head wgrad)
 #endif
@@ -560,7 +566,7 @@ __device__ __forceinline__ void gemm_chunk_scale(float ma, float mb, unsigned (&
 }
 
 template <class AL, class CS, int BN, bool V4, int NS = 3>
-__global__ __launch_bounds__(256, 2) void k_gemm_x(AL A, const float* __restrict__ B, CS C,
+__global__ __launch_bounds__(256, BN <= SPFF_GEMM_OCC3_BN ? 3 : 2) void k_gemm_x(AL A, const float* __restrict__ B, CS C,
                                                    int kpad, int npad) {
   constexpr int CB = BN / 16, NRB = BN / 32;  // 16-wide col blocks; B float4 per thread
   constexpr int APL = G_BM * G_BK, BPL = G_BK * BN;  // bf16 per plane
